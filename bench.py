@@ -1,0 +1,175 @@
+"""bench.py -- vertex-updates/s of the MCMC colour-resampling sweep on MI355X.
+
+Workload (BASELINE.json configs[1]): `--mcmcgpu --simulate 0.01 -n 100000`, 16 colours, seed 1.
+The graph is the reference's exact setupRnd2 graph, generated on the GPU (5e9 glibc draws replayed
+by jump-ahead); data = synthetic, as the reference's own --simulate is. A step is one sweep: all
+n vertices resampled (fused sweep kernel + commit kernel). Inputs are resident in HBM before the
+timed region; the timed region is K back-to-back sweeps bracketed by barrier + synchronize.
+
+Prints ONE JSON line (rank 0). Besides the driver contract fields it carries
+  roofline     : dominant kernel (sweep_kernel) algorithmic bytes / its average duration, measured
+                 with hipEvents on the kernel's own stream, against the 8 TB/s HBM peak; traffic =
+                 PMC HBM bytes per launch from the committed rocprofv3 summary, when present
+  cpu_baseline : the oracle (faithful single-thread restatement of --mcmccpu, kind "port") timed on
+                 this host on a bounded number of sweeps of the same graph
+Multi-GPU (torchrun, one process per GPU): each rank sweeps its own replica of the workload
+(replicas only, "weak" scaling) -- the vertex-partitioned RCCL path is reported separately.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(n: int, m: int, taboo: bool = False) -> int:
+    """Bytes one sweep must move at minimum in this build's layout (DESIGN.md "Roofline"):
+    uint64 row offsets, uint32 neighbour ids, uint8 colour read + write (+ uint32 taboo r/w)."""
+    return 8 * (n + 1) + 4 * m + n + n + (8 * n if taboo else 0)
+
+
+def load_traffic(config: str):
+    """HBM bytes per sweep_kernel launch from the committed rocprofv3 PMC summary (or None)."""
+    p = ROOT / "profiles" / "pmc_summary.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(config, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window: np.ndarray, n: int,
+                 max_seconds: float = 20.0):
+    """Oracle (tests/oracle_ref.py) on this host, single thread, bounded sample of sweeps."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as O
+
+    O.set_glibc_window(window)
+    t0 = time.perf_counter()
+    r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=1, nthreads=1)
+    one = r.res.loopSeconds
+    k = max(1, min(30, int(max_seconds / max(one, 1e-3))))
+    O.set_glibc_window(window)
+    r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=k, nthreads=1)
+    return {
+        "value": n * r.res.sweepsRun / r.res.loopSeconds,
+        "unit": "vertex-updates/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {r.res.sweepsRun} sweeps of the same graph/seed (oracle single-thread restatement of "
+                  f"ColoringMCMC_CPU::run incl. its 4 arc passes/sweep, debugger hook excluded); "
+                  f"{time.perf_counter() - t0:.1f} s wall",
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--prob", type=float, default=0.01)
+    ap.add_argument("--ncol", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    import mcmc_colorer_amd.colorer as M
+    from mcmc_colorer_amd._lib import check, lib
+
+    dev = local
+    t_gen = time.perf_counter()
+    rng = M.GlibcRand(1)
+    window0 = rng.window.copy()
+    g = M.Graph.simulate(a.n, a.prob, rng, device=dev)
+    t_gen = time.perf_counter() - t_gen
+    params = M.ColoringMCMCParams(nCol=a.ncol)
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
+    col.init(0)
+    tot = ctypes.c_double()
+    ker = ctypes.c_double()
+    if a.warmup:
+        check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
+    barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+
+    n, m = g.nNodes, g.nEdges
+    value = world * n * a.steps / wall
+    kernel_ms = ker.value
+    b_alg = algorithmic_bytes(n, m)
+    achieved = b_alg / (kernel_ms * 1e-3) / 1e9
+    out = {
+        "metric": "vertex-updates/sec per MCMC sweep",
+        "value": value,
+        "unit": "vertex-updates/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (reference --simulate generator replayed exactly on the GPU)",
+        "config": {"workload": f"--mcmcgpu --simulate {a.prob} -n {a.n} --nCol {a.ncol} --seed {a.seed}",
+                   "n": n, "arcs": m, "nCol": a.ncol, "parallelism": "replicas" if world > 1 else "single",
+                   "graph_gen_s": round(t_gen, 3)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("c2"),
+                     "kernel": "sweep_kernel", "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        s = g.getStruct()
+        out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed,
+                                           M.GlibcRand(1, a.n * (a.n + 1) // 2).window, n)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,139 @@
+/* include/mcmc_hip.h -- C ABI of libmcmc_hip.so, the MI355X-native MCMC colour-resampling sweep.
+ *
+ * This is the drop-in boundary for the reference's GPU colorer. The reference has no FFI layer;
+ * its boundary is the C++ class surface called from src/main.cu:170-202:
+ *   ColoringMCMC(Graph* inGraph_d, curandState* randStates, ColoringMCMCParams)
+ *                                                      graph_coloring/coloringMCMC.h:47
+ *   void ColoringMCMC::run(int iteration)              graph_coloring/coloringMCMC.h:50
+ *   void ColoringMCMC::setDirectoryPath(std::string)   graph_coloring/coloringMCMC.h:51
+ *   Graph(Graph* host) -- device copy of the CSR        graph/graph.h:100, graphGPU.cu:210-226
+ *   GPURand(n, seed)   -- per-vertex RNG states         GPUutils/GPURandomizer.h:42-55
+ * Each entry point below names the piece of that surface it replaces. The C++ wrapper
+ * (include/mcmc_colorer.hpp) and the Python mirror (mcmc_colorer_amd/) rebuild the class surface
+ * on top of these functions.
+ *
+ * Semantics: results are bit-identical to the reference's --mcmccpu path
+ * (graph_coloring/coloringMCMC_CPU.cpp) under the same seed and glibc rand() stream position:
+ * same final coloring, same per-sweep conflict counts ("C violations", :152), same sweep count.
+ *
+ * Conventions: every function returns 0 on success and a negative MCMC_E* code on failure, with a
+ * thread-local message in mcmc_last_error(); nothing aborts (the reference prints and aborts,
+ * GPUutils/GPUutils.h:20-26 -- the C++ wrapper restores that behaviour). Host arrays belong to the
+ * caller and are copied; device buffers belong to the context. A context is not thread-safe.
+ */
+#ifndef MCMC_HIP_H
+#define MCMC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCMC_OK 0
+#define MCMC_E_ARG (-1)      /* invalid argument                       */
+#define MCMC_E_HIP (-2)      /* HIP runtime error                      */
+#define MCMC_E_NOMEM (-3)    /* device or host allocation failed       */
+#define MCMC_E_STATE (-4)    /* call out of order / context unusable   */
+#define MCMC_E_DEVICE (-5)   /* device-side failure flag (see message) */
+
+typedef struct mcmc_ctx mcmc_ctx;
+typedef struct mcmc_graph mcmc_graph;
+
+/* Mirrors ColoringMCMCParams (graph_coloring/coloring.h:65-74) plus the colorer seed, which the
+ * reference passes separately (ColoringMCMC_CPU ctor, coloringMCMC_CPU.h:15; main.cu:171 seed+i). */
+typedef struct {
+    uint32_t nCol;           /* number of colours; main.cu:162 default maxDeg * numColorRatio       */
+    float    epsilon;        /* 1e-8f (main.cu:163)                                                 */
+    float    lambda;         /* 1.0f  (main.cu:164; unused by the sweep, kept for the surface)      */
+    float    ratioFreezed;   /* 1e-2  (main.cu:165; unused)                                         */
+    float    numColorRatio;  /* 1/numColRatio (main.cu:53,161)                                      */
+    uint32_t maxRip;         /* 250   (main.cu:166): at most maxRip+1 sweeps (coloringMCMC_CPU.cpp:264-269) */
+    uint32_t tabooIteration; /* --tabooIteration (main.cu:167), default 0                           */
+    int32_t  tailcut;        /* --tailcut: loop exits when Cviol <= max(50, n/2000) (:89-97)        */
+    uint32_t seed;           /* engine seed (std::default_random_engine(seed), :53)                */
+} mcmc_params;
+
+/* Per-run summary; the fields the reference writes to its .log (coloringMCMC_CPUutils.cpp:177-210). */
+typedef struct {
+    uint32_t iter;             /* "Iteration performed"                                          */
+    int32_t  maxIterReached;   /* "Max iteration reached"                                        */
+    uint64_t finalViol;        /* conflicting vertices of the returned coloring                  */
+    uint64_t trajLen;          /* = iter + 1 entries of per-sweep Cviol (mcmc_get_trajectory)    */
+    uint64_t glibcDraws;       /* rand() draws consumed by CDF-overflow events                   */
+    uint64_t initDraws;        /* engine draws of the initial coloring (n + rejections)          */
+    double   loopMs;           /* device time of the sweep loop (hipEvent)                       */
+    uint32_t sweepsRun;        /* sweeps executed (= iter, plus the final count-only pass)       */
+    uint32_t reserved;
+} mcmc_run_stats;
+
+const char* mcmc_last_error(void);
+int mcmc_version(void);
+
+/* ---- glibc rand() stream (the process-global stream the reference shares between setupRnd2
+ *      (graphCPU.cpp:441) and the overflow fallback (coloringMCMC_CPU.cpp:518)) ---------------
+ * A position is the 31-word window of glibc TYPE_3 state. srand(seed) followed by `draws` calls
+ * of rand(); jumps in O(31^2 log draws). Replaces nothing in the reference (it used the libc
+ * global); needed because the GPU replays the reference's exact rand() draws. */
+int mcmc_glibc_window(uint32_t seed, uint64_t draws, uint32_t window[31]);
+int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out); /* advances window */
+
+/* ---- Graph: Graph(Graph* host) device copy (graph/graph.h:100, graphGPU.cu:210-226) -------- */
+/* Copies a host CSR (uint64 offsets: the reference's uint32 node_sz overflows beyond 2^32 arcs,
+ * graph.h:19-20) to the device. */
+int mcmc_graph_upload(const uint64_t* row_off, const uint32_t* col_idx, uint32_t n, uint64_t m,
+                      int device, mcmc_graph** out);
+/* Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537) generated ON the device, bit-exact:
+ * the n(n+1)/2 glibc draws start at `window` (advanced on return, as the reference's global
+ * stream is). Neighbour lists ascending, as the reference's. */
+int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device, mcmc_graph** out);
+/* Fast Erdos-Renyi G(n,p) stand-in (counter-based, geometric skips) for sizes where the
+ * reference's O(n^2) generator is infeasible. Not the reference's graph. */
+int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out);
+int mcmc_graph_info(const mcmc_graph* g, uint32_t* n, uint64_t* m, uint32_t* maxDeg, uint32_t* minDeg);
+/* Device pointers (row_off: uint64[n+1], col_idx: uint32[m]) for zero-copy callers. */
+int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const uint32_t** col_idx);
+int mcmc_graph_download(const mcmc_graph* g, uint64_t* row_off, uint32_t* col_idx);
+void mcmc_graph_destroy(mcmc_graph* g);
+
+/* ---- Colorer: ColoringMCMC(Graph*, curandState*, ColoringMCMCParams) (coloringMCMC.h:47) ---- */
+/* Rows [v_begin, v_end) are swept by this context (the whole graph: 0, n). Colour replicas are
+ * always full-length, so a vertex-partitioned multi-GPU run keeps global ids. The context
+ * borrows `g` (it must outlive the context). */
+int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end,
+                mcmc_ctx** out);
+/* Position of the glibc stream the overflow fallback draws from (default: srand(1), no draws). */
+int mcmc_set_glibc_window(mcmc_ctx* c, const uint32_t window[31]);
+int mcmc_get_glibc_window(mcmc_ctx* c, uint32_t window[31]);
+/* ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:53-61): C[v] = uniform_int(0, nCol-1)
+ * from std::default_random_engine(seed) in vertex order, or the caller's C0 if non-NULL. */
+int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0);
+/* run() main loop (coloringMCMC_CPU.cpp:127-270) on the device: sweeps until Cviol <= z or the
+ * maxRip cap. max_sweeps > 0 stops early after that many sweeps (bounded samples). */
+int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats);
+int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out /* n */);
+int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
+/* Timed throughput mode for benchmarks: exactly `sweeps` sweeps of the loop body (no
+ * convergence exit, no cap), returns device ms measured with hipEvents on the sweep stream, and
+ * the average duration of the dominant sweep kernel. */
+int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms);
+void mcmc_destroy(mcmc_ctx* c);
+
+/* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------
+ * One sweep = mcmc_part_sweep (local rows) -> caller all-gathers the owned colour slabs and the
+ * (viol, events) footers of every rank -> mcmc_part_commit with the concatenated, rank-ordered
+ * event list. Every rank replays the same glibc draws, so replicas stay identical. */
+int mcmc_part_sweep(mcmc_ctx* c, uint64_t* local_viol, uint32_t* n_events);
+int mcmc_part_events(mcmc_ctx* c, uint32_t* out, uint32_t cap);
+/* Device pointer of the next-colour buffer (full length n, element size mcmc_color_bytes). */
+int mcmc_part_next_colors(mcmc_ctx* c, void** dev_ptr, uint32_t* elem_bytes);
+/* total_viol: the global Cviol of the current colouring (sum of all ranks' local_viol).
+ * Returns *finished = 1 when the loop is over (colouring not advanced); else applies the
+ * events, swaps the buffers and advances the RNG. */
+int mcmc_part_commit(mcmc_ctx* c, uint64_t total_viol, const uint32_t* events, uint32_t n_events,
+                     int32_t* finished);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCMC_HIP_H */

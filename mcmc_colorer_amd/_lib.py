@@ -1,0 +1,116 @@
+"""ctypes binding of libmcmc_hip.so (include/mcmc_hip.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load, importing
+the colorer raises. Build it with ``python -m mcmc_colorer_amd.build`` (or ``__graft_entry__.build``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_char_p, c_double, c_float, c_int, c_int32, c_uint32, c_uint64, c_void_p
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(os.environ.get("MCMC_HIP_LIB", Path(__file__).resolve().parent / "libmcmc_hip.so"))
+
+# Every symbol declared in include/mcmc_hip.h, with (restype, argtypes).
+_u32p = POINTER(c_uint32)
+_u64p = POINTER(c_uint64)
+SIGNATURES: dict[str, tuple] = {
+    "mcmc_last_error": (c_char_p, []),
+    "mcmc_version": (c_int, []),
+    "mcmc_glibc_window": (c_int, [c_uint32, c_uint64, _u32p]),
+    "mcmc_glibc_draw": (c_int, [_u32p, c_uint32, _u32p]),
+    "mcmc_graph_upload": (c_int, [_u64p, _u32p, c_uint32, c_uint64, c_int, POINTER(c_void_p)]),
+    "mcmc_graph_simulate": (c_int, [c_uint32, c_float, _u32p, c_int, POINTER(c_void_p)]),
+    "mcmc_graph_er_fast": (c_int, [c_uint32, c_double, c_uint64, c_int, POINTER(c_void_p)]),
+    "mcmc_graph_info": (c_int, [c_void_p, _u32p, _u64p, _u32p, _u32p]),
+    "mcmc_graph_device_ptrs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
+    "mcmc_graph_download": (c_int, [c_void_p, _u64p, _u32p]),
+    "mcmc_graph_destroy": (None, [c_void_p]),
+    "mcmc_create": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "mcmc_set_glibc_window": (c_int, [c_void_p, _u32p]),
+    "mcmc_get_glibc_window": (c_int, [c_void_p, _u32p]),
+    "mcmc_init_coloring": (c_int, [c_void_p, _u32p]),
+    "mcmc_run": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "mcmc_get_coloring": (c_int, [c_void_p, _u32p]),
+    "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
+    "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
+    "mcmc_destroy": (None, [c_void_p]),
+    "mcmc_part_sweep": (c_int, [c_void_p, _u64p, _u32p]),
+    "mcmc_part_events": (c_int, [c_void_p, _u32p, c_uint32]),
+    "mcmc_part_next_colors": (c_int, [c_void_p, POINTER(c_void_p), _u32p]),
+    "mcmc_part_commit": (c_int, [c_void_p, c_uint64, _u32p, c_uint32, POINTER(c_int32)]),
+}
+
+
+class MCMCParams(ctypes.Structure):
+    """mcmc_params == ColoringMCMCParams (graph_coloring/coloring.h:65-74) + seed."""
+
+    _fields_ = [
+        ("nCol", c_uint32),
+        ("epsilon", c_float),
+        ("lambda_", c_float),
+        ("ratioFreezed", c_float),
+        ("numColorRatio", c_float),
+        ("maxRip", c_uint32),
+        ("tabooIteration", c_uint32),
+        ("tailcut", c_int32),
+        ("seed", c_uint32),
+    ]
+
+
+class MCMCRunStats(ctypes.Structure):
+    _fields_ = [
+        ("iter", c_uint32),
+        ("maxIterReached", c_int32),
+        ("finalViol", c_uint64),
+        ("trajLen", c_uint64),
+        ("glibcDraws", c_uint64),
+        ("initDraws", c_uint64),
+        ("loopMs", c_double),
+        ("sweepsRun", c_uint32),
+        ("reserved", c_uint32),
+    ]
+
+
+class MCMCError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Loads libmcmc_hip.so once. Raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise MCMCError(f"{LIB_PATH} not found: build it with `python -m mcmc_colorer_amd.build`")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().mcmc_last_error()
+        raise MCMCError(f"libmcmc_hip error {rc}: {msg.decode() if msg else ''}")
+
+
+def u32ptr(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u32p)
+
+
+def u64ptr(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_u64p)
+
+
+__all__ = ["lib", "check", "MCMCParams", "MCMCRunStats", "MCMCError", "SIGNATURES", "u32ptr", "u64ptr", "byref"]

@@ -1,0 +1,286 @@
+"""Host-side mirror of the reference's colorer surface, over libmcmc_hip.so.
+
+Reference classes (paths relative to /root/reference/src):
+  ColoringMCMCParams        graph_coloring/coloring.h:65-74
+  Graph<float,float>        graph/graph.h:84-133  (ctor (n, prob, seed) -> setupRnd2; (Graph*) device copy)
+  GraphStruct               graph/graph.h:37-79
+  GPURand                   GPUutils/GPURandomizer.h:42-55 (per-vertex RNG handle passed to the colorer)
+  ColoringMCMC<float,float> graph_coloring/coloringMCMC.h:44-140 (ctor, run(int), setDirectoryPath)
+
+Semantics are those of ColoringMCMC_CPU (graph_coloring/coloringMCMC_CPU.cpp): the north star
+requires --mcmcgpu to be bit-identical to --mcmccpu. Where the reference shares process-global
+state (glibc rand(), used by setupRnd2 and by the CDF-overflow fallback), it is an explicit
+``GlibcRand`` object here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+from ._lib import MCMCParams, MCMCRunStats, check, lib, u32ptr, u64ptr
+
+F32_EPS = float(np.float32(1e-8))
+
+
+@dataclass
+class ColoringMCMCParams:
+    """ColoringMCMCParams (coloring.h:65-74) with main.cu:160-168 defaults."""
+
+    nCol: int = 0
+    numColorRatio: float = 1.0
+    lambda_: float = 1.0
+    epsilon: float = F32_EPS
+    ratioFreezed: float = 1e-2
+    maxRip: int = 250
+    tabooIteration: int = 0
+    tailcut: bool = False
+
+    def to_c(self, seed: int) -> MCMCParams:
+        return MCMCParams(self.nCol, self.epsilon, self.lambda_, self.ratioFreezed, self.numColorRatio,
+                          self.maxRip, self.tabooIteration, int(bool(self.tailcut)), seed & 0xFFFFFFFF)
+
+
+class GlibcRand:
+    """Position in glibc's rand() stream (TYPE_3 window of 31 words).
+
+    The reference uses the process-global stream: unseeded (== srand(1)) when --seed is given
+    (ArgHandle.cpp:272-276), advanced n(n+1)/2 draws by setupRnd2 (graphCPU.cpp:441) and one
+    draw per CDF overflow (coloringMCMC_CPU.cpp:518)."""
+
+    def __init__(self, seed: int = 1, draws: int = 0):
+        self.window = np.zeros(31, dtype=np.uint32)
+        check(lib().mcmc_glibc_window(seed & 0xFFFFFFFF, draws, u32ptr(self.window)))
+
+    def rand(self, count: int = 1) -> np.ndarray:
+        out = np.zeros(count, dtype=np.uint32)
+        check(lib().mcmc_glibc_draw(u32ptr(self.window), count, u32ptr(out)))
+        return out
+
+
+@dataclass
+class GraphStruct:
+    """GraphStruct (graph.h:37-79): nNodes, nEdges, cumulDegs (uint64 here), neighs."""
+
+    nNodes: int
+    nEdges: int
+    cumulDegs: np.ndarray
+    neighs: np.ndarray
+
+    def deg(self, i: int) -> int:
+        return int(self.cumulDegs[i + 1] - self.cumulDegs[i])
+
+
+class Graph:
+    """Device-resident CSR graph (Graph<float,float> after its (Graph*) device copy)."""
+
+    def __init__(self, handle: ctypes.c_void_p, prob: float = 0.0, device: int = 0):
+        self._h = handle
+        self.prob = float(prob)
+        self.device = device
+        n = ctypes.c_uint32()
+        m = ctypes.c_uint64()
+        mx = ctypes.c_uint32()
+        mn = ctypes.c_uint32()
+        check(lib().mcmc_graph_info(self._h, ctypes.byref(n), ctypes.byref(m), ctypes.byref(mx), ctypes.byref(mn)))
+        self.nNodes, self.nEdges, self.maxDeg, self.minDeg = n.value, m.value, mx.value, mn.value
+        self._struct: Optional[GraphStruct] = None
+
+    @classmethod
+    def simulate(cls, n: int, prob: float, rand: GlibcRand, device: int = 0) -> "Graph":
+        """Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537), generated on the GPU.
+        Advances ``rand`` by n(n+1)/2 draws, as the reference's global stream is."""
+        h = ctypes.c_void_p()
+        check(lib().mcmc_graph_simulate(n, ctypes.c_float(prob), u32ptr(rand.window), device, ctypes.byref(h)))
+        return cls(h, prob=float(np.float32(prob)), device=device)
+
+    @classmethod
+    def from_csr(cls, row_off: np.ndarray, col_idx: np.ndarray, device: int = 0, prob: float = 0.0) -> "Graph":
+        """Graph(Graph* host) device copy (graphGPU.cu:210-226) of a host CSR."""
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        col_idx = np.ascontiguousarray(col_idx, dtype=np.uint32)
+        n = len(row_off) - 1
+        h = ctypes.c_void_p()
+        check(lib().mcmc_graph_upload(u64ptr(row_off), u32ptr(col_idx) if len(col_idx) else None, n,
+                                      len(col_idx), device, ctypes.byref(h)))
+        if prob == 0.0 and n > 0:
+            prob = len(col_idx) / float(np.float32(n) * np.float32(n))   # graphCPU.cpp:158 (without the overflow)
+        return cls(h, prob=prob, device=device)
+
+    def getStruct(self) -> GraphStruct:
+        if self._struct is None:
+            off = np.zeros(self.nNodes + 1, dtype=np.uint64)
+            idx = np.zeros(max(self.nEdges, 1), dtype=np.uint32)
+            check(lib().mcmc_graph_download(self._h, u64ptr(off), u32ptr(idx)))
+            self._struct = GraphStruct(self.nNodes, self.nEdges, off, idx[: self.nEdges])
+        return self._struct
+
+    def getMaxNodeDeg(self) -> int:
+        return self.maxDeg
+
+    def getMinNodeDeg(self) -> int:
+        return self.minDeg
+
+    def getMeanNodeDeg(self) -> float:
+        return float(np.float32(self.nEdges) / np.float32(self.nNodes)) if self.nNodes else 0.0
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            lib().mcmc_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GPURand:
+    """GPURand(n, seed) (GPURandomizer.h:42-55). The reference keeps 48-byte cuRAND states per
+    vertex; this build needs none (counter-based minstd skip-ahead), only the seed and the glibc
+    stream the CDF-overflow fallback draws from."""
+
+    def __init__(self, n: int, seed: int, glibc: Optional[GlibcRand] = None):
+        self.n = n
+        self.seed = seed
+        self.glibc = glibc if glibc is not None else GlibcRand(1)
+        self.randStates = self   # the reference's public member name
+
+
+def default_ncol(graph: Graph, params: ColoringMCMCParams, nColFromC: int = 0) -> int:
+    """main.cu:162: nCol = --nCol, else (uint32)(maxDeg * numColorRatio) in float."""
+    if nColFromC:
+        return nColFromC
+    return int(np.float32(graph.getMaxNodeDeg()) * np.float32(params.numColorRatio))
+
+
+class ColoringMCMC:
+    """ColoringMCMC<float,float> (coloringMCMC.h:44-140) on the MI355X sweep.
+
+    ``run(iteration)`` colours with engine seed ``rand.seed + iteration`` (main.cu:171's seed+i)
+    from the glibc stream position held by ``rand.glibc`` (advanced in place), and, when a
+    directory path is set, writes ``<dir>.log`` and ``<dir>-colors.txt`` like the reference's
+    colorers (coloringMCMC_prints.cu:37-38; report fields of coloringMCMC_CPUutils.cpp:177-217)."""
+
+    def __init__(self, graph_d: Graph, randStates: GPURand, params: ColoringMCMCParams,
+                 v_begin: int = 0, v_end: Optional[int] = None):
+        if params.nCol == 0:
+            params = ColoringMCMCParams(**{**params.__dict__, "nCol": default_ncol(graph_d, params)})
+        self.graph = graph_d
+        self.rand = randStates
+        self.param = params
+        self.v_begin = v_begin
+        self.v_end = graph_d.nNodes if v_end is None else v_end
+        self.directory: Optional[str] = None
+        self._ctx = ctypes.c_void_p()
+        self._cparams = params.to_c(randStates.seed)
+        check(lib().mcmc_create(graph_d.handle, ctypes.byref(self._cparams), self.v_begin, self.v_end,
+                                ctypes.byref(self._ctx)))
+        self.stats: Optional[MCMCRunStats] = None
+        self.duration = 0.0
+
+    def setDirectoryPath(self, directory: str) -> None:
+        self.directory = directory
+
+    def init(self, iteration: int = 0, C0: Optional[np.ndarray] = None) -> None:
+        self._cparams.seed = (self.rand.seed + iteration) & 0xFFFFFFFF
+        lib().mcmc_destroy(self._ctx)
+        self._ctx = ctypes.c_void_p()
+        check(lib().mcmc_create(self.graph.handle, ctypes.byref(self._cparams), self.v_begin, self.v_end,
+                                ctypes.byref(self._ctx)))
+        check(lib().mcmc_set_glibc_window(self._ctx, u32ptr(self.rand.glibc.window)))
+        c0 = None if C0 is None else u32ptr(np.ascontiguousarray(C0, dtype=np.uint32))
+        check(lib().mcmc_init_coloring(self._ctx, c0))
+
+    def run(self, iteration: int = 0, max_sweeps: int = 0) -> MCMCRunStats:
+        self.init(iteration)
+        st = MCMCRunStats()
+        check(lib().mcmc_run(self._ctx, max_sweeps, ctypes.byref(st)))
+        check(lib().mcmc_get_glibc_window(self._ctx, u32ptr(self.rand.glibc.window)))
+        self.stats = st
+        self.duration = st.loopMs / 1000.0
+        if self.directory:
+            self.save(iteration)
+        return st
+
+    # -- results ------------------------------------------------------------------------------
+    def coloring(self) -> np.ndarray:
+        out = np.zeros(self.graph.nNodes, dtype=np.uint32)
+        check(lib().mcmc_get_coloring(self._ctx, u32ptr(out)))
+        return out
+
+    def trajectory(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        check(lib().mcmc_get_trajectory(self._ctx, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            check(lib().mcmc_get_trajectory(self._ctx, u64ptr(out), n.value, ctypes.byref(n)))
+        return out
+
+    def save(self, iteration: int) -> None:
+        d = self.directory
+        Path(d).parent.mkdir(parents=True, exist_ok=True)
+        C = self.coloring()
+        write_report(d + ".log", "GPU (MI355X)", self.graph, self.param, self.rand.seed + iteration, iteration,
+                     self.duration, self.stats, C)
+        with open(d + "-colors.txt", "w") as f:
+            f.write("".join(f"{i} {c}\n" for i, c in enumerate(C.tolist())))
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().mcmc_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def write_report(path: str, flavour: str, graph: Graph, p: ColoringMCMCParams, seed: int, rep: int,
+                 duration: float, st: MCMCRunStats, C: np.ndarray) -> None:
+    """The .log block of saveStats (coloringMCMC_CPUutils.cpp:177-210), parseable by the
+    reference's pyScripts/logParser.py lineParser."""
+    nCol = p.nCol
+    hist = np.bincount(C, minlength=nCol).astype(np.int64)
+    used = int((hist > 0).sum())
+    mean = np.float32(hist.sum()) / np.float32(nCol)
+    var = np.float32(0)
+    for h in hist:
+        var = np.float32(var + np.float32((np.float32(h) - mean) * (np.float32(h) - mean)))
+    var = np.float32(var / np.float32(nCol))
+    lines = [
+        f"MCMC Colorer - {flavour} version - Report",
+        "-------------------------------------------",
+        "GRAPH INFO",
+        f"Nodes: {graph.nNodes} - Edges: {graph.nEdges}",
+        f"Max deg: {graph.getMaxNodeDeg()} - Min deg: {graph.getMinNodeDeg()} - Avg deg: {graph.getMeanNodeDeg():g}",
+        f"Edge probability (for randomly generated graphs): {graph.prob:g}",
+        f"Seed: {seed}",
+        "-------------------------------------------",
+        "EXECUTION INFO",
+        f"Repetition: {rep}",
+        f"Execution time: {duration:g}",
+        f"Iteration performed: {st.iter}",
+        f"Max iteration reached: {'yes' if st.maxIterReached else 'no'}",
+        "-------------------------------------------",
+        "Color histogram:",
+        *[f"{i}: {int(h)}" for i, h in enumerate(hist)],
+        f"Number of colors: {nCol} - Used colors: {used}",
+        f"Color ratio: {p.numColorRatio:g}",
+        f"Average number of nodes for each color: {float(mean):g}",
+        f"Variance: {float(var):g}",
+        f"StD: {float(np.sqrt(var)):g}",
+    ]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")

@@ -1,0 +1,885 @@
+// mcmc_colorer_amd/csrc/mcmc_sweep.hip -- the MCMC colour-resampling sweep for gfx950.
+//
+// Replaces the reference's per-sweep kernel chain (graph_coloring/coloringMCMC_main.cu:160-269:
+// conflictCounter + sumReduction twice, a host histogram round trip, genDynamicDistribution,
+// selectStarColoringBalanceDynamic) with ONE fused kernel per sweep plus a one-workgroup commit
+// kernel, and implements the --mcmccpu semantics bit-exactly:
+//
+//   sweep_kernel   one neighbour scan per vertex builds the occupancy mask of the colours of N(v)
+//                  (count_free_colors, coloringMCMC_CPU.cpp:362-383); viol_v = own colour
+//                  occupied (violation_count, :329-351); p(c) in fp32 (fill_p, :393-481);
+//                  u_v = minstd draw K_t + v + 1 by skip-ahead (:139); CDF walk with strict >
+//                  (extract_new_color, :493-528); Cstar, taboo; Cviol_t by ballot/popcount;
+//                  CDF overflows appended to an event list.
+//   commit_kernel  loop control of run() (:136, :264-269): records Cviol_t, stops on
+//                  Cviol_t <= z or the maxRip cap, otherwise replays overflow events in ascending
+//                  vertex order against the glibc rand() window (`rand() % (nCol-1)`, :518),
+//                  advances the minstd position by n and flips the colour buffers.
+//
+// The loop is device-resident: both kernels read the sweep index and RNG position from DevState,
+// so a batch of (sweep, commit) pairs is captured once into a hipGraph and replayed until the
+// commit kernel raises `done`. No host synchronisation inside a batch.
+//
+// Compiled with -ffp-contract=off: fill_p's products and quotients must round exactly as the
+// reference's SSE code (no FMA), and fp32 division stays IEEE-correct (hipcc default).
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "mcmc_common.h"
+#include "rng.h"
+
+namespace mcmc {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Device-resident loop state (one per context).
+struct DevState {
+    uint32_t t;                 // sweep index == ColoringMCMC_CPU::iter
+    uint32_t done;              // loop finished (set by commit)
+    uint32_t x_t;               // minstd state after K0 + t*n draws
+    uint32_t err;               // bit0: event list overflow
+    unsigned long long viol;    // sum of viol_v over the swept rows (Cviol_t)
+    uint32_t ev_count;          // overflow events this sweep
+    uint32_t glibc_head;        // ring head of the glibc window
+    uint32_t glibc_ring[31];
+    uint32_t init_rejections;
+    unsigned long long glibc_draws;
+    unsigned long long finalViol;
+    uint32_t iter;
+    uint32_t maxIterReached;
+};
+
+struct SweepArgs {
+    const uint64_t* row_off;    // local rows: row_off[v - v_begin], length (v_end - v_begin) + 1
+    const uint32_t* col_idx;    // global vertex ids
+    uint8_t* colors0;           // full-length colour replicas (C_t lives in colors[t & 1])
+    uint8_t* colors1;
+    uint32_t* taboo;            // local rows, nullptr when tabooIteration == 0
+    uint32_t* events;           // overflow event list (global vertex ids)
+    DevState* st;
+    unsigned long long* traj;   // per-sweep Cviol, traj_cap entries
+    uint32_t traj_cap;
+    uint32_t ev_cap;
+    uint32_t n, v_begin, v_end;
+    uint32_t nCol, tabooIteration, maxRip, z;
+    uint32_t tile;              // vertices per wave-tile (<= 64)
+    uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
+    float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
+    int check_done;             // device-resident loop: exit immediately once done
+};
+
+__constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
+__constant__ uint32_t kMinstdPow2[64];      // 16807^(2^i) mod (2^31-1), i = 0..63
+
+// 16807^e mod (2^31-1) from the squares table: one mulmod per set bit of e.
+__device__ __forceinline__ uint32_t minstd_pow_tab(uint64_t e) {
+    uint32_t r = 1;
+    for (int i = 0; e; i++, e >>= 1)
+        if (e & 1) r = minstd_mulmod(r, kMinstdPow2[i]);
+    return r;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int NW>
+__device__ __forceinline__ void set_color_bit(uint32_t (&m)[NW], uint32_t c) {
+    if (NW == 1) {
+        m[0] |= 1u << c;
+    } else {
+        const uint32_t w = c >> 5, bit = 1u << (c & 31);
+#pragma unroll
+        for (int i = 0; i < NW; i++) m[i] |= (w == (uint32_t)i) ? bit : 0u;
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t get_color_bit(const uint32_t (&m)[NW], uint32_t c) {
+    if (NW == 1) return (m[0] >> c) & 1u;
+    uint32_t r = 0;
+    const uint32_t w = c >> 5;
+#pragma unroll
+    for (int i = 0; i < NW; i++) r |= (w == (uint32_t)i) ? ((m[i] >> (c & 31)) & 1u) : 0u;
+    return r;
+}
+
+template <int NW>
+__device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        uint32_t x = m[i];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x |= __shfl_xor(x, off, 64);
+        m[i] = x;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// The fused sweep. One wave owns a tile of `tile` consecutive vertices: for each of them the 64
+// lanes stride its CSR row (coalesced col_idx loads, colour gathers) and OR-reduce the occupancy
+// mask; lane j keeps vertex j's mask. Then every lane evaluates its own vertex: viol, p, u, the
+// CDF walk and the writes.
+template <int NW>
+__global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
+    DevState* __restrict__ st = a.st;
+    if (a.check_done && st->done) return;
+    const uint32_t t = st->t;
+    const uint32_t x_t = st->x_t;
+    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
+    uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
+    const uint32_t* __restrict__ col_idx = a.col_idx;
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint32_t ntiles = (nloc + a.tile - 1) / a.tile;
+
+    for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += gridDim.x * wpb) {
+        const uint32_t l0 = tile * a.tile;
+        const uint32_t cnt = min(a.tile, nloc - l0);
+        uint64_t myoff = 0;
+        if ((uint32_t)lane <= cnt) myoff = a.row_off[l0 + lane];
+
+        uint32_t acc[NW];
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = 0;
+
+        for (uint32_t j = 0; j < cnt; j++) {
+            const uint64_t beg = readlane64(myoff, j);
+            const uint64_t end = readlane64(myoff, j + 1);
+            uint32_t m[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) m[i] = 0;
+            uint64_t k = beg + lane;
+            for (; k + 192 < end; k += 256) {
+                const uint32_t w0 = col_idx[k], w1 = col_idx[k + 64], w2 = col_idx[k + 128], w3 = col_idx[k + 192];
+                const uint32_t c0 = C[w0], c1 = C[w1], c2 = C[w2], c3 = C[w3];
+                set_color_bit<NW>(m, c0);
+                set_color_bit<NW>(m, c1);
+                set_color_bit<NW>(m, c2);
+                set_color_bit<NW>(m, c3);
+            }
+            for (; k < end; k += 64) set_color_bit<NW>(m, C[col_idx[k]]);
+            wave_or<NW>(m);
+            if ((uint32_t)lane == j) {
+#pragma unroll
+                for (int i = 0; i < NW; i++) acc[i] = m[i];
+            }
+        }
+
+        // ---- per-vertex evaluation: lane -> vertex v = v_begin + l0 + lane ----
+        const bool valid = (uint32_t)lane < cnt;
+        const uint32_t l = l0 + lane;
+        const uint32_t v = a.v_begin + l;
+        const uint32_t cv = valid ? (uint32_t)C[v] : 0u;
+        uint32_t pop = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) pop += __popc(acc[i]);
+        const bool viol = valid && get_color_bit<NW>(acc, cv);
+        const uint32_t Zvcomp = a.nCol - pop;
+
+        uint32_t tab = 0;
+        if (a.taboo != nullptr && valid) tab = a.taboo[l];
+
+        // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
+        const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
+        const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
+        const float u = minstd_canonical(x);
+
+        // fill_p cases: (ii) viol with free colours -> occupied eps, free pf;
+        //               (i)/(iii) otherwise      -> own colour hi, others eps.
+        uint32_t sel[NW];
+        float pA, pB;
+        if (viol && Zvcomp > 0) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) sel[i] = acc[i];
+            pA = a.eps;
+            pB = (1.0f - a.eps * (float)pop) / (float)Zvcomp;
+        } else {
+#pragma unroll
+            for (int i = 0; i < NW; i++) sel[i] = 0;
+            set_color_bit<NW>(sel, cv);
+            pA = a.hi;
+            pB = a.eps;
+        }
+        // extract_new_color: cdf += p[c]; break on cdf > u (strict).
+        uint32_t newc = a.nCol;
+        if (valid && tab == 0) {
+            float cdf = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                const uint32_t bits = sel[i];
+                const uint32_t cmax = min(32u, a.nCol > (uint32_t)(32 * i) ? a.nCol - 32u * i : 0u);
+                for (uint32_t cc = 0; cc < cmax && newc == a.nCol; cc++) {
+                    cdf += ((bits >> cc) & 1u) ? pA : pB;
+                    if (cdf > u) newc = 32u * i + cc;
+                }
+            }
+        }
+        const bool event = valid && tab == 0 && newc == a.nCol;
+        if (valid) {
+            if (tab > 0) {
+                Cs[v] = (uint8_t)cv;
+                a.taboo[l] = tab - 1;
+            } else if (!event) {
+                Cs[v] = (uint8_t)newc;
+                if (a.taboo != nullptr) a.taboo[l] = (newc == cv) ? a.tabooIteration : 0u;
+            } else {
+                Cs[v] = (uint8_t)cv;   // placeholder, overwritten by the commit's glibc replay
+            }
+        }
+
+        const uint64_t vb = __ballot(viol);
+        if (lane == 0 && vb) atomicAdd(&st->viol, (unsigned long long)__popcll(vb));
+        const uint64_t eb = __ballot(event);
+        if (eb) {
+            uint32_t basei = 0;
+            if (lane == 0) basei = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
+            basei = __shfl(basei, 0, 64);
+            if (event) {
+                const uint32_t idx = basei + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
+                if (idx < a.ev_cap) a.events[idx] = v;
+                else atomicOr(&st->err, 1u);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Commit: loop control + ordered glibc replay. One workgroup.
+constexpr int kCommitThreads = 256;
+constexpr uint32_t kLdsSortCap = 8192;
+
+__device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    const uint32_t x = s[i], y = s[ixj];
+                    if ((x > y) == up) { s[i] = y; s[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Applies the accepted sweep: replays E sorted events, advances the RNG, flips buffers.
+// `ev` holds the events (global ids, any order) and is sorted in place (via LDS when small).
+__device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds) {
+    DevState* st = a.st;
+    const uint8_t* C = (t & 1) ? a.colors1 : a.colors0;
+    uint8_t* Cs = (t & 1) ? a.colors0 : a.colors1;
+    if (E > 0) {
+        uint32_t P = 1;
+        while (P < E) P <<= 1;
+        uint32_t* s = (P <= kLdsSortCap) ? lds : ev;
+        if (s == ev) {
+            for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
+        } else {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        bitonic_sort_block(s, P);
+        if (threadIdx.x == 0) {
+            uint32_t ring[31];
+            for (int i = 0; i < 31; i++) ring[i] = st->glibc_ring[i];
+            uint32_t head = st->glibc_head;
+            for (uint32_t i = 0; i < E; i++) {
+                const uint32_t v = s[i];
+                const uint32_t r = glibc_next(ring, head);
+                const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                Cs[v] = (uint8_t)c;
+                if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
+                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
+            }
+            for (int i = 0; i < 31; i++) st->glibc_ring[i] = ring[i];
+            st->glibc_head = head;
+        }
+    }
+    if (threadIdx.x == 0) {
+        st->glibc_draws += E;
+        st->x_t = minstd_mulmod(st->x_t, a.aN);
+        st->t = t + 1;
+        st->viol = 0;
+        st->ev_count = 0;
+    }
+}
+
+// Loop control of run() (coloringMCMC_CPU.cpp:136, :259-269) for the single-context loop.
+__global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
+    __shared__ uint32_t lds[kLdsSortCap];
+    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
+    __shared__ unsigned long long sh_viol;
+    DevState* st = a.st;
+    if (threadIdx.x == 0) {
+        sh_done = st->done;
+        sh_t = st->t;
+        sh_viol = st->viol;
+        sh_E = st->ev_count;
+        sh_err = st->err;
+    }
+    __syncthreads();
+    if (sh_done) return;
+    const uint32_t t = sh_t;
+    const unsigned long long viol = sh_viol;
+    if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
+    const bool stop_cap = t == a.maxRip + 1;     // iter > maxiter after sweep maxRip
+    const bool stop_conv = viol <= a.z;          // while (Cviol > z)
+    if (stop_cap || stop_conv) {
+        if (threadIdx.x == 0) {
+            st->done = 1;
+            st->iter = t;
+            st->maxIterReached = stop_cap;
+            st->finalViol = viol;
+        }
+        return;
+    }
+    const uint32_t E = sh_E;
+    if (E > a.ev_cap || sh_err) {
+        if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
+        return;
+    }
+    commit_accept(a, t, a.events, E, lds);
+}
+
+// Commit of a vertex-partitioned sweep: global Cviol and the global event list come from the host.
+__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, uint32_t t, uint32_t E) {
+    __shared__ uint32_t lds[kLdsSortCap];
+    commit_accept(a, t, a.events, E, lds);
+}
+
+// ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61): vertex v uses engine draw v + 1 when
+// no earlier draw was rejected by uniform_int_distribution; rejections (P ~ nCol/2^31 each) are
+// counted and handed to the exact sequential host path.
+__global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st) {
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        const uint32_t x = minstd_mulmod(x0, minstd_pow_tab((uint64_t)v + 1));
+        const uint32_t r = x - 1u;
+        if (r >= k.past) atomicAdd(&st->init_rejections, 1u);
+        C[v] = (uint8_t)min(r / k.scaling, 255u);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, hipStream_t);
+template <int NW>
+void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, hipStream_t s) {
+    sweep_kernel<NW><<<g, b, 0, s>>>(a);
+}
+
+static std::once_flag g_const_once;
+static hipError_t g_const_err = hipSuccess;
+
+}  // namespace mcmc
+
+using namespace mcmc;
+
+struct mcmc_ctx {
+    const GraphDev* g = nullptr;
+    mcmc_params p{};
+    uint32_t n = 0, v_begin = 0, v_end = 0;
+    uint32_t nw = 1;
+    uint32_t z = 0;
+    uint8_t* colors[2] = {nullptr, nullptr};
+    uint32_t* taboo = nullptr;
+    uint32_t* events = nullptr;
+    uint32_t ev_cap = 0;
+    DevState* st = nullptr;
+    unsigned long long* traj = nullptr;
+    uint32_t traj_cap = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipGraphExec_t batch_exec = nullptr;
+    uint32_t batch = 0;
+    GlibcWindow glibc{};
+    bool initialized = false;
+    bool ran = false;
+    uint32_t x0 = 0;            // minstd state after the initial colouring (position K0)
+    uint64_t initDraws = 0;
+    mcmc_run_stats last{};
+    SweepLaunch sweep = nullptr;
+    dim3 grid, block;
+    std::vector<uint32_t> host_events;
+};
+
+namespace {
+
+int upload_state(mcmc_ctx* c, uint32_t t) {
+    DevState h{};
+    h.t = t;
+    h.x_t = c->x0;
+    h.glibc_head = 0;
+    for (int i = 0; i < 31; i++) h.glibc_ring[i] = c->glibc.r[i];
+    MCMC_HIP_TRY(hipMemcpyAsync(c->st, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
+
+int download_state(mcmc_ctx* c, DevState* h) {
+    MCMC_HIP_TRY(hipMemcpyAsync(h, c->st, sizeof(*h), hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
+
+SweepArgs make_args(const mcmc_ctx* c, int check_done) {
+    SweepArgs a{};
+    a.row_off = c->g->row_off + c->v_begin;
+    a.col_idx = c->g->col_idx;
+    a.colors0 = c->colors[0];
+    a.colors1 = c->colors[1];
+    a.taboo = c->taboo;
+    a.events = c->events;
+    a.st = c->st;
+    a.traj = c->traj;
+    a.traj_cap = c->traj_cap;
+    a.ev_cap = c->ev_cap;
+    a.n = c->n;
+    a.v_begin = c->v_begin;
+    a.v_end = c->v_end;
+    a.nCol = c->p.nCol;
+    a.tabooIteration = c->p.tabooIteration;
+    a.maxRip = c->p.maxRip;
+    a.z = c->z;
+    a.aN = minstd_pow(kMinstdA, c->n);
+    a.eps = c->p.epsilon;
+    a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
+    a.check_done = check_done;
+    // tile: enough waves to fill 256 CUs x 8 waves, at most 64 vertices per wave
+    const uint32_t nloc = c->v_end - c->v_begin;
+    uint32_t tile = 64;
+    while (tile > 16 && (nloc + tile - 1) / tile < 8192) tile >>= 1;
+    a.tile = tile;
+    return a;
+}
+
+int ensure_constants() {
+    std::call_once(g_const_once, [] {
+        uint32_t pw[64], p2[64];
+        pw[0] = 1;
+        for (int j = 1; j < 64; j++) pw[j] = minstd_mulmod(pw[j - 1], kMinstdA);
+        p2[0] = kMinstdA;
+        for (int j = 1; j < 64; j++) p2[j] = minstd_mulmod(p2[j - 1], p2[j - 1]);
+        g_const_err = hipMemcpyToSymbol(HIP_SYMBOL(kMinstdLanePow), pw, sizeof(pw));
+        if (g_const_err == hipSuccess) g_const_err = hipMemcpyToSymbol(HIP_SYMBOL(kMinstdPow2), p2, sizeof(p2));
+    });
+    if (g_const_err != hipSuccess) return fail(MCMC_E_HIP, std::string("constant upload: ") + hipGetErrorString(g_const_err));
+    return MCMC_OK;
+}
+
+// Host launch of one (sweep, commit) pair on the context stream.
+void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
+    c->sweep(a, c->grid, c->block, c->stream);
+    commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+}
+
+int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
+    if (c->batch_exec && c->batch == batch) return MCMC_OK;
+    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }
+    SweepArgs a = make_args(c, 1);
+    hipGraph_t graph;
+    MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (uint32_t i = 0; i < batch; i++) launch_pair(c, a);
+    MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
+    hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    c->batch = batch;
+    return MCMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mcmc_last_error(void) { return g_last_error.c_str(); }
+int mcmc_version(void) { return 1; }
+
+int mcmc_glibc_window(uint32_t seed, uint64_t draws, uint32_t window[31]) {
+    if (!window) return fail(MCMC_E_ARG, "window is NULL");
+    GlibcWindow w = glibc_srand(seed);
+    if (draws) w = glibc_jump(w, draws);
+    std::memcpy(window, w.r, sizeof(w.r));
+    return MCMC_OK;
+}
+
+int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out) {
+    if (!window || (count && !out)) return fail(MCMC_E_ARG, "NULL argument");
+    uint32_t ring[31];
+    std::memcpy(ring, window, sizeof(ring));
+    uint32_t head = 0;
+    for (uint32_t i = 0; i < count; i++) out[i] = glibc_next(ring, head);
+    for (int i = 0; i < 31; i++) window[i] = ring[(head + i) % 31];
+    return MCMC_OK;
+}
+
+int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end, mcmc_ctx** out) {
+    if (!g || !p || !out) return fail(MCMC_E_ARG, "NULL argument");
+    *out = nullptr;
+    const GraphDev& gd = g->g;
+    if (p->nCol == 0) return fail(MCMC_E_ARG, "nCol must be >= 1");
+    if (p->nCol > 256)
+        return fail(MCMC_E_ARG, "nCol > 256 is not supported by this build (uint8 colour replicas)");
+    if (v_begin > v_end || v_end > gd.n) return fail(MCMC_E_ARG, "bad vertex range");
+    int rc = ensure_constants();
+    if (rc) return rc;
+    MCMC_HIP_TRY(hipSetDevice(gd.device));
+    mcmc_ctx* c = new mcmc_ctx();
+    c->g = &gd;
+    c->p = *p;
+    c->n = gd.n;
+    c->v_begin = v_begin;
+    c->v_end = v_end;
+    c->z = p->tailcut ? std::max<uint32_t>(50u, gd.n / 2000u) : 0u;   // :89-97
+    c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
+    static const SweepLaunch table[4] = {launch_sweep<1>, launch_sweep<2>, launch_sweep<4>, launch_sweep<8>};
+    c->sweep = table[c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3];
+    c->glibc = glibc_srand(1);
+    const uint32_t nloc = v_end - v_begin;
+    c->ev_cap = std::max<uint32_t>(nloc, 1u);
+    c->traj_cap = p->maxRip + 2;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
+    chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    chk(hipEventCreate(&c->ev0));
+    chk(hipEventCreate(&c->ev1));
+    // colour replicas carry 256 B of slack so equal-size partition slabs can be all-gathered in place
+    chk(hipMalloc(&c->colors[0], (size_t)gd.n + 256));
+    chk(hipMalloc(&c->colors[1], (size_t)gd.n + 256));
+    if (p->tabooIteration > 0) chk(hipMalloc(&c->taboo, sizeof(uint32_t) * std::max<uint32_t>(nloc, 1)));
+    // event list sized n (+ pow2 padding room for the in-place sort fallback)
+    uint32_t pcap = 1;
+    while (pcap < c->ev_cap) pcap <<= 1;
+    chk(hipMalloc(&c->events, sizeof(uint32_t) * pcap));
+    chk(hipMalloc(&c->st, sizeof(DevState)));
+    chk(hipMalloc(&c->traj, sizeof(unsigned long long) * c->traj_cap));
+    if (e != hipSuccess) {
+        mcmc_destroy(c);
+        return fail(MCMC_E_NOMEM, std::string("allocation: ") + hipGetErrorString(e));
+    }
+    if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
+    SweepArgs a = make_args(c, 1);
+    const uint32_t tiles = (nloc + a.tile - 1) / a.tile;
+    c->block = dim3(256);
+    c->grid = dim3(std::max<uint32_t>(1u, std::min<uint32_t>((tiles + 3) / 4, 8192u)));
+    *out = c;
+    return MCMC_OK;
+}
+
+int mcmc_set_glibc_window(mcmc_ctx* c, const uint32_t window[31]) {
+    if (!c || !window) return fail(MCMC_E_ARG, "NULL argument");
+    std::memcpy(c->glibc.r, window, sizeof(c->glibc.r));
+    return MCMC_OK;
+}
+
+int mcmc_get_glibc_window(mcmc_ctx* c, uint32_t window[31]) {
+    if (!c || !window) return fail(MCMC_E_ARG, "NULL argument");
+    if (c->ran) {
+        DevState h;
+        int rc = download_state(c, &h);
+        if (rc) return rc;
+        for (int i = 0; i < 31; i++) window[i] = h.glibc_ring[(h.glibc_head + i) % 31];
+    } else {
+        std::memcpy(window, c->glibc.r, sizeof(c->glibc.r));
+    }
+    return MCMC_OK;
+}
+
+int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    const uint32_t n = c->n;
+    const uint32_t s0 = minstd_seed_state(c->p.seed);
+    if (C0) {
+        std::vector<uint8_t> h(n);
+        for (uint32_t v = 0; v < n; v++) {
+            if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
+            h[v] = (uint8_t)C0[v];
+        }
+        MCMC_HIP_TRY(hipMemcpyAsync(c->colors[0], h.data(), n, hipMemcpyHostToDevice, c->stream));
+        c->initDraws = n;
+    } else {
+        DevState zero{};
+        MCMC_HIP_TRY(hipMemcpyAsync(c->st, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
+        const UniformIntConst k = uniform_int_const(c->p.nCol);
+        const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
+        init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st);
+        MCMC_HIP_TRY(hipGetLastError());
+        DevState h;
+        int rc = download_state(c, &h);
+        if (rc) return rc;
+        uint64_t draws = n;
+        if (h.init_rejections > 0) {
+            // Exact sequential replay of uniform_int_distribution's rejection loop.
+            std::vector<uint8_t> hc(n);
+            uint32_t x = s0;
+            draws = 0;
+            for (uint32_t v = 0; v < n; v++) {
+                uint32_t r;
+                do { x = minstd_mulmod(x, kMinstdA); r = x - 1u; draws++; } while (r >= k.past);
+                hc[v] = (uint8_t)(r / k.scaling);
+            }
+            MCMC_HIP_TRY(hipMemcpyAsync(c->colors[0], hc.data(), n, hipMemcpyHostToDevice, c->stream));
+        }
+        c->initDraws = draws;
+    }
+    c->x0 = minstd_mulmod(s0, minstd_pow(kMinstdA, c->initDraws));
+    if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * (c->v_end - c->v_begin), c->stream));
+    int rc = upload_state(c, 0);
+    if (rc) return rc;
+    c->initialized = true;
+    c->ran = false;
+    return MCMC_OK;
+}
+
+int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_run");
+    if (c->v_begin != 0 || c->v_end != c->n)
+        return fail(MCMC_E_STATE, "mcmc_run drives whole-graph contexts; use mcmc_part_* for partitions");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    const uint32_t total = max_sweeps ? max_sweeps : c->p.maxRip + 2;   // +1 final count pass
+    const uint32_t batch = std::min<uint32_t>(16u, total);
+    int rc = build_batch_graph(c, batch);
+    if (rc) return rc;
+    c->ran = true;
+    MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    uint32_t launched = 0;
+    DevState h{};
+    while (launched < total) {
+        if (total - launched >= batch) {
+            MCMC_HIP_TRY(hipGraphLaunch(c->batch_exec, c->stream));
+            launched += batch;
+        } else {
+            SweepArgs a = make_args(c, 1);
+            for (; launched < total; launched++) launch_pair(c, a);
+            MCMC_HIP_TRY(hipGetLastError());
+        }
+        rc = download_state(c, &h);
+        if (rc) return rc;
+        if (h.done || h.err) break;
+    }
+    MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0;
+    MCMC_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
+    mcmc_run_stats s{};
+    if (h.done) {
+        s.iter = h.iter;
+        s.maxIterReached = (int32_t)h.maxIterReached;
+        s.finalViol = h.finalViol;
+        s.trajLen = (uint64_t)h.iter + 1;
+        s.sweepsRun = h.iter + 1;
+    } else {
+        // early stop (max_sweeps): h.t sweeps accepted, no final count
+        s.iter = h.t;
+        s.maxIterReached = 0;
+        s.finalViol = ~0ull;
+        s.trajLen = h.t;
+        s.sweepsRun = h.t;
+    }
+    s.glibcDraws = h.glibc_draws;
+    s.initDraws = c->initDraws;
+    s.loopMs = ms;
+    c->last = s;
+    // keep the host copy of the glibc window in step with the device stream
+    for (int i = 0; i < 31; i++) c->glibc.r[i] = h.glibc_ring[(h.glibc_head + i) % 31];
+    if (stats) *stats = s;
+    return MCMC_OK;
+}
+
+int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    DevState h{};
+    uint32_t which = 0;
+    if (c->ran) {
+        int rc = download_state(c, &h);
+        if (rc) return rc;
+        which = h.t & 1;
+    }
+    std::vector<uint8_t> tmp(c->n);
+    MCMC_HIP_TRY(hipMemcpyAsync(tmp.data(), c->colors[which], c->n, hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    for (uint32_t v = 0; v < c->n; v++) out[v] = tmp[v];
+    return MCMC_OK;
+}
+
+int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    const uint64_t L = std::min<uint64_t>(c->last.trajLen, c->traj_cap);
+    if (len) *len = L;
+    if (out && cap) {
+        std::vector<unsigned long long> tmp(L);
+        if (L) {
+            MCMC_HIP_TRY(hipMemcpyAsync(tmp.data(), c->traj, L * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+            MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        for (uint64_t i = 0; i < std::min(L, cap); i++) out[i] = tmp[i];
+    }
+    return MCMC_OK;
+}
+
+int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    // Throughput mode: the same kernels with the stop tests disabled (no cap, z = 0 only stops
+    // on a proper colouring). Sweep kernels are timed individually with events on the stream.
+    SweepArgs a = make_args(c, 1);
+    a.maxRip = 0xFFFFFFF0u;
+    a.traj_cap = 0;
+    c->ran = true;
+    std::vector<hipEvent_t> evs(2 * sweeps + 2);
+    for (auto& e : evs) MCMC_HIP_TRY(hipEventCreate(&e));
+    MCMC_HIP_TRY(hipEventRecord(evs[0], c->stream));
+    for (uint32_t i = 0; i < sweeps; i++) {
+        MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 1], c->stream));
+        c->sweep(a, c->grid, c->block, c->stream);
+        MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 2], c->stream));
+        commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    }
+    MCMC_HIP_TRY(hipGetLastError());
+    MCMC_HIP_TRY(hipEventRecord(evs[2 * sweeps + 1], c->stream));
+    MCMC_HIP_TRY(hipEventSynchronize(evs[2 * sweeps + 1]));
+    float tot = 0;
+    MCMC_HIP_TRY(hipEventElapsedTime(&tot, evs[0], evs[2 * sweeps + 1]));
+    double ks = 0;
+    for (uint32_t i = 0; i < sweeps; i++) {
+        float ms = 0;
+        MCMC_HIP_TRY(hipEventElapsedTime(&ms, evs[2 * i + 1], evs[2 * i + 2]));
+        ks += ms;
+    }
+    for (auto& e : evs) (void)hipEventDestroy(e);
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
+    if (total_ms) *total_ms = tot;
+    if (sweep_kernel_ms) *sweep_kernel_ms = sweeps ? ks / sweeps : 0.0;
+    return MCMC_OK;
+}
+
+void mcmc_destroy(mcmc_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->g->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->batch_exec) (void)hipGraphExecDestroy(c->batch_exec);
+    (void)hipFree(c->colors[0]);
+    (void)hipFree(c->colors[1]);
+    (void)hipFree(c->taboo);
+    (void)hipFree(c->events);
+    (void)hipFree(c->st);
+    (void)hipFree(c->traj);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ---- vertex-partitioned step ----------------------------------------------------------------
+int mcmc_part_sweep(mcmc_ctx* c, uint64_t* local_viol, uint32_t* n_events) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    c->ran = true;
+    SweepArgs a = make_args(c, 0);
+    c->sweep(a, c->grid, c->block, c->stream);
+    MCMC_HIP_TRY(hipGetLastError());
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    if (h.err || h.ev_count > c->ev_cap) return fail(MCMC_E_DEVICE, "event list overflow");
+    if (local_viol) *local_viol = h.viol;
+    if (n_events) *n_events = h.ev_count;
+    c->host_events.resize(h.ev_count);
+    if (h.ev_count) {
+        MCMC_HIP_TRY(hipMemcpyAsync(c->host_events.data(), c->events, sizeof(uint32_t) * h.ev_count,
+                                    hipMemcpyDeviceToHost, c->stream));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        std::sort(c->host_events.begin(), c->host_events.end());
+    }
+    return MCMC_OK;
+}
+
+int mcmc_part_events(mcmc_ctx* c, uint32_t* out, uint32_t cap) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (cap < c->host_events.size()) return fail(MCMC_E_ARG, "event buffer too small");
+    if (!c->host_events.empty()) std::memcpy(out, c->host_events.data(), sizeof(uint32_t) * c->host_events.size());
+    return MCMC_OK;
+}
+
+int mcmc_part_next_colors(mcmc_ctx* c, void** dev_ptr, uint32_t* elem_bytes) {
+    if (!c || !dev_ptr) return fail(MCMC_E_ARG, "NULL argument");
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    *dev_ptr = c->colors[(h.t + 1) & 1];
+    if (elem_bytes) *elem_bytes = 1;
+    return MCMC_OK;
+}
+
+int mcmc_part_commit(mcmc_ctx* c, uint64_t total_viol, const uint32_t* events, uint32_t n_events,
+                     int32_t* finished) {
+    if (!c || !finished) return fail(MCMC_E_ARG, "NULL argument");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    const uint32_t t = h.t;
+    if (t < c->traj_cap) {
+        unsigned long long v = total_viol;
+        MCMC_HIP_TRY(hipMemcpyAsync(c->traj + t, &v, sizeof(v), hipMemcpyHostToDevice, c->stream));
+    }
+    const bool stop_cap = t == c->p.maxRip + 1;
+    if (stop_cap || total_viol <= c->z) {
+        h.done = 1;
+        h.iter = t;
+        h.maxIterReached = stop_cap;
+        h.finalViol = total_viol;
+        MCMC_HIP_TRY(hipMemcpyAsync(c->st, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        c->last.iter = t;
+        c->last.maxIterReached = stop_cap;
+        c->last.finalViol = total_viol;
+        c->last.trajLen = (uint64_t)t + 1;
+        c->last.glibcDraws = h.glibc_draws;
+        c->last.initDraws = c->initDraws;
+        *finished = 1;
+        return MCMC_OK;
+    }
+    if (n_events > 0) {
+        uint32_t pcap = 1;
+        while (pcap < c->ev_cap) pcap <<= 1;
+        if (n_events > pcap) {
+            // global event list larger than the local buffer: reallocate
+            (void)hipFree(c->events);
+            uint32_t p2 = 1;
+            while (p2 < n_events) p2 <<= 1;
+            MCMC_HIP_TRY(hipMalloc(&c->events, sizeof(uint32_t) * p2));
+            c->ev_cap = p2;
+        }
+        MCMC_HIP_TRY(hipMemcpyAsync(c->events, events, sizeof(uint32_t) * n_events, hipMemcpyHostToDevice, c->stream));
+    }
+    SweepArgs a = make_args(c, 0);
+    part_commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a, t, n_events);
+    MCMC_HIP_TRY(hipGetLastError());
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    *finished = 0;
+    return MCMC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// oracle/mcmc_cpu_ref.h -- TEST INFRASTRUCTURE ONLY (parity oracle + CPU baseline).
+//
+// CPU restatement of the reference's `--mcmccpu` path, written from the source text of
+//   src/graph_coloring/coloringMCMC_CPU.{h,cpp}   (ColoringMCMC_CPU)
+//   src/graph/graphCPU.cpp:424-537                 (Graph::setupRnd2, the --simulate generator)
+//   src/graph/graphCPU.cpp:566-583                 (Graph::doStats -> maxDeg)
+//   src/main.cu:160-171                            (ColoringMCMCParams defaults, seed+i per repetition)
+// It calls the SAME third-party arithmetic the reference calls: libstdc++ <random>
+// (std::default_random_engine = minstd_rand0, uniform_int_distribution<uint32_t>,
+// uniform_real_distribution<float>) and glibc rand().
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this.
+// The product (mcmc_colorer_amd/) never links or calls it.
+//
+// Parity status: the reference ships no tests or golden vectors and executing
+// it here was refused, so this restatement is pinned by standard KATs
+// (C++ [rand.predef], glibc rand()) and by a second, independent numpy restatement
+// (oracle/oracle_np.py) on small graphs -- see DESIGN.md "Oracle".
+#pragma once
+#include <cstdint>
+#include <cstddef>
+
+extern "C" {
+
+typedef struct {
+    uint32_t nCol;            // ColoringMCMCParams::nCol          (coloring.h:65-74)
+    float    epsilon;         // 1e-8f                              (main.cu:163)
+    float    lambda;          // 1.0f (unused by the CPU path)      (main.cu:164)
+    float    ratioFreezed;    // 1e-2 (unused)                      (main.cu:165)
+    float    numColorRatio;   // 1/numColRatio                      (main.cu:53,161)
+    uint32_t maxRip;          // 250                                (main.cu:166)
+    uint32_t tabooIteration;  // --tabooIteration, default 0        (main.cu:167)
+    int32_t  tailcut;         // --tailcut                          (main.cu:168)
+    int32_t  tailcutRepair;   // 0: stop and report when Cviol > 0 at loop exit (the reference
+                              //    hangs there: coloringMCMC_CPU.cpp:296 increments i, not k);
+                              // 1: run the tail cut with that one bug fixed, bounded passes
+} oracle_params;
+
+typedef struct {
+    uint32_t iter;              // ColoringMCMC_CPU::iter at loop exit ("Iteration performed")
+    int32_t  maxIterReached;    // loop left through the maxRip cap
+    uint64_t finalViol;         // Cviol at loop exit (vertices with a same-colored neighbour)
+    uint64_t trajLen;           // entries written to traj (= iter + 1 when not truncated)
+    uint64_t glibcDraws;        // rand() calls made by overflow events during run()
+    uint64_t initDraws;         // engine draws consumed by the initial coloring (K0 = n + rejections)
+    double   loopSeconds;       // steady_clock wall time of the sweep loop
+    uint32_t sweepsRun;         // sweeps actually executed
+    uint32_t tailcutPasses;     // tail-cut passes executed (bounded; the reference loops forever)
+} oracle_result;
+
+// ---- glibc rand() stream (the process-global one the reference uses) ----
+void     oracle_srand(uint32_t seed);
+int32_t  oracle_rand(void);
+void     oracle_rand_skip(uint64_t k);
+// Points glibc's rand() at a given TYPE_3 window (31 words, oldest first) by initstate() on a
+// static buffer and writing the words where glibc's fptr/rptr expect them. Lets the oracle run
+// from a stream position reached by jump-ahead instead of ~n^2/2 sequential rand() calls.
+void     oracle_set_glibc_window(const uint32_t window[31]);
+
+// ---- libstdc++ <random> probes (for RNG known-answer tests) ----
+void     oracle_minstd_seq(uint32_t seed, uint64_t count, uint32_t* out);
+void     oracle_canonical_seq(uint32_t seed, uint64_t skip, uint64_t count, float* out);
+uint64_t oracle_uniform_int_seq(uint32_t seed, uint32_t nCol, uint64_t count, uint32_t* out);
+
+// ---- graph: Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537) ----
+// Consumes n(n+1)/2 glibc rand() draws from the current process stream.
+// Allocates *row_off (n+1) and *col_idx (m) with malloc; free with oracle_free.
+int      oracle_setup_rnd2(uint32_t n, float prob, uint64_t** row_off, uint32_t** col_idx, uint64_t* m);
+uint32_t oracle_max_deg(uint32_t n, const uint64_t* row_off);
+void     oracle_free(void* p);
+
+// ---- MCMC: ColoringMCMC_CPU(g, params, seed) + run() ----
+// out_init   : optional [n]  initial coloring (after the ctor)
+// out_colors : [n]           final coloring C
+// traj       : optional [traj_cap] Cviol at the top of every sweep, then the final Cviol
+// sweep_limit: 0 = reference semantics; k > 0 stops after k sweeps (bounded baseline samples)
+// nthreads   : 1 = faithful single-thread restatement; >1 = OpenMP variant (bit-identical)
+int      oracle_mcmc_run(uint32_t n, const uint64_t* row_off, const uint32_t* col_idx,
+                         const oracle_params* prm, uint32_t seed,
+                         uint32_t* out_init, uint32_t* out_colors,
+                         uint64_t* traj, uint64_t traj_cap,
+                         uint32_t sweep_limit, int nthreads, oracle_result* res);
+
+// Writes the reference's saveStats / saveColor text outputs (coloringMCMC_CPUutils.cpp:177-217).
+int      oracle_save_outputs(const char* log_path, const char* colors_path, uint32_t n, uint64_t nEdges,
+                             uint32_t maxDeg, uint32_t minDeg, float meanDeg, float prob, uint32_t seed,
+                             uint32_t repetition, float duration, const oracle_params* prm,
+                             const oracle_result* res, const uint32_t* colors);
+}

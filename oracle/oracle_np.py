@@ -1,0 +1,168 @@
+"""oracle/oracle_np.py -- TEST INFRASTRUCTURE ONLY.
+
+An independent float32 restatement of the reference's ``--mcmccpu`` path, written without
+libstdc++ or glibc: its own minstd_rand0, generate_canonical<float,24>, uniform_int_distribution
+and glibc TYPE_3 rand(). It exists to cross-check ``oracle/mcmc_cpu_ref.cpp`` (which calls the
+real libraries, exactly like the reference) on small graphs, so that the C++ oracle is pinned by
+two restatements that share no code. Pure-Python loops: keep n small (<= a few hundred).
+
+Reference lines restated (paths relative to /root/reference/src):
+  graph/graphCPU.cpp:424-537            setupRnd2 (Erdos-Renyi via glibc rand())
+  graph_coloring/coloringMCMC_CPU.cpp   ctor :53-61, run :115-270, violation_count :329-351,
+                                        count_free_colors :362-383, fill_p :393-481,
+                                        extract_new_color :493-528
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M31 = 2147483647
+A_MINSTD = 16807
+F32 = np.float32
+
+
+class Minstd:
+    """std::minstd_rand0 (C++ [rand.predef]): x <- 16807 x mod (2^31 - 1)."""
+
+    def __init__(self, seed: int):
+        s = seed % M31
+        self.x = 1 if s == 0 else s
+
+    def __call__(self) -> int:
+        self.x = (self.x * A_MINSTD) % M31
+        return self.x
+
+
+def canonical(x: int) -> np.float32:
+    """generate_canonical<float,24> over minstd: float(x-1) / 2^31, clamped below 1."""
+    r = F32(x - 1) / F32(2147483648.0)
+    if r >= F32(1.0):
+        r = np.nextafter(F32(1.0), F32(0.0))
+    return F32(r)
+
+
+def uniform_int(gen: Minstd, ncol: int) -> tuple[int, int]:
+    """uniform_int_distribution<uint32_t>(0, ncol-1), libstdc++ 'fallback (2 divisions)' path.
+    Returns (value, engine draws consumed)."""
+    urngrange = 2147483645
+    scaling = urngrange // ncol
+    past = ncol * scaling
+    draws = 0
+    while True:
+        r = gen() - 1
+        draws += 1
+        if r < past:
+            return r // scaling, draws
+
+
+class GlibcRand:
+    """glibc random_r.c TYPE_3 (degree 31, separation 3): r[i] = r[i-3] + r[i-31] mod 2^32,
+    output r >> 1, first 310 outputs discarded; srand(0) behaves as srand(1)."""
+
+    def __init__(self, seed: int = 1):
+        seed = seed & 0xFFFFFFFF
+        if seed == 0:
+            seed = 1
+        r = [0] * 34
+        r[0] = seed
+        for i in range(1, 31):
+            # Schrage's method on a signed 32-bit word with C (truncating) division, as glibc does
+            w = r[i - 1] if r[i - 1] < 2**31 else r[i - 1] - 2**32
+            hi = abs(w) // 127773 * (1 if w >= 0 else -1)
+            lo = w - hi * 127773
+            word = 16807 * lo - 2836 * hi
+            if word < 0:
+                word += 2147483647
+            r[i] = word & 0xFFFFFFFF
+        for i in range(31, 34):
+            r[i] = r[i - 31]
+        self.win = r[3:34]  # the last 31 values r[3..33]
+        for _ in range(310):
+            self._step()
+
+    def _step(self) -> int:
+        v = (self.win[-31] + self.win[-3]) & 0xFFFFFFFF
+        self.win.append(v)
+        del self.win[0]
+        return v
+
+    def __call__(self) -> int:
+        return self._step() >> 1
+
+
+def setup_rnd2(n: int, prob: float, rng: GlibcRand):
+    """Graph::setupRnd2 -> CSR (row_off uint64[n+1], col_idx uint32[m]), neighbours ascending."""
+    p = float(np.float32(prob))
+    adj = [[] for _ in range(n)]
+    for j in range(n):
+        for i in range(j, n):
+            bit = (rng() / 2147483647.0) < p
+            if bit and i != j:
+                adj[j].append(i)
+                adj[i].append(j)
+    for lst in adj:
+        lst.sort()
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(a) for a in adj])
+    idx = np.array([w for a in adj for w in a], dtype=np.uint32)
+    return off, idx
+
+
+def mcmc_run(off, idx, ncol: int, seed: int, glibc: GlibcRand, max_rip: int = 250,
+             taboo_iter: int = 0, z: int = 0, eps: np.float32 = F32(1e-8)):
+    """ColoringMCMC_CPU ctor + run(); returns (colors, trajectory, iter, max_iter_reached, init)."""
+    n = len(off) - 1
+    gen = Minstd(seed)
+    C = np.array([uniform_int(gen, ncol)[0] for _ in range(n)], dtype=np.int64)
+    init = C.copy()
+    taboo = np.zeros(n, dtype=np.int64)
+    hi = F32(F32(1.0) - F32(ncol - 1) * eps)
+    nbrs = [idx[off[v]:off[v + 1]].astype(np.int64) for v in range(n)]
+
+    def viol_vec(col):
+        return np.array([bool(np.any(col[nb] == col[v])) for v, nb in enumerate(nbrs)])
+
+    traj = []
+    it = 0
+    max_reached = False
+    cviol = int(viol_vec(C).sum())
+    while cviol > z:
+        u = [canonical(gen()) for _ in range(n)]
+        viols = viol_vec(C)
+        cviol = int(viols.sum())
+        traj.append(cviol)
+        Cs = C.copy()
+        for v in range(n):
+            occ = np.zeros(ncol, dtype=bool)
+            occ[C[nbrs[v]]] = True
+            zvcomp = ncol - int(occ.sum())
+            zv = ncol - zvcomp
+            if viols[v] and zvcomp > 0:
+                pf = F32(F32(F32(1.0) - F32(eps * F32(zv))) / F32(zvcomp))
+                p = [eps if occ[c] else pf for c in range(ncol)]
+            else:
+                p = [hi if c == C[v] else eps for c in range(ncol)]
+            if taboo[v] > 0:
+                taboo[v] -= 1
+                Cs[v] = C[v]
+                continue
+            cdf = F32(0.0)
+            new = ncol
+            for c in range(ncol):
+                cdf = F32(cdf + p[c])
+                if cdf > u[v]:
+                    new = c
+                    break
+            if new >= ncol:
+                new = glibc() % (ncol - 1)
+            Cs[v] = new
+            taboo[v] = (1 if new == C[v] else 0) * taboo_iter
+        cstar_viol = int(viol_vec(Cs).sum())
+        C = Cs
+        cviol = cstar_viol
+        it += 1
+        if it > max_rip:
+            max_reached = True
+            break
+    traj.append(cviol)
+    return C.astype(np.uint32), traj, it, max_reached, init.astype(np.uint32)

@@ -1,0 +1,194 @@
+"""GPU parity: the HIP sweep (through the C ABI) against the oracle and the golden fixtures.
+
+Bar: bit-exact -- final colouring, per-sweep conflict trajectory (the reference's
+"C violations" log, coloringMCMC_CPU.cpp:152), iteration count, max-iteration flag and the
+number of glibc rand() draws taken by CDF-overflow events must all be identical.
+"""
+import hashlib
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def M(hip_lib):
+    import mcmc_colorer_amd.colorer as M
+
+    return M
+
+
+def gpu_run(M, off, idx, ncol, seed, draws_before, *, eps=1e-8, maxRip=250, taboo=0, tailcut=False,
+            iteration=0, glibc=None):
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, epsilon=eps, maxRip=maxRip, tabooIteration=taboo, tailcut=tailcut)
+    rs = M.GPURand(g.nNodes, seed, glibc if glibc is not None else M.GlibcRand(1, draws_before))
+    col = M.ColoringMCMC(g, rs, params)
+    st = col.run(iteration)
+    return col, st, rs
+
+
+def oracle_case(n, p, ncol, seed, **kw):
+    O.srand(1)
+    off, idx = O.setup_rnd2(n, p)
+    nc = ncol or O.max_deg(off)
+    r = O.mcmc_run(off, idx, nc, seed, **kw)
+    return off, idx, nc, r
+
+
+def assert_same(col, st, r):
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws, st.initDraws) == (
+        r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws, r.res.initDraws)
+
+
+def test_c1_graph_generated_on_gpu_is_exact(M):
+    """configs[0]: --simulate 0.1 -n 1000 -- the GPU setupRnd2 replay equals the reference's CSR."""
+    O.srand(1)
+    off, idx = O.setup_rnd2(1000, 0.1)
+    rng = M.GlibcRand(1)
+    g = M.Graph.simulate(1000, 0.1, rng)
+    s = g.getStruct()
+    assert np.array_equal(s.cumulDegs, off) and np.array_equal(s.neighs, idx)
+    assert g.getMaxNodeDeg() == O.max_deg(off)
+    # the stream advanced by n(n+1)/2 draws
+    assert np.array_equal(rng.window, M.GlibcRand(1, 1000 * 1001 // 2).window)
+
+
+@pytest.mark.parametrize("n,p", [(1, 0.5), (2, 1.0), (37, 0.5), (400, 0.03), (2500, 0.01), (3000, 0.9)])
+def test_gpu_generator_exact(M, n, p):
+    O.srand(1)
+    off, idx = O.setup_rnd2(n, p)
+    g = M.Graph.simulate(n, p, M.GlibcRand(1))
+    s = g.getStruct()
+    assert np.array_equal(s.cumulDegs, off) and np.array_equal(s.neighs, idx)
+
+
+SMALL = json.loads((GOLDEN / "small.json").read_text())
+
+
+@pytest.mark.parametrize("name", sorted(SMALL))
+def test_gpu_matches_golden(M, name):
+    d = SMALL[name]
+    rng = M.GlibcRand(1)
+    g = M.Graph.simulate(d["n"], d["prob"], rng)
+    s = g.getStruct()
+    assert sha(s.cumulDegs.astype(np.uint64)) == d["row_off_sha256"]
+    assert sha(s.neighs.astype(np.uint32)) == d["col_idx_sha256"]
+    params = M.ColoringMCMCParams(nCol=d["nCol"], epsilon=d["epsilon"], maxRip=d["maxRip"],
+                                  tabooIteration=d["tabooIteration"], tailcut=d["tailcut"])
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, d["seed"], rng), params)
+    st = col.run(0)
+    assert col.coloring().tolist() == d["colors"]
+    assert col.trajectory().tolist() == d["traj"]
+    assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws) == (
+        d["iter"], d["maxIterReached"], d["finalViol"], d["glibcDraws"])
+
+
+GRID = [
+    # n, p, nCol, seed, eps, taboo, maxRip, tailcut
+    (500, 0.05, 0, 1, 1e-8, 0, 250, False),
+    (700, 0.1, 16, 2, 1e-8, 0, 30, False),
+    (900, 0.08, 31, 3, 1e-8, 0, 40, False),
+    (900, 0.08, 32, 3, 1e-8, 4, 40, False),
+    (900, 0.08, 33, 3, 1e-8, 0, 40, False),
+    (1200, 0.05, 64, 4, 1e-8, 1, 40, False),
+    (1200, 0.05, 65, 4, 1e-8, 0, 40, False),
+    (1500, 0.1, 128, 5, 1e-8, 0, 20, False),
+    (1500, 0.15, 129, 6, 1e-8, 2, 20, False),
+    (2000, 0.12, 256, 7, 1e-8, 0, 10, False),
+    (800, 0.3, 3, 8, 3.3e6, 0, 25, False),
+    (800, 0.3, 7, 9, 3.3e6, 3, 25, False),
+    (3000, 0.01, 9, 10, 1e-8, 0, 250, True),
+    (64, 0.5, 2, 11, 1e-8, 0, 50, False),
+    (1, 0.5, 1, 12, 1e-8, 0, 5, False),
+    (100, 0.0, 4, 13, 1e-8, 0, 5, False),
+]
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip,tailcut", GRID)
+def test_gpu_matches_oracle_grid(M, n, p, ncol, seed, eps, taboo, maxrip, tailcut):
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip,
+                                  tailcut=tailcut)
+    col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo,
+                         tailcut=tailcut)
+    assert_same(col, st, r)
+
+
+def circulant(n, K):
+    """Ring lattice: v ~ v +- 1..K (sorted rows), a CSR the tests can build without setupRnd2."""
+    nb = sorted([d for k in range(1, K + 1) for d in (k, -k)])
+    idx = ((np.arange(n)[:, None] + np.array(nb)[None, :]) % n).astype(np.uint32)
+    idx.sort(axis=1)
+    off = np.arange(0, n * len(nb) + 1, len(nb), dtype=np.uint64)
+    return off, idx.ravel()
+
+
+def test_many_events_global_sort_path(M):
+    """~20000 CDF-overflow events in ONE sweep (epsilon = 3e7 makes the fp32 CDF of a vertex whose
+    colour is 0 cancel to 0): exercises the commit's in-global-memory sort and a long ordered
+    glibc replay."""
+    off, idx = circulant(60000, 4)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 3, 21, epsilon=3e7, maxRip=0, nthreads=8)
+    assert r.res.glibcDraws > 16384          # all in the single sweep
+    col, st, _ = gpu_run(M, off, idx, 3, 21, 0, eps=3e7, maxRip=0)
+    assert_same(col, st, r)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 3, 22, epsilon=3e7, maxRip=4, nthreads=8)
+    col, st, _ = gpu_run(M, off, idx, 3, 22, 0, eps=3e7, maxRip=4)
+    assert_same(col, st, r)
+
+
+def test_repetitions_share_glibc_stream(M):
+    """--repet: seed + i per repetition (main.cu:171), one glibc stream across them."""
+    n, p, ncol = 600, 0.3, 7
+    O.srand(1)
+    off, idx = O.setup_rnd2(n, p)
+    refs = [O.mcmc_run(off, idx, ncol, 100 + i, epsilon=3.3e6, maxRip=8) for i in range(3)]
+    assert sum(r.res.glibcDraws for r in refs) > 0
+    g = M.Graph.from_csr(off, idx)
+    rs = M.GPURand(n, 100, M.GlibcRand(1, n * (n + 1) // 2))
+    col = M.ColoringMCMC(g, rs, M.ColoringMCMCParams(nCol=ncol, epsilon=3.3e6, maxRip=8))
+    for i, r in enumerate(refs):
+        st = col.run(i)
+        assert_same(col, st, r)
+
+
+def test_early_stop_max_sweeps(M):
+    off, idx, nc, r = oracle_case(2000, 0.05, 12, 3, maxRip=250, sweep_limit=5)
+    g = M.Graph.from_csr(off, idx)
+    c2 = M.ColoringMCMC(g, M.GPURand(2000, 3, M.GlibcRand(1, 2000 * 2001 // 2)), M.ColoringMCMCParams(nCol=nc))
+    st2 = c2.run(0, max_sweeps=5)
+    assert st2.iter == 5 and c2.coloring().tolist() == r.colors.tolist()
+    assert c2.trajectory().tolist() == r.traj.tolist()[:5]
+
+
+def test_c2_full_run_matches_golden(M):
+    """configs[1]: --mcmcgpu --simulate 0.01 -n 100000, 16 colours: exact graph (5e9 glibc draws on
+    the GPU), 251 sweeps, trajectory and final colouring identical to the oracle's."""
+    d = json.loads((GOLDEN / "c2.json").read_text())
+    rng = M.GlibcRand(1)
+    g = M.Graph.simulate(d["n"], d["prob"], rng)
+    s = g.getStruct()
+    assert g.nEdges == d["m"] and g.getMaxNodeDeg() == d["maxDeg"]
+    assert sha(s.cumulDegs.astype(np.uint64)) == d["row_off_sha256"]
+    assert sha(s.neighs.astype(np.uint32)) == d["col_idx_sha256"]
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, d["seed"], rng), M.ColoringMCMCParams(nCol=d["nCol"]))
+    st = col.run(0)
+    assert col.trajectory().tolist() == d["traj"]
+    assert sha(col.coloring()) == d["colors_sha256"]
+    assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws) == (
+        d["iter"], d["maxIterReached"], d["finalViol"], d["glibcDraws"])

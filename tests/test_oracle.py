@@ -1,0 +1,112 @@
+"""Pins the oracle (oracle/mcmc_cpu_ref.cpp) before anything is checked against it.
+
+1. Known-answer tests for the third-party arithmetic the reference calls:
+   C++ [rand.predef] minstd_rand0, glibc rand(), generate_canonical<float,24>, uniform_int.
+2. An independent numpy restatement (oracle/oracle_np.py, no libstdc++/glibc) must agree with
+   the C++ oracle bit-for-bit on small graphs, including taboo, tail-cut threshold and
+   CDF-overflow (glibc replay) cases.
+3. The OpenMP variant (CPU baseline on many cores) equals the faithful single-thread run.
+"""
+import numpy as np
+import pytest
+
+import oracle_np as NP
+import oracle_ref as O
+
+
+def test_minstd_kat():
+    out = np.zeros(10000, dtype=np.uint32)
+    O.lib().oracle_minstd_seq(1, 10000, out.ctypes.data)
+    assert out[:3].tolist() == [16807, 282475249, 1622650073]
+    assert int(out[9999]) == 1043618065          # C++ [rand.predef]: 10000th output
+
+
+def test_glibc_kat():
+    O.srand(1)
+    assert O.rand(5) == [1804289383, 846930886, 1681692777, 1714636915, 1957747793]
+    g = NP.GlibcRand(1)
+    assert [g() for _ in range(5)] == [1804289383, 846930886, 1681692777, 1714636915, 1957747793]
+
+
+@pytest.mark.parametrize("seed", [0, 2, 12345, 2**31 + 5, 2**32 - 1])
+def test_glibc_seeds_match_numpy(seed):
+    O.srand(seed)
+    g = NP.GlibcRand(seed)
+    assert O.rand(400) == [g() for _ in range(400)]
+
+
+def test_canonical_clamp_and_values():
+    # generate_canonical<float,24>: x - 1 >= 2147483584 rounds to 2^31 and clamps to 1 - 2^-24.
+    for x in (1, 2, 1000, 2147483520, 2147483521, 2147483584, 2147483585, 2147483646):
+        u = NP.canonical(x)
+        assert np.float32(u) < np.float32(1.0)
+    assert NP.canonical(2147483646) == np.nextafter(np.float32(1), np.float32(0))
+    assert NP.canonical(1) == np.float32(0.0)
+    out = np.zeros(2000, dtype=np.float32)
+    O.lib().oracle_canonical_seq(7, 0, 2000, out.ctypes.data)
+    m = NP.Minstd(7)
+    assert np.array_equal(out, np.array([NP.canonical(m()) for _ in range(2000)], dtype=np.float32))
+
+
+@pytest.mark.parametrize("ncol", [1, 2, 3, 16, 32, 137, 1000])
+def test_uniform_int_matches_numpy(ncol):
+    out = np.zeros(3000, dtype=np.uint32)
+    draws = O.lib().oracle_uniform_int_seq(3, ncol, 3000, out.ctypes.data)
+    m = NP.Minstd(3)
+    ref, d = [], 0
+    for _ in range(3000):
+        v, k = NP.uniform_int(m, ncol)
+        ref.append(v)
+        d += k
+    assert out.tolist() == ref and draws == d
+
+
+CASES = [
+    # n, p, nCol, seed, eps, taboo, maxRip
+    (40, 0.3, 6, 1, 1e-8, 0, 250),
+    (60, 0.2, 5, 7, 1e-8, 0, 20),
+    (50, 0.5, 8, 3, 1e-8, 2, 30),
+    (30, 0.9, 4, 11, 3.3e6, 1, 15),
+    (80, 0.3, 7, 5, 3.3e6, 0, 12),
+    (70, 0.1, 2, 9, 1e-8, 0, 10),
+    (45, 0.4, 40, 2, 1e-8, 0, 30),
+]
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", CASES)
+def test_cpp_oracle_equals_numpy_restatement(n, p, ncol, seed, eps, taboo, maxrip):
+    O.srand(1)
+    off, idx = O.setup_rnd2(n, p)
+    r = O.mcmc_run(off, idx, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
+    g = NP.GlibcRand(1)
+    off2, idx2 = NP.setup_rnd2(n, p, g)
+    assert np.array_equal(off, off2) and np.array_equal(idx, idx2)
+    C, traj, it, maxr, init = NP.mcmc_run(off2, idx2, ncol, seed, g, max_rip=maxrip, taboo_iter=taboo,
+                                         eps=np.float32(eps))
+    assert np.array_equal(r.init, init)
+    assert np.array_equal(r.colors, C)
+    assert r.traj.tolist() == traj
+    assert r.res.iter == it and bool(r.res.maxIterReached) == maxr
+    # the glibc streams must have advanced identically (events drew the same number of rand())
+    assert O.rand(3) == [g() for _ in range(3)]
+
+
+def test_events_case_really_draws_glibc():
+    O.srand(1)
+    off, idx = O.setup_rnd2(80, 0.3)
+    r = O.mcmc_run(off, idx, 7, 5, epsilon=3.3e6, maxRip=12)
+    assert r.res.glibcDraws > 0
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_openmp_variant_bit_identical(threads):
+    O.srand(1)
+    off, idx = O.setup_rnd2(600, 0.05)
+    for eps, taboo in ((1e-8, 0), (3.3e6, 2)):
+        O.srand(77)
+        a = O.mcmc_run(off, idx, 9, 4, epsilon=eps, tabooIteration=taboo, maxRip=40)
+        O.srand(77)
+        b = O.mcmc_run(off, idx, 9, 4, epsilon=eps, tabooIteration=taboo, maxRip=40, nthreads=threads)
+        assert np.array_equal(a.colors, b.colors)
+        assert a.traj.tolist() == b.traj.tolist()
+        assert a.res.glibcDraws == b.res.glibcDraws
