@@ -160,8 +160,9 @@ int mcmc_graph_upload(const uint64_t* row_off, const uint32_t* col_idx, uint32_t
     g->g.n = n;
     g->g.m = m;
     hipError_t e = hipMalloc(&g->g.row_off, sizeof(uint64_t) * ((size_t)n + 1));
-    if (e == hipSuccess) e = hipMalloc(&g->g.col_idx, sizeof(uint32_t) * std::max<uint64_t>(m, 1));
+    if (e == hipSuccess) e = hipMalloc(&g->g.col_idx, sizeof(uint32_t) * (m + 4));
     if (e == hipSuccess) e = hipMemcpy(g->g.row_off, row_off, sizeof(uint64_t) * ((size_t)n + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(g->g.col_idx, 0, sizeof(uint32_t) * (m + 4));   // zero pad: valid ids
     if (e == hipSuccess && m) e = hipMemcpy(g->g.col_idx, col_idx, sizeof(uint32_t) * m, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         mcmc_graph_destroy(g);
@@ -250,11 +251,13 @@ int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device,
         mcmc_graph_destroy(g);
         return fail(MCMC_E_ARG, "mcmc_graph_simulate: more than 2^31 arcs (use a smaller n)");
     }
-    GTRY(hipMalloc(&g->g.col_idx, sizeof(uint32_t) * std::max<uint64_t>(m, 1)));
+    GTRY(hipMalloc(&g->g.col_idx, sizeof(uint32_t) * (m + 4)));
+    GTRY(hipMemset(g->g.col_idx, 0, sizeof(uint32_t) * (m + 4)));
     er_exact_kernel<1><<<blocks, threads>>>(n, total, thr, d_w0, d_J, nbits, nullptr, g->g.row_off, d_cur, g->g.col_idx);
     GTRY(hipGetLastError());
     if (m) {
-        GTRY(hipMalloc(&d_sorted, sizeof(uint32_t) * m));
+        GTRY(hipMalloc(&d_sorted, sizeof(uint32_t) * (m + 4)));
+        GTRY(hipMemset(d_sorted, 0, sizeof(uint32_t) * (m + 4)));   // zero pad survives the swap
         (void)hipFree(d_tmp);
         d_tmp = nullptr;
         tmp_bytes = 0;

@@ -23,6 +23,7 @@
 // Compiled with -ffp-contract=off: fill_p's products and quotients must round exactly as the
 // reference's SSE code (no FMA), and fp32 division stays IEEE-correct (hipcc default).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -71,6 +72,8 @@ struct SweepArgs {
     uint32_t n, v_begin, v_end;
     uint32_t nCol, tabooIteration, maxRip, z;
     uint32_t tile;              // vertices per wave-tile (<= 64)
+    const uint32_t* wave_start; // arc-balanced static partition: wave w sweeps local rows
+                                // [wave_start[w], wave_start[w+1])
     uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
     float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
     int check_done;             // device-resident loop: exit immediately once done
@@ -126,134 +129,249 @@ __device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
 }
 
 // ----------------------------------------------------------------------------------------------
-// The fused sweep. One wave owns a tile of `tile` consecutive vertices: for each of them the 64
-// lanes stride its CSR row (coalesced col_idx loads, colour gathers) and OR-reduce the occupancy
-// mask; lane j keeps vertex j's mask. Then every lane evaluates its own vertex: viol, p, u, the
-// CDF walk and the writes.
+// Per-vertex evaluation of one tile, after the occupancy masks are built: lane j < cnt holds the
+// mask of vertex v = v_begin + l0 + j in `acc`. viol, fill_p, u_v, the CDF walk, the writes, the
+// Cviol ballot and the overflow-event append.
 template <int NW>
-__global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
+__device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* __restrict__ st,
+                                              const uint8_t* __restrict__ Cown, uint8_t* __restrict__ Cs,
+                                              uint32_t x_t, uint32_t l0, uint32_t cnt, const uint32_t (&acc)[NW],
+                                              int lane) {
+    const bool valid = (uint32_t)lane < cnt;
+    const uint32_t l = l0 + lane;
+    const uint32_t v = a.v_begin + l;
+    const uint32_t cv = valid ? (uint32_t)Cown[v] : 0u;
+    uint32_t pop = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) pop += __popc(acc[i]);
+    const bool viol = valid && get_color_bit<NW>(acc, cv);
+    const uint32_t Zvcomp = a.nCol - pop;
+
+    uint32_t tab = 0;
+    if (a.taboo != nullptr && valid) tab = a.taboo[l];
+
+    // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
+    const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
+    const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
+    const float u = minstd_canonical(x);
+
+    // fill_p cases: (ii) viol with free colours -> occupied eps, free pf;
+    //               (i)/(iii) otherwise      -> own colour hi, others eps.
+    uint32_t sel[NW];
+    float pA, pB;
+    if (viol && Zvcomp > 0) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) sel[i] = acc[i];
+        pA = a.eps;
+        pB = (1.0f - a.eps * (float)pop) / (float)Zvcomp;
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; i++) sel[i] = 0;
+        set_color_bit<NW>(sel, cv);
+        pA = a.hi;
+        pB = a.eps;
+    }
+    // extract_new_color: cdf += p[c]; break on cdf > u (strict).
+    uint32_t newc = a.nCol;
+    if (valid && tab == 0) {
+        float cdf = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t bits = sel[i];
+            const uint32_t cmax = min(32u, a.nCol > (uint32_t)(32 * i) ? a.nCol - 32u * i : 0u);
+            for (uint32_t cc = 0; cc < cmax && newc == a.nCol; cc++) {
+                cdf += ((bits >> cc) & 1u) ? pA : pB;
+                if (cdf > u) newc = 32u * i + cc;
+            }
+        }
+    }
+    const bool event = valid && tab == 0 && newc == a.nCol;
+    if (valid) {
+        if (tab > 0) {
+            Cs[v] = (uint8_t)cv;
+            a.taboo[l] = tab - 1;
+        } else if (!event) {
+            Cs[v] = (uint8_t)newc;
+            if (a.taboo != nullptr) a.taboo[l] = (newc == cv) ? a.tabooIteration : 0u;
+        } else {
+            Cs[v] = (uint8_t)cv;   // placeholder, overwritten by the commit's glibc replay
+        }
+    }
+
+    const uint32_t nviol = (uint32_t)__popcll(__ballot(viol));
+    const uint64_t eb = __ballot(event);
+    if (eb) {
+        uint32_t basei = 0;
+        if (lane == 0) basei = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
+        basei = __shfl(basei, 0, 64);
+        if (event) {
+            const uint32_t idx = basei + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
+            if (idx < a.ev_cap) a.events[idx] = v;
+            else atomicOr(&st->err, 1u);
+        }
+    }
+    return nviol;
+}
+
+// ----------------------------------------------------------------------------------------------
+// The fused sweep. Every wave owns a contiguous, arc-balanced range of rows (wave_start, computed
+// once per context) and walks it in tiles of `tile` vertices. For each vertex of the tile the 64 lanes stream its CSR
+// row in passes of 64 x 16 B x U (aligned dwordx4 loads of neighbour ids, the next pass issued
+// before the current one is consumed), gather the neighbours' colours and OR them into the
+// occupancy mask; a wave OR-reduction leaves vertex j's mask in lane j. Then evaluate_tile.
+// LDSC: the whole colour replica (n bytes) is first staged in LDS so the byte gathers never pull
+// cache lines through L1/L2 (1 persistent 1024-thread workgroup per CU).
+#ifndef MCMC_PASS_U
+#define MCMC_PASS_U 4
+#endif
+constexpr int kPassU = MCMC_PASS_U;          // dwordx4 loads per lane per pass
+constexpr uint32_t kPassArcs = 256u * kPassU;
+
+template <int NW, bool LDSC>
+__global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
+    extern __shared__ uint4 sc_raw[];
+    __shared__ uint32_t wg_viol;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
+    if (threadIdx.x == 0) wg_viol = 0;
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
-    const uint32_t* __restrict__ col_idx = a.col_idx;
+    const uint8_t* __restrict__ Cg = C;
+    if (LDSC) {
+        // stage the colour replica: 8 independent 16-B loads in flight per thread
+        const uint32_t nq = (a.n + 15u) >> 4;
+        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(C);
+        for (uint32_t i0 = threadIdx.x; i0 < nq; i0 += 8u * blockDim.x) {
+            uint4 r[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t i = i0 + k * blockDim.x;
+                r[k] = src[i < nq ? i : 0u];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t i = i0 + k * blockDim.x;
+                if (i < nq) sc_raw[i] = r[k];
+            }
+        }
+        __syncthreads();
+        Cg = reinterpret_cast<const uint8_t*>(sc_raw);
+    }
 
+    if (!LDSC) __syncthreads();   // wg_viol initialised (the LDS path synchronises above)
     const int lane = threadIdx.x & 63;
-    const uint32_t wpb = blockDim.x >> 6;
-    const uint32_t nloc = a.v_end - a.v_begin;
-    const uint32_t ntiles = (nloc + a.tile - 1) / a.tile;
+    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t wbeg = a.wave_start[gw], wend = a.wave_start[gw + 1];
+    uint32_t wave_viol = 0;   // Cviol of this wave's rows; one L2 atomic per workgroup at the end
 
-    for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntiles; tile += gridDim.x * wpb) {
-        const uint32_t l0 = tile * a.tile;
-        const uint32_t cnt = min(a.tile, nloc - l0);
+    for (uint32_t l0 = wbeg; l0 < wend; l0 += a.tile) {
+        const uint32_t cnt = min(a.tile, wend - l0);
         uint64_t myoff = 0;
         if ((uint32_t)lane <= cnt) myoff = a.row_off[l0 + lane];
+        // tile-relative 32-bit arc positions from an aligned, wave-uniform base pointer
+        const uint64_t tb = readlane64(myoff, 0) & ~3ull;
+        const uint32_t* __restrict__ tcol = a.col_idx + tb;
+        const uint32_t myrel = (uint32_t)(myoff - tb);
 
         uint32_t acc[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) acc[i] = 0;
 
-        for (uint32_t j = 0; j < cnt; j++) {
-            const uint64_t beg = readlane64(myoff, j);
-            const uint64_t end = readlane64(myoff, j + 1);
-            uint32_t m[NW];
-#pragma unroll
-            for (int i = 0; i < NW; i++) m[i] = 0;
-            uint64_t k = beg + lane;
-            for (; k + 192 < end; k += 256) {
-                const uint32_t w0 = col_idx[k], w1 = col_idx[k + 64], w2 = col_idx[k + 128], w3 = col_idx[k + 192];
-                const uint32_t c0 = C[w0], c1 = C[w1], c2 = C[w2], c3 = C[w3];
-                set_color_bit<NW>(m, c0);
-                set_color_bit<NW>(m, c1);
-                set_color_bit<NW>(m, c2);
-                set_color_bit<NW>(m, c3);
-            }
-            for (; k < end; k += 64) set_color_bit<NW>(m, C[col_idx[k]]);
-            wave_or<NW>(m);
-            if ((uint32_t)lane == j) {
-#pragma unroll
-                for (int i = 0; i < NW; i++) acc[i] = m[i];
-            }
+        // first non-empty row
+        uint32_t j = 0, pbeg = 0, pend = 0;
+        while (j < cnt) {
+            pbeg = __builtin_amdgcn_readlane(myrel, j);
+            pend = __builtin_amdgcn_readlane(myrel, j + 1);
+            if (pend > pbeg) break;
+            j++;
         }
-
-        // ---- per-vertex evaluation: lane -> vertex v = v_begin + l0 + lane ----
-        const bool valid = (uint32_t)lane < cnt;
-        const uint32_t l = l0 + lane;
-        const uint32_t v = a.v_begin + l;
-        const uint32_t cv = valid ? (uint32_t)C[v] : 0u;
-        uint32_t pop = 0;
+        uint32_t pbase = pbeg & ~3u;
+        // loads are unconditional: quads past the row end re-read the row's last quad (cache hit)
+        uint4 cur[kPassU];
 #pragma unroll
-        for (int i = 0; i < NW; i++) pop += __popc(acc[i]);
-        const bool viol = valid && get_color_bit<NW>(acc, cv);
-        const uint32_t Zvcomp = a.nCol - pop;
-
-        uint32_t tab = 0;
-        if (a.taboo != nullptr && valid) tab = a.taboo[l];
-
-        // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
-        const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
-        const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
-        const float u = minstd_canonical(x);
-
-        // fill_p cases: (ii) viol with free colours -> occupied eps, free pf;
-        //               (i)/(iii) otherwise      -> own colour hi, others eps.
-        uint32_t sel[NW];
-        float pA, pB;
-        if (viol && Zvcomp > 0) {
-#pragma unroll
-            for (int i = 0; i < NW; i++) sel[i] = acc[i];
-            pA = a.eps;
-            pB = (1.0f - a.eps * (float)pop) / (float)Zvcomp;
-        } else {
-#pragma unroll
-            for (int i = 0; i < NW; i++) sel[i] = 0;
-            set_color_bit<NW>(sel, cv);
-            pA = a.hi;
-            pB = a.eps;
+        for (int u = 0; u < kPassU; u++) {
+            const uint32_t q = min(pbase + 256u * u + 4u * lane, (pend - 1u) & ~3u);
+            cur[u] = *reinterpret_cast<const uint4*>(tcol + (j < cnt ? q : 0u));
         }
-        // extract_new_color: cdf += p[c]; break on cdf > u (strict).
-        uint32_t newc = a.nCol;
-        if (valid && tab == 0) {
-            float cdf = 0.0f;
+        uint32_t m[NW];
 #pragma unroll
-            for (int i = 0; i < NW; i++) {
-                const uint32_t bits = sel[i];
-                const uint32_t cmax = min(32u, a.nCol > (uint32_t)(32 * i) ? a.nCol - 32u * i : 0u);
-                for (uint32_t cc = 0; cc < cmax && newc == a.nCol; cc++) {
-                    cdf += ((bits >> cc) & 1u) ? pA : pB;
-                    if (cdf > u) newc = 32u * i + cc;
+        for (int i = 0; i < NW; i++) m[i] = 0;
+
+        while (j < cnt) {
+            // next pass (wave-uniform): same row, or the next non-empty row of the tile
+            uint32_t nj = j, nbeg = pbeg, nend = pend, nbase = pbase + kPassArcs;
+            const bool row_done = nbase >= pend;
+            if (row_done) {
+                nj = j + 1;
+                while (nj < cnt) {
+                    nbeg = __builtin_amdgcn_readlane(myrel, nj);
+                    nend = __builtin_amdgcn_readlane(myrel, nj + 1);
+                    if (nend > nbeg) break;
+                    nj++;
+                }
+                nbase = nbeg & ~3u;
+                if (nj >= cnt) { nbeg = pbeg; nend = pend; nbase = pbase; }   // nothing left: re-read (hits)
+            }
+            uint4 nxt[kPassU];
+#pragma unroll
+            for (int u = 0; u < kPassU; u++) {
+                const uint32_t q = min(nbase + 256u * u + 4u * lane, (nend - 1u) & ~3u);
+                nxt[u] = *reinterpret_cast<const uint4*>(tcol + q);
+            }
+            // consume the current pass: every word of a loaded quad is a valid vertex id (rows are
+            // contiguous and the array tail is zero-padded), so all 4*U gathers issue unmasked and
+            // back to back; the per-quad row mask only gates the bit merge.
+            uint32_t qm[kPassU];
+#pragma unroll
+            for (int u = 0; u < kPassU; u++) {
+                const int32_t q = (int32_t)(pbase + 256u * u + 4u * lane);
+                const int32_t lo = min(max((int32_t)pbeg - q, 0), 4);
+                const int32_t hi = min(max((int32_t)pend - q, 0), 4);
+                qm[u] = (0xFu << lo) & ((1u << hi) - 1u);
+            }
+            uint32_t cg[4 * kPassU];
+#pragma unroll
+            for (int u = 0; u < kPassU; u++) {
+                cg[4 * u + 0] = Cg[cur[u].x];
+                cg[4 * u + 1] = Cg[cur[u].y];
+                cg[4 * u + 2] = Cg[cur[u].z];
+                cg[4 * u + 3] = Cg[cur[u].w];
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * kPassU; i++) {
+                const uint32_t ok = (qm[i >> 2] >> (i & 3)) & 1u;
+                if (NW == 1) {
+                    m[0] |= ok << cg[i];
+                } else {
+                    const uint32_t c = cg[i];
+                    const uint32_t bit = ok << (c & 31);
+#pragma unroll
+                    for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
                 }
             }
-        }
-        const bool event = valid && tab == 0 && newc == a.nCol;
-        if (valid) {
-            if (tab > 0) {
-                Cs[v] = (uint8_t)cv;
-                a.taboo[l] = tab - 1;
-            } else if (!event) {
-                Cs[v] = (uint8_t)newc;
-                if (a.taboo != nullptr) a.taboo[l] = (newc == cv) ? a.tabooIteration : 0u;
-            } else {
-                Cs[v] = (uint8_t)cv;   // placeholder, overwritten by the commit's glibc replay
+            if (row_done) {
+                wave_or<NW>(m);
+                if ((uint32_t)lane == j) {
+#pragma unroll
+                    for (int i = 0; i < NW; i++) acc[i] = m[i];
+                }
+#pragma unroll
+                for (int i = 0; i < NW; i++) m[i] = 0;
             }
+            j = nj;
+            pbeg = nbeg;
+            pend = nend;
+            pbase = nbase;
+#pragma unroll
+            for (int u = 0; u < kPassU; u++) cur[u] = nxt[u];
         }
-
-        const uint64_t vb = __ballot(viol);
-        if (lane == 0 && vb) atomicAdd(&st->viol, (unsigned long long)__popcll(vb));
-        const uint64_t eb = __ballot(event);
-        if (eb) {
-            uint32_t basei = 0;
-            if (lane == 0) basei = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
-            basei = __shfl(basei, 0, 64);
-            if (event) {
-                const uint32_t idx = basei + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
-                if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
-            }
-        }
+        wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane);
     }
+    if (lane == 0 && wave_viol) atomicAdd(&wg_viol, wave_viol);
+    __syncthreads();
+    if (threadIdx.x == 0 && wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -362,6 +480,23 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
     commit_accept(a, t, a.events, E, lds);
 }
 
+// Arc-balanced static partition of the local rows over W waves: wave w starts at the first row
+// whose offset reaches w*m/W (lower bound), so every wave streams about m/W arcs.
+__global__ void partition_kernel(const uint64_t* __restrict__ row_off, uint32_t nloc, uint32_t W,
+                                 uint32_t* __restrict__ wave_start) {
+    const uint64_t a0 = row_off[0], m = row_off[nloc] - a0;
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w <= W; w += gridDim.x * blockDim.x) {
+        if (w == W) { wave_start[w] = nloc; continue; }
+        const uint64_t target = a0 + (m * w) / W;
+        uint32_t lo = 0, hi = nloc;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (row_off[mid] < target) lo = mid + 1; else hi = mid;
+        }
+        wave_start[w] = lo;
+    }
+}
+
 // ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61): vertex v uses engine draw v + 1 when
 // no earlier draw was rejected by uniform_int_distribution; rejections (P ~ nCol/2^31 each) are
 // counted and handed to the exact sequential host path.
@@ -375,11 +510,17 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
 }
 
 // ----------------------------------------------------------------------------------------------
-using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, hipStream_t);
-template <int NW>
-void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, hipStream_t s) {
-    sweep_kernel<NW><<<g, b, 0, s>>>(a);
+using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
+template <int NW, bool LDSC>
+void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
+    sweep_kernel<NW, LDSC><<<g, b, lds, s>>>(a);
 }
+template <int NW, bool LDSC>
+hipError_t allow_lds(size_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_kernel<NW, LDSC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+constexpr size_t kMaxLdsBytes = 160 * 1024;
 
 static std::once_flag g_const_once;
 static hipError_t g_const_err = hipSuccess;
@@ -413,6 +554,8 @@ struct mcmc_ctx {
     mcmc_run_stats last{};
     SweepLaunch sweep = nullptr;
     dim3 grid, block;
+    size_t lds = 0;             // dynamic LDS of the sweep kernel (colour replica staging)
+    uint32_t* wave_start = nullptr;
     std::vector<uint32_t> host_events;
 };
 
@@ -458,11 +601,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
-    // tile: enough waves to fill 256 CUs x 8 waves, at most 64 vertices per wave
-    const uint32_t nloc = c->v_end - c->v_begin;
-    uint32_t tile = 64;
-    while (tile > 16 && (nloc + tile - 1) / tile < 8192) tile >>= 1;
-    a.tile = tile;
+    a.tile = 32;  // vertices per wave-tile (evaluation batch)
+    a.wave_start = c->wave_start;
     return a;
 }
 
@@ -482,7 +622,7 @@ int ensure_constants() {
 
 // Host launch of one (sweep, commit) pair on the context stream.
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
-    c->sweep(a, c->grid, c->block, c->stream);
+    c->sweep(a, c->grid, c->block, c->lds, c->stream);
     commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
@@ -545,8 +685,28 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     c->v_end = v_end;
     c->z = p->tailcut ? std::max<uint32_t>(50u, gd.n / 2000u) : 0u;   // :89-97
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
-    static const SweepLaunch table[4] = {launch_sweep<1>, launch_sweep<2>, launch_sweep<4>, launch_sweep<8>};
-    c->sweep = table[c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3];
+    // Colour replica staged in LDS when it fits one workgroup's 160 KiB (n <= 163840).
+    const size_t lds_bytes = (((size_t)gd.n + 15) / 16) * 16;
+    // MCMC_GATHER=global forces the L2-gather variant (testing knob: covers both code paths).
+    const char* gv = getenv("MCMC_GATHER");
+    const bool ldsc = lds_bytes <= kMaxLdsBytes && !(gv && std::strcmp(gv, "global") == 0);
+    static const SweepLaunch tab_lds[4] = {launch_sweep<1, true>, launch_sweep<2, true>, launch_sweep<4, true>,
+                                           launch_sweep<8, true>};
+    static const SweepLaunch tab_glb[4] = {launch_sweep<1, false>, launch_sweep<2, false>, launch_sweep<4, false>,
+                                           launch_sweep<8, false>};
+    const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
+    c->sweep = ldsc ? tab_lds[wi] : tab_glb[wi];
+    if (ldsc) {
+        hipError_t ea = wi == 0 ? allow_lds<1, true>(lds_bytes) : wi == 1 ? allow_lds<2, true>(lds_bytes)
+                      : wi == 2 ? allow_lds<4, true>(lds_bytes) : allow_lds<8, true>(lds_bytes);
+        if (ea != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
+        }
+        c->lds = lds_bytes;
+    }
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, gd.device);
     c->glibc = glibc_srand(1);
     const uint32_t nloc = v_end - v_begin;
     c->ev_cap = std::max<uint32_t>(nloc, 1u);
@@ -571,10 +731,28 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         return fail(MCMC_E_NOMEM, std::string("allocation: ") + hipGetErrorString(e));
     }
     if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
-    SweepArgs a = make_args(c, 1);
-    const uint32_t tiles = (nloc + a.tile - 1) / a.tile;
-    c->block = dim3(256);
-    c->grid = dim3(std::max<uint32_t>(1u, std::min<uint32_t>((tiles + 3) / 4, 8192u)));
+    // persistent grids; rows statically arc-balanced over all waves
+    if (ldsc) {
+        c->block = dim3(1024);
+        c->grid = dim3((uint32_t)cus);
+    } else {
+        c->block = dim3(256);
+        c->grid = dim3((uint32_t)cus * 8u);
+    }
+    {
+        const uint32_t W = c->grid.x * (c->block.x / 64);
+        hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
+        if (ew != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_NOMEM, std::string("allocation: ") + hipGetErrorString(ew));
+        }
+        partition_kernel<<<(W + 256) / 256, 256, 0, c->stream>>>(gd.row_off + v_begin, nloc, W, c->wave_start);
+        ew = hipStreamSynchronize(c->stream);
+        if (ew != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("partition: ") + hipGetErrorString(ew));
+        }
+    }
     *out = c;
     return MCMC_OK;
 }
@@ -748,7 +926,7 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     MCMC_HIP_TRY(hipEventRecord(evs[0], c->stream));
     for (uint32_t i = 0; i < sweeps; i++) {
         MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 1], c->stream));
-        c->sweep(a, c->grid, c->block, c->stream);
+        c->sweep(a, c->grid, c->block, c->lds, c->stream);
         MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 2], c->stream));
         commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
     }
@@ -784,6 +962,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->events);
     (void)hipFree(c->st);
     (void)hipFree(c->traj);
+    (void)hipFree(c->wave_start);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -797,7 +976,7 @@ int mcmc_part_sweep(mcmc_ctx* c, uint64_t* local_viol, uint32_t* n_events) {
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     c->ran = true;
     SweepArgs a = make_args(c, 0);
-    c->sweep(a, c->grid, c->block, c->stream);
+    c->sweep(a, c->grid, c->block, c->lds, c->stream);
     MCMC_HIP_TRY(hipGetLastError());
     DevState h{};
     int rc = download_state(c, &h);

@@ -136,6 +136,18 @@ def circulant(n, K):
     return off, idx.ravel()
 
 
+@pytest.mark.parametrize("gather", ["lds", "global"])
+@pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", [(3000, 0.02, 16, 31, 1e-8, 0, 60),
+                                                            (2000, 0.05, 100, 32, 1e-8, 2, 20),
+                                                            (1500, 0.3, 5, 33, 3.3e6, 1, 15)])
+def test_both_gather_variants(M, monkeypatch, gather, n, p, ncol, seed, eps, taboo, maxrip):
+    """The LDS-staged and the L2-gather sweep kernels give the same bit-exact results."""
+    monkeypatch.setenv("MCMC_GATHER", gather)
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
+    col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo)
+    assert_same(col, st, r)
+
+
 def test_many_events_global_sort_path(M):
     """~20000 CDF-overflow events in ONE sweep (epsilon = 3e7 makes the fp32 CDF of a vertex whose
     colour is 0 cancel to 0): exercises the commit's in-global-memory sort and a long ordered
