@@ -114,8 +114,9 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats);
 int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out /* n */);
 int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 /* Timed throughput mode for benchmarks: exactly `sweeps` sweeps of the loop body (no
- * convergence exit, no cap), returns device ms measured with hipEvents on the sweep stream, and
- * the average duration of the dominant sweep kernel. */
+ * convergence exit, no cap), captured into one hipGraph and timed with hipEvents on the sweep
+ * stream. total_ms = device wall of the loop; sweep_kernel_ms = total / sweeps = average duration
+ * of one launch of the (fused) sweep kernel, inter-launch gap included. */
 int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms);
 void mcmc_destroy(mcmc_ctx* c);
 

@@ -49,6 +49,7 @@ struct DevState {
     uint32_t err;               // bit0: event list overflow
     unsigned long long viol;    // sum of viol_v over the swept rows (Cviol_t)
     uint32_t ev_count;          // overflow events this sweep
+    uint32_t arrive;            // workgroups finished with the running sweep (fused commit)
     uint32_t glibc_head;        // ring head of the glibc window
     uint32_t glibc_ring[31];
     uint32_t init_rejections;
@@ -77,6 +78,8 @@ struct SweepArgs {
     uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
     float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
     int check_done;             // device-resident loop: exit immediately once done
+    int fused;                  // last-arriving workgroup runs the commit (single-context loop)
+    uint32_t lds_sort_cap;      // words of the sweep kernel's dynamic LDS reusable by the commit sort
 };
 
 __constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
@@ -117,6 +120,17 @@ __device__ __forceinline__ uint32_t get_color_bit(const uint32_t (&m)[NW], uint3
     return r;
 }
 
+// OR over the 64 lanes into a wave-uniform value: quad swaps and row rotations (DPP, VALU
+// latency) reduce each row of 16 lanes, four readlanes and scalar ORs finish.
+__device__ __forceinline__ uint32_t wave_or_uniform(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);   // row_ror:4
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) | (uint32_t)__builtin_amdgcn_readlane((int)x, 16) |
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 32) | (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
+
 template <int NW>
 __device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
 #pragma unroll
@@ -126,6 +140,121 @@ __device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
         for (int off = 32; off >= 1; off >>= 1) x |= __shfl_xor(x, off, 64);
         m[i] = x;
     }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Commit: loop control + ordered glibc replay. One workgroup.
+constexpr int kCommitThreads = 256;
+constexpr uint32_t kLdsSortCap = 8192;
+
+__device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    const uint32_t x = s[i], y = s[ixj];
+                    if ((x > y) == up) { s[i] = y; s[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Applies the accepted sweep: replays E sorted events, advances the RNG, flips buffers.
+// `ev` holds the events (global ids, any order) and is sorted in place (via LDS when small).
+__device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
+                              uint32_t lds_cap) {
+    DevState* st = a.st;
+    const uint8_t* C = (t & 1) ? a.colors1 : a.colors0;
+    uint8_t* Cs = (t & 1) ? a.colors0 : a.colors1;
+    if (E > 0) {
+        uint32_t P = 1;
+        while (P < E) P <<= 1;
+        uint32_t* s = (P <= lds_cap) ? lds : ev;
+        if (s == ev) {
+            for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
+        } else {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        bitonic_sort_block(s, P);
+        if (threadIdx.x == 0) {
+            uint32_t ring[31];
+            for (int i = 0; i < 31; i++) ring[i] = st->glibc_ring[i];
+            uint32_t head = st->glibc_head;
+            for (uint32_t i = 0; i < E; i++) {
+                const uint32_t v = s[i];
+                const uint32_t r = glibc_next(ring, head);
+                const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                Cs[v] = (uint8_t)c;
+                if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
+                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
+            }
+            for (int i = 0; i < 31; i++) st->glibc_ring[i] = ring[i];
+            st->glibc_head = head;
+        }
+    }
+    if (threadIdx.x == 0) {
+        st->glibc_draws += E;
+        st->x_t = minstd_mulmod(st->x_t, a.aN);
+        st->t = t + 1;
+        st->viol = 0;
+        st->ev_count = 0;
+        st->arrive = 0;
+    }
+}
+
+// Loop control of run() (coloringMCMC_CPU.cpp:136, :259-269): records Cviol_t, stops on the cap or
+// on Cviol_t <= z, otherwise accepts the sweep. All threads of one workgroup call it with the same
+// state values; thread 0 writes the state.
+__device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
+                               uint32_t* lds, uint32_t lds_cap) {
+    DevState* st = a.st;
+    if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
+    const bool stop_cap = t == a.maxRip + 1;     // iter > maxiter after sweep maxRip
+    const bool stop_conv = viol <= a.z;          // while (Cviol > z)
+    if (stop_cap || stop_conv) {
+        if (threadIdx.x == 0) {
+            st->done = 1;
+            st->iter = t;
+            st->maxIterReached = stop_cap;
+            st->finalViol = viol;
+            st->arrive = 0;
+        }
+        return;
+    }
+    if (E > a.ev_cap || err) {
+        if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
+        return;
+    }
+    commit_accept(a, t, a.events, E, lds, lds_cap);
+}
+
+// Stand-alone commit (MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
+__global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
+    __shared__ uint32_t lds[kLdsSortCap];
+    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
+    __shared__ unsigned long long sh_viol;
+    DevState* st = a.st;
+    if (threadIdx.x == 0) {
+        sh_done = st->done;
+        sh_t = st->t;
+        sh_viol = st->viol;
+        sh_E = st->ev_count;
+        sh_err = st->err;
+    }
+    __syncthreads();
+    if (sh_done) return;
+    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+}
+
+// Commit of a vertex-partitioned sweep: global Cviol and the global event list come from the host.
+__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, uint32_t t, uint32_t E) {
+    __shared__ uint32_t lds[kLdsSortCap];
+    commit_accept(a, t, a.events, E, lds, kLdsSortCap);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -230,7 +359,10 @@ constexpr uint32_t kPassArcs = 256u * kPassU;
 template <int NW, bool LDSC>
 __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     extern __shared__ uint4 sc_raw[];
-    __shared__ uint32_t wg_viol;
+    __shared__ uint32_t wg_viol, wg_last;
+    __shared__ uint32_t sort_static[LDSC ? 1 : 2048];
+    __shared__ uint32_t sh_t, sh_E, sh_err;
+    __shared__ unsigned long long sh_viol;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
     if (threadIdx.x == 0) wg_viol = 0;
@@ -352,10 +484,10 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
                 }
             }
             if (row_done) {
-                wave_or<NW>(m);
-                if ((uint32_t)lane == j) {
 #pragma unroll
-                    for (int i = 0; i < NW; i++) acc[i] = m[i];
+                for (int i = 0; i < NW; i++) {
+                    const uint32_t r = wave_or_uniform(m[i]);
+                    acc[i] = ((uint32_t)lane == j) ? r : acc[i];
                 }
 #pragma unroll
                 for (int i = 0; i < NW; i++) m[i] = 0;
@@ -370,114 +502,36 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
         wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane);
     }
     if (lane == 0 && wave_viol) atomicAdd(&wg_viol, wave_viol);
-    __syncthreads();
-    if (threadIdx.x == 0 && wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
-}
-
-// ----------------------------------------------------------------------------------------------
-// Commit: loop control + ordered glibc replay. One workgroup.
-constexpr int kCommitThreads = 256;
-constexpr uint32_t kLdsSortCap = 8192;
-
-__device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & k) == 0;
-                    const uint32_t x = s[i], y = s[ixj];
-                    if ((x > y) == up) { s[i] = y; s[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// Applies the accepted sweep: replays E sorted events, advances the RNG, flips buffers.
-// `ev` holds the events (global ids, any order) and is sorted in place (via LDS when small).
-__device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds) {
-    DevState* st = a.st;
-    const uint8_t* C = (t & 1) ? a.colors1 : a.colors0;
-    uint8_t* Cs = (t & 1) ? a.colors0 : a.colors1;
-    if (E > 0) {
-        uint32_t P = 1;
-        while (P < E) P <<= 1;
-        uint32_t* s = (P <= kLdsSortCap) ? lds : ev;
-        if (s == ev) {
-            for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
-        } else {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
-        }
+    if (!a.fused) {
         __syncthreads();
-        bitonic_sort_block(s, P);
-        if (threadIdx.x == 0) {
-            uint32_t ring[31];
-            for (int i = 0; i < 31; i++) ring[i] = st->glibc_ring[i];
-            uint32_t head = st->glibc_head;
-            for (uint32_t i = 0; i < E; i++) {
-                const uint32_t v = s[i];
-                const uint32_t r = glibc_next(ring, head);
-                const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
-                Cs[v] = (uint8_t)c;
-                if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
-                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
-            }
-            for (int i = 0; i < 31; i++) st->glibc_ring[i] = ring[i];
-            st->glibc_head = head;
+        if (threadIdx.x == 0 && wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
+        return;
+    }
+    // Fused commit (MI355X_MICROARCH.md "Workgroup dispatch ... visibility"): every storing wave
+    // drains its stores, the workgroup meets, lane 0 publishes Cviol, releases at agent scope and
+    // arrives; the workgroup whose arrival is last acquires and runs the commit.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = atomicAdd(&st->arrive, 1u);
+        wg_last = (prev == gridDim.x - 1) ? 1u : 0u;
+        if (wg_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sh_t = st->t;
+            sh_viol = st->viol;
+            sh_E = st->ev_count;
+            sh_err = st->err;
         }
-    }
-    if (threadIdx.x == 0) {
-        st->glibc_draws += E;
-        st->x_t = minstd_mulmod(st->x_t, a.aN);
-        st->t = t + 1;
-        st->viol = 0;
-        st->ev_count = 0;
-    }
-}
-
-// Loop control of run() (coloringMCMC_CPU.cpp:136, :259-269) for the single-context loop.
-__global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
-    __shared__ uint32_t lds[kLdsSortCap];
-    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
-    __shared__ unsigned long long sh_viol;
-    DevState* st = a.st;
-    if (threadIdx.x == 0) {
-        sh_done = st->done;
-        sh_t = st->t;
-        sh_viol = st->viol;
-        sh_E = st->ev_count;
-        sh_err = st->err;
     }
     __syncthreads();
-    if (sh_done) return;
-    const uint32_t t = sh_t;
-    const unsigned long long viol = sh_viol;
-    if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
-    const bool stop_cap = t == a.maxRip + 1;     // iter > maxiter after sweep maxRip
-    const bool stop_conv = viol <= a.z;          // while (Cviol > z)
-    if (stop_cap || stop_conv) {
-        if (threadIdx.x == 0) {
-            st->done = 1;
-            st->iter = t;
-            st->maxIterReached = stop_cap;
-            st->finalViol = viol;
-        }
-        return;
-    }
-    const uint32_t E = sh_E;
-    if (E > a.ev_cap || sh_err) {
-        if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
-        return;
-    }
-    commit_accept(a, t, a.events, E, lds);
-}
-
-// Commit of a vertex-partitioned sweep: global Cviol and the global event list come from the host.
-__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, uint32_t t, uint32_t E) {
-    __shared__ uint32_t lds[kLdsSortCap];
-    commit_accept(a, t, a.events, E, lds);
+    if (!wg_last) return;
+    uint32_t* lds = LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static;
+    const uint32_t cap = LDSC ? a.lds_sort_cap : 2048u;
+    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, cap);
 }
 
 // Arc-balanced static partition of the local rows over W waves: wave w starts at the first row
@@ -520,7 +574,7 @@ hipError_t allow_lds(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_kernel<NW, LDSC>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-constexpr size_t kMaxLdsBytes = 160 * 1024;
+constexpr size_t kMaxLdsBytes = 160 * 1024 - 1024;   // leave room for the static shared variables
 
 static std::once_flag g_const_once;
 static hipError_t g_const_err = hipSuccess;
@@ -556,6 +610,7 @@ struct mcmc_ctx {
     dim3 grid, block;
     size_t lds = 0;             // dynamic LDS of the sweep kernel (colour replica staging)
     uint32_t* wave_start = nullptr;
+    int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     std::vector<uint32_t> host_events;
 };
 
@@ -601,6 +656,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
+    a.fused = check_done ? c->fused : 0;
+    a.lds_sort_cap = (uint32_t)(c->lds / 4);
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
     return a;
@@ -623,7 +680,7 @@ int ensure_constants() {
 // Host launch of one (sweep, commit) pair on the context stream.
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     c->sweep(a, c->grid, c->block, c->lds, c->stream);
-    commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (!a.fused) commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
 int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
@@ -687,6 +744,8 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
     // Colour replica staged in LDS when it fits one workgroup's 160 KiB (n <= 163840).
     const size_t lds_bytes = (((size_t)gd.n + 15) / 16) * 16;
+    const char* fv = getenv("MCMC_FUSED_COMMIT");
+    c->fused = (fv && std::strcmp(fv, "0") == 0) ? 0 : 1;
     // MCMC_GATHER=global forces the L2-gather variant (testing knob: covers both code paths).
     const char* gv = getenv("MCMC_GATHER");
     const bool ldsc = lds_bytes <= kMaxLdsBytes && !(gv && std::strcmp(gv, "global") == 0);
@@ -914,40 +973,39 @@ int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len)
 int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
+    if (sweeps == 0) return fail(MCMC_E_ARG, "sweeps must be > 0");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    // Throughput mode: the same kernels with the stop tests disabled (no cap, z = 0 only stops
-    // on a proper colouring). Sweep kernels are timed individually with events on the stream.
+    // Throughput mode: the loop body with the stop tests disabled (no cap; z = 0 stops only on a
+    // proper colouring). The `sweeps` launches are captured into one hipGraph and replayed between
+    // two events on the sweep stream: total = wall of the device loop, per-launch average = total
+    // / sweeps (each launch is one fused sweep; the average includes the inter-launch gap).
     SweepArgs a = make_args(c, 1);
     a.maxRip = 0xFFFFFFF0u;
     a.traj_cap = 0;
     c->ran = true;
-    std::vector<hipEvent_t> evs(2 * sweeps + 2);
-    for (auto& e : evs) MCMC_HIP_TRY(hipEventCreate(&e));
-    MCMC_HIP_TRY(hipEventRecord(evs[0], c->stream));
-    for (uint32_t i = 0; i < sweeps; i++) {
-        MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 1], c->stream));
-        c->sweep(a, c->grid, c->block, c->lds, c->stream);
-        MCMC_HIP_TRY(hipEventRecord(evs[2 * i + 2], c->stream));
-        commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
-    }
-    MCMC_HIP_TRY(hipGetLastError());
-    MCMC_HIP_TRY(hipEventRecord(evs[2 * sweeps + 1], c->stream));
-    MCMC_HIP_TRY(hipEventSynchronize(evs[2 * sweeps + 1]));
+    hipGraph_t graph;
+    hipGraphExec_t exec = nullptr;
+    MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (uint32_t i = 0; i < sweeps; i++) launch_pair(c, a);
+    MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
+    hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    MCMC_HIP_TRY(hipGraphUpload(exec, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    MCMC_HIP_TRY(hipGraphLaunch(exec, c->stream));
+    MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
     float tot = 0;
-    MCMC_HIP_TRY(hipEventElapsedTime(&tot, evs[0], evs[2 * sweeps + 1]));
-    double ks = 0;
-    for (uint32_t i = 0; i < sweeps; i++) {
-        float ms = 0;
-        MCMC_HIP_TRY(hipEventElapsedTime(&ms, evs[2 * i + 1], evs[2 * i + 2]));
-        ks += ms;
-    }
-    for (auto& e : evs) (void)hipEventDestroy(e);
+    MCMC_HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
+    (void)hipGraphExecDestroy(exec);
     DevState h{};
     int rc = download_state(c, &h);
     if (rc) return rc;
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
-    if (sweep_kernel_ms) *sweep_kernel_ms = sweeps ? ks / sweeps : 0.0;
+    if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
     return MCMC_OK;
 }
 
