@@ -1,0 +1,246 @@
+// include/mcmc_colorer.hpp -- header-only C++ class surface of the reference's MCMC colorer,
+// rebuilt over the C ABI in mcmc_hip.h (link with -lmcmc_hip).
+//
+// Reference surface (paths relative to /root/reference/src), as called from src/main.cu:60-202:
+//   struct ColoringMCMCParams                      graph_coloring/coloring.h:65-74
+//   template<nodeW,edgeW> struct GraphStruct       graph/graph.h:37-79  (uint64 cumulDegs here)
+//   template<nodeW,edgeW> class Graph              graph/graph.h:84-133
+//       Graph(node nn, float prob, uint32_t seed)  -> setupRnd2 (graphCPU.cpp:424-537), on the GPU
+//       Graph(fileImporter*, bool)                 -> setupImporterNew (graphCPU.cpp:245-303)
+//       Graph(Graph* host)                         -> device copy (graphGPU.cu:210-226)
+//   class GPURand(n, seed), member randStates      GPUutils/GPURandomizer.h:42-55
+//   template<nodeW,edgeW> class ColoringMCMC       graph_coloring/coloringMCMC.h:44-140
+//       ColoringMCMC(Graph* g_d, randStates, ColoringMCMCParams); run(int); setDirectoryPath(string)
+//
+// Behaviour: run(i) computes exactly what ColoringMCMC_CPU(g, params, seed + i).run() computes
+// (main.cu:171), on the GPU. The reference's process-global glibc rand() stream (setupRnd2 draws and
+// CDF-overflow draws) is a process-global glibc window here (mcmc::glibc_global()). Like the
+// reference (GPUutils/GPUutils.h:20-26), errors print and abort.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "mcmc_hip.h"
+
+typedef uint32_t node;
+typedef uint32_t node_sz;
+typedef uint32_t col;
+typedef uint32_t col_sz;
+
+namespace mcmc {
+
+inline void check(int rc, const char* file, int line) {
+    if (rc != MCMC_OK) {
+        std::fprintf(stderr, "libmcmc_hip error %d: %s (%s:%d)\n", rc, mcmc_last_error(), file, line);
+        std::abort();
+    }
+}
+#define MCMC_CHECK(x) ::mcmc::check((x), __FILE__, __LINE__)
+
+// The process-wide glibc rand() position (unseeded == srand(1), ArgHandle.cpp:272-276).
+struct GlibcWindow {
+    uint32_t w[31];
+};
+inline GlibcWindow& glibc_global() {
+    static GlibcWindow g = [] {
+        GlibcWindow x;
+        MCMC_CHECK(mcmc_glibc_window(1, 0, x.w));
+        return x;
+    }();
+    return g;
+}
+// srand(seed) (ArgHandle.cpp:275, used when --seed is 0).
+inline void glibc_srand(uint32_t seed) { MCMC_CHECK(mcmc_glibc_window(seed, 0, glibc_global().w)); }
+
+}  // namespace mcmc
+
+// ColoringMCMCParams (coloring.h:65-74)
+struct ColoringMCMCParams {
+    uint32_t maxRip;
+    col_sz nCol;
+    float numColorRatio;
+    float lambda;
+    float epsilon;
+    float ratioFreezed;
+    uint32_t tabooIteration;
+    bool tailcut;
+};
+
+// GraphStruct (graph.h:37-79) -- host view; cumulDegs widened to uint64.
+template <typename nodeW, typename edgeW>
+struct GraphStruct {
+    node nNodes{0};
+    uint64_t nEdges{0};
+    std::vector<uint64_t> cumulDegsV;
+    std::vector<node> neighsV;
+    uint64_t* cumulDegs{nullptr};
+    node* neighs{nullptr};
+    uint64_t deg(node i) const { return cumulDegs[i + 1] - cumulDegs[i]; }
+};
+
+template <typename nodeW, typename edgeW>
+class Graph {
+public:
+    // Graph(n, prob, seed) -> setupRnd2; `seed` is unused by the reference too (graphCPU.cpp:424).
+    Graph(node nn, float prob_, uint32_t /*seed*/, int device = 0) : prob(prob_), device_(device) {
+        MCMC_CHECK(mcmc_graph_simulate(nn, prob_, mcmc::glibc_global().w, device, &h_));
+        info();
+    }
+    // Host CSR (e.g. from the edge-list importer) -> device copy.
+    Graph(const std::vector<uint64_t>& cumulDegs, const std::vector<node>& neighs, float prob_, int device = 0)
+        : prob(prob_), device_(device) {
+        MCMC_CHECK(mcmc_graph_upload(cumulDegs.data(), neighs.data(), (uint32_t)(cumulDegs.size() - 1),
+                                     neighs.size(), device, &h_));
+        info();
+    }
+    ~Graph() { mcmc_graph_destroy(h_); }
+    Graph(const Graph&) = delete;
+    Graph& operator=(const Graph&) = delete;
+
+    GraphStruct<nodeW, edgeW>* getStruct() {
+        if (!str_.cumulDegs) {
+            str_.nNodes = n_;
+            str_.nEdges = m_;
+            str_.cumulDegsV.resize((size_t)n_ + 1);
+            str_.neighsV.resize(m_ ? m_ : 1);
+            MCMC_CHECK(mcmc_graph_download(h_, str_.cumulDegsV.data(), str_.neighsV.data()));
+            str_.cumulDegs = str_.cumulDegsV.data();
+            str_.neighs = str_.neighsV.data();
+        }
+        return &str_;
+    }
+    node getNNodes() const { return n_; }
+    uint64_t getNEdges() const { return m_; }
+    node getMaxNodeDeg() const { return maxDeg_; }
+    node getMinNodeDeg() const { return minDeg_; }
+    float getMeanNodeDeg() const { return n_ ? (float)m_ / (float)n_ : 0.0f; }
+    const mcmc_graph* handle() const { return h_; }
+    float prob{0.0f};
+
+private:
+    void info() { MCMC_CHECK(mcmc_graph_info(h_, &n_, &m_, &maxDeg_, &minDeg_)); }
+    mcmc_graph* h_{nullptr};
+    int device_{0};
+    node n_{0};
+    uint64_t m_{0};
+    node maxDeg_{0}, minDeg_{0};
+    GraphStruct<nodeW, edgeW> str_;
+};
+
+// GPURand (GPURandomizer.h:42-55): the reference keeps one cuRAND state per vertex; the sweep
+// derives every draw by minstd skip-ahead, so only the seed is kept.
+struct GPURandHandle {
+    uint32_t seed;
+};
+class GPURand {
+public:
+    GPURand(uint32_t n, long seed) : num(n) { state.seed = (uint32_t)seed; randStates = &state; }
+    uint32_t num;
+    GPURandHandle* randStates;
+
+private:
+    GPURandHandle state{};
+};
+
+template <typename nodeW, typename edgeW>
+class ColoringMCMC {
+public:
+    ColoringMCMC(Graph<nodeW, edgeW>* inGraph_d, GPURandHandle* randStates, ColoringMCMCParams params)
+        : graph(inGraph_d), seed(randStates->seed), param(params) {}
+    ~ColoringMCMC() { if (ctx) mcmc_destroy(ctx); }
+
+    void setDirectoryPath(std::string directory) { this->directory = directory; }
+
+    // One repetition: engine seed = seed + iteration (main.cu:171), glibc stream = process global.
+    void run(int iteration) {
+        if (ctx) mcmc_destroy(ctx);
+        mcmc_params p{};
+        p.nCol = param.nCol;
+        p.epsilon = param.epsilon;
+        p.lambda = param.lambda;
+        p.ratioFreezed = param.ratioFreezed;
+        p.numColorRatio = param.numColorRatio;
+        p.maxRip = param.maxRip;
+        p.tabooIteration = param.tabooIteration;
+        p.tailcut = param.tailcut;
+        p.seed = seed + (uint32_t)iteration;
+        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
+        MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));
+        MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
+        MCMC_CHECK(mcmc_run(ctx, 0, &stats));
+        MCMC_CHECK(mcmc_get_glibc_window(ctx, mcmc::glibc_global().w));
+        coloring.resize(graph->getNNodes());
+        MCMC_CHECK(mcmc_get_coloring(ctx, coloring.data()));
+        trajectory.resize(stats.trajLen);
+        uint64_t len = 0;
+        MCMC_CHECK(mcmc_get_trajectory(ctx, trajectory.data(), trajectory.size(), &len));
+        lastSeed = p.seed;
+        lastRepetition = iteration;
+        if (!directory.empty()) save();
+    }
+
+    // Report in the layout of saveStats (coloringMCMC_CPUutils.cpp:177-210), parseable by the
+    // reference's pyScripts/logParser.py, plus the per-sweep trajectory; colours as "<v> <c>".
+    void save() const {
+        std::ofstream out(directory + ".log");
+        const uint32_t nCol = param.nCol;
+        out << "MCMC Colorer - GPU (MI355X) version - Report" << std::endl;
+        out << "-------------------------------------------" << std::endl;
+        out << "GRAPH INFO" << std::endl;
+        out << "Nodes: " << graph->getNNodes() << " - Edges: " << graph->getNEdges() << std::endl;
+        out << "Max deg: " << graph->getMaxNodeDeg() << " - Min deg: " << graph->getMinNodeDeg()
+            << " - Avg deg: " << graph->getMeanNodeDeg() << std::endl;
+        out << "Edge probability (for randomly generated graphs): " << graph->prob << std::endl;
+        out << "Seed: " << lastSeed << std::endl;
+        out << "-------------------------------------------" << std::endl;
+        out << "EXECUTION INFO" << std::endl;
+        out << "Repetition: " << lastRepetition << std::endl;
+        out << "Execution time: " << stats.loopMs / 1000.0 << std::endl;
+        out << "Iteration performed: " << stats.iter << std::endl;
+        out << "Max iteration reached: " << (stats.maxIterReached ? "yes" : "no") << std::endl;
+        out << "-------------------------------------------" << std::endl;
+        out << "Color histogram:" << std::endl;
+        std::vector<size_t> hist(nCol, 0);
+        for (uint32_t c : coloring) hist[c]++;
+        size_t used = 0;
+        for (size_t i = 0; i < nCol; i++) { out << i << ": " << hist[i] << std::endl; if (hist[i]) used++; }
+        out << "Number of colors: " << nCol << " - Used colors: " << used << std::endl;
+        out << "Color ratio: " << param.numColorRatio << std::endl;
+        float mean = 0;
+        for (size_t h : hist) mean += (float)h;
+        mean /= (float)nCol;
+        float var = 0;
+        for (size_t h : hist) var += ((h - mean) * (h - mean));
+        var /= (float)nCol;
+        out << "Average number of nodes for each color: " << mean << std::endl;
+        out << "Variance: " << var << std::endl;
+        out << "StD: " << std::sqrt(var) << std::endl;
+        out << "Conflicts per sweep (C violations):";
+        for (uint64_t x : trajectory) out << " " << x;
+        out << std::endl;
+        std::ofstream cf(directory + "-colors.txt");
+        for (size_t i = 0; i < coloring.size(); i++) cf << i << " " << coloring[i] << "\n";
+    }
+
+    const std::vector<uint32_t>& getColoring() const { return coloring; }
+    const std::vector<uint64_t>& getTrajectory() const { return trajectory; }
+    const mcmc_run_stats& getStats() const { return stats; }
+
+private:
+    Graph<nodeW, edgeW>* graph;
+    uint32_t seed;
+    ColoringMCMCParams param;
+    std::string directory;
+    mcmc_ctx* ctx{nullptr};
+    mcmc_run_stats stats{};
+    std::vector<uint32_t> coloring;
+    std::vector<uint64_t> trajectory;
+    uint32_t lastSeed{0};
+    int lastRepetition{0};
+};

@@ -121,18 +121,24 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
 void mcmc_destroy(mcmc_ctx* c);
 
 /* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------
- * One sweep = mcmc_part_sweep (local rows) -> caller all-gathers the owned colour slabs and the
- * (viol, events) footers of every rank -> mcmc_part_commit with the concatenated, rank-ordered
- * event list. Every rank replays the same glibc draws, so replicas stay identical. */
-int mcmc_part_sweep(mcmc_ctx* c, uint64_t* local_viol, uint32_t* n_events);
-int mcmc_part_events(mcmc_ctx* c, uint32_t* out, uint32_t cap);
-/* Device pointer of the next-colour buffer (full length n, element size mcmc_color_bytes). */
-int mcmc_part_next_colors(mcmc_ctx* c, void** dev_ptr, uint32_t* elem_bytes);
-/* total_viol: the global Cviol of the current colouring (sum of all ranks' local_viol).
- * Returns *finished = 1 when the loop is over (colouring not advanced); else applies the
- * events, swaps the buffers and advances the RNG. */
-int mcmc_part_commit(mcmc_ctx* c, uint64_t total_viol, const uint32_t* events, uint32_t n_events,
-                     int32_t* finished);
+ * SURVEY.md §8e. Rank r of `world` sweeps rows [r*S, min(n,(r+1)*S)), S = ceil(n/world), with global
+ * ids and full-length colour replicas. Per sweep, all on the caller's stream, no host sync:
+ *   mcmc_part_sweep_async  sweep of the local rows; writes the local slab of the next-colour
+ *                          buffer and this rank's footer (local Cviol + sorted overflow events)
+ *   caller                 all-gathers the slabs (in place, S bytes per rank, into the next-colour
+ *                          buffer colors[(t+1)&1]) and the footers (MCMC_FOOTER_WORDS uint32 each)
+ *   mcmc_part_commit_async global Cviol, stop test, rank-ordered glibc replay -- identical on
+ *                          every replica -- RNG advance, buffer flip
+ * The colour buffers (>= world*S and n+16 bytes each), footer and footers_all are caller-owned
+ * device memory (e.g. torch tensors); `stream` is the caller's hipStream_t, used as given (0 = the
+ * legacy null stream, torch's default current stream). */
+#define MCMC_FOOTER_WORDS 1024
+int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
+                     uint64_t colors_bytes, void* footer, void* footers_all, void* stream);
+int mcmc_part_sweep_async(mcmc_ctx* c);
+int mcmc_part_commit_async(mcmc_ctx* c);
+/* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final). */
+int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
 
 #ifdef __cplusplus
 }

@@ -38,10 +38,11 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_destroy": (None, [c_void_p]),
-    "mcmc_part_sweep": (c_int, [c_void_p, _u64p, _u32p]),
-    "mcmc_part_events": (c_int, [c_void_p, _u32p, c_uint32]),
-    "mcmc_part_next_colors": (c_int, [c_void_p, POINTER(c_void_p), _u32p]),
-    "mcmc_part_commit": (c_int, [c_void_p, c_uint64, _u32p, c_uint32, POINTER(c_int32)]),
+    "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+                                 c_void_p]),
+    "mcmc_part_sweep_async": (c_int, [c_void_p]),
+    "mcmc_part_commit_async": (c_int, [c_void_p]),
+    "mcmc_part_state": (c_int, [c_void_p, POINTER(c_int32), _u32p, _u32p]),
 }
 
 

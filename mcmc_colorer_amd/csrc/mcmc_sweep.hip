@@ -78,7 +78,11 @@ struct SweepArgs {
     uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
     float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
     int check_done;             // device-resident loop: exit immediately once done
-    int fused;                  // last-arriving workgroup runs the commit (single-context loop)
+    int fused;                  // last-arriving workgroup: 1 = runs the commit (single-context loop),
+                                //                          2 = packs this rank's footer (partitioned)
+    uint32_t* footer;           // partitioned: this rank's footer [viol lo, viol hi, E, flags, events...]
+    const uint32_t* footers_all;// partitioned: all ranks' footers after the all-gather
+    uint32_t world;
     uint32_t lds_sort_cap;      // words of the sweep kernel's dynamic LDS reusable by the commit sort
 };
 
@@ -251,10 +255,75 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
     commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
 }
 
-// Commit of a vertex-partitioned sweep: global Cviol and the global event list come from the host.
-__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, uint32_t t, uint32_t E) {
+// ---- vertex-partitioned sweep: footer exchange ------------------------------------------------
+constexpr uint32_t kFooterWords = 1024;                 // MCMC_FOOTER_WORDS
+constexpr uint32_t kFooterEvents = kFooterWords - 4;
+
+// Last workgroup of a partitioned sweep: sort this rank's overflow events and publish
+// [Cviol_local, E, flags, events] for the all-gather; reset the local accumulators.
+__device__ void pack_footer(const SweepArgs& a, unsigned long long viol, uint32_t E, uint32_t err, uint32_t* lds,
+                            uint32_t lds_cap) {
+    DevState* st = a.st;
+    uint32_t* s = a.events;
+    if (E > 0 && E <= a.ev_cap) {
+        uint32_t P = 1;
+        while (P < E) P <<= 1;
+        s = (P <= lds_cap) ? lds : a.events;
+        if (s == a.events) {
+            for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
+        } else {
+            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? a.events[i] : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        bitonic_sort_block(s, P);
+    }
+    const uint32_t En = min(E, kFooterEvents);
+    for (uint32_t i = threadIdx.x; i < En; i += blockDim.x) a.footer[4 + i] = s[i];
+    if (threadIdx.x == 0) {
+        a.footer[0] = (uint32_t)viol;
+        a.footer[1] = (uint32_t)(viol >> 32);
+        a.footer[2] = E;
+        a.footer[3] = (E > kFooterEvents || E > a.ev_cap || err) ? 1u : 0u;
+        st->viol = 0;
+        st->ev_count = 0;
+        st->arrive = 0;
+    }
+}
+
+// Every rank, after the all-gathers: global Cviol = sum of the footers, events = rank-ordered
+// concatenation (ranks own ascending vertex ranges, so it is ascending), then the same commit as
+// the single-context loop -- identical glibc replay on every replica.
+__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a) {
     __shared__ uint32_t lds[kLdsSortCap];
-    commit_accept(a, t, a.events, E, lds, kLdsSortCap);
+    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
+    __shared__ unsigned long long sh_viol;
+    __shared__ uint32_t sh_off[65];
+    DevState* st = a.st;
+    if (threadIdx.x == 0) {
+        sh_done = st->done;
+        sh_t = st->t;
+        unsigned long long v = 0;
+        uint32_t E = 0, err = st->err;
+        for (uint32_t r = 0; r < a.world; r++) {
+            const uint32_t* f = a.footers_all + (size_t)r * kFooterWords;
+            v += (unsigned long long)f[0] | ((unsigned long long)f[1] << 32);
+            sh_off[r] = E;
+            E += min(f[2], kFooterEvents);
+            err |= f[3];
+        }
+        sh_viol = v;
+        sh_E = E;
+        sh_err = err;
+    }
+    __syncthreads();
+    if (sh_done) return;
+    for (uint32_t r = 0; r < a.world; r++) {
+        const uint32_t* f = a.footers_all + (size_t)r * kFooterWords;
+        const uint32_t Er = min(f[2], kFooterEvents);
+        for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = f[4 + i];
+    }
+    __syncthreads();
+    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -531,7 +600,8 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     if (!wg_last) return;
     uint32_t* lds = LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static;
     const uint32_t cap = LDSC ? a.lds_sort_cap : 2048u;
-    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, cap);
+    if (a.fused == 1) commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, cap);
+    else pack_footer(a, sh_viol, sh_E, sh_err, lds, cap);
 }
 
 // Arc-balanced static partition of the local rows over W waves: wave w starts at the first row
@@ -599,6 +669,7 @@ struct mcmc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipGraphExec_t batch_exec = nullptr;
+    bool borrowed_stream = false;
     uint32_t batch = 0;
     GlibcWindow glibc{};
     bool initialized = false;
@@ -611,6 +682,11 @@ struct mcmc_ctx {
     size_t lds = 0;             // dynamic LDS of the sweep kernel (colour replica staging)
     uint32_t* wave_start = nullptr;
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
+    bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
+    uint32_t world = 1, rank = 0;
+    uint32_t* footer = nullptr;
+    const uint32_t* footers_all = nullptr;
+    uint8_t* own_colors[2] = {nullptr, nullptr};   // the context's own replicas (freed at destroy)
     std::vector<uint32_t> host_events;
 };
 
@@ -656,7 +732,10 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
-    a.fused = check_done ? c->fused : 0;
+    a.fused = c->part ? 2 : (check_done ? c->fused : 0);
+    a.footer = c->footer;
+    a.footers_all = c->footers_all;
+    a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
@@ -768,7 +847,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, gd.device);
     c->glibc = glibc_srand(1);
     const uint32_t nloc = v_end - v_begin;
-    c->ev_cap = std::max<uint32_t>(nloc, 1u);
+    c->ev_cap = std::max<uint32_t>(nloc, 64u * 1024u);   // local events; also >= 64 ranks x footer events
     c->traj_cap = p->maxRip + 2;
     hipError_t e = hipSuccess;
     auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
@@ -778,6 +857,8 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     // colour replicas carry 256 B of slack so equal-size partition slabs can be all-gathered in place
     chk(hipMalloc(&c->colors[0], (size_t)gd.n + 256));
     chk(hipMalloc(&c->colors[1], (size_t)gd.n + 256));
+    c->own_colors[0] = c->colors[0];
+    c->own_colors[1] = c->colors[1];
     if (p->tabooIteration > 0) chk(hipMalloc(&c->taboo, sizeof(uint32_t) * std::max<uint32_t>(nloc, 1)));
     // event list sized n (+ pow2 padding room for the in-place sort fallback)
     uint32_t pcap = 1;
@@ -1014,8 +1095,8 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipSetDevice(c->g->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->batch_exec) (void)hipGraphExecDestroy(c->batch_exec);
-    (void)hipFree(c->colors[0]);
-    (void)hipFree(c->colors[1]);
+    (void)hipFree(c->own_colors[0]);
+    (void)hipFree(c->own_colors[1]);
     (void)hipFree(c->taboo);
     (void)hipFree(c->events);
     (void)hipFree(c->st);
@@ -1023,99 +1104,75 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wave_start);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
-// ---- vertex-partitioned step ----------------------------------------------------------------
-int mcmc_part_sweep(mcmc_ctx* c, uint64_t* local_viol, uint32_t* n_events) {
-    if (!c) return fail(MCMC_E_ARG, "NULL context");
-    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep");
-    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+// ---- vertex-partitioned step (device-resident; exchange by the caller) -----------------------
+int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
+                     uint64_t colors_bytes, void* footer, void* footers_all, void* stream) {
+    if (!c || !colors0 || !colors1 || !footer || !footers_all) return fail(MCMC_E_ARG, "NULL argument");
+    if (world == 0 || world > 64 || rank >= world) return fail(MCMC_E_ARG, "bad world/rank (1..64 ranks)");
+    const uint64_t S = ((uint64_t)c->n + world - 1) / world;
+    if (colors_bytes < S * world || colors_bytes < (uint64_t)c->n + 16)
+        return fail(MCMC_E_ARG, "colour buffers must hold world * ceil(n/world) and n + 16 bytes");
+    if (c->v_begin != std::min<uint64_t>(S * rank, c->n) || c->v_end != std::min<uint64_t>(S * (rank + 1), c->n))
+        return fail(MCMC_E_ARG, "context rows must be [rank*S, min(n,(rank+1)*S)), S = ceil(n/world)");
+    c->colors[0] = static_cast<uint8_t*>(colors0);
+    c->colors[1] = static_cast<uint8_t*>(colors1);
+    c->footer = static_cast<uint32_t*>(footer);
+    c->footers_all = static_cast<const uint32_t*>(footers_all);
+    c->world = world;
+    c->rank = rank;
+    c->part = true;
+    // the caller's stream as given: 0 is the legacy null stream (torch's default current stream)
+    if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
+    c->stream = static_cast<hipStream_t>(stream);
+    c->borrowed_stream = true;
+    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
+    return MCMC_OK;
+}
+
+int mcmc_part_sweep_async(mcmc_ctx* c) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
     c->ran = true;
-    SweepArgs a = make_args(c, 0);
+    SweepArgs a = make_args(c, 1);
     c->sweep(a, c->grid, c->block, c->lds, c->stream);
     MCMC_HIP_TRY(hipGetLastError());
-    DevState h{};
-    int rc = download_state(c, &h);
-    if (rc) return rc;
-    if (h.err || h.ev_count > c->ev_cap) return fail(MCMC_E_DEVICE, "event list overflow");
-    if (local_viol) *local_viol = h.viol;
-    if (n_events) *n_events = h.ev_count;
-    c->host_events.resize(h.ev_count);
-    if (h.ev_count) {
-        MCMC_HIP_TRY(hipMemcpyAsync(c->host_events.data(), c->events, sizeof(uint32_t) * h.ev_count,
-                                    hipMemcpyDeviceToHost, c->stream));
-        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
-        std::sort(c->host_events.begin(), c->host_events.end());
-    }
     return MCMC_OK;
 }
 
-int mcmc_part_events(mcmc_ctx* c, uint32_t* out, uint32_t cap) {
-    if (!c) return fail(MCMC_E_ARG, "NULL context");
-    if (cap < c->host_events.size()) return fail(MCMC_E_ARG, "event buffer too small");
-    if (!c->host_events.empty()) std::memcpy(out, c->host_events.data(), sizeof(uint32_t) * c->host_events.size());
-    return MCMC_OK;
-}
-
-int mcmc_part_next_colors(mcmc_ctx* c, void** dev_ptr, uint32_t* elem_bytes) {
-    if (!c || !dev_ptr) return fail(MCMC_E_ARG, "NULL argument");
-    DevState h{};
-    int rc = download_state(c, &h);
-    if (rc) return rc;
-    *dev_ptr = c->colors[(h.t + 1) & 1];
-    if (elem_bytes) *elem_bytes = 1;
-    return MCMC_OK;
-}
-
-int mcmc_part_commit(mcmc_ctx* c, uint64_t total_viol, const uint32_t* events, uint32_t n_events,
-                     int32_t* finished) {
-    if (!c || !finished) return fail(MCMC_E_ARG, "NULL argument");
-    MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    DevState h{};
-    int rc = download_state(c, &h);
-    if (rc) return rc;
-    const uint32_t t = h.t;
-    if (t < c->traj_cap) {
-        unsigned long long v = total_viol;
-        MCMC_HIP_TRY(hipMemcpyAsync(c->traj + t, &v, sizeof(v), hipMemcpyHostToDevice, c->stream));
-    }
-    const bool stop_cap = t == c->p.maxRip + 1;
-    if (stop_cap || total_viol <= c->z) {
-        h.done = 1;
-        h.iter = t;
-        h.maxIterReached = stop_cap;
-        h.finalViol = total_viol;
-        MCMC_HIP_TRY(hipMemcpyAsync(c->st, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
-        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
-        c->last.iter = t;
-        c->last.maxIterReached = stop_cap;
-        c->last.finalViol = total_viol;
-        c->last.trajLen = (uint64_t)t + 1;
-        c->last.glibcDraws = h.glibc_draws;
-        c->last.initDraws = c->initDraws;
-        *finished = 1;
-        return MCMC_OK;
-    }
-    if (n_events > 0) {
-        uint32_t pcap = 1;
-        while (pcap < c->ev_cap) pcap <<= 1;
-        if (n_events > pcap) {
-            // global event list larger than the local buffer: reallocate
-            (void)hipFree(c->events);
-            uint32_t p2 = 1;
-            while (p2 < n_events) p2 <<= 1;
-            MCMC_HIP_TRY(hipMalloc(&c->events, sizeof(uint32_t) * p2));
-            c->ev_cap = p2;
-        }
-        MCMC_HIP_TRY(hipMemcpyAsync(c->events, events, sizeof(uint32_t) * n_events, hipMemcpyHostToDevice, c->stream));
-    }
-    SweepArgs a = make_args(c, 0);
-    part_commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a, t, n_events);
+int mcmc_part_commit_async(mcmc_ctx* c) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    SweepArgs a = make_args(c, 1);
+    part_commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
     MCMC_HIP_TRY(hipGetLastError());
-    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
-    *finished = 0;
+    return MCMC_OK;
+}
+
+int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    if (done) *done = (int32_t)h.done;
+    if (t) *t = h.t;
+    if (err) *err = h.err;
+    if (h.done) {
+        c->last.iter = h.iter;
+        c->last.maxIterReached = (int32_t)h.maxIterReached;
+        c->last.finalViol = h.finalViol;
+        c->last.trajLen = (uint64_t)h.iter + 1;
+        c->last.sweepsRun = h.iter + 1;
+    } else {
+        c->last.iter = h.t;
+        c->last.trajLen = h.t;
+        c->last.finalViol = ~0ull;
+    }
+    c->last.glibcDraws = h.glibc_draws;
+    c->last.initDraws = c->initDraws;
+    for (int i = 0; i < 31; i++) c->glibc.r[i] = h.glibc_ring[(h.glibc_head + i) % 31];
     return MCMC_OK;
 }
 

@@ -204,3 +204,71 @@ def test_c2_full_run_matches_golden(M):
     assert sha(col.coloring()) == d["colors_sha256"]
     assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws) == (
         d["iter"], d["maxIterReached"], d["finalViol"], d["glibcDraws"])
+
+
+def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, draws=None):
+    """`world` HipRank backends on one GPU, exchanged by tensor copies in lock-step: the device
+    side of the partitioned protocol (footer pack, all-gather layout, rank-ordered replay)."""
+    import torch
+
+    from mcmc_colorer_amd.distributed import HipRank
+
+    n = len(off) - 1
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, epsilon=eps, maxRip=maxRip, tabooIteration=taboo)
+    ranks = [HipRank(g, params, seed, world, r, torch.device("cuda", 0)) for r in range(world)]
+    for b in ranks:
+        b.init(seed, M.GlibcRand(1, n * (n + 1) // 2 if draws is None else draws))
+    t = 0
+    while t < maxRip + 2:
+        for b in ranks:
+            b.sweep()
+        slabs = torch.cat([b.slab(t)[1] for b in ranks])
+        foot = torch.cat([b.footer for b in ranks])
+        for b in ranks:
+            b.slab(t)[0][: world * b.S].copy_(slabs)
+            b.footers_all.copy_(foot)
+        for b in ranks:
+            b.commit()
+        t += 1
+        if ranks[0].state()[0]:
+            break
+    return ranks
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", [(3000, 0.02, 16, 41, 1e-8, 0, 40),
+                                                            (1500, 0.3, 5, 42, 3.3e6, 2, 12)])
+def test_partitioned_lockstep(M, world, n, p, ncol, seed, eps, taboo, maxrip):
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
+    ranks = _lockstep(M, off, idx, nc, seed, world, eps=eps, taboo=taboo, maxRip=maxrip)
+    for b in ranks:
+        assert b.state()[0]
+        assert b.coloring().tolist() == r.colors.tolist()
+        assert b.trajectory().tolist() == r.traj.tolist()
+
+
+def test_partitioned_driver_nccl_world1(M):
+    """The real driver over torch.distributed 'nccl' (RCCL), world_size 1."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from mcmc_colorer_amd.distributed import PartitionedColoringMCMC
+
+    n, p, ncol, seed = 2000, 0.05, 12, 43
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, maxRip=250)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        g = M.Graph.from_csr(off, idx)
+        drv = PartitionedColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1, n * (n + 1) // 2)),
+                                      M.ColoringMCMCParams(nCol=nc))
+        drv.run(0)
+        assert drv.coloring().tolist() == r.colors.tolist()
+        assert drv.trajectory().tolist() == r.traj.tolist()
+    finally:
+        dist.destroy_process_group()
