@@ -143,6 +143,29 @@ int stats_from_offsets(GraphDev& g) {
 }
 
 }  // namespace
+
+int sort_rows_inplace(GraphDev& g) {
+    if (g.sorted || g.m == 0) { g.sorted = true; return MCMC_OK; }
+    if (g.m >= (1ull << 31)) return fail(MCMC_E_ARG, "sort_rows_inplace: more than 2^31 arcs");
+    MCMC_HIP_TRY(hipSetDevice(g.device));
+    uint32_t* sorted = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    MCMC_HIP_TRY(hipMalloc(&sorted, sizeof(uint32_t) * (g.m + 4)));
+    MCMC_HIP_TRY(hipMemset(sorted, 0, sizeof(uint32_t) * (g.m + 4)));
+    MCMC_HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tmp_bytes, g.col_idx, sorted, (int)g.m, (int)g.n,
+                                                            g.row_off, g.row_off + 1));
+    MCMC_HIP_TRY(hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 1)));
+    MCMC_HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tmp_bytes, g.col_idx, sorted, (int)g.m, (int)g.n,
+                                                            g.row_off, g.row_off + 1));
+    MCMC_HIP_TRY(hipDeviceSynchronize());
+    (void)hipFree(tmp);
+    (void)hipFree(g.col_idx);
+    g.col_idx = sorted;
+    g.sorted = true;
+    return MCMC_OK;
+}
+
 }  // namespace mcmc
 
 using namespace mcmc;
@@ -170,11 +193,14 @@ int mcmc_graph_upload(const uint64_t* row_off, const uint32_t* col_idx, uint32_t
     }
     g->g.maxDeg = 0;
     g->g.minDeg = n;
+    bool sorted = true;
     for (uint32_t v = 0; v < n; v++) {
         const uint32_t d = (uint32_t)(row_off[v + 1] - row_off[v]);
         g->g.maxDeg = std::max(g->g.maxDeg, d);
         g->g.minDeg = std::min(g->g.minDeg, d);
+        for (uint64_t k = row_off[v] + 1; sorted && k < row_off[v + 1]; k++) sorted = col_idx[k - 1] <= col_idx[k];
     }
+    g->g.sorted = sorted;
     *out = g;
     return MCMC_OK;
 }
@@ -273,6 +299,7 @@ int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device,
     cleanup();
     rc = stats_from_offsets(g->g);
     if (rc) { mcmc_graph_destroy(g); return rc; }
+    g->g.sorted = true;
     // advance the caller's glibc stream past the generator's draws, as the reference's is
     GlibcWindow w;
     std::memcpy(w.r, window, sizeof(w.r));

@@ -27,9 +27,13 @@ struct GraphDev {
     uint32_t n = 0;
     uint64_t m = 0;
     uint32_t maxDeg = 0, minDeg = 0;
+    bool sorted = false;           // every neighbour list ascending
     uint64_t* row_off = nullptr;   // [n+1]
     uint32_t* col_idx = nullptr;   // [m]
 };
+
+// Sorts every neighbour list ascending on the device, in place (graph.hip).
+int sort_rows_inplace(GraphDev& g);
 
 }  // namespace mcmc
 

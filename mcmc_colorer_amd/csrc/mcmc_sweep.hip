@@ -84,6 +84,10 @@ struct SweepArgs {
     const uint32_t* footers_all;// partitioned: all ranks' footers after the all-gather
     uint32_t world;
     uint32_t lds_sort_cap;      // words of the sweep kernel's dynamic LDS reusable by the commit sort
+    const uint32_t* seg;        // blocked: per-(block, local row) segment offsets, (nb+1) x nloc
+    uint32_t nblocks;           // blocked: column blocks of 2^block_log2 vertices
+    uint32_t block_log2;        // blocked: log2 of the column block (17: 128 KiB of uint8 colours)
+    uint32_t chunk_rows;        // blocked: rows whose masks a workgroup keeps in LDS at once
 };
 
 __constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
@@ -425,16 +429,156 @@ __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* 
 constexpr int kPassU = MCMC_PASS_U;          // dwordx4 loads per lane per pass
 constexpr uint32_t kPassArcs = 256u * kPassU;
 
+// Streams the CSR rows of one wave tile and leaves the occupancy mask of row j in lane j's `acc`.
+// Lane j < cnt holds its row's arc range [rb, re) relative to `tcol` (a 16-B aligned, wave-uniform
+// base). Rows are read in passes of 64 lanes x U dwordx4; the next pass is issued before the
+// current one is consumed; loads are clamped instead of branched (countable vmcnt); every loaded
+// word is a valid vertex id (rows are contiguous, the array tail is zero-padded), so all 4U colour
+// gathers issue unmasked -- Cg[(w - gbase) & gmask] -- and a per-quad row mask gates the merge.
+template <int NW>
+__device__ __forceinline__ void scan_tile(const uint32_t* __restrict__ tcol, const uint8_t* __restrict__ Cg,
+                                          uint32_t gbase, uint32_t gmask, uint32_t rb, uint32_t re,
+                                          uint32_t cnt, int lane, uint32_t (&acc)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NW; i++) acc[i] = 0;
+    uint32_t j = 0, pbeg = 0, pend = 0;
+    while (j < cnt) {   // first non-empty row
+        pbeg = __builtin_amdgcn_readlane(rb, j);
+        pend = __builtin_amdgcn_readlane(re, j);
+        if (pend > pbeg) break;
+        j++;
+    }
+    uint32_t pbase = pbeg & ~3u;
+    uint4 cur[kPassU];
+#pragma unroll
+    for (int u = 0; u < kPassU; u++) {
+        const uint32_t q = min(pbase + 256u * u + 4u * lane, (pend - 1u) & ~3u);
+        cur[u] = *reinterpret_cast<const uint4*>(tcol + (j < cnt ? q : 0u));
+    }
+    uint32_t m[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) m[i] = 0;
+
+    while (j < cnt) {
+        // next pass (wave-uniform): same row, or the next non-empty row of the tile
+        uint32_t nj = j, nbeg = pbeg, nend = pend, nbase = pbase + kPassArcs;
+        const bool row_done = nbase >= pend;
+        if (row_done) {
+            nj = j + 1;
+            while (nj < cnt) {
+                nbeg = __builtin_amdgcn_readlane(rb, nj);
+                nend = __builtin_amdgcn_readlane(re, nj);
+                if (nend > nbeg) break;
+                nj++;
+            }
+            nbase = nbeg & ~3u;
+            if (nj >= cnt) { nbeg = pbeg; nend = pend; nbase = pbase; }   // nothing left: re-read (hits)
+        }
+        uint4 nxt[kPassU];
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) {
+            const uint32_t q = min(nbase + 256u * u + 4u * lane, (nend - 1u) & ~3u);
+            nxt[u] = *reinterpret_cast<const uint4*>(tcol + q);
+        }
+        uint32_t qm[kPassU];
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) {
+            const int32_t q = (int32_t)(pbase + 256u * u + 4u * lane);
+            const int32_t lo = min(max((int32_t)pbeg - q, 0), 4);
+            const int32_t hi = min(max((int32_t)pend - q, 0), 4);
+            qm[u] = (0xFu << lo) & ((1u << hi) - 1u);
+        }
+        uint32_t cg[4 * kPassU];
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) {
+            cg[4 * u + 0] = Cg[(cur[u].x - gbase) & gmask];
+            cg[4 * u + 1] = Cg[(cur[u].y - gbase) & gmask];
+            cg[4 * u + 2] = Cg[(cur[u].z - gbase) & gmask];
+            cg[4 * u + 3] = Cg[(cur[u].w - gbase) & gmask];
+        }
+#pragma unroll
+        for (int i = 0; i < 4 * kPassU; i++) {
+            const uint32_t ok = (qm[i >> 2] >> (i & 3)) & 1u;
+            if (NW == 1) {
+                m[0] |= ok << cg[i];
+            } else {
+                const uint32_t c = cg[i];
+                const uint32_t bit = ok << (c & 31);
+#pragma unroll
+                for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
+            }
+        }
+        if (row_done) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                const uint32_t r = wave_or_uniform(m[i]);
+                acc[i] = ((uint32_t)lane == j) ? r : acc[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NW; i++) m[i] = 0;
+        }
+        j = nj;
+        pbeg = nbeg;
+        pend = nend;
+        pbase = nbase;
+#pragma unroll
+        for (int u = 0; u < kPassU; u++) cur[u] = nxt[u];
+    }
+}
+
+// Shared tail of every sweep kernel: Cviol per workgroup, then (fused) the last-arriving
+// workgroup runs the commit (single context) or packs this rank's footer (partitioned).
+// Fused protocol (MI355X_MICROARCH.md "Workgroup dispatch ... visibility"): every storing wave
+// drains its stores, the workgroup meets, lane 0 publishes Cviol, releases at agent scope and
+// arrives; the workgroup whose arrival is last acquires.
+struct TailShared {
+    uint32_t wg_viol, wg_last, t, E, err;
+    unsigned long long viol;
+};
+
+__device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, TailShared& sh, uint32_t wave_viol,
+                                           int lane, uint32_t* lds, uint32_t cap) {
+    if (lane == 0 && wave_viol) atomicAdd(&sh.wg_viol, wave_viol);
+    if (!a.fused) {
+        __syncthreads();
+        if (threadIdx.x == 0 && sh.wg_viol) atomicAdd(&st->viol, (unsigned long long)sh.wg_viol);
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (sh.wg_viol) atomicAdd(&st->viol, (unsigned long long)sh.wg_viol);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = atomicAdd(&st->arrive, 1u);
+        sh.wg_last = (prev == gridDim.x - 1) ? 1u : 0u;
+        if (sh.wg_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sh.t = st->t;
+            sh.viol = st->viol;
+            sh.E = st->ev_count;
+            sh.err = st->err;
+        }
+    }
+    __syncthreads();
+    if (!sh.wg_last) return;
+    if (a.fused == 1) commit_control(a, sh.t, sh.viol, sh.E, sh.err, lds, cap);
+    else pack_footer(a, sh.viol, sh.E, sh.err, lds, cap);
+}
+
+// The fused sweep (n fits LDS, or the L2-gather variant). Every wave owns a contiguous,
+// arc-balanced range of rows (wave_start, computed once per context) and walks it in tiles.
+// LDSC: the whole colour replica (n bytes) is first staged in LDS so the byte gathers never pull
+// cache lines through L1/L2 (1 persistent 1024-thread workgroup per CU).
 template <int NW, bool LDSC>
 __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     extern __shared__ uint4 sc_raw[];
-    __shared__ uint32_t wg_viol, wg_last;
+    __shared__ TailShared sh;
     __shared__ uint32_t sort_static[LDSC ? 1 : 2048];
-    __shared__ uint32_t sh_t, sh_E, sh_err;
-    __shared__ unsigned long long sh_viol;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
-    if (threadIdx.x == 0) wg_viol = 0;
+    if (threadIdx.x == 0) sh.wg_viol = 0;
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
@@ -457,151 +601,146 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
                 if (i < nq) sc_raw[i] = r[k];
             }
         }
-        __syncthreads();
         Cg = reinterpret_cast<const uint8_t*>(sc_raw);
     }
+    __syncthreads();   // colours staged, sh initialised
 
-    if (!LDSC) __syncthreads();   // wg_viol initialised (the LDS path synchronises above)
     const int lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t wbeg = a.wave_start[gw], wend = a.wave_start[gw + 1];
-    uint32_t wave_viol = 0;   // Cviol of this wave's rows; one L2 atomic per workgroup at the end
+    uint32_t wave_viol = 0;   // Cviol of this wave's rows
 
     for (uint32_t l0 = wbeg; l0 < wend; l0 += a.tile) {
         const uint32_t cnt = min(a.tile, wend - l0);
-        uint64_t myoff = 0;
-        if ((uint32_t)lane <= cnt) myoff = a.row_off[l0 + lane];
-        // tile-relative 32-bit arc positions from an aligned, wave-uniform base pointer
-        const uint64_t tb = readlane64(myoff, 0) & ~3ull;
-        const uint32_t* __restrict__ tcol = a.col_idx + tb;
-        const uint32_t myrel = (uint32_t)(myoff - tb);
-
+        uint64_t ob = 0, oe = 0;
+        if ((uint32_t)lane < cnt) {
+            ob = a.row_off[l0 + lane];
+            oe = a.row_off[l0 + lane + 1];
+        }
+        const uint64_t tb = readlane64(ob, 0) & ~3ull;   // tile-relative 32-bit arc positions
         uint32_t acc[NW];
-#pragma unroll
-        for (int i = 0; i < NW; i++) acc[i] = 0;
-
-        // first non-empty row
-        uint32_t j = 0, pbeg = 0, pend = 0;
-        while (j < cnt) {
-            pbeg = __builtin_amdgcn_readlane(myrel, j);
-            pend = __builtin_amdgcn_readlane(myrel, j + 1);
-            if (pend > pbeg) break;
-            j++;
-        }
-        uint32_t pbase = pbeg & ~3u;
-        // loads are unconditional: quads past the row end re-read the row's last quad (cache hit)
-        uint4 cur[kPassU];
-#pragma unroll
-        for (int u = 0; u < kPassU; u++) {
-            const uint32_t q = min(pbase + 256u * u + 4u * lane, (pend - 1u) & ~3u);
-            cur[u] = *reinterpret_cast<const uint4*>(tcol + (j < cnt ? q : 0u));
-        }
-        uint32_t m[NW];
-#pragma unroll
-        for (int i = 0; i < NW; i++) m[i] = 0;
-
-        while (j < cnt) {
-            // next pass (wave-uniform): same row, or the next non-empty row of the tile
-            uint32_t nj = j, nbeg = pbeg, nend = pend, nbase = pbase + kPassArcs;
-            const bool row_done = nbase >= pend;
-            if (row_done) {
-                nj = j + 1;
-                while (nj < cnt) {
-                    nbeg = __builtin_amdgcn_readlane(myrel, nj);
-                    nend = __builtin_amdgcn_readlane(myrel, nj + 1);
-                    if (nend > nbeg) break;
-                    nj++;
-                }
-                nbase = nbeg & ~3u;
-                if (nj >= cnt) { nbeg = pbeg; nend = pend; nbase = pbase; }   // nothing left: re-read (hits)
-            }
-            uint4 nxt[kPassU];
-#pragma unroll
-            for (int u = 0; u < kPassU; u++) {
-                const uint32_t q = min(nbase + 256u * u + 4u * lane, (nend - 1u) & ~3u);
-                nxt[u] = *reinterpret_cast<const uint4*>(tcol + q);
-            }
-            // consume the current pass: every word of a loaded quad is a valid vertex id (rows are
-            // contiguous and the array tail is zero-padded), so all 4*U gathers issue unmasked and
-            // back to back; the per-quad row mask only gates the bit merge.
-            uint32_t qm[kPassU];
-#pragma unroll
-            for (int u = 0; u < kPassU; u++) {
-                const int32_t q = (int32_t)(pbase + 256u * u + 4u * lane);
-                const int32_t lo = min(max((int32_t)pbeg - q, 0), 4);
-                const int32_t hi = min(max((int32_t)pend - q, 0), 4);
-                qm[u] = (0xFu << lo) & ((1u << hi) - 1u);
-            }
-            uint32_t cg[4 * kPassU];
-#pragma unroll
-            for (int u = 0; u < kPassU; u++) {
-                cg[4 * u + 0] = Cg[cur[u].x];
-                cg[4 * u + 1] = Cg[cur[u].y];
-                cg[4 * u + 2] = Cg[cur[u].z];
-                cg[4 * u + 3] = Cg[cur[u].w];
-            }
-#pragma unroll
-            for (int i = 0; i < 4 * kPassU; i++) {
-                const uint32_t ok = (qm[i >> 2] >> (i & 3)) & 1u;
-                if (NW == 1) {
-                    m[0] |= ok << cg[i];
-                } else {
-                    const uint32_t c = cg[i];
-                    const uint32_t bit = ok << (c & 31);
-#pragma unroll
-                    for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
-                }
-            }
-            if (row_done) {
-#pragma unroll
-                for (int i = 0; i < NW; i++) {
-                    const uint32_t r = wave_or_uniform(m[i]);
-                    acc[i] = ((uint32_t)lane == j) ? r : acc[i];
-                }
-#pragma unroll
-                for (int i = 0; i < NW; i++) m[i] = 0;
-            }
-            j = nj;
-            pbeg = nbeg;
-            pend = nend;
-            pbase = nbase;
-#pragma unroll
-            for (int u = 0; u < kPassU; u++) cur[u] = nxt[u];
-        }
+        scan_tile<NW>(a.col_idx + tb, Cg, 0u, 0xFFFFFFFFu, (uint32_t)(ob - tb), (uint32_t)(oe - tb), cnt, lane, acc);
         wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane);
     }
-    if (lane == 0 && wave_viol) atomicAdd(&wg_viol, wave_viol);
-    if (!a.fused) {
-        __syncthreads();
-        if (threadIdx.x == 0 && wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
-        return;
-    }
-    // Fused commit (MI355X_MICROARCH.md "Workgroup dispatch ... visibility"): every storing wave
-    // drains its stores, the workgroup meets, lane 0 publishes Cviol, releases at agent scope and
-    // arrives; the workgroup whose arrival is last acquires and runs the commit.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (wg_viol) atomicAdd(&st->viol, (unsigned long long)wg_viol);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t prev = atomicAdd(&st->arrive, 1u);
-        wg_last = (prev == gridDim.x - 1) ? 1u : 0u;
-        if (wg_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sh_t = st->t;
-            sh_viol = st->viol;
-            sh_E = st->ev_count;
-            sh_err = st->err;
+    sweep_tail(a, st, sh, wave_viol, lane, LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static,
+               LDSC ? a.lds_sort_cap : 2048u);
+}
+
+// Column-blocked sweep: for colour replicas larger than one workgroup's LDS (multi-GPU replicas,
+// n >= 159 Ki). Column block b = vertices [b*B, (b+1)*B) (B = 2^17 uint8 colours = 128 KiB of
+// LDS). Each workgroup owns an arc-balanced range of rows (wg_start) and takes it in chunks of R
+// rows whose occupancy masks live in LDS; for every column block it stages that colour slice in
+// LDS, and its waves pull 8-row tiles (LDS counter) and scan each row's block-b segment
+// (seg[b][row], rows ascending) with scan_tile, OR-ing into the chunk masks. After the last block
+// the chunk rows are evaluated exactly as in sweep_kernel.
+constexpr uint32_t kBlockLog2Max = 17;
+
+template <int NW>
+__global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
+    extern __shared__ uint4 lds_raw[];
+    __shared__ TailShared sh;
+    __shared__ uint32_t tile_ctr;
+    DevState* __restrict__ st = a.st;
+    if (a.check_done && st->done) return;
+    if (threadIdx.x == 0) sh.wg_viol = 0;
+    const uint32_t t = st->t;
+    const uint32_t x_t = st->x_t;
+    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
+    uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
+    const uint32_t B = 1u << a.block_log2;
+    uint8_t* sc = reinterpret_cast<uint8_t*>(lds_raw);
+    uint32_t* smask = reinterpret_cast<uint32_t*>(sc + B);
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const uint32_t R = a.chunk_rows;
+    const uint32_t nb = a.nblocks;
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint32_t gbeg = a.wave_start[blockIdx.x], gend = a.wave_start[blockIdx.x + 1];
+    uint32_t wave_viol = 0;
+
+    for (uint32_t c0 = gbeg; c0 < gend; c0 += R) {
+        const uint32_t cn = min(R, gend - c0);
+        for (uint32_t b = 0; b < nb; b++) {
+            __syncthreads();   // previous block's scans (or the previous chunk's evaluation) are done
+            if (b == 0)
+                for (uint32_t i = threadIdx.x; i < cn * NW; i += blockDim.x) smask[i] = 0;
+            // stage colour slice b (16-B chunks; the replica has >= 16 B of slack past n)
+            const uint32_t lo = b << a.block_log2;
+            const uint32_t bytes = min(B, ((a.n + 15u) & ~15u) - lo);
+            const uint4* __restrict__ src = reinterpret_cast<const uint4*>(C + lo);
+            for (uint32_t i0 = threadIdx.x; i0 < (bytes >> 4); i0 += 8u * blockDim.x) {
+                uint4 r[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t i = i0 + k * blockDim.x;
+                    r[k] = src[i < (bytes >> 4) ? i : 0u];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t i = i0 + k * blockDim.x;
+                    if (i < (bytes >> 4)) lds_raw[i] = r[k];
+                }
+            }
+            if (threadIdx.x == 0) tile_ctr = 0;
+            __syncthreads();
+            const uint32_t* __restrict__ segb = a.seg + (size_t)b * nloc;
+            const uint32_t* __restrict__ sege = a.seg + (size_t)(b + 1) * nloc;
+            for (;;) {
+                uint32_t tt = 0;
+                if (lane == 0) tt = atomicAdd(&tile_ctr, 1u);
+                tt = __builtin_amdgcn_readfirstlane(tt);
+                const uint32_t r0 = tt * 8u;
+                if (r0 >= cn) break;
+                const uint32_t cnt = min(8u, cn - r0);
+                const uint32_t l = c0 + r0 + (uint32_t)lane;
+                uint64_t ob = 0, oe = 0;
+                if ((uint32_t)lane < cnt) {
+                    const uint64_t rs = a.row_off[l];
+                    ob = rs + segb[l];
+                    oe = rs + sege[l];
+                }
+                const uint64_t tb = readlane64(a.row_off[c0 + r0], 0) & ~3ull;
+                uint32_t acc[NW];
+                scan_tile<NW>(a.col_idx + tb, sc, lo, B - 1u, (uint32_t)(ob - tb), (uint32_t)(oe - tb),
+                              cnt, lane, acc);
+                if ((uint32_t)lane < cnt) {
+#pragma unroll
+                    for (int i = 0; i < NW; i++) smask[(r0 + lane) * NW + i] |= acc[i];
+                }
+            }
+        }
+        __syncthreads();   // all blocks scanned: evaluate the chunk
+        for (uint32_t e0 = wid * 64u; e0 < cn; e0 += nwaves * 64u) {
+            const uint32_t cnt = min(64u, cn - e0);
+            uint32_t acc[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
+            wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, c0 + e0, cnt, acc, lane);
         }
     }
-    __syncthreads();
-    if (!wg_last) return;
-    uint32_t* lds = LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static;
-    const uint32_t cap = LDSC ? a.lds_sort_cap : 2048u;
-    if (a.fused == 1) commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, cap);
-    else pack_footer(a, sh_viol, sh_E, sh_err, lds, cap);
+    __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
+    sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), B / 4u);
+}
+
+// Segment offsets of every local row by column block: seg[b][l] = #neighbours of row l with id
+// < b*B (rows ascending), b = 0..nb. Thread per (block boundary, row) binary search.
+__global__ void segment_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
+                               uint32_t nloc, uint32_t nb, uint32_t block_log2, uint32_t* __restrict__ seg) {
+    const uint64_t total = (uint64_t)(nb + 1) * nloc;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = (uint32_t)(i / nloc), l = (uint32_t)(i % nloc);
+        const uint64_t rs = row_off[l], re = row_off[l + 1];
+        if (b == 0) { seg[i] = 0; continue; }
+        if (b == nb) { seg[i] = (uint32_t)(re - rs); continue; }
+        const uint64_t key = (uint64_t)b << block_log2;
+        uint64_t lo = rs, hi = re;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (col_idx[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        seg[i] = (uint32_t)(lo - rs);
+    }
 }
 
 // Arc-balanced static partition of the local rows over W waves: wave w starts at the first row
@@ -638,6 +777,15 @@ using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
 template <int NW, bool LDSC>
 void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
     sweep_kernel<NW, LDSC><<<g, b, lds, s>>>(a);
+}
+template <int NW>
+void launch_blocked(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
+    sweep_blocked_kernel<NW><<<g, b, lds, s>>>(a);
+}
+template <int NW>
+hipError_t allow_lds_blocked(size_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_blocked_kernel<NW>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 template <int NW, bool LDSC>
 hipError_t allow_lds(size_t bytes) {
@@ -681,6 +829,9 @@ struct mcmc_ctx {
     dim3 grid, block;
     size_t lds = 0;             // dynamic LDS of the sweep kernel (colour replica staging)
     uint32_t* wave_start = nullptr;
+    uint32_t* seg = nullptr;    // blocked variant: segment offsets
+    uint32_t nblocks = 0, block_log2 = 0, chunk_rows = 0;
+    int variant = 0;            // 0 LDS-staged, 1 column-blocked, 2 L2-gather
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     uint32_t world = 1, rank = 0;
@@ -733,6 +884,10 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
+    a.seg = c->seg;
+    a.nblocks = c->nblocks;
+    a.block_log2 = c->block_log2;
+    a.chunk_rows = c->chunk_rows;
     a.footer = c->footer;
     a.footers_all = c->footers_all;
     a.world = c->world;
@@ -821,27 +976,40 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     c->v_end = v_end;
     c->z = p->tailcut ? std::max<uint32_t>(50u, gd.n / 2000u) : 0u;   // :89-97
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
-    // Colour replica staged in LDS when it fits one workgroup's 160 KiB (n <= 163840).
+    // Variant: colour replica staged whole in LDS when it fits one workgroup (n <= ~159 Ki),
+    // otherwise column-blocked. Test knobs: MCMC_GATHER=lds|blocked|global, MCMC_BLOCK_LOG2=k.
     const size_t lds_bytes = (((size_t)gd.n + 15) / 16) * 16;
-    const char* fv = getenv("MCMC_FUSED_COMMIT");
-    c->fused = (fv && std::strcmp(fv, "0") == 0) ? 0 : 1;
-    // MCMC_GATHER=global forces the L2-gather variant (testing knob: covers both code paths).
     const char* gv = getenv("MCMC_GATHER");
-    const bool ldsc = lds_bytes <= kMaxLdsBytes && !(gv && std::strcmp(gv, "global") == 0);
-    static const SweepLaunch tab_lds[4] = {launch_sweep<1, true>, launch_sweep<2, true>, launch_sweep<4, true>,
-                                           launch_sweep<8, true>};
-    static const SweepLaunch tab_glb[4] = {launch_sweep<1, false>, launch_sweep<2, false>, launch_sweep<4, false>,
-                                           launch_sweep<8, false>};
+    const std::string gsel = gv ? gv : "";
+    c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : (lds_bytes <= kMaxLdsBytes ? 0 : 1);
+    if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 1;
     const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
-    c->sweep = ldsc ? tab_lds[wi] : tab_glb[wi];
-    if (ldsc) {
-        hipError_t ea = wi == 0 ? allow_lds<1, true>(lds_bytes) : wi == 1 ? allow_lds<2, true>(lds_bytes)
-                      : wi == 2 ? allow_lds<4, true>(lds_bytes) : allow_lds<8, true>(lds_bytes);
-        if (ea != hipSuccess) {
-            mcmc_destroy(c);
-            return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
-        }
+    hipError_t ea = hipSuccess;
+    if (c->variant == 0) {
+        static const SweepLaunch tab[4] = {launch_sweep<1, true>, launch_sweep<2, true>, launch_sweep<4, true>,
+                                           launch_sweep<8, true>};
+        c->sweep = tab[wi];
         c->lds = lds_bytes;
+        ea = wi == 0 ? allow_lds<1, true>(lds_bytes) : wi == 1 ? allow_lds<2, true>(lds_bytes)
+           : wi == 2 ? allow_lds<4, true>(lds_bytes) : allow_lds<8, true>(lds_bytes);
+    } else if (c->variant == 1) {
+        static const SweepLaunch tab[4] = {launch_blocked<1>, launch_blocked<2>, launch_blocked<4>, launch_blocked<8>};
+        c->sweep = tab[wi];
+        const char* bl = getenv("MCMC_BLOCK_LOG2");
+        c->block_log2 = bl ? (uint32_t)std::max(6, std::min((int)kBlockLog2Max, atoi(bl))) : kBlockLog2Max;
+        c->nblocks = (uint32_t)((((uint64_t)gd.n + 15) / 16 * 16 + (1ull << c->block_log2) - 1) >> c->block_log2);
+        c->chunk_rows = 4096u / c->nw;
+        c->lds = (size_t)(1u << c->block_log2) + (size_t)c->chunk_rows * c->nw * 4u;
+        ea = wi == 0 ? allow_lds_blocked<1>(c->lds) : wi == 1 ? allow_lds_blocked<2>(c->lds)
+           : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
+    } else {
+        static const SweepLaunch tab[4] = {launch_sweep<1, false>, launch_sweep<2, false>, launch_sweep<4, false>,
+                                           launch_sweep<8, false>};
+        c->sweep = tab[wi];
+    }
+    if (ea != hipSuccess) {
+        mcmc_destroy(c);
+        return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
     }
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, gd.device);
@@ -871,8 +1039,8 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         return fail(MCMC_E_NOMEM, std::string("allocation: ") + hipGetErrorString(e));
     }
     if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
-    // persistent grids; rows statically arc-balanced over all waves
-    if (ldsc) {
+    // persistent grids; rows statically arc-balanced over all waves (blocked: over workgroups)
+    if (c->variant != 2) {
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);
     } else {
@@ -880,7 +1048,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         c->grid = dim3((uint32_t)cus * 8u);
     }
     {
-        const uint32_t W = c->grid.x * (c->block.x / 64);
+        const uint32_t W = c->variant == 1 ? c->grid.x : c->grid.x * (c->block.x / 64);
         hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
         if (ew != hipSuccess) {
             mcmc_destroy(c);
@@ -891,6 +1059,26 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         if (ew != hipSuccess) {
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("partition: ") + hipGetErrorString(ew));
+        }
+    }
+    if (c->variant == 1) {
+        // segments need ascending rows (setupRnd2 graphs are; uploaded ones are sorted once, in
+        // place -- neighbour order does not affect the sweep)
+        if (!gd.sorted) {
+            int rs = sort_rows_inplace(const_cast<GraphDev&>(gd));
+            if (rs) { mcmc_destroy(c); return rs; }
+        }
+        const size_t segn = (size_t)(c->nblocks + 1) * std::max<uint32_t>(nloc, 1);
+        hipError_t es = hipMalloc(&c->seg, sizeof(uint32_t) * segn);
+        if (es == hipSuccess) {
+            const uint32_t blocks = (uint32_t)std::min<size_t>((segn + 255) / 256, 65536);
+            segment_kernel<<<blocks, 256, 0, c->stream>>>(gd.row_off + v_begin, gd.col_idx, nloc, c->nblocks,
+                                                          c->block_log2, c->seg);
+            es = hipStreamSynchronize(c->stream);
+        }
+        if (es != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("segments: ") + hipGetErrorString(es));
         }
     }
     *out = c;
@@ -1102,6 +1290,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->st);
     (void)hipFree(c->traj);
     (void)hipFree(c->wave_start);
+    (void)hipFree(c->seg);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -100,6 +100,7 @@ class HipRank:
         return out
 
     def trajectory(self) -> np.ndarray:
+        self.state()   # refreshes the context's run summary (trajectory length) from the device
         k = ctypes.c_uint64()
         check(lib().mcmc_get_trajectory(self._ctx, None, 0, ctypes.byref(k)))
         out = np.zeros(k.value, dtype=np.uint64)

@@ -136,13 +136,18 @@ def circulant(n, K):
     return off, idx.ravel()
 
 
-@pytest.mark.parametrize("gather", ["lds", "global"])
+@pytest.mark.parametrize("gather", ["lds", "global", "blocked:17", "blocked:8", "blocked:6"])
 @pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", [(3000, 0.02, 16, 31, 1e-8, 0, 60),
                                                             (2000, 0.05, 100, 32, 1e-8, 2, 20),
-                                                            (1500, 0.3, 5, 33, 3.3e6, 1, 15)])
-def test_both_gather_variants(M, monkeypatch, gather, n, p, ncol, seed, eps, taboo, maxrip):
-    """The LDS-staged and the L2-gather sweep kernels give the same bit-exact results."""
-    monkeypatch.setenv("MCMC_GATHER", gather)
+                                                            (1500, 0.3, 5, 33, 3.3e6, 1, 15),
+                                                            (2500, 0.1, 200, 34, 1e-8, 0, 10)])
+def test_all_gather_variants(M, monkeypatch, gather, n, p, ncol, seed, eps, taboo, maxrip):
+    """LDS-staged, L2-gather and column-blocked sweeps (down to 64-vertex blocks, i.e. dozens of
+    column blocks and many chunks) give the same bit-exact results."""
+    var, _, blog = gather.partition(":")
+    monkeypatch.setenv("MCMC_GATHER", var)
+    if blog:
+        monkeypatch.setenv("MCMC_BLOCK_LOG2", blog)
     off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
     col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo)
     assert_same(col, st, r)
@@ -272,3 +277,44 @@ def test_partitioned_driver_nccl_world1(M):
         assert drv.trajectory().tolist() == r.traj.tolist()
     finally:
         dist.destroy_process_group()
+
+
+def test_blocked_unsorted_upload(M, monkeypatch):
+    """Uploaded rows in arbitrary order (as --graph produces) are sorted once for the blocked
+    variant; the result is unchanged (the sweep is order-independent)."""
+    monkeypatch.setenv("MCMC_GATHER", "blocked")
+    monkeypatch.setenv("MCMC_BLOCK_LOG2", "7")
+    n, p, ncol, seed = 2000, 0.05, 9, 51
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, maxRip=40)
+    rnd = np.random.default_rng(0)
+    shuf = idx.copy()
+    for v in range(n):
+        seg = shuf[off[v]:off[v + 1]]
+        rnd.shuffle(seg)
+    col, st, _ = gpu_run(M, off, shuf, nc, seed, n * (n + 1) // 2, maxRip=40)
+    assert_same(col, st, r)
+
+
+@pytest.mark.parametrize("blog", ["15", "12"])
+def test_c2_blocked_matches_golden(M, monkeypatch, blog):
+    """configs[1] full run through the column-blocked kernel (4 and 25 column blocks)."""
+    monkeypatch.setenv("MCMC_GATHER", "blocked")
+    monkeypatch.setenv("MCMC_BLOCK_LOG2", blog)
+    d = json.loads((GOLDEN / "c2.json").read_text())
+    rng = M.GlibcRand(1)
+    g = M.Graph.simulate(d["n"], d["prob"], rng)
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, d["seed"], rng), M.ColoringMCMCParams(nCol=d["nCol"]))
+    st = col.run(0)
+    assert col.trajectory().tolist() == d["traj"]
+    assert sha(col.coloring()) == d["colors_sha256"]
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_partitioned_lockstep_blocked(M, monkeypatch, world):
+    monkeypatch.setenv("MCMC_GATHER", "blocked")
+    monkeypatch.setenv("MCMC_BLOCK_LOG2", "9")
+    off, idx, nc, r = oracle_case(3000, 0.03, 20, 61, maxRip=30)
+    ranks = _lockstep(M, off, idx, nc, 61, world, maxRip=30)
+    for b in ranks:
+        assert b.coloring().tolist() == r.colors.tolist()
+        assert b.trajectory().tolist() == r.traj.tolist()
