@@ -12,8 +12,11 @@ Prints ONE JSON line (rank 0). Besides the driver contract fields it carries
                  PMC HBM bytes per launch from the committed rocprofv3 summary, when present
   cpu_baseline : the oracle (faithful single-thread restatement of --mcmccpu, kind "port") timed on
                  this host on a bounded number of sweeps of the same graph
-Multi-GPU (torchrun, one process per GPU): each rank sweeps its own replica of the workload
-(replicas only, "weak" scaling) -- the vertex-partitioned RCCL path is reported separately.
+Multi-GPU (torchrun, one process per GPU, RCCL): the vertex-partitioned sweep with its per-sweep
+exchange (all-gather of colour slabs + footers, mcmc_colorer_amd/distributed.py). Weak scaling by
+default: N GPUs sweep `--simulate (0.01/N) -n (N*1e5)` -- every GPU owns 1e5 rows of mean degree
+~1000, the configs[1] shape, and N=1 is exactly configs[1]. `--scaling strong` keeps configs[1]
+fixed and splits it.
 """
 from __future__ import annotations
 
@@ -85,13 +88,15 @@ def main() -> int:
     ap.add_argument("--ncol", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or a.force_dist:
         import torch
         import torch.distributed as dist
 
@@ -102,18 +107,16 @@ def main() -> int:
     from mcmc_colorer_amd._lib import check, lib
 
     dev = local
+    n_req, p_req = a.n, a.prob
+    if world > 1 and a.scaling == "weak":
+        n_req, p_req = a.n * world, a.prob / world
     t_gen = time.perf_counter()
     rng = M.GlibcRand(1)
-    window0 = rng.window.copy()
-    g = M.Graph.simulate(a.n, a.prob, rng, device=dev)
+    g = M.Graph.simulate(n_req, p_req, rng, device=dev)
     t_gen = time.perf_counter() - t_gen
-    params = M.ColoringMCMCParams(nCol=a.ncol)
-    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
-    col.init(0)
+    params = M.ColoringMCMCParams(nCol=a.ncol, maxRip=0x7FFFFFF0)   # throughput mode: no cap
     tot = ctypes.c_double()
     ker = ctypes.c_double()
-    if a.warmup:
-        check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
 
     def barrier():
         if dist is not None:
@@ -122,22 +125,46 @@ def main() -> int:
             torch.cuda.synchronize()
             dist.barrier()
 
-    barrier()
-    t0 = time.perf_counter()
-    check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
-    barrier()
-    wall = time.perf_counter() - t0
-    if dist is not None:
+    if dist is None:
+        col = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
+        col.init(0)
+        if a.warmup:
+            check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
+        check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
+        t0 = time.perf_counter()
+        check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
+        wall = time.perf_counter() - t0
+        kernel_ms = ker.value
+    else:
         import torch
 
+        from mcmc_colorer_amd.distributed import PartitionedColoringMCMC
+
+        drv = PartitionedColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
+        drv.b.init(a.seed, rng)
+        for t in range(a.warmup):
+            drv._step(t)
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for t in range(a.warmup, a.warmup + a.steps):
+            drv._step(t)
+        ev1.record()
+        barrier()
+        wall = time.perf_counter() - t0
+        done, _, err = drv.b.state()
+        if err:
+            raise RuntimeError("device error flag during the partitioned bench")
+        kernel_ms = ev0.elapsed_time(ev1) / a.steps   # whole step per rank: sweep + exchange + commit
         w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
 
     n, m = g.nNodes, g.nEdges
-    value = world * n * a.steps / wall
-    kernel_ms = ker.value
-    b_alg = algorithmic_bytes(n, m)
+    value = n * a.steps / wall          # all ranks together update n vertices per sweep
+    # per-rank algorithmic bytes of the dominant kernel (its own rows' CSR + colours)
+    b_alg = algorithmic_bytes(n // world, m // world)
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9
     out = {
         "metric": "vertex-updates/sec per MCMC sweep",
@@ -148,22 +175,24 @@ def main() -> int:
         "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if (world == 1 or a.scaling == "weak") else "strong",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (reference --simulate generator replayed exactly on the GPU)",
-        "config": {"workload": f"--mcmcgpu --simulate {a.prob} -n {a.n} --nCol {a.ncol} --seed {a.seed}",
-                   "n": n, "arcs": m, "nCol": a.ncol, "parallelism": "replicas" if world > 1 else "single",
+        "config": {"workload": f"--mcmcgpu --simulate {p_req:g} -n {n_req} --nCol {a.ncol} --seed {a.seed}",
+                   "n": n, "arcs": m, "nCol": a.ncol,
+                   "parallelism": f"vertex-partitioned x{world} (RCCL all-gather per sweep)" if world > 1 else "single",
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("c2"),
-                     "kernel": "sweep_kernel", "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("c2") if world == 1 else None,
+                     "kernel": "sweep_kernel" if world == 1 else "sweep_blocked_kernel + exchange (per-rank step)",
+                     "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         s = g.getStruct()
         out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed,
-                                           M.GlibcRand(1, a.n * (a.n + 1) // 2).window, n)
+                                           M.GlibcRand(1, n_req * (n_req + 1) // 2).window, n)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -118,6 +118,9 @@ int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len)
  * stream. total_ms = device wall of the loop; sweep_kernel_ms = total / sweeps = average duration
  * of one launch of the (fused) sweep kernel, inter-launch gap included. */
 int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms);
+/* Captures and uploads the `sweeps`-launch graph ahead of mcmc_bench_sweeps (keeps graph
+ * instantiation out of a host-timed region). */
+int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps);
 void mcmc_destroy(mcmc_ctx* c);
 
 /* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------

@@ -37,6 +37,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_coloring": (c_int, [c_void_p, _u32p]),
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
+    "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
     "mcmc_destroy": (None, [c_void_p]),
     "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                  c_void_p]),

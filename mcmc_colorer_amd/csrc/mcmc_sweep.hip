@@ -817,6 +817,8 @@ struct mcmc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipGraphExec_t batch_exec = nullptr;
+    hipGraphExec_t bench_exec = nullptr;   // mcmc_bench_prepare
+    uint32_t bench_n = 0;
     bool borrowed_stream = false;
     uint32_t batch = 0;
     GlibcWindow glibc{};
@@ -1239,38 +1241,46 @@ int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len)
     return MCMC_OK;
 }
 
-int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
+int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
-    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
     if (sweeps == 0) return fail(MCMC_E_ARG, "sweeps must be > 0");
+    if (c->bench_exec && c->bench_n == sweeps) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
     // Throughput mode: the loop body with the stop tests disabled (no cap; z = 0 stops only on a
-    // proper colouring). The `sweeps` launches are captured into one hipGraph and replayed between
-    // two events on the sweep stream: total = wall of the device loop, per-launch average = total
-    // / sweeps (each launch is one fused sweep; the average includes the inter-launch gap).
+    // proper colouring), `sweeps` launches captured into one hipGraph.
     SweepArgs a = make_args(c, 1);
     a.maxRip = 0xFFFFFFF0u;
     a.traj_cap = 0;
-    c->ran = true;
     hipGraph_t graph;
-    hipGraphExec_t exec = nullptr;
     MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     for (uint32_t i = 0; i < sweeps; i++) launch_pair(c, a);
     MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
-    hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    hipError_t e = hipGraphInstantiate(&c->bench_exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    MCMC_HIP_TRY(hipGraphUpload(exec, c->stream));
+    MCMC_HIP_TRY(hipGraphUpload(c->bench_exec, c->stream));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    c->bench_n = sweeps;
+    return MCMC_OK;
+}
+
+int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
+    int rc = mcmc_bench_prepare(c, sweeps);   // no-op when already prepared for `sweeps`
+    if (rc) return rc;
+    c->ran = true;
+    // one graph replay between two events on the sweep stream: total = device wall of the loop,
+    // per-launch average = total / sweeps (each launch is one fused sweep, gap included)
     MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    MCMC_HIP_TRY(hipGraphLaunch(exec, c->stream));
+    MCMC_HIP_TRY(hipGraphLaunch(c->bench_exec, c->stream));
     MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
     MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
     float tot = 0;
     MCMC_HIP_TRY(hipEventElapsedTime(&tot, c->ev0, c->ev1));
-    (void)hipGraphExecDestroy(exec);
     DevState h{};
-    int rc = download_state(c, &h);
+    rc = download_state(c, &h);
     if (rc) return rc;
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
@@ -1283,6 +1293,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipSetDevice(c->g->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->batch_exec) (void)hipGraphExecDestroy(c->batch_exec);
+    if (c->bench_exec) (void)hipGraphExecDestroy(c->bench_exec);
     (void)hipFree(c->own_colors[0]);
     (void)hipFree(c->own_colors[1]);
     (void)hipFree(c->taboo);
