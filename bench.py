@@ -36,20 +36,18 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def algorithmic_bytes(n: int, m: int, taboo: bool = False) -> int:
-    """Bytes one sweep must move at minimum in this build's layout (DESIGN.md "Roofline"):
-    uint64 row offsets, uint32 neighbour ids, uint8 colour read + write (+ uint32 taboo r/w)."""
-    return 8 * (n + 1) + 4 * m + n + n + (8 * n if taboo else 0)
+KERNELS = {"lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
+           "tiled": "sweep_tiled_kernel"}
 
 
-def load_traffic(config: str):
-    """HBM bytes per sweep_kernel launch from the committed rocprofv3 PMC summary (or None)."""
+def load_traffic(key: str):
+    """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary (or None)."""
     p = ROOT / "profiles" / "pmc_summary.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        return d.get(config, {}).get("hbm_bytes_per_launch")
+        return d.get(key, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -90,7 +88,15 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
+    ap.add_argument("--variant", default=None,
+                    help="sweep kernel: lds | tiled | blocked | global[:block_log2[:lanes_log2[:group_rows"
+                         "[:stream]]]] (empty field / default: the library's choice)")
     a = ap.parse_args()
+    if a.variant:
+        for key, v in zip(("MCMC_GATHER", "MCMC_BLOCK_LOG2", "MCMC_SUB_LOG2", "MCMC_GROUP_ROWS",
+                           "MCMC_TILE_STREAM"), a.variant.split(":")):
+            if v:
+                os.environ[key] = v
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -135,6 +141,7 @@ def main() -> int:
         check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
         wall = time.perf_counter() - t0
         kernel_ms = ker.value
+        info = col.info()
     else:
         import torch
 
@@ -157,15 +164,20 @@ def main() -> int:
         if err:
             raise RuntimeError("device error flag during the partitioned bench")
         kernel_ms = ev0.elapsed_time(ev1) / a.steps   # whole step per rank: sweep + exchange + commit
+        info = drv.b.info()
         w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
 
     n, m = g.nNodes, g.nEdges
     value = n * a.steps / wall          # all ranks together update n vertices per sweep
-    # per-rank algorithmic bytes of the dominant kernel (its own rows' CSR + colours)
-    b_alg = algorithmic_bytes(n // world, m // world)
-    achieved = b_alg / (kernel_ms * 1e-3) / 1e9
+    # dominant kernel's bytes per launch on this rank: B_fmt of the layout it streams (SURVEY.md
+    # §8d: with a compressed format the fraction is taken against the format's bytes), and the
+    # same rows' B_alg in the reference's uint32 layout for comparison
+    b_fmt, b_ref = info["sweep_bytes"], info["ref_bytes"]
+    achieved = b_fmt / (kernel_ms * 1e-3) / 1e9
+    variant = info["variant"]
+    key = f"c2/{variant}" if (world == 1 and n_req == 100000) else None
     out = {
         "metric": "vertex-updates/sec per MCMC sweep",
         "value": value,
@@ -184,9 +196,11 @@ def main() -> int:
                    "parallelism": f"vertex-partitioned x{world} (RCCL all-gather per sweep)" if world > 1 else "single",
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic("c2") if world == 1 else None,
-                     "kernel": "sweep_kernel" if world == 1 else "sweep_blocked_kernel + exchange (per-rank step)",
-                     "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,
+                     "kernel": KERNELS.get(variant, variant) + ("" if world == 1 else " + exchange (per-rank step)"),
+                     "kernel_ms": kernel_ms, "algorithmic_bytes": b_fmt,
+                     "ref_layout_bytes": b_ref, "ref_layout_equiv_GBs": b_ref / (kernel_ms * 1e-3) / 1e9,
+                     "layout": info},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

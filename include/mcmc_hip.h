@@ -121,6 +121,28 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
 /* Captures and uploads the `sweeps`-launch graph ahead of mcmc_bench_sweeps (keeps graph
  * instantiation out of a host-timed region). */
 int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps);
+
+/* Sweep kernel and adjacency layout a context chose (no reference counterpart: the reference's
+ * sweep has one fixed CSR layout). sweep_bytes = B_fmt of SURVEY.md §8d, the HBM bytes one sweep
+ * of this context's rows must move in its layout (adjacency + offsets/segment tables + colour
+ * replica read once + local colour write [+ taboo r/w]); ref_bytes = the same rows' B_alg in the
+ * reference's uint32 layout (4(n+1) + 4m + 4n + 4n [+ 8n]). */
+typedef struct mcmc_ctx_info {
+    int32_t variant;          /* 0 LDS-staged CSR, 1 column-blocked CSR, 2 L2-gather CSR, 3 tiled */
+    int32_t resident;         /* tiled: whole colour replica LDS-resident (else streamed slices) */
+    uint32_t block_log2;      /* tiled / blocked: column block = 2^block_log2 vertices */
+    uint32_t nblocks;
+    uint32_t grp_rows;        /* tiled: rows per group */
+    uint32_t ngroups;
+    uint32_t sub_log2;        /* tiled: lanes per row segment = 2^sub_log2 */
+    uint32_t grid, block;     /* sweep launch geometry */
+    uint32_t reserved;
+    uint64_t lds_bytes;       /* dynamic LDS per workgroup */
+    uint64_t layout_bytes;    /* device bytes of the adjacency layout the sweep streams */
+    uint64_t sweep_bytes;     /* B_fmt per sweep */
+    uint64_t ref_bytes;       /* B_alg per sweep, reference uint32 layout */
+} mcmc_ctx_info;
+int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out);
 void mcmc_destroy(mcmc_ctx* c);
 
 /* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------

@@ -38,6 +38,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
+    "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
     "mcmc_destroy": (None, [c_void_p]),
     "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
                                  c_void_p]),
@@ -75,6 +76,33 @@ class MCMCRunStats(ctypes.Structure):
         ("sweepsRun", c_uint32),
         ("reserved", c_uint32),
     ]
+
+
+class MCMCCtxInfo(ctypes.Structure):
+    _fields_ = [
+        ("variant", c_int32),
+        ("resident", c_int32),
+        ("block_log2", c_uint32),
+        ("nblocks", c_uint32),
+        ("grp_rows", c_uint32),
+        ("ngroups", c_uint32),
+        ("sub_log2", c_uint32),
+        ("grid", c_uint32),
+        ("block", c_uint32),
+        ("reserved", c_uint32),
+        ("lds_bytes", c_uint64),
+        ("layout_bytes", c_uint64),
+        ("sweep_bytes", c_uint64),
+        ("ref_bytes", c_uint64),
+    ]
+
+    VARIANTS = {0: "lds", 1: "blocked", 2: "global", 3: "tiled"}
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        d["variant"] = self.VARIANTS.get(self.variant, str(self.variant))
+        d["resident"] = bool(self.resident)
+        return d
 
 
 class MCMCError(RuntimeError):

@@ -22,7 +22,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import MCMCParams, MCMCRunStats, check, lib, u32ptr, u64ptr
+from ._lib import MCMCCtxInfo, MCMCParams, MCMCRunStats, check, lib, u32ptr, u64ptr
 
 F32_EPS = float(np.float32(1e-8))
 
@@ -225,6 +225,15 @@ class ColoringMCMC:
         if n.value:
             check(lib().mcmc_get_trajectory(self._ctx, u64ptr(out), n.value, ctypes.byref(n)))
         return out
+
+    def info(self) -> dict:
+        """Sweep kernel / adjacency layout of the current context and its bytes per sweep
+        (mcmc_get_info: B_fmt and the reference-layout B_alg of SURVEY.md §8d)."""
+        if not self._ctx:
+            self.init(0)
+        i = MCMCCtxInfo()
+        check(lib().mcmc_get_info(self._ctx, ctypes.byref(i)))
+        return i.as_dict()
 
     def save(self, iteration: int) -> None:
         d = self.directory

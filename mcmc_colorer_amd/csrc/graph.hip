@@ -338,6 +338,7 @@ int mcmc_graph_download(const mcmc_graph* g, uint64_t* row_off, uint32_t* col_id
 void mcmc_graph_destroy(mcmc_graph* g) {
     if (!g) return;
     (void)hipSetDevice(g->g.device);
+    g->tiles.clear();
     (void)hipFree(g->g.row_off);
     (void)hipFree(g->g.col_idx);
     delete g;

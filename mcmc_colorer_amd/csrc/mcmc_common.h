@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <string>
+#include <vector>
 
 #include "../../include/mcmc_hip.h"
 
@@ -37,6 +39,21 @@ int sort_rows_inplace(GraphDev& g);
 
 }  // namespace mcmc
 
+namespace mcmc {
+// Tiled copy of a row range of the CSR (sweep variant 3, mcmc_sweep.hip): rows in groups of
+// grp_rows, per group the arcs block-major as 16-bit block-local ids, every (row, block) segment
+// padded to a multiple of 8 ids. Cached on the graph, so contexts re-created per repetition reuse it.
+struct TiledLayout {
+    uint32_t v_begin = 0, v_end = 0, grp_rows = 0, block_log2 = 0, nblocks = 0, ngroups = 0;
+    uint64_t ids = 0;              // padded length of tcol
+    uint16_t* tcol = nullptr;
+    uint64_t* gbase = nullptr;     // [ngroups + 1]
+    uint32_t* tseg = nullptr;      // [ngroups][nblocks][grp_rows + 1]
+    ~TiledLayout();
+};
+}  // namespace mcmc
+
 struct mcmc_graph {
     mcmc::GraphDev g;
+    std::vector<std::unique_ptr<mcmc::TiledLayout>> tiles;   // freed with the graph
 };

@@ -22,6 +22,8 @@
 //
 // Compiled with -ffp-contract=off: fill_p's products and quotients must round exactly as the
 // reference's SSE code (no FMA), and fp32 division stays IEEE-correct (hipcc default).
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -88,6 +90,14 @@ struct SweepArgs {
     uint32_t nblocks;           // blocked: column blocks of 2^block_log2 vertices
     uint32_t block_log2;        // blocked: log2 of the column block (17: 128 KiB of uint8 colours)
     uint32_t chunk_rows;        // blocked: rows whose masks a workgroup keeps in LDS at once
+    // tiled layout (variant 3): rows in groups of grp_rows; per group, arcs block-major, 16-bit
+    // block-local ids, every (row, block) segment padded to a multiple of 8 ids
+    const uint16_t* tcol;
+    const uint64_t* gbase;      // [ngroups + 1] group start in tcol (ids)
+    const uint32_t* tseg;       // [ngroups][nblocks][grp_rows + 1] segment start relative to gbase
+    uint32_t grp_rows, ngroups;
+    uint32_t sub_log2;          // lanes per row segment = 2^sub_log2
+    uint32_t slice_bytes;       // tiled: LDS bytes of the colour slice (masks follow it)
 };
 
 __constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
@@ -598,7 +608,7 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const uint32_t i = i0 + k * blockDim.x;
-                if (i < nq) sc_raw[i] = r[k];
+                sc_raw[i < nq ? i : 0u] = r[k];   // out-of-range lanes rewrite src[0] at 0: keeps the loads unconditional
             }
         }
         Cg = reinterpret_cast<const uint8_t*>(sc_raw);
@@ -678,7 +688,7 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const uint32_t i = i0 + k * blockDim.x;
-                    if (i < (bytes >> 4)) lds_raw[i] = r[k];
+                    lds_raw[i < (bytes >> 4) ? i : 0u] = r[k];
                 }
             }
             if (threadIdx.x == 0) tile_ctr = 0;
@@ -720,6 +730,333 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
     }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
     sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), B / 4u);
+}
+
+// Tiled sweep (variant 3). Group g = local rows [g*R, (g+1)*R); for every column block b the group's
+// row segments are contiguous in `tcol` (16-bit block-local ids, each segment padded to whole
+// quads of 8 ids), so a dwordx4 load is 8 valid ids of one row. Workgroups take groups
+// round-robin. Resident mode (the whole colour replica fits LDS): the replica is staged once and
+// block b is the LDS window at b*B; otherwise (2 workgroups/CU) the block's 64 KiB colour slice is
+// staged per (group, block). Per block the waves split the group's rows; inside a wave, sub-groups
+// of L = 2^sub_log2 lanes walk one row segment each, kTileU quads per lane per step, loads for the
+// next step issued before the current step's LDS gathers; a finished segment is OR-reduced over
+// its L lanes and OR-ed into the row's LDS mask. After the last block the rows are evaluated.
+#ifndef MCMC_TILE_U
+#define MCMC_TILE_U 4
+#endif
+constexpr uint32_t kTileU = MCMC_TILE_U;   // quads per lane per step of the tiled scan
+
+template <int NW>
+__device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, const uint4& v, uint32_t okb,
+                                            uint32_t (&m)[NW]) {
+    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+    uint32_t cg[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        cg[2 * e] = sc[w8[e] & 0xFFFFu];
+        cg[2 * e + 1] = sc[w8[e] >> 16];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        if (NW == 1) {
+            m[0] |= okb << cg[e];
+        } else {
+            const uint32_t c = cg[e];
+            const uint32_t bit = okb << (c & 31);
+#pragma unroll
+            for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
+        }
+    }
+}
+
+// RES: the whole replica is LDS-resident (1024 threads, 1 workgroup/CU); otherwise a 64 KiB slice
+// per (group, block) (512 threads, 2 workgroups/CU). A workgroup walks its (group, block) pairs
+// in order; while it scans pair k, the colour slice (streaming mode) and segment table of pair
+// k+1 are already in flight into registers, and land in LDS after the scan's barrier.
+constexpr uint32_t kTileSegPer = 4;   // segment-table entries per thread per pair: R + 1 <= 4 * blockDim
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable 16 B
+template <bool RES>
+constexpr int kTileSlicePer = RES ? 1 : (65536 / 16) / 512;   // uint4 of a 64 KiB slice per thread
+
+// Issue the loads of pair (g, b)'s segment table (and streaming: colour slice) into registers.
+template <bool RES>
+__device__ __forceinline__ void tile_prefetch(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
+                                              uint32_t b, uint32_t nloc, uint32_t (&pseg)[kTileSegPer],
+                                              u32x4 (&pslice)[kTileSlicePer<RES>]) {
+    const uint32_t R = a.grp_rows;
+    const uint32_t rows = min(R, nloc - g * R);
+    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * (R + 1);
+#pragma unroll
+    for (uint32_t k = 0; k < kTileSegPer; k++) {
+        const uint32_t i = threadIdx.x + k * blockDim.x;
+        pseg[k] = gs[i <= rows ? i : 0u];
+    }
+    if (!RES) {
+        const uint32_t lo = b << a.block_log2;
+        const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
+        const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(C + lo);
+#pragma unroll
+        for (int k = 0; k < kTileSlicePer<RES>; k++) {
+            const uint32_t i = threadIdx.x + k * blockDim.x;
+            pslice[k] = src[i < nq16 ? i : 0u];
+        }
+    }
+}
+
+// Store the prefetched pair into LDS (after the barrier that ends the previous pair's scan).
+template <bool RES>
+__device__ __forceinline__ void tile_land(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
+                                          uint32_t* sseg, uint4* lds_raw, const uint32_t (&pseg)[kTileSegPer],
+                                          const u32x4 (&pslice)[kTileSlicePer<RES>]) {
+    const uint32_t R = a.grp_rows;
+    const uint32_t rows = min(R, nloc - g * R);
+#pragma unroll
+    for (uint32_t k = 0; k < kTileSegPer; k++) {
+        const uint32_t i = threadIdx.x + k * blockDim.x;
+        sseg[i <= rows ? i : 0u] = pseg[k];   // out-of-range threads rewrite entry 0 with its value
+    }
+    if (!RES) {
+        const uint32_t lo = b << a.block_log2;
+        const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
+#pragma unroll
+        for (int k = 0; k < kTileSlicePer<RES>; k++) {
+            const uint32_t i = threadIdx.x + k * blockDim.x;
+            reinterpret_cast<u32x4*>(lds_raw)[i < nq16 ? i : 0u] = pslice[k];
+        }
+    }
+}
+
+template <int NW, bool RES>
+__global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs a) {
+    extern __shared__ uint4 lds_raw[];
+    __shared__ TailShared sh;
+    DevState* __restrict__ st = a.st;
+    if (a.check_done && st->done) return;
+    if (threadIdx.x == 0) sh.wg_viol = 0;
+    const uint32_t t = st->t;
+    const uint32_t x_t = st->x_t;
+    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
+    uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
+    uint8_t* sc = reinterpret_cast<uint8_t*>(lds_raw);
+    const uint32_t R = a.grp_rows, nb = a.nblocks;
+    uint32_t* smask = reinterpret_cast<uint32_t*>(sc + a.slice_bytes);
+    uint32_t* sseg = smask + R * NW;   // [R + 1] segment starts of the pair being scanned
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const uint32_t L = 1u << a.sub_log2, nsub = 64u >> a.sub_log2;
+    const uint32_t sub = (uint32_t)lane >> a.sub_log2, li = (uint32_t)lane & (L - 1u);
+    const uint32_t step = 8u * L * kTileU;
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint32_t nbytes16 = (a.n + 15u) & ~15u;
+    uint32_t wave_viol = 0;
+
+    // prefetch registers: the next pair's segment table and (streaming mode) its colour slice
+    uint32_t pseg[kTileSegPer];
+    u32x4 pslice[kTileSlicePer<RES>];
+    uint32_t g = blockIdx.x, b = 0;
+    // (unconditional, clamped to a valid pair: keeps the scan loop's vmcnt accounting exact)
+    tile_prefetch<RES>(a, C, min(g, a.ngroups ? a.ngroups - 1u : 0u), 0, nloc, pseg, pslice);
+    if (RES) {   // whole replica once
+        const uint32_t nq16 = nbytes16 >> 4;
+        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(C);
+        for (uint32_t i0 = threadIdx.x; i0 < nq16; i0 += 8u * blockDim.x) {
+            uint4 r[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t i = i0 + k * blockDim.x;
+                r[k] = src[i < nq16 ? i : 0u];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t i = i0 + k * blockDim.x;
+                lds_raw[i < nq16 ? i : 0u] = r[k];   // (src[0] again at 0): loads stay unconditional
+            }
+        }
+    }
+    while (g < a.ngroups) {
+        const uint32_t r0 = g * R;
+        const uint32_t rows = min(R, nloc - r0);
+        const uint16_t* __restrict__ gcol = a.tcol + a.gbase[g];
+        const uint32_t q = (rows + nwaves - 1) / nwaves;
+        const uint32_t wr0 = min(rows, wid * q), wr1 = min(rows, wr0 + q);
+        __syncthreads();   // previous pair's scan (or the previous group's evaluation) is done
+        if (b == 0)
+            for (uint32_t i = threadIdx.x; i < rows * NW; i += blockDim.x) smask[i] = 0;
+        tile_land<RES>(a, g, b, nloc, sseg, lds_raw, pseg, pslice);
+        __syncthreads();
+        const uint32_t ng = (b + 1 < nb) ? g : g + gridDim.x, nbn = (b + 1 < nb) ? b + 1 : 0u;
+        tile_prefetch<RES>(a, C, ng < a.ngroups ? ng : g, ng < a.ngroups ? nbn : b, nloc, pseg, pslice);
+        const uint8_t* __restrict__ scb = RES ? sc + (b << a.block_log2) : sc;
+        // sub-group state: current row, this lane's next quad, the row's end (ids, from gbase)
+        uint32_t row = wr0 + sub, pos = 0, end = 0;
+        if (row < wr1) { pos = sseg[row] + 8u * li; end = sseg[row + 1]; }
+        uint4 v[kTileU];
+#pragma unroll
+        for (int u = 0; u < kTileU; u++) {
+            const uint32_t pu = pos + 8u * L * u;
+            v[u] = *reinterpret_cast<const uint4*>(gcol + ((row < wr1 && pu < end) ? pu : 0u));
+        }
+        uint32_t m[NW];
+#pragma unroll
+        for (int i = 0; i < NW; i++) m[i] = 0;
+        while (__ballot(row < wr1)) {
+            const bool act = row < wr1;
+            // next step's position (same row, or the sub-group's next row) and its loads first
+            uint32_t npos = pos + step, nrow = row, nend = end;
+            const bool fin = act && (npos - 8u * li >= end);
+            if (fin) {
+                nrow = row + nsub;
+                if (nrow < wr1) { npos = sseg[nrow] + 8u * li; nend = sseg[nrow + 1]; }
+            }
+            uint4 vn[kTileU];
+#pragma unroll
+            for (int u = 0; u < kTileU; u++) {
+                const uint32_t pu = npos + 8u * L * u;
+                vn[u] = *reinterpret_cast<const uint4*>(gcol + ((nrow < wr1 && pu < nend) ? pu : 0u));
+            }
+#pragma unroll
+            for (int u = 0; u < kTileU; u++)
+                tile_gather<NW>(scb, v[u], (act && pos + 8u * L * u < end) ? 1u : 0u, m);
+            if (__ballot(fin)) {
+                // OR over the L lanes of every sub-group (all lanes take part; only finished
+                // sub-groups use the result)
+                uint32_t red[NW];
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    uint32_t x = m[i];
+                    for (uint32_t off = 1; off < L; off <<= 1) x |= __shfl_xor(x, (int)off, 64);
+                    red[i] = x;
+                }
+                if (fin) {
+                    if (li == 0) {
+#pragma unroll
+                        for (int i = 0; i < NW; i++) atomicOr(&smask[row * NW + i], red[i]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < NW; i++) m[i] = 0;
+                }
+            }
+            row = nrow;
+            pos = npos;
+            end = nend;
+#pragma unroll
+            for (int u = 0; u < kTileU; u++) v[u] = vn[u];
+        }
+        if (b + 1 == nb) {
+            __syncthreads();   // all blocks scanned: every wave evaluates a share of the group's rows
+            for (uint32_t e0 = wid * min(q, 64u); e0 < rows; e0 += nwaves * min(q, 64u)) {
+                const uint32_t cnt = min(min(q, 64u), rows - e0);
+                uint32_t acc[NW];
+#pragma unroll
+                for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
+                wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, r0 + e0, cnt, acc, lane);
+            }
+        }
+        g = ng;
+        b = nbn;
+    }
+    __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
+    sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+}
+
+// ---- tiled layout construction (once per context) ----------------------------------------------
+// Padded (to 8 ids) total of every group over all blocks.
+__global__ void tile_group_total_kernel(const uint32_t* __restrict__ seg, uint32_t nloc, uint32_t nb, uint32_t R,
+                                        uint32_t G, uint64_t* __restrict__ totals) {
+    __shared__ unsigned long long red[256];
+    for (uint32_t g = blockIdx.x; g < G; g += gridDim.x) {
+        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
+        unsigned long long s = 0;
+        for (uint32_t i = threadIdx.x; i < rows * nb; i += blockDim.x) {
+            const uint32_t b = i / rows, r = i % rows;
+            const uint32_t len = seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r];
+            s += (len + 7u) & ~7u;
+        }
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (uint32_t k = blockDim.x / 2; k > 0; k >>= 1) {
+            if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) totals[g] = red[0];
+        __syncthreads();
+    }
+}
+
+// tseg[g][b][r] = padded start of row r's block-b segment relative to the group base; entry R of
+// every block = its end (= the next block's start). Block scan over the rows, blocks in order.
+__global__ void tile_seg_kernel(const uint32_t* __restrict__ seg, uint32_t nloc, uint32_t nb, uint32_t R,
+                                uint32_t G, uint32_t* __restrict__ tseg) {
+    __shared__ uint32_t part[256];
+    __shared__ uint32_t run_sh;
+    for (uint32_t g = blockIdx.x; g < G; g += gridDim.x) {
+        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
+        const uint32_t per = (R + blockDim.x - 1) / blockDim.x;   // consecutive rows per thread
+        if (threadIdx.x == 0) run_sh = 0;
+        __syncthreads();
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t ra = threadIdx.x * per, rb = min(R, ra + per);
+            uint32_t local = 0;
+            for (uint32_t r = ra; r < rb; r++) {
+                const uint32_t len = (r < rows) ? seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r] : 0u;
+                local += (len + 7u) & ~7u;
+            }
+            part[threadIdx.x] = local;
+            __syncthreads();
+            if (threadIdx.x == 0) {   // exclusive scan of the per-thread sums (blockDim <= 256)
+                uint32_t acc = 0;
+                for (uint32_t k = 0; k < blockDim.x; k++) { const uint32_t x = part[k]; part[k] = acc; acc += x; }
+            }
+            __syncthreads();
+            const uint32_t run = run_sh;
+            uint32_t* out = tseg + ((size_t)g * nb + b) * (R + 1);
+            uint32_t acc = run + part[threadIdx.x];
+            for (uint32_t r = ra; r < rb; r++) {
+                out[r] = acc;
+                const uint32_t len = (r < rows) ? seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r] : 0u;
+                acc += (len + 7u) & ~7u;
+            }
+            __syncthreads();
+            if (threadIdx.x == blockDim.x - 1) {
+                out[R] = acc;   // the last thread's running value is the block's end
+                run_sh = acc;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Scatter: wave per local row; every arc to its padded block segment as a 16-bit local id, then
+// each segment's padding filled with copies of its first id (OR-idempotent).
+__global__ void tile_scatter_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
+                                    const uint32_t* __restrict__ seg, const uint64_t* __restrict__ gbase,
+                                    const uint32_t* __restrict__ tseg, uint32_t nloc, uint32_t nb, uint32_t R,
+                                    uint32_t block_log2, uint16_t* __restrict__ tcol) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t bmask = (1u << block_log2) - 1u;
+    for (uint32_t l = gw; l < nloc; l += nw) {
+        const uint32_t g = l / R, r = l % R;
+        const uint64_t rs = row_off[l], re = row_off[l + 1];
+        const uint64_t base = gbase[g];
+        const uint32_t* ts = tseg + (size_t)g * nb * (R + 1);
+        for (uint64_t k = rs + lane; k < re; k += 64) {
+            const uint32_t c = col_idx[k];
+            const uint32_t b = c >> block_log2;
+            const uint32_t rel = (uint32_t)(k - rs) - seg[(size_t)b * nloc + l];
+            tcol[base + ts[(size_t)b * (R + 1) + r] + rel] = (uint16_t)(c & bmask);
+        }
+        for (uint32_t b = lane; b < nb; b += 64) {
+            const uint32_t s0 = seg[(size_t)b * nloc + l], s1 = seg[(size_t)(b + 1) * nloc + l];
+            const uint32_t len = s1 - s0;
+            if (len & 7u) {
+                const uint16_t first = (uint16_t)(col_idx[rs + s0] & bmask);
+                const uint64_t p0 = base + ts[(size_t)b * (R + 1) + r];
+                for (uint32_t i = len; i < ((len + 7u) & ~7u); i++) tcol[p0 + i] = first;
+            }
+        }
+    }
 }
 
 // Segment offsets of every local row by column block: seg[b][l] = #neighbours of row l with id
@@ -787,12 +1124,89 @@ hipError_t allow_lds_blocked(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_blocked_kernel<NW>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
+template <int NW, bool RES>
+void launch_tiled(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
+    sweep_tiled_kernel<NW, RES><<<g, b, lds, s>>>(a);
+}
+template <int NW, bool RES>
+hipError_t allow_lds_tiled(size_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
 template <int NW, bool LDSC>
 hipError_t allow_lds(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_kernel<NW, LDSC>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 constexpr size_t kMaxLdsBytes = 160 * 1024 - 1024;   // leave room for the static shared variables
+
+TiledLayout::~TiledLayout() {
+    (void)hipFree(tcol);
+    (void)hipFree(gbase);
+    (void)hipFree(tseg);
+}
+
+// Builds (or finds in the graph's cache) the tiled layout of rows [v_begin, v_end).
+int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t R, uint32_t block_log2,
+                     hipStream_t s, const TiledLayout** out) {
+    for (auto& t : gh->tiles)
+        if (t->v_begin == v_begin && t->v_end == v_end && t->grp_rows == R && t->block_log2 == block_log2) {
+            *out = t.get();
+            return MCMC_OK;
+        }
+    GraphDev& gd = gh->g;
+    if (!gd.sorted) {   // segments need ascending rows; neighbour order does not affect the sweep
+        int rs = sort_rows_inplace(gd);
+        if (rs) return rs;
+    }
+    auto L = std::make_unique<TiledLayout>();
+    const uint32_t nloc = v_end - v_begin;
+    L->v_begin = v_begin;
+    L->v_end = v_end;
+    L->grp_rows = R;
+    L->block_log2 = block_log2;
+    L->nblocks = (uint32_t)((((uint64_t)gd.n + 15) / 16 * 16 + (1ull << block_log2) - 1) >> block_log2);
+    L->ngroups = (nloc + R - 1) / R;
+    const uint32_t nb = L->nblocks, G = L->ngroups;
+    uint32_t* seg = nullptr;
+    uint64_t* totals = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
+    const size_t segn = (size_t)(nb + 1) * std::max<uint32_t>(nloc, 1);
+    chk(hipMalloc(&seg, sizeof(uint32_t) * segn));
+    chk(hipMalloc(&totals, sizeof(uint64_t) * (G + 1)));
+    chk(hipMalloc(&L->gbase, sizeof(uint64_t) * (G + 1)));
+    chk(hipMalloc(&L->tseg, sizeof(uint32_t) * std::max<size_t>((size_t)G * nb * (R + 1), 1)));
+    if (e == hipSuccess && nloc) {
+        segment_kernel<<<(uint32_t)std::min<size_t>((segn + 255) / 256, 65536), 256, 0, s>>>(
+            gd.row_off + v_begin, gd.col_idx, nloc, nb, block_log2, seg);
+        tile_group_total_kernel<<<std::min<uint32_t>(G, 65535), 256, 0, s>>>(seg, nloc, nb, R, G, totals);
+        chk(hipMemsetAsync(totals + G, 0, sizeof(uint64_t), s));
+        chk(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, totals, L->gbase, G + 1, s));
+        chk(hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)));
+        if (e == hipSuccess) chk(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, totals, L->gbase, G + 1, s));
+        chk(hipMemcpyAsync(&L->ids, L->gbase + G, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        chk(hipStreamSynchronize(s));
+    }
+    if (e == hipSuccess) chk(hipMalloc(&L->tcol, sizeof(uint16_t) * (L->ids + 64)));
+    if (e == hipSuccess && nloc) {
+        chk(hipMemsetAsync(L->tcol, 0, sizeof(uint16_t) * (L->ids + 64), s));
+        tile_seg_kernel<<<std::min<uint32_t>(G, 65535), 256, 0, s>>>(seg, nloc, nb, R, G, L->tseg);
+        tile_scatter_kernel<<<2048, 256, 0, s>>>(gd.row_off + v_begin, gd.col_idx, seg, L->gbase, L->tseg, nloc, nb,
+                                                 R, block_log2, L->tcol);
+        chk(hipGetLastError());
+        chk(hipStreamSynchronize(s));
+    }
+    (void)hipFree(seg);
+    (void)hipFree(totals);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("tiled layout: ") + hipGetErrorString(e));
+    *out = L.get();
+    gh->tiles.push_back(std::move(L));
+    return MCMC_OK;
+}
 
 static std::once_flag g_const_once;
 static hipError_t g_const_err = hipSuccess;
@@ -833,7 +1247,10 @@ struct mcmc_ctx {
     uint32_t* wave_start = nullptr;
     uint32_t* seg = nullptr;    // blocked variant: segment offsets
     uint32_t nblocks = 0, block_log2 = 0, chunk_rows = 0;
-    int variant = 0;            // 0 LDS-staged, 1 column-blocked, 2 L2-gather
+    int variant = 0;            // 0 LDS-staged, 1 column-blocked, 2 L2-gather, 3 tiled
+    const TiledLayout* tl = nullptr;   // variant 3 (owned by the graph's cache)
+    uint32_t sub_log2 = 0, slice_bytes = 0;
+    bool variant_res = false;          // variant 3: replica LDS-resident
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     uint32_t world = 1, rank = 0;
@@ -894,6 +1311,17 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.footers_all = c->footers_all;
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
+    if (c->tl) {
+        a.tcol = c->tl->tcol;
+        a.gbase = c->tl->gbase;
+        a.tseg = c->tl->tseg;
+        a.grp_rows = c->tl->grp_rows;
+        a.ngroups = c->tl->ngroups;
+        a.nblocks = c->tl->nblocks;
+        a.block_log2 = c->tl->block_log2;
+        a.sub_log2 = c->sub_log2;
+        a.slice_bytes = c->slice_bytes;
+    }
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
     return a;
@@ -978,13 +1406,15 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     c->v_end = v_end;
     c->z = p->tailcut ? std::max<uint32_t>(50u, gd.n / 2000u) : 0u;   // :89-97
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
-    // Variant: colour replica staged whole in LDS when it fits one workgroup (n <= ~159 Ki),
-    // otherwise column-blocked. Test knobs: MCMC_GATHER=lds|blocked|global, MCMC_BLOCK_LOG2=k.
+    // Variant: the tiled layout (16-bit block-local ids, replica LDS-resident when it fits, else
+    // streamed 64 KiB slices) -- fastest on every measured shape. The CSR variants stay selectable
+    // for A/B runs and parity tests. Knobs: MCMC_GATHER=tiled|lds|blocked|global, MCMC_BLOCK_LOG2,
+    // MCMC_SUB_LOG2, MCMC_GROUP_ROWS, MCMC_TILE_STREAM.
     const size_t lds_bytes = (((size_t)gd.n + 15) / 16) * 16;
     const char* gv = getenv("MCMC_GATHER");
     const std::string gsel = gv ? gv : "";
-    c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : (lds_bytes <= kMaxLdsBytes ? 0 : 1);
-    if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 1;
+    c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
+    if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
     const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
     hipError_t ea = hipSuccess;
     if (c->variant == 0) {
@@ -1004,6 +1434,9 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         c->lds = (size_t)(1u << c->block_log2) + (size_t)c->chunk_rows * c->nw * 4u;
         ea = wi == 0 ? allow_lds_blocked<1>(c->lds) : wi == 1 ? allow_lds_blocked<2>(c->lds)
            : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
+    } else if (c->variant == 3) {
+        const char* bl = getenv("MCMC_BLOCK_LOG2");
+        c->block_log2 = bl ? (uint32_t)std::max(4, std::min(16, atoi(bl))) : 16u;
     } else {
         static const SweepLaunch tab[4] = {launch_sweep<1, false>, launch_sweep<2, false>, launch_sweep<4, false>,
                                            launch_sweep<8, false>};
@@ -1042,14 +1475,66 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     }
     if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
     // persistent grids; rows statically arc-balanced over all waves (blocked: over workgroups)
-    if (c->variant != 2) {
+    if (c->variant == 3) {
+        // Resident (replica + masks + segment table fit one workgroup's LDS): 1024-thread
+        // workgroups, one per CU, replica staged once. Otherwise 512-thread workgroups, two per
+        // CU, a 2^block_log2-byte colour slice staged per (group, block). Groups of R rows: one
+        // group per workgroup while the mask LDS allows (fixed per-pair costs paid once), and
+        // R + 1 <= kTileSegPer * blockDim (segment-table prefetch registers).
+        const size_t rep = lds_bytes;
+        const char* gr = getenv("MCMC_GROUP_ROWS");
+        const bool resident = rep + 256u * (c->nw + 1) * 4u + 4u <= kMaxLdsBytes &&
+                              !(getenv("MCMC_TILE_STREAM") && atoi(getenv("MCMC_TILE_STREAM")));
+        if (!resident) c->block_log2 = std::min<uint32_t>(c->block_log2, 16u);
+        c->block = dim3(resident ? 1024 : 512);
+        c->grid = dim3((uint32_t)cus * (resident ? 1u : 2u));
+        c->slice_bytes = resident ? (uint32_t)rep : (uint32_t)std::min<size_t>(1ull << c->block_log2, rep);
+        const uint32_t lds_budget = resident ? (uint32_t)(kMaxLdsBytes - rep) : (uint32_t)(80u * 1024u - 1024u - c->slice_bytes);
+        const uint32_t rmax = std::max<uint32_t>(1u, std::min<uint32_t>(kTileSegPer * c->block.x - 1u,
+                                                                        (lds_budget - 4u) / ((c->nw + 1) * 4u)));
+        uint32_t R = (nloc + c->grid.x - 1) / std::max<uint32_t>(c->grid.x, 1);
+        R = std::max<uint32_t>(std::min<uint32_t>(32u, rmax), std::min<uint32_t>(rmax, R));
+        if (gr) R = (uint32_t)std::max(1, std::min((int)rmax, atoi(gr)));
+        c->variant_res = resident;
+        int rs = get_tiled_layout(const_cast<mcmc_graph*>(g), v_begin, v_end, R, c->block_log2, c->stream, &c->tl);
+        if (rs) { mcmc_destroy(c); return rs; }
+        c->nblocks = c->tl->nblocks;
+        // lanes per row segment: the smallest power of two L >= 4 with L * kTileU quads per step
+        // covering half a mean segment (measured on C2 / n = 8e5: fewer lanes make the
+        // finish/reduce path run nearly every step; more leave lanes idle)
+        const double arcs = (double)c->tl->ids;
+        const double quads = arcs / 8.0 / std::max(1.0, (double)nloc * c->nblocks);
+        uint32_t sl = 2;
+        while (sl < 6 && 2.0 * (double)(1u << sl) * kTileU < quads) sl++;
+        const char* sv = getenv("MCMC_SUB_LOG2");
+        if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));
+        c->sub_log2 = sl;
+        c->lds = (size_t)c->slice_bytes + (size_t)R * c->nw * 4u + (size_t)(R + 1) * 4u;
+        if (resident) {
+            static const SweepLaunch tab[4] = {launch_tiled<1, true>, launch_tiled<2, true>, launch_tiled<4, true>,
+                                               launch_tiled<8, true>};
+            c->sweep = tab[wi];
+            ea = wi == 0 ? allow_lds_tiled<1, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, true>(c->lds)
+               : wi == 2 ? allow_lds_tiled<4, true>(c->lds) : allow_lds_tiled<8, true>(c->lds);
+        } else {
+            static const SweepLaunch tab[4] = {launch_tiled<1, false>, launch_tiled<2, false>, launch_tiled<4, false>,
+                                               launch_tiled<8, false>};
+            c->sweep = tab[wi];
+            ea = wi == 0 ? allow_lds_tiled<1, false>(c->lds) : wi == 1 ? allow_lds_tiled<2, false>(c->lds)
+               : wi == 2 ? allow_lds_tiled<4, false>(c->lds) : allow_lds_tiled<8, false>(c->lds);
+        }
+        if (ea != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
+        }
+    } else if (c->variant != 2) {
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);
     } else {
         c->block = dim3(256);
         c->grid = dim3((uint32_t)cus * 8u);
     }
-    {
+    if (c->variant != 3) {
         const uint32_t W = c->variant == 1 ? c->grid.x : c->grid.x * (c->block.x / 64);
         hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
         if (ew != hipSuccess) {
@@ -1285,6 +1770,42 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
     if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
+    return MCMC_OK;
+}
+
+int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    mcmc_ctx_info i{};
+    const uint64_t nloc = c->v_end - c->v_begin;
+    uint64_t mloc = 0;
+    {
+        uint64_t ends[2];
+        MCMC_HIP_TRY(hipMemcpy(&ends[0], c->g->row_off + c->v_begin, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        MCMC_HIP_TRY(hipMemcpy(&ends[1], c->g->row_off + c->v_end, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        mloc = ends[1] - ends[0];
+    }
+    const uint64_t taboo = c->p.tabooIteration > 0 ? 8 * nloc : 0;
+    i.variant = c->variant;
+    i.resident = c->variant_res ? 1 : 0;
+    i.block_log2 = c->block_log2;
+    i.nblocks = c->nblocks;
+    i.grid = c->grid.x;
+    i.block = c->block.x;
+    i.lds_bytes = c->lds;
+    i.ref_bytes = 4 * (nloc + 1) + 4 * mloc + 4 * (uint64_t)c->n + 4 * nloc + taboo;
+    if (c->tl) {
+        const TiledLayout& t = *c->tl;
+        i.grp_rows = t.grp_rows;
+        i.ngroups = t.ngroups;
+        i.sub_log2 = c->sub_log2;
+        const uint64_t segb = 4ull * (t.grp_rows + 1) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
+        i.layout_bytes = 2 * t.ids + segb;
+        i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;
+    } else {
+        i.layout_bytes = 8 * (nloc + 1) + 4 * mloc;
+        i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;
+    }
+    *out = i;
     return MCMC_OK;
 }
 

@@ -25,7 +25,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import check, lib, u32ptr, u64ptr
+from ._lib import MCMCCtxInfo, check, lib, u32ptr, u64ptr
 from .colorer import ColoringMCMCParams, GlibcRand, GPURand, Graph, default_ncol
 
 FOOTER_WORDS = 1024   # MCMC_FOOTER_WORDS
@@ -107,6 +107,11 @@ class HipRank:
         if k.value:
             check(lib().mcmc_get_trajectory(self._ctx, u64ptr(out), k.value, ctypes.byref(k)))
         return out
+
+    def info(self) -> dict:
+        i = MCMCCtxInfo()
+        check(lib().mcmc_get_info(self._ctx, ctypes.byref(i)))
+        return i.as_dict()
 
     def close(self) -> None:
         if self._ctx:

@@ -1,0 +1,47 @@
+"""Folds rocprofv3 PMC passes (scripts_gpu_prof.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE) into
+profiles/pmc_summary.json, which bench.py reads for roofline.traffic.
+
+  python profiles/make_pmc_summary.py <prof_dir> <key> [kernel-substring]
+
+FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read (MI355X_MICROARCH.md, HBM/rocprofv3 section), so it is doubled;
+WRITE_SIZE is taken as is. Values are averaged over the kernel's profiled launches.
+"""
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def mean_counter(path: Path, counter: str, kernel: str) -> tuple[float, int]:
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+    if not vals:
+        raise SystemExit(f"no {counter} rows for kernel '{kernel}' in {path}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main() -> None:
+    prof, key = Path(sys.argv[1]), sys.argv[2]
+    kernel = sys.argv[3] if len(sys.argv) > 3 else "sweep_"
+    fetch_kib, nf = mean_counter(prof / "pmc1" / "run_counter_collection.csv", "FETCH_SIZE", kernel)
+    write_kib, nw = mean_counter(prof / "pmc2" / "run_counter_collection.csv", "WRITE_SIZE", kernel)
+    out = Path(__file__).resolve().parent / "pmc_summary.json"
+    d = json.loads(out.read_text()) if out.exists() else {}
+    d[key] = {
+        "kernel_substring": kernel,
+        "fetch_size_kib_raw": fetch_kib,
+        "write_size_kib": write_kib,
+        "launches": [nf, nw],
+        "hbm_read_bytes_per_launch": 2 * fetch_kib * 1024,
+        "hbm_write_bytes_per_launch": write_kib * 1024,
+        "hbm_bytes_per_launch": 2 * fetch_kib * 1024 + write_kib * 1024,
+        "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB -> bytes",
+        "source": str(prof),
+    }
+    out.write_text(json.dumps(d, indent=1) + "\n")
+    print(key, json.dumps(d[key]))
+
+
+if __name__ == "__main__":
+    main()

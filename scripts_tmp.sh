@@ -1,11 +1,6 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-run() { name=$1; shift; timeout -k 10 300 "$@" > gpurun_out/b_$name.log 2>&1 || { echo "FAIL $name"; tail -5 gpurun_out/b_$name.log; exit 1; }; python -c "
-import json,sys
-d=json.loads(open('gpurun_out/b_$name.log').read().strip().splitlines()[-1]); print('$name', '%.3e'%d['value'], 'step %.4f ms'%d['ms_per_step'], 'kern %.4f ms'%d['roofline']['kernel_ms'], 'frac %.3f'%d['roofline']['frac'], d['config']['workload'])"; }
-run lds python bench.py --steps 100 --warmup 5 --no-cpu-baseline
-MCMC_GATHER=blocked MCMC_BLOCK_LOG2=17 run blk17 python bench.py --steps 100 --warmup 5 --no-cpu-baseline
-MCMC_GATHER=blocked MCMC_BLOCK_LOG2=15 run blk15 python bench.py --steps 100 --warmup 5 --no-cpu-baseline
-run n8e5 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --n 800000 --prob 0.00125
-run dist1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --steps 100 --warmup 5 --force-dist
+timeout -k 10 300 python bench.py > gpurun_out/b_default.log 2>&1 || { echo "bench FAIL"; tail -5 gpurun_out/b_default.log; exit 1; }
+tail -1 gpurun_out/b_default.log | cut -c1-600
+bash scripts_gpu_prof.sh r01_tiled

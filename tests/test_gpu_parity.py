@@ -39,6 +39,16 @@ def gpu_run(M, off, idx, ncol, seed, draws_before, *, eps=1e-8, maxRip=250, tabo
     return col, st, rs
 
 
+def set_gather(monkeypatch, spec):
+    """MCMC_GATHER[:MCMC_BLOCK_LOG2[:MCMC_SUB_LOG2[:MCMC_GROUP_ROWS[:MCMC_TILE_STREAM]]]] test knobs
+    (an empty field keeps the library's choice)."""
+    parts = spec.split(":")
+    monkeypatch.setenv("MCMC_GATHER", parts[0])
+    for key, v in zip(("MCMC_BLOCK_LOG2", "MCMC_SUB_LOG2", "MCMC_GROUP_ROWS", "MCMC_TILE_STREAM"), parts[1:]):
+        if v:
+            monkeypatch.setenv(key, v)
+
+
 def oracle_case(n, p, ncol, seed, **kw):
     O.srand(1)
     off, idx = O.setup_rnd2(n, p)
@@ -136,18 +146,18 @@ def circulant(n, K):
     return off, idx.ravel()
 
 
-@pytest.mark.parametrize("gather", ["lds", "global", "blocked:17", "blocked:8", "blocked:6"])
+@pytest.mark.parametrize("gather", ["lds", "global", "blocked:17", "blocked:8", "blocked:6", "tiled",
+                                    "tiled:8", "tiled:6:0:7", "tiled:7:3:1", "tiled:4:6:33", "tiled:9:2:100",
+                                    "tiled::::1", "tiled:8:1:50:1", "tiled:6:2:7:1", "tiled:10:5:1:1"])
 @pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", [(3000, 0.02, 16, 31, 1e-8, 0, 60),
                                                             (2000, 0.05, 100, 32, 1e-8, 2, 20),
                                                             (1500, 0.3, 5, 33, 3.3e6, 1, 15),
                                                             (2500, 0.1, 200, 34, 1e-8, 0, 10)])
 def test_all_gather_variants(M, monkeypatch, gather, n, p, ncol, seed, eps, taboo, maxrip):
-    """LDS-staged, L2-gather and column-blocked sweeps (down to 64-vertex blocks, i.e. dozens of
-    column blocks and many chunks) give the same bit-exact results."""
-    var, _, blog = gather.partition(":")
-    monkeypatch.setenv("MCMC_GATHER", var)
-    if blog:
-        monkeypatch.setenv("MCMC_BLOCK_LOG2", blog)
+    """LDS-staged, L2-gather, column-blocked (down to 64-vertex blocks, i.e. dozens of column
+    blocks and many chunks) and tiled sweeps (spec tiled:block_log2:lanes_log2:group_rows -- 16-vertex
+    blocks, 1..64 lanes per row segment, odd group sizes) give the same bit-exact results."""
+    set_gather(monkeypatch, gather)
     off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
     col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo)
     assert_same(col, st, r)
@@ -279,11 +289,11 @@ def test_partitioned_driver_nccl_world1(M):
         dist.destroy_process_group()
 
 
-def test_blocked_unsorted_upload(M, monkeypatch):
-    """Uploaded rows in arbitrary order (as --graph produces) are sorted once for the blocked
-    variant; the result is unchanged (the sweep is order-independent)."""
-    monkeypatch.setenv("MCMC_GATHER", "blocked")
-    monkeypatch.setenv("MCMC_BLOCK_LOG2", "7")
+@pytest.mark.parametrize("gather", ["blocked:7", "tiled:7", "tiled:7:::1"])
+def test_blocked_unsorted_upload(M, monkeypatch, gather):
+    """Uploaded rows in arbitrary order (as --graph produces) are sorted once for the blocked and
+    tiled variants; the result is unchanged (the sweep is order-independent)."""
+    set_gather(monkeypatch, gather)
     n, p, ncol, seed = 2000, 0.05, 9, 51
     off, idx, nc, r = oracle_case(n, p, ncol, seed, maxRip=40)
     rnd = np.random.default_rng(0)
@@ -295,11 +305,11 @@ def test_blocked_unsorted_upload(M, monkeypatch):
     assert_same(col, st, r)
 
 
-@pytest.mark.parametrize("blog", ["15", "12"])
-def test_c2_blocked_matches_golden(M, monkeypatch, blog):
-    """configs[1] full run through the column-blocked kernel (4 and 25 column blocks)."""
-    monkeypatch.setenv("MCMC_GATHER", "blocked")
-    monkeypatch.setenv("MCMC_BLOCK_LOG2", blog)
+@pytest.mark.parametrize("gather", ["blocked:15", "blocked:12", "tiled", "tiled:12", "tiled::::1", "tiled:14:2::1"])
+def test_c2_blocked_matches_golden(M, monkeypatch, gather):
+    """configs[1] full run through the column-blocked kernel (4 and 25 column blocks) and the tiled
+    kernel (resident replica with 2 and 25 column blocks; streamed 64 KiB / 16 KiB slices)."""
+    set_gather(monkeypatch, gather)
     d = json.loads((GOLDEN / "c2.json").read_text())
     rng = M.GlibcRand(1)
     g = M.Graph.simulate(d["n"], d["prob"], rng)
@@ -310,9 +320,9 @@ def test_c2_blocked_matches_golden(M, monkeypatch, blog):
 
 
 @pytest.mark.parametrize("world", [2, 5])
-def test_partitioned_lockstep_blocked(M, monkeypatch, world):
-    monkeypatch.setenv("MCMC_GATHER", "blocked")
-    monkeypatch.setenv("MCMC_BLOCK_LOG2", "9")
+@pytest.mark.parametrize("gather", ["blocked:9", "tiled:9", "tiled:9:::1"])
+def test_partitioned_lockstep_blocked(M, monkeypatch, world, gather):
+    set_gather(monkeypatch, gather)
     off, idx, nc, r = oracle_case(3000, 0.03, 20, 61, maxRip=30)
     ranks = _lockstep(M, off, idx, nc, 61, world, maxRip=30)
     for b in ranks:
