@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -98,7 +99,15 @@ struct SweepArgs {
     uint32_t grp_rows, ngroups;
     uint32_t sub_log2;          // lanes per row segment = 2^sub_log2
     uint32_t slice_bytes;       // tiled: LDS bytes of the colour slice (masks follow it)
+    unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
 };
+
+// Phase timestamps of the last sweep, 8 slots per workgroup (wall_clock64, 100 MHz): 0 start,
+// 1 first scan begins, 2 scans done, 3 evaluation done, 4 tail done (last workgroup: commit done).
+#define MCMC_PHASE(a, k)                                                                  \
+    do {                                                                                  \
+        if ((a).phase_ts && threadIdx.x == 0) (a).phase_ts[blockIdx.x * 8u + (k)] = wall_clock64(); \
+    } while (0)
 
 __constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
 __constant__ uint32_t kMinstdPow2[64];      // 16807^(2^i) mod (2^31-1), i = 0..63
@@ -769,14 +778,15 @@ __device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, cons
     }
 }
 
-// RES: the whole replica is LDS-resident (1024 threads, 1 workgroup/CU); otherwise a 64 KiB slice
-// per (group, block) (512 threads, 2 workgroups/CU). A workgroup walks its (group, block) pairs
+// RES: the whole replica is LDS-resident; otherwise a 64 KiB slice per (group, block). Both run
+// one 1024-thread workgroup per CU (two smaller workgroups per CU were measured to split the CU's
+// issue unevenly: the younger one finished 30% later and the tail ran at half occupancy). A workgroup walks its (group, block) pairs
 // in order; while it scans pair k, the colour slice (streaming mode) and segment table of pair
 // k+1 are already in flight into registers, and land in LDS after the scan's barrier.
 constexpr uint32_t kTileSegPer = 4;   // segment-table entries per thread per pair: R + 1 <= 4 * blockDim
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable 16 B
 template <bool RES>
-constexpr int kTileSlicePer = RES ? 1 : (65536 / 16) / 512;   // uint4 of a 64 KiB slice per thread
+constexpr int kTileSlicePer = RES ? 1 : (65536 / 16) / 1024;   // uint4 of a 64 KiB slice per thread
 
 // Issue the loads of pair (g, b)'s segment table (and streaming: colour slice) into registers.
 template <bool RES>
@@ -803,6 +813,22 @@ __device__ __forceinline__ void tile_prefetch(const SweepArgs& a, const uint8_t*
     }
 }
 
+// Segment bounds (ids from the group base) of this lane's first row in pair (g, b): the
+// sub-group's first row of its wave's share, read from the global segment table. Branch-free
+// (idle sub-groups read the empty range [s(wr1), s(wr1)) ), so the loads stay in flight until used.
+__device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
+                                               uint32_t wid, uint32_t nwaves, uint32_t sub,
+                                               uint32_t& s0, uint32_t& s1) {
+    const uint32_t R = a.grp_rows;
+    const uint32_t rows = min(R, nloc - g * R);
+    const uint32_t q = (rows + nwaves - 1) / nwaves;
+    const uint32_t wr0 = min(rows, wid * q), wr1 = min(rows, wr0 + q);
+    const uint32_t row = wr0 + sub;
+    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * (R + 1);
+    s0 = gs[min(row, wr1)];
+    s1 = gs[min(row + 1, wr1)];
+}
+
 // Store the prefetched pair into LDS (after the barrier that ends the previous pair's scan).
 template <bool RES>
 __device__ __forceinline__ void tile_land(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
@@ -827,11 +853,12 @@ __device__ __forceinline__ void tile_land(const SweepArgs& a, uint32_t g, uint32
 }
 
 template <int NW, bool RES>
-__global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs a) {
+__global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
     __shared__ TailShared sh;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
+    MCMC_PHASE(a, 0);
     if (threadIdx.x == 0) sh.wg_viol = 0;
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
@@ -854,29 +881,40 @@ __global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs
     uint32_t pseg[kTileSegPer];
     u32x4 pslice[kTileSlicePer<RES>];
     uint32_t g = blockIdx.x, b = 0;
-    // (unconditional, clamped to a valid pair: keeps the scan loop's vmcnt accounting exact)
-    tile_prefetch<RES>(a, C, min(g, a.ngroups ? a.ngroups - 1u : 0u), 0, nloc, pseg, pslice);
-    if (RES) {   // whole replica once
+    const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
+    // Issue order: the first pair's segment table and first-row bounds, then (once the bounds are
+    // back) its first quads, then the resident replica -- the quads fly across the staging.
+    tile_prefetch<RES>(a, C, gclamp, 0, nloc, pseg, pslice);
+    uint32_t fpos, fend;
+    tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend);
+    fpos += 8u * li;
+    const uint16_t* __restrict__ gcol = a.tcol + a.gbase[gclamp];
+    uint4 v[kTileU];
+#pragma unroll
+    for (int u = 0; u < kTileU; u++) {
+        const uint32_t pu = fpos + 8u * L * u;
+        v[u] = *reinterpret_cast<const uint4*>(gcol + (pu < fend ? pu : 0u));
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the staging below the first quads
+    if (RES) {
+        constexpr int kResPer = 10;   // uint4 per thread: replica <= 160 KiB over 1024 threads
+        u32x4 rr[kResPer];
         const uint32_t nq16 = nbytes16 >> 4;
-        const uint4* __restrict__ src = reinterpret_cast<const uint4*>(C);
-        for (uint32_t i0 = threadIdx.x; i0 < nq16; i0 += 8u * blockDim.x) {
-            uint4 r[8];
+        const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(C);
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t i = i0 + k * blockDim.x;
-                r[k] = src[i < nq16 ? i : 0u];
-            }
+        for (int k = 0; k < kResPer; k++) {
+            const uint32_t i = threadIdx.x + k * blockDim.x;
+            rr[k] = src[i < nq16 ? i : 0u];
+        }
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t i = i0 + k * blockDim.x;
-                lds_raw[i < nq16 ? i : 0u] = r[k];   // (src[0] again at 0): loads stay unconditional
-            }
+        for (int k = 0; k < kResPer; k++) {
+            const uint32_t i = threadIdx.x + k * blockDim.x;
+            reinterpret_cast<u32x4*>(lds_raw)[i < nq16 ? i : 0u] = rr[k];   // (src[0] again at 0)
         }
     }
     while (g < a.ngroups) {
         const uint32_t r0 = g * R;
         const uint32_t rows = min(R, nloc - r0);
-        const uint16_t* __restrict__ gcol = a.tcol + a.gbase[g];
         const uint32_t q = (rows + nwaves - 1) / nwaves;
         const uint32_t wr0 = min(rows, wid * q), wr1 = min(rows, wr0 + q);
         __syncthreads();   // previous pair's scan (or the previous group's evaluation) is done
@@ -885,17 +923,16 @@ __global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs
         tile_land<RES>(a, g, b, nloc, sseg, lds_raw, pseg, pslice);
         __syncthreads();
         const uint32_t ng = (b + 1 < nb) ? g : g + gridDim.x, nbn = (b + 1 < nb) ? b + 1 : 0u;
-        tile_prefetch<RES>(a, C, ng < a.ngroups ? ng : g, ng < a.ngroups ? nbn : b, nloc, pseg, pslice);
+        const uint32_t pg = ng < a.ngroups ? ng : g, pb = ng < a.ngroups ? nbn : b;
+        tile_prefetch<RES>(a, C, pg, pb, nloc, pseg, pslice);
+        uint32_t npos, nend;
+        tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend);
+        const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
+        if (b == 0 && g == blockIdx.x) MCMC_PHASE(a, 1);
         const uint8_t* __restrict__ scb = RES ? sc + (b << a.block_log2) : sc;
-        // sub-group state: current row, this lane's next quad, the row's end (ids, from gbase)
-        uint32_t row = wr0 + sub, pos = 0, end = 0;
-        if (row < wr1) { pos = sseg[row] + 8u * li; end = sseg[row + 1]; }
-        uint4 v[kTileU];
-#pragma unroll
-        for (int u = 0; u < kTileU; u++) {
-            const uint32_t pu = pos + 8u * L * u;
-            v[u] = *reinterpret_cast<const uint4*>(gcol + ((row < wr1 && pu < end) ? pu : 0u));
-        }
+        // sub-group state: current row, this lane's next quad, the row's end (ids, from gbase);
+        // the first step's quads are already in v
+        uint32_t row = wr0 + sub, pos = fpos, end = fend;
         uint32_t m[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) m[i] = 0;
@@ -942,8 +979,18 @@ __global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs
 #pragma unroll
             for (int u = 0; u < kTileU; u++) v[u] = vn[u];
         }
+        // the next pair's first quads: in flight across the barriers, landing and evaluation
+        gcol = ngcol;
+        fpos = npos + 8u * li;
+        fend = nend;
+#pragma unroll
+        for (int u = 0; u < kTileU; u++) {
+            const uint32_t pu = fpos + 8u * L * u;
+            v[u] = *reinterpret_cast<const uint4*>(gcol + (pu < fend ? pu : 0u));
+        }
         if (b + 1 == nb) {
             __syncthreads();   // all blocks scanned: every wave evaluates a share of the group's rows
+            MCMC_PHASE(a, 2);
             for (uint32_t e0 = wid * min(q, 64u); e0 < rows; e0 += nwaves * min(q, 64u)) {
                 const uint32_t cnt = min(min(q, 64u), rows - e0);
                 uint32_t acc[NW];
@@ -955,8 +1002,10 @@ __global__ __launch_bounds__(RES ? 1024 : 512) void sweep_tiled_kernel(SweepArgs
         g = ng;
         b = nbn;
     }
+    MCMC_PHASE(a, 3);
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
     sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+    MCMC_PHASE(a, 4);
 }
 
 // ---- tiled layout construction (once per context) ----------------------------------------------
@@ -1251,6 +1300,7 @@ struct mcmc_ctx {
     const TiledLayout* tl = nullptr;   // variant 3 (owned by the graph's cache)
     uint32_t sub_log2 = 0, slice_bytes = 0;
     bool variant_res = false;          // variant 3: replica LDS-resident
+    unsigned long long* phase_ts = nullptr;   // MCMC_PHASE_DUMP diagnostics
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     uint32_t world = 1, rank = 0;
@@ -1322,6 +1372,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.sub_log2 = c->sub_log2;
         a.slice_bytes = c->slice_bytes;
     }
+    a.phase_ts = c->phase_ts;
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
     return a;
@@ -1469,6 +1520,10 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     chk(hipMalloc(&c->events, sizeof(uint32_t) * pcap));
     chk(hipMalloc(&c->st, sizeof(DevState)));
     chk(hipMalloc(&c->traj, sizeof(unsigned long long) * c->traj_cap));
+    if (getenv("MCMC_PHASE_DUMP")) {
+        chk(hipMalloc(&c->phase_ts, sizeof(unsigned long long) * 8u * 4096u));
+        chk(hipMemset(c->phase_ts, 0, sizeof(unsigned long long) * 8u * 4096u));
+    }
     if (e != hipSuccess) {
         mcmc_destroy(c);
         return fail(MCMC_E_NOMEM, std::string("allocation: ") + hipGetErrorString(e));
@@ -1476,20 +1531,20 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
     // persistent grids; rows statically arc-balanced over all waves (blocked: over workgroups)
     if (c->variant == 3) {
-        // Resident (replica + masks + segment table fit one workgroup's LDS): 1024-thread
-        // workgroups, one per CU, replica staged once. Otherwise 512-thread workgroups, two per
-        // CU, a 2^block_log2-byte colour slice staged per (group, block). Groups of R rows: one
+        // Resident (replica + masks + segment table fit one workgroup's LDS): replica staged once.
+        // Otherwise a 2^block_log2-byte colour slice per (group, block). One 1024-thread
+        // workgroup per CU either way. Groups of R rows: one
         // group per workgroup while the mask LDS allows (fixed per-pair costs paid once), and
         // R + 1 <= kTileSegPer * blockDim (segment-table prefetch registers).
         const size_t rep = lds_bytes;
         const char* gr = getenv("MCMC_GROUP_ROWS");
-        const bool resident = rep + 256u * (c->nw + 1) * 4u + 4u <= kMaxLdsBytes &&
+        const bool resident = rep + 256u * (c->nw + 1) * 4u + 4u <= kMaxLdsBytes && rep <= 10u * 16u * 1024u &&
                               !(getenv("MCMC_TILE_STREAM") && atoi(getenv("MCMC_TILE_STREAM")));
         if (!resident) c->block_log2 = std::min<uint32_t>(c->block_log2, 16u);
-        c->block = dim3(resident ? 1024 : 512);
-        c->grid = dim3((uint32_t)cus * (resident ? 1u : 2u));
+        c->block = dim3(1024);
+        c->grid = dim3((uint32_t)cus);
         c->slice_bytes = resident ? (uint32_t)rep : (uint32_t)std::min<size_t>(1ull << c->block_log2, rep);
-        const uint32_t lds_budget = resident ? (uint32_t)(kMaxLdsBytes - rep) : (uint32_t)(80u * 1024u - 1024u - c->slice_bytes);
+        const uint32_t lds_budget = resident ? (uint32_t)(kMaxLdsBytes - rep) : (uint32_t)(kMaxLdsBytes - c->slice_bytes);
         const uint32_t rmax = std::max<uint32_t>(1u, std::min<uint32_t>(kTileSegPer * c->block.x - 1u,
                                                                         (lds_budget - 4u) / ((c->nw + 1) * 4u)));
         uint32_t R = (nloc + c->grid.x - 1) / std::max<uint32_t>(c->grid.x, 1);
@@ -1770,6 +1825,14 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
     if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
+    if (c->phase_ts) {   // diagnostics: the last sweep's per-workgroup phase timestamps
+        std::vector<unsigned long long> h_ts((size_t)8 * c->grid.x);
+        MCMC_HIP_TRY(hipMemcpy(h_ts.data(), c->phase_ts, h_ts.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("MCMC_PHASE_DUMP"), "wb")) {
+            fwrite(h_ts.data(), sizeof(unsigned long long), h_ts.size(), f);
+            fclose(f);
+        }
+    }
     return MCMC_OK;
 }
 
@@ -1823,6 +1886,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->traj);
     (void)hipFree(c->wave_start);
     (void)hipFree(c->seg);
+    (void)hipFree(c->phase_ts);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -1,0 +1,18 @@
+"""Summarise MCMC_PHASE_DUMP files: per-workgroup phase durations of the last benchmarked sweep."""
+import sys
+
+import numpy as np
+
+for path in sys.argv[1:]:
+    t = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    t = t[t[:, 0] > 0]
+    t0 = t[:, 0].min()
+    rel = (t - t0) / 100.0   # wall_clock64 = 100 MHz -> us
+    names = ["start", "scan0", "scans_done", "eval_done", "tail_done"]
+    print(path, "workgroups", len(t))
+    for k, nm in enumerate(names):
+        c = rel[:, k]
+        print(f"  {nm:11s} min {c.min():7.2f} med {np.median(c):7.2f} max {c.max():7.2f} us")
+    d = np.diff(rel[:, :5], axis=1)
+    for k, nm in enumerate(["stage", "scan", "evaluate", "tail"]):
+        print(f"  d_{nm:9s} min {d[:, k].min():7.2f} med {np.median(d[:, k]):7.2f} max {d[:, k].max():7.2f} us")
