@@ -81,7 +81,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--vertices", type=int, default=100000, help="n of --simulate (per GPU under weak scaling)")
     ap.add_argument("--prob", type=float, default=0.01)
     ap.add_argument("--ncol", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
@@ -113,9 +113,9 @@ def main() -> int:
     from mcmc_colorer_amd._lib import check, lib
 
     dev = local
-    n_req, p_req = a.n, a.prob
+    n_req, p_req = a.vertices, a.prob
     if world > 1 and a.scaling == "weak":
-        n_req, p_req = a.n * world, a.prob / world
+        n_req, p_req = a.vertices * world, a.prob / world
     t_gen = time.perf_counter()
     rng = M.GlibcRand(1)
     g = M.Graph.simulate(n_req, p_req, rng, device=dev)

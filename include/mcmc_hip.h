@@ -146,20 +146,25 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out);
 void mcmc_destroy(mcmc_ctx* c);
 
 /* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------
- * SURVEY.md §8e. Rank r of `world` sweeps rows [r*S, min(n,(r+1)*S)), S = ceil(n/world), with global
- * ids and full-length colour replicas. Per sweep, all on the caller's stream, no host sync:
- *   mcmc_part_sweep_async  sweep of the local rows; writes the local slab of the next-colour
- *                          buffer and this rank's footer (local Cviol + sorted overflow events)
- *   caller                 all-gathers the slabs (in place, S bytes per rank, into the next-colour
- *                          buffer colors[(t+1)&1]) and the footers (MCMC_FOOTER_WORDS uint32 each)
+ * SURVEY.md §8e. Rank r of `world` sweeps rows [r*S, min(n,(r+1)*S)) with global
+ * ids and full-length colour replicas. A partitioned colour buffer is a sequence of per-rank
+ * regions: region r = [r*P, (r+1)*P) holds the colours of vertices [r*S, r*S + S) followed by
+ * rank r's footer (MCMC_FOOTER_WORDS uint32: local Cviol, event count, flags, sorted overflow
+ * events); S = ceil(n/world) rounded up to 16, P = S + 4*MCMC_FOOTER_WORDS. Vertex v lives at
+ * byte v + (v/S) * 4*MCMC_FOOTER_WORDS. Per sweep, all on the caller's stream, no host sync:
+ *   mcmc_part_sweep_async  sweep of the local rows into the local region of the next-colour
+ *                          buffer colors[(t+1)&1]: colours and footer
+ *   caller                 ONE in-place all-gather of the regions (P bytes per rank) of that
+ *                          buffer -- colours and footers travel together
  *   mcmc_part_commit_async global Cviol, stop test, rank-ordered glibc replay -- identical on
  *                          every replica -- RNG advance, buffer flip
- * The colour buffers (>= world*S and n+16 bytes each), footer and footers_all are caller-owned
- * device memory (e.g. torch tensors); `stream` is the caller's hipStream_t, used as given (0 = the
- * legacy null stream, torch's default current stream). */
+ * The colour buffers (>= world*P bytes each) are caller-owned device memory (e.g. torch tensors);
+ * `stream` is the caller's hipStream_t, used as given (0 = the legacy null stream, torch's default
+ * current stream). Partitioned contexts need the tiled sweep (the default variant). */
 #define MCMC_FOOTER_WORDS 1024
+int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P);
 int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
-                     uint64_t colors_bytes, void* footer, void* footers_all, void* stream);
+                     uint64_t colors_bytes, void* stream);
 int mcmc_part_sweep_async(mcmc_ctx* c);
 int mcmc_part_commit_async(mcmc_ctx* c);
 /* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final). */

@@ -40,8 +40,8 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
     "mcmc_destroy": (None, [c_void_p]),
-    "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
-                                 c_void_p]),
+    "mcmc_part_layout": (c_int, [c_uint32, c_uint32, _u64p, _u64p]),
+    "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]),
     "mcmc_part_sweep_async": (c_int, [c_void_p]),
     "mcmc_part_commit_async": (c_int, [c_void_p]),
     "mcmc_part_state": (c_int, [c_void_p, POINTER(c_int32), _u32p, _u32p]),

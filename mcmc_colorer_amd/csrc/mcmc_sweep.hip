@@ -83,8 +83,6 @@ struct SweepArgs {
     int check_done;             // device-resident loop: exit immediately once done
     int fused;                  // last-arriving workgroup: 1 = runs the commit (single-context loop),
                                 //                          2 = packs this rank's footer (partitioned)
-    uint32_t* footer;           // partitioned: this rank's footer [viol lo, viol hi, E, flags, events...]
-    const uint32_t* footers_all;// partitioned: all ranks' footers after the all-gather
     uint32_t world;
     uint32_t lds_sort_cap;      // words of the sweep kernel's dynamic LDS reusable by the commit sort
     const uint32_t* seg;        // blocked: per-(block, local row) segment offsets, (nb+1) x nloc
@@ -100,7 +98,16 @@ struct SweepArgs {
     uint32_t sub_log2;          // lanes per row segment = 2^sub_log2
     uint32_t slice_bytes;       // tiled: LDS bytes of the colour slice (masks follow it)
     unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
+    // partitioned colour buffers: vertex v at byte v + (v / part_S) * part_FB (part_FB = 0: plain)
+    uint32_t part_S, part_FB;
+    uint32_t own_off;           // rank * part_FB: byte offset of this rank's own vertices
+    uint64_t footer_off;        // rank * (part_S + part_FB) + part_S: this rank's footer slot
 };
+
+// Byte address of vertex v in a colour buffer (partitioned buffers interleave per-rank footers).
+__device__ __forceinline__ uint32_t caddr(const SweepArgs& a, uint32_t v) {
+    return a.part_FB ? v + (v / a.part_S) * a.part_FB : v;
+}
 
 // Phase timestamps of the last sweep, 8 slots per workgroup (wall_clock64, 100 MHz): 0 start,
 // 1 first scan begins, 2 scans done, 3 evaluation done, 4 tail done (last workgroup: commit done).
@@ -216,9 +223,9 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
                 const uint32_t v = s[i];
                 const uint32_t r = glibc_next(ring, head);
                 const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
-                Cs[v] = (uint8_t)c;
+                Cs[caddr(a, v)] = (uint8_t)c;
                 if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
-                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
+                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
             }
             for (int i = 0; i < 31; i++) st->glibc_ring[i] = ring[i];
             st->glibc_head = head;
@@ -284,9 +291,11 @@ constexpr uint32_t kFooterEvents = kFooterWords - 4;
 
 // Last workgroup of a partitioned sweep: sort this rank's overflow events and publish
 // [Cviol_local, E, flags, events] for the all-gather; reset the local accumulators.
-__device__ void pack_footer(const SweepArgs& a, unsigned long long viol, uint32_t E, uint32_t err, uint32_t* lds,
-                            uint32_t lds_cap) {
+__device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
+                            uint32_t* lds, uint32_t lds_cap) {
     DevState* st = a.st;
+    // this rank's footer slot: after its colour slab, in the next-colour buffer
+    uint32_t* footer = reinterpret_cast<uint32_t*>(((t & 1) ? a.colors0 : a.colors1) + a.footer_off);
     uint32_t* s = a.events;
     if (E > 0 && E <= a.ev_cap) {
         uint32_t P = 1;
@@ -301,12 +310,12 @@ __device__ void pack_footer(const SweepArgs& a, unsigned long long viol, uint32_
         bitonic_sort_block(s, P);
     }
     const uint32_t En = min(E, kFooterEvents);
-    for (uint32_t i = threadIdx.x; i < En; i += blockDim.x) a.footer[4 + i] = s[i];
+    for (uint32_t i = threadIdx.x; i < En; i += blockDim.x) footer[4 + i] = s[i];
     if (threadIdx.x == 0) {
-        a.footer[0] = (uint32_t)viol;
-        a.footer[1] = (uint32_t)(viol >> 32);
-        a.footer[2] = E;
-        a.footer[3] = (E > kFooterEvents || E > a.ev_cap || err) ? 1u : 0u;
+        footer[0] = (uint32_t)viol;
+        footer[1] = (uint32_t)(viol >> 32);
+        footer[2] = E;
+        footer[3] = (E > kFooterEvents || E > a.ev_cap || err) ? 1u : 0u;
         st->viol = 0;
         st->ev_count = 0;
         st->arrive = 0;
@@ -322,13 +331,16 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
     __shared__ unsigned long long sh_viol;
     __shared__ uint32_t sh_off[65];
     DevState* st = a.st;
+    const uint32_t t0 = st->t;
+    const uint8_t* nxt = (t0 & 1) ? a.colors0 : a.colors1;
+    const size_t P = (size_t)a.part_S + a.part_FB;
     if (threadIdx.x == 0) {
         sh_done = st->done;
-        sh_t = st->t;
+        sh_t = t0;
         unsigned long long v = 0;
         uint32_t E = 0, err = st->err;
         for (uint32_t r = 0; r < a.world; r++) {
-            const uint32_t* f = a.footers_all + (size_t)r * kFooterWords;
+            const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + a.part_S);
             v += (unsigned long long)f[0] | ((unsigned long long)f[1] << 32);
             sh_off[r] = E;
             E += min(f[2], kFooterEvents);
@@ -341,7 +353,7 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
     __syncthreads();
     if (sh_done) return;
     for (uint32_t r = 0; r < a.world; r++) {
-        const uint32_t* f = a.footers_all + (size_t)r * kFooterWords;
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + a.part_S);
         const uint32_t Er = min(f[2], kFooterEvents);
         for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = f[4 + i];
     }
@@ -583,7 +595,7 @@ __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, Tai
     __syncthreads();
     if (!sh.wg_last) return;
     if (a.fused == 1) commit_control(a, sh.t, sh.viol, sh.E, sh.err, lds, cap);
-    else pack_footer(a, sh.viol, sh.E, sh.err, lds, cap);
+    else pack_footer(a, sh.t, sh.viol, sh.E, sh.err, lds, cap);
 }
 
 // The fused sweep (n fits LDS, or the L2-gather variant). Every wave owns a contiguous,
@@ -804,11 +816,10 @@ __device__ __forceinline__ void tile_prefetch(const SweepArgs& a, const uint8_t*
     if (!RES) {
         const uint32_t lo = b << a.block_log2;
         const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
-        const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(C + lo);
 #pragma unroll
         for (int k = 0; k < kTileSlicePer<RES>; k++) {
             const uint32_t i = threadIdx.x + k * blockDim.x;
-            pslice[k] = src[i < nq16 ? i : 0u];
+            pslice[k] = *reinterpret_cast<const u32x4*>(C + caddr(a, lo + 16u * (i < nq16 ? i : 0u)));
         }
     }
 }
@@ -900,11 +911,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         constexpr int kResPer = 10;   // uint4 per thread: replica <= 160 KiB over 1024 threads
         u32x4 rr[kResPer];
         const uint32_t nq16 = nbytes16 >> 4;
-        const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(C);
 #pragma unroll
         for (int k = 0; k < kResPer; k++) {
             const uint32_t i = threadIdx.x + k * blockDim.x;
-            rr[k] = src[i < nq16 ? i : 0u];
+            rr[k] = *reinterpret_cast<const u32x4*>(C + caddr(a, 16u * (i < nq16 ? i : 0u)));
         }
 #pragma unroll
         for (int k = 0; k < kResPer; k++) {
@@ -996,7 +1006,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 uint32_t acc[NW];
 #pragma unroll
                 for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
-                wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, r0 + e0, cnt, acc, lane);
+                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane);
             }
         }
         g = ng;
@@ -1149,12 +1159,13 @@ __global__ void partition_kernel(const uint64_t* __restrict__ row_off, uint32_t 
 // ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61): vertex v uses engine draw v + 1 when
 // no earlier draw was rejected by uniform_int_distribution; rejections (P ~ nCol/2^31 each) are
 // counted and handed to the exact sequential host path.
-__global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st) {
+__global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st,
+                                     uint32_t part_S, uint32_t part_FB) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         const uint32_t x = minstd_mulmod(x0, minstd_pow_tab((uint64_t)v + 1));
         const uint32_t r = x - 1u;
         if (r >= k.past) atomicAdd(&st->init_rejections, 1u);
-        C[v] = (uint8_t)min(r / k.scaling, 255u);
+        C[part_FB ? v + (v / part_S) * part_FB : v] = (uint8_t)min(r / k.scaling, 255u);
     }
 }
 
@@ -1304,13 +1315,40 @@ struct mcmc_ctx {
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     uint32_t world = 1, rank = 0;
-    uint32_t* footer = nullptr;
-    const uint32_t* footers_all = nullptr;
+    uint32_t part_S = 0;                     // partitioned: slab stride (vertices), multiple of 16
     uint8_t* own_colors[2] = {nullptr, nullptr};   // the context's own replicas (freed at destroy)
     std::vector<uint32_t> host_events;
 };
 
 namespace {
+
+// Host <-> device colour transfers (n bytes in vertex order); partitioned buffers are per-rank
+// regions of S colours followed by a footer.
+int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
+    if (!c->part) {
+        MCMC_HIP_TRY(hipMemcpyAsync(dst, h, c->n, hipMemcpyHostToDevice, c->stream));
+    } else {
+        const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
+        for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
+            MCMC_HIP_TRY(hipMemcpyAsync(dst + r * P, h + v, std::min<uint64_t>(c->part_S, c->n - v),
+                                        hipMemcpyHostToDevice, c->stream));
+    }
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
+
+int download_colors(mcmc_ctx* c, const uint8_t* src, uint8_t* h) {
+    if (!c->part) {
+        MCMC_HIP_TRY(hipMemcpyAsync(h, src, c->n, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
+        for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
+            MCMC_HIP_TRY(hipMemcpyAsync(h + v, src + r * P, std::min<uint64_t>(c->part_S, c->n - v),
+                                        hipMemcpyDeviceToHost, c->stream));
+    }
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
 
 int upload_state(mcmc_ctx* c, uint32_t t) {
     DevState h{};
@@ -1357,8 +1395,12 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.nblocks = c->nblocks;
     a.block_log2 = c->block_log2;
     a.chunk_rows = c->chunk_rows;
-    a.footer = c->footer;
-    a.footers_all = c->footers_all;
+    if (c->part) {
+        a.part_S = c->part_S;
+        a.part_FB = 4u * kFooterWords;
+        a.own_off = c->rank * a.part_FB;
+        a.footer_off = (uint64_t)c->rank * (c->part_S + a.part_FB) + c->part_S;
+    }
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
     if (c->tl) {
@@ -1657,14 +1699,16 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
             h[v] = (uint8_t)C0[v];
         }
-        MCMC_HIP_TRY(hipMemcpyAsync(c->colors[0], h.data(), n, hipMemcpyHostToDevice, c->stream));
+        int rc = upload_colors(c, c->colors[0], h.data());
+        if (rc) return rc;
         c->initDraws = n;
     } else {
         DevState zero{};
         MCMC_HIP_TRY(hipMemcpyAsync(c->st, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
         const UniformIntConst k = uniform_int_const(c->p.nCol);
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
-        init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st);
+        init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st, c->part ? c->part_S : 0u,
+                                                             c->part ? 4u * kFooterWords : 0u);
         MCMC_HIP_TRY(hipGetLastError());
         DevState h;
         int rc = download_state(c, &h);
@@ -1680,7 +1724,8 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
                 do { x = minstd_mulmod(x, kMinstdA); r = x - 1u; draws++; } while (r >= k.past);
                 hc[v] = (uint8_t)(r / k.scaling);
             }
-            MCMC_HIP_TRY(hipMemcpyAsync(c->colors[0], hc.data(), n, hipMemcpyHostToDevice, c->stream));
+            rc = upload_colors(c, c->colors[0], hc.data());
+            if (rc) return rc;
         }
         c->initDraws = draws;
     }
@@ -1760,8 +1805,8 @@ int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out) {
         which = h.t & 1;
     }
     std::vector<uint8_t> tmp(c->n);
-    MCMC_HIP_TRY(hipMemcpyAsync(tmp.data(), c->colors[which], c->n, hipMemcpyDeviceToHost, c->stream));
-    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    int rc = download_colors(c, c->colors[which], tmp.data());
+    if (rc) return rc;
     for (uint32_t v = 0; v < c->n; v++) out[v] = tmp[v];
     return MCMC_OK;
 }
@@ -1894,19 +1939,30 @@ void mcmc_destroy(mcmc_ctx* c) {
 }
 
 // ---- vertex-partitioned step (device-resident; exchange by the caller) -----------------------
+int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P) {
+    if (!S || !P) return fail(MCMC_E_ARG, "NULL argument");
+    if (world == 0 || world > 64) return fail(MCMC_E_ARG, "bad world (1..64 ranks)");
+    const uint64_t s = (((uint64_t)n + world - 1) / world + 15) / 16 * 16;
+    *S = s;
+    *P = s + 4ull * kFooterWords;
+    return MCMC_OK;
+}
+
 int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
-                     uint64_t colors_bytes, void* footer, void* footers_all, void* stream) {
-    if (!c || !colors0 || !colors1 || !footer || !footers_all) return fail(MCMC_E_ARG, "NULL argument");
+                     uint64_t colors_bytes, void* stream) {
+    if (!c || !colors0 || !colors1) return fail(MCMC_E_ARG, "NULL argument");
     if (world == 0 || world > 64 || rank >= world) return fail(MCMC_E_ARG, "bad world/rank (1..64 ranks)");
-    const uint64_t S = ((uint64_t)c->n + world - 1) / world;
-    if (colors_bytes < S * world || colors_bytes < (uint64_t)c->n + 16)
-        return fail(MCMC_E_ARG, "colour buffers must hold world * ceil(n/world) and n + 16 bytes");
+    if (c->variant != 3) return fail(MCMC_E_STATE, "partitioned contexts need the tiled sweep (MCMC_GATHER=tiled)");
+    uint64_t S = 0, P = 0;
+    (void)mcmc_part_layout(c->n, world, &S, &P);
+    if (colors_bytes < P * world) return fail(MCMC_E_ARG, "colour buffers must hold world * P bytes (mcmc_part_layout)");
+    if (S * world + 4ull * kFooterWords * world > 0xFFFFFFF0ull)
+        return fail(MCMC_E_ARG, "partitioned colour buffers beyond 4 GiB are not supported");
     if (c->v_begin != std::min<uint64_t>(S * rank, c->n) || c->v_end != std::min<uint64_t>(S * (rank + 1), c->n))
-        return fail(MCMC_E_ARG, "context rows must be [rank*S, min(n,(rank+1)*S)), S = ceil(n/world)");
+        return fail(MCMC_E_ARG, "context rows must be [rank*S, min(n,(rank+1)*S)) (mcmc_part_layout)");
     c->colors[0] = static_cast<uint8_t*>(colors0);
     c->colors[1] = static_cast<uint8_t*>(colors1);
-    c->footer = static_cast<uint32_t*>(footer);
-    c->footers_all = static_cast<const uint32_t*>(footers_all);
+    c->part_S = (uint32_t)S;
     c->world = world;
     c->rank = rank;
     c->part = true;

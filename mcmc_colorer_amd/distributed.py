@@ -2,15 +2,17 @@
 
 SURVEY.md §8e. The sweep of vertex v depends only on the colours of N(v), on u_v (a function of the
 global id and the sweep number) and on taboo[v], so rows shard exactly. Rank r of R owns rows
-[r*S, min(n,(r+1)*S)), S = ceil(n/R), keeps global ids and a full colour replica. Per sweep:
+[r*S, min(n,(r+1)*S)), S = ceil(n/R) rounded up to 16, keeps global ids and a full colour replica.
+A colour buffer is R regions of P = S + 4096 bytes: region r holds the colours of rank r's rows
+followed by rank r's footer (local Cviol + sorted overflow events). Per sweep:
 
-  1. local sweep (HIP kernel): next colours of the owned rows + a footer with the local Cviol and
-     the sorted overflow events,
-  2. ``all_gather_into_tensor`` of the colour slabs (n bytes in total) and of the footers,
+  1. local sweep (HIP kernel): next colours of the owned rows + the footer, into the rank's own
+     region of the next-colour buffer,
+  2. ONE in-place ``all_gather_into_tensor`` of the regions (colours and footers together),
   3. commit (HIP kernel) on every rank: global Cviol, stop test, the rank-ordered (= ascending)
      glibc replay with the replicated glibc window -- replicas stay identical.
 
-Everything is enqueued on torch's current stream (the RCCL collectives synchronise with it), and
+Everything is enqueued on torch's current stream (the RCCL collective synchronises with it), and
 the host only reads the device ``done`` flag every ``check_every`` sweeps. The result is
 bit-identical to the single-GPU run and to --mcmccpu (tests/test_gpu_parity.py,
 tests/test_distributed.py).
@@ -32,9 +34,15 @@ FOOTER_WORDS = 1024   # MCMC_FOOTER_WORDS
 
 
 def partition(n: int, world: int, rank: int) -> tuple[int, int, int]:
-    """(S, v_begin, v_end) of rank ``rank``: S = ceil(n/world), rows [rank*S, min(n,(rank+1)*S))."""
-    S = (n + world - 1) // world
+    """(S, v_begin, v_end) of rank ``rank``: S = ceil(n/world) rounded up to 16 (mcmc_part_layout),
+    rows [rank*S, min(n,(rank+1)*S))."""
+    S = ((n + world - 1) // world + 15) // 16 * 16
     return S, min(rank * S, n), min((rank + 1) * S, n)
+
+
+def region_bytes(n: int, world: int) -> int:
+    """P: bytes of one rank's region of a partitioned colour buffer (slab + footer)."""
+    return partition(n, world, 0)[0] + 4 * FOOTER_WORDS
 
 
 class HipRank:
@@ -49,11 +57,12 @@ class HipRank:
         self.S, self.v_begin, self.v_end = partition(self.n, world, rank)
         self.graph = graph
         self.params = params
-        size = max(world * self.S, self.n + 16) + 256
+        S, P = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().mcmc_part_layout(self.n, world, ctypes.byref(S), ctypes.byref(P)))
+        assert S.value == self.S
+        self.P = P.value
+        size = world * self.P + 256
         self.colors = [torch.zeros(size, dtype=torch.uint8, device=device) for _ in range(2)]
-        self.footer = torch.zeros(FOOTER_WORDS, dtype=torch.int32, device=device)
-        self.footers_all = torch.zeros(world * FOOTER_WORDS, dtype=torch.int32, device=device)
-        self.send = torch.zeros(self.S, dtype=torch.uint8, device=device)
         self._ctx = ctypes.c_void_p()
         self._size = size
         self._make(seed)
@@ -67,8 +76,7 @@ class HipRank:
                                 ctypes.byref(self._ctx)))
         stream = self.torch.cuda.current_stream().cuda_stream
         check(lib().mcmc_part_attach(self._ctx, self.world, self.rank, self.colors[0].data_ptr(),
-                                     self.colors[1].data_ptr(), self._size, self.footer.data_ptr(),
-                                     self.footers_all.data_ptr(), ctypes.c_void_p(stream)))
+                                     self.colors[1].data_ptr(), self._size, ctypes.c_void_p(stream)))
 
     def init(self, seed: int, glibc: GlibcRand) -> None:
         self._make(seed)
@@ -86,10 +94,10 @@ class HipRank:
         check(lib().mcmc_part_state(self._ctx, ctypes.byref(done), ctypes.byref(t), ctypes.byref(err)))
         return bool(done.value), t.value, err.value
 
-    def slab(self, t: int):
-        """(full next-colour buffer of sweep t, this rank's slab of it)."""
+    def region(self, t: int):
+        """(all regions of sweep t's next-colour buffer, this rank's region of it)."""
         nxt = self.colors[(t + 1) & 1]
-        return nxt, nxt[self.rank * self.S:(self.rank + 1) * self.S]
+        return nxt[: self.world * self.P], nxt[self.rank * self.P:(self.rank + 1) * self.P]
 
     def glibc_window(self, glibc: GlibcRand) -> None:
         check(lib().mcmc_get_glibc_window(self._ctx, u32ptr(glibc.window)))
@@ -144,14 +152,18 @@ class PartitionedColoringMCMC:
                               torch.device("cuda", torch.cuda.current_device()))
         self.b = backend
         self.sweeps = 0
+        # RCCL gathers in place (send = this rank's slot of the receive buffer); other backends
+        # get a copy of the region
+        self.inplace = dist.get_backend(group) == "nccl"
 
     def _step(self, t: int) -> None:
         b = self.b
         b.sweep()
-        nxt, mine = b.slab(t)
-        b.send.copy_(mine)
-        self.dist.all_gather_into_tensor(nxt[: self.world * b.S], b.send, group=self.group)
-        self.dist.all_gather_into_tensor(b.footers_all, b.footer, group=self.group)
+        regions, mine = b.region(t)
+        if self.inplace:
+            self.dist.all_gather_into_tensor(regions, mine, group=self.group)   # one collective per sweep
+        else:
+            self.dist.all_gather_into_tensor(regions, mine.clone(), group=self.group)
         b.commit()
 
     def run(self, iteration: int = 0, max_sweeps: int = 0):

@@ -2,7 +2,8 @@
 
 It restates, in numpy/float32, the partitioned protocol the HIP kernels implement (sweep of the
 owned rows -> footer [Cviol_local, E, flags, sorted events] -> all-gather -> commit with the
-rank-ordered glibc replay), using the oracle_np RNG restatements. Driving the product's driver
+rank-ordered glibc replay), with the same partitioned buffer layout (per-rank regions of colours
+followed by the footer, one all-gather per sweep), using the oracle_np RNG restatements. Driving the product's driver
 over gloo with this backend checks the exchange sequence and the protocol on CPU; the HIP side of
 the same protocol is checked on the GPU (tests/test_gpu_parity.py::test_partitioned_lockstep).
 """
@@ -23,13 +24,19 @@ class NumpyRank:
         self.n = len(off) - 1
         self.nCol, self.eps, self.maxRip, self.tabooIter, self.z = nCol, np.float32(eps), maxRip, taboo, z
         self.world, self.rank = world, rank
-        self.S = (self.n + world - 1) // world
+        # region layout of mcmc_part_layout: S = ceil(n/world) rounded up to 16, region r =
+        # [colours of rows r*S .. r*S+S-1 | footer of rank r], P = S + 4*FOOTER_WORDS bytes
+        self.S = ((self.n + world - 1) // world + 15) // 16 * 16
+        self.P = self.S + 4 * FOOTER_WORDS
         self.v_begin, self.v_end = min(rank * self.S, self.n), min((rank + 1) * self.S, self.n)
-        size = max(world * self.S, self.n + 16) + 256
-        self.colors = [torch.zeros(size, dtype=torch.uint8) for _ in range(2)]
-        self.footer = torch.zeros(FOOTER_WORDS, dtype=torch.int32)
-        self.footers_all = torch.zeros(world * FOOTER_WORDS, dtype=torch.int32)
-        self.send = torch.zeros(self.S, dtype=torch.uint8)
+        self.colors = [torch.zeros(world * self.P + 256, dtype=torch.uint8) for _ in range(2)]
+
+    def _view(self, buf):
+        """Colours of all n vertices (a copy) from a partitioned buffer."""
+        return np.concatenate([buf[r * self.P: r * self.P + self.S].numpy() for r in range(self.world)])[: self.n]
+
+    def _put(self, buf, v, c):
+        buf[(v // self.S) * self.P + v % self.S] = c
 
     # -- interface used by PartitionedColoringMCMC ------------------------------------------------
     def init(self, seed, glibc):
@@ -39,7 +46,8 @@ class NumpyRank:
         for v in range(self.n):
             C[v], d = NP.uniform_int(gen, self.nCol)
             draws += d
-        self.colors[0][: self.n] = torch.from_numpy(C.astype(np.uint8))
+        for v in range(self.n):
+            self._put(self.colors[0], v, int(C[v]))
         self.x0 = gen.x                      # engine state after K0 draws
         self.t, self.done, self.err = 0, False, 0
         self.ring = [int(w) for w in glibc.window]   # oldest first
@@ -56,7 +64,7 @@ class NumpyRank:
         if self.done:
             return
         t, n = self.t, self.n
-        C = self.colors[t & 1][:n].numpy().astype(np.int64)
+        C = self._view(self.colors[t & 1]).astype(np.int64)
         nxt = self.colors[(t + 1) & 1]
         viol_local, events = 0, []
         xt = (self.x0 * pow(NP.A_MINSTD, t * n, M31)) % M31
@@ -71,7 +79,7 @@ class NumpyRank:
             l = v - self.v_begin
             if self.taboo[l] > 0:
                 self.taboo[l] -= 1
-                nxt[v] = int(C[v])
+                self._put(nxt, v, int(C[v]))
                 continue
             u = NP.canonical((xt * pow(NP.A_MINSTD, v + 1, M31)) % M31)
             if viol and zvcomp > 0:
@@ -87,19 +95,21 @@ class NumpyRank:
                     break
             if new == self.nCol:
                 events.append(v)
-                nxt[v] = int(C[v])
+                self._put(nxt, v, int(C[v]))
             else:
-                nxt[v] = new
+                self._put(nxt, v, new)
                 self.taboo[l] = self.tabooIter if new == C[v] else 0
         f = np.zeros(FOOTER_WORDS, dtype=np.uint32)
         f[0], f[1], f[2] = viol_local & 0xFFFFFFFF, viol_local >> 32, len(events)
         f[4:4 + len(events)] = sorted(events)
-        self.footer.copy_(torch.from_numpy(f.view(np.int32)))
+        off = self.rank * self.P + self.S
+        nxt[off: off + 4 * FOOTER_WORDS] = torch.from_numpy(f.view(np.uint8))
 
     def commit(self):
         if self.done:
             return
-        F = self.footers_all.numpy().view(np.uint32).reshape(self.world, FOOTER_WORDS)
+        nb = self.colors[(self.t + 1) & 1].numpy()
+        F = np.stack([nb[r * self.P + self.S: (r + 1) * self.P].view(np.uint32) for r in range(self.world)])
         viol = int(sum(int(r[0]) | (int(r[1]) << 32) for r in F))
         events = [int(e) for r in F for e in r[4:4 + int(r[2])]]
         t = self.t
@@ -107,11 +117,11 @@ class NumpyRank:
         if t == self.maxRip + 1 or viol <= self.z:
             self.done, self.iter, self.final = True, t, viol
             return
-        C = self.colors[t & 1]
+        C = self._view(self.colors[t & 1])
         nxt = self.colors[(t + 1) & 1]
         for v in events:                     # ascending: ranks own ascending ranges
             c = self._glibc() % (self.nCol - 1)
-            nxt[v] = c
+            self._put(nxt, v, c)
             if self.v_begin <= v < self.v_end:
                 self.taboo[v - self.v_begin] = self.tabooIter if c == int(C[v]) else 0
         self.t = t + 1
@@ -119,15 +129,15 @@ class NumpyRank:
     def state(self):
         return self.done, self.t, self.err
 
-    def slab(self, t):
+    def region(self, t):
         nxt = self.colors[(t + 1) & 1]
-        return nxt, nxt[self.rank * self.S:(self.rank + 1) * self.S]
+        return nxt[: self.world * self.P], nxt[self.rank * self.P:(self.rank + 1) * self.P]
 
     def glibc_window(self, glibc):
         glibc.window[:] = np.array(self.ring, dtype=np.uint32)
 
     def coloring(self):
-        return self.colors[self.t & 1][: self.n].numpy().astype(np.uint32)
+        return self._view(self.colors[self.t & 1]).astype(np.uint32)
 
     def trajectory(self):
         return np.array(self.traj, dtype=np.uint64)

@@ -223,7 +223,8 @@ def test_c2_full_run_matches_golden(M):
 
 def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, draws=None):
     """`world` HipRank backends on one GPU, exchanged by tensor copies in lock-step: the device
-    side of the partitioned protocol (footer pack, all-gather layout, rank-ordered replay)."""
+    side of the partitioned protocol (region layout: colours + footer per rank, one all-gather,
+    rank-ordered replay)."""
     import torch
 
     from mcmc_colorer_amd.distributed import HipRank
@@ -238,11 +239,9 @@ def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, dra
     while t < maxRip + 2:
         for b in ranks:
             b.sweep()
-        slabs = torch.cat([b.slab(t)[1] for b in ranks])
-        foot = torch.cat([b.footer for b in ranks])
+        gathered = torch.cat([b.region(t)[1] for b in ranks])   # the all-gather of the regions
         for b in ranks:
-            b.slab(t)[0][: world * b.S].copy_(slabs)
-            b.footers_all.copy_(foot)
+            b.region(t)[0].copy_(gathered)
         for b in ranks:
             b.commit()
         t += 1
@@ -320,8 +319,8 @@ def test_c2_blocked_matches_golden(M, monkeypatch, gather):
 
 
 @pytest.mark.parametrize("world", [2, 5])
-@pytest.mark.parametrize("gather", ["blocked:9", "tiled:9", "tiled:9:::1"])
-def test_partitioned_lockstep_blocked(M, monkeypatch, world, gather):
+@pytest.mark.parametrize("gather", ["tiled:9", "tiled:9:::1", "tiled:6:1:5:1"])
+def test_partitioned_lockstep_tiled(M, monkeypatch, world, gather):
     set_gather(monkeypatch, gather)
     off, idx, nc, r = oracle_case(3000, 0.03, 20, 61, maxRip=30)
     ranks = _lockstep(M, off, idx, nc, 61, world, maxRip=30)
