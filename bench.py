@@ -76,6 +76,22 @@ def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window:
     }
 
 
+def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: float) -> dict:
+    """The reference CUDA path's per-sweep structure re-expressed in HIP (mcmc_refstruct_bench):
+    the stand-in for 'the reference CUDA path's vertex-updates/sec', which cannot run on MI355X."""
+    from mcmc_colorer_amd._lib import check, lib
+
+    ms = ctypes.c_double()
+    conf = ctypes.c_uint64()
+    check(lib().mcmc_refstruct_bench(g.handle, ncol, sweeps, seed, ctypes.byref(ms), ctypes.byref(conf)))
+    v = n / (ms.value * 1e-3)
+    return {"value": v, "unit": "vertex-updates/s", "ms_per_sweep": ms.value, "sweeps": sweeps,
+            "speedup": value / v,
+            "what": "HIP re-expression of ColoringMCMC::run's per-sweep structure (thread-per-vertex serial "
+                    "row walks, 64-thread blocks, n*nCol checker memset, 2 conflict passes + host sums, 4n B "
+                    "D2H + host histogram + H2D), same graph, host wall per sweep"}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,6 +102,8 @@ def main() -> int:
     ap.add_argument("--ncol", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-refstruct", action="store_true", help="skip the refstruct (reference-structure) leg")
+    ap.add_argument("--refstruct-sweeps", type=int, default=10)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
     ap.add_argument("--variant", default=None,
@@ -203,6 +221,8 @@ def main() -> int:
                      "layout": info},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not a.no_refstruct:
+        out["refstruct"] = refstruct_baseline(g, a.ncol, a.refstruct_sweeps, a.seed, n, value)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         s = g.getStruct()
         out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed,

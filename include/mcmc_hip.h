@@ -145,6 +145,16 @@ typedef struct mcmc_ctx_info {
 int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out);
 void mcmc_destroy(mcmc_ctx* c);
 
+/* ---- measurement baseline (not part of the colouring path) ----------------------------------
+ * "refstruct" (SURVEY.md §8d): the reference CUDA path's per-sweep structure re-expressed in HIP --
+ * thread-per-vertex serial row walks in 64-thread blocks, an n*nCol byte checker reset per sweep, two
+ * edge-conflict passes with host-side sums, a 4n-byte D2H + host histogram + H2D per sweep
+ * (coloringMCMC_main.cu:168-262, coloringMCMC_utils.cu:103-198, coloringMCMC_balance.cu:79-143).
+ * Runs `sweeps` sweeps of it on `g` and returns the host wall time per sweep. Its colouring follows
+ * the reference GPU semantics (XORWOW draws), so it is timed, never compared. */
+int mcmc_refstruct_bench(const mcmc_graph* g, uint32_t nCol, uint32_t sweeps, uint32_t seed,
+                         double* ms_per_sweep, uint64_t* conflicts);
+
 /* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------
  * SURVEY.md §8e. Rank r of `world` sweeps rows [r*S, min(n,(r+1)*S)) with global
  * ids and full-length colour replicas. A partitioned colour buffer is a sequence of per-rank

@@ -39,6 +39,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
+    "mcmc_refstruct_bench": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_double), _u64p]),
     "mcmc_destroy": (None, [c_void_p]),
     "mcmc_part_layout": (c_int, [c_uint32, c_uint32, _u64p, _u64p]),
     "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]),

@@ -327,3 +327,19 @@ def test_partitioned_lockstep_tiled(M, monkeypatch, world, gather):
     for b in ranks:
         assert b.coloring().tolist() == r.colors.tolist()
         assert b.trajectory().tolist() == r.traj.tolist()
+
+
+def test_refstruct_baseline_runs(M):
+    """The refstruct timing baseline (reference per-sweep structure) runs and counts conflicts."""
+    import ctypes
+
+    from mcmc_colorer_amd._lib import check, lib
+
+    O.srand(1)
+    off, idx = O.setup_rnd2(2000, 0.05)
+    g = M.Graph.from_csr(off, idx)
+    ms, conf = ctypes.c_double(), ctypes.c_uint64()
+    check(lib().mcmc_refstruct_bench(g.handle, 8, 3, 1, ctypes.byref(ms), ctypes.byref(conf)))
+    assert ms.value > 0
+    # monochromatic edges of a colouring with 8 colours on ~50 000 edges: some, not all
+    assert 0 < conf.value < len(idx) // 2
