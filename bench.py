@@ -95,6 +95,10 @@ def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: floa
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2: configs[1] (--simulate 0.01 -n 1e5, 16 colours; weak scaling at N > 1); "
+                         "c3: configs[2]/[3] (n 1e7, p 0.001, 32 colours, the build's G(n,p) generator; "
+                         "N > 1 partitions the same graph: strong scaling)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--vertices", type=int, default=100000, help="n of --simulate (per GPU under weak scaling)")
@@ -132,11 +136,19 @@ def main() -> int:
 
     dev = local
     n_req, p_req = a.vertices, a.prob
-    if world > 1 and a.scaling == "weak":
+    if a.config == "c3":
+        n_req, p_req, a.ncol, a.scaling = 10_000_000, 0.001, 32, "strong"
+    elif world > 1 and a.scaling == "weak":
         n_req, p_req = a.vertices * world, a.prob / world
     t_gen = time.perf_counter()
     rng = M.GlibcRand(1)
-    g = M.Graph.simulate(n_req, p_req, rng, device=dev)
+    if a.config == "c3":
+        # setupRnd2 is infeasible at n = 1e7 (5e13 draws): the build's documented generator, fixed seed 1,
+        # written straight into the tiled layout; under torchrun each rank generates only its rows
+        g = M.Graph.er_fast(n_req, p_req, 1, device=dev, world=world if dist is not None else 1,
+                            rank=rank if dist is not None else 0)
+    else:
+        g = M.Graph.simulate(n_req, p_req, rng, device=dev)
     t_gen = time.perf_counter() - t_gen
     params = M.ColoringMCMCParams(nCol=a.ncol, maxRip=0x7FFFFFF0)   # throughput mode: no cap
     tot = ctypes.c_double()
@@ -188,6 +200,12 @@ def main() -> int:
         wall = float(w.item())
 
     n, m = g.nNodes, g.nEdges
+    if dist is not None and a.config == "c3":   # per-rank graphs hold their rows' arcs only
+        import torch
+
+        mt = torch.tensor([m], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(mt)
+        m = int(mt.item())
     value = n * a.steps / wall          # all ranks together update n vertices per sweep
     # dominant kernel's bytes per launch on this rank: B_fmt of the layout it streams (SURVEY.md
     # §8d: with a compressed format the fraction is taken against the format's bytes), and the
@@ -195,7 +213,7 @@ def main() -> int:
     b_fmt, b_ref = info["sweep_bytes"], info["ref_bytes"]
     achieved = b_fmt / (kernel_ms * 1e-3) / 1e9
     variant = info["variant"]
-    key = f"c2/{variant}" if (world == 1 and n_req == 100000) else None
+    key = f"{a.config}/{variant}" if (world == 1 and (a.config == "c3" or n_req == 100000)) else None
     out = {
         "metric": "vertex-updates/sec per MCMC sweep",
         "value": value,
@@ -208,8 +226,10 @@ def main() -> int:
         "scaling": "weak" if (world == 1 or a.scaling == "weak") else "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (reference --simulate generator replayed exactly on the GPU)",
+        "data": ("synthetic (reference --simulate generator replayed exactly on the GPU)" if a.config == "c2" else
+                 "synthetic G(n,p) (the build's counter-based generator, er_gen.h, seed 1; setupRnd2 infeasible at n=1e7)"),
         "config": {"workload": f"--mcmcgpu --simulate {p_req:g} -n {n_req} --nCol {a.ncol} --seed {a.seed}",
+                   "config": a.config,
                    "n": n, "arcs": m, "nCol": a.ncol,
                    "parallelism": f"vertex-partitioned x{world} (RCCL all-gather per sweep)" if world > 1 else "single",
                    "graph_gen_s": round(t_gen, 3)},
@@ -221,12 +241,27 @@ def main() -> int:
                      "layout": info},
         "cpu_baseline": None,
     }
+    # CPU and refstruct legs: on the benchmarked graph for c2; for c3 (no CSR can exist: 400 GB) on
+    # --simulate 0.1 -n 100000, which has C3's mean degree 1e4 (per-vertex work is per-degree)
+    sample, sample_n, sample_window, sample_note = g, n, None, None
+    if rank == 0 and world == 1 and not (a.no_refstruct and a.no_cpu_baseline):
+        if a.config == "c3":
+            g.close()
+            r2 = M.GlibcRand(1)
+            sample = M.Graph.simulate(100000, 0.1, r2, device=dev)
+            sample_n, sample_window = 100000, r2.window.copy()
+            sample_note = "--simulate 0.1 -n 100000 (mean degree 1e4 = C3's; C3's CSR cannot exist: 400 GB)"
+        else:
+            sample_window = M.GlibcRand(1, n_req * (n_req + 1) // 2).window
     if rank == 0 and world == 1 and not a.no_refstruct:
-        out["refstruct"] = refstruct_baseline(g, a.ncol, a.refstruct_sweeps, a.seed, n, value)
+        out["refstruct"] = refstruct_baseline(sample, a.ncol, a.refstruct_sweeps, a.seed, sample_n, value)
+        if sample_note:
+            out["refstruct"]["graph"] = sample_note
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        s = g.getStruct()
-        out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed,
-                                           M.GlibcRand(1, n_req * (n_req + 1) // 2).window, n)
+        s = sample.getStruct()
+        out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed, sample_window, sample_n)
+        if sample_note:
+            out["cpu_baseline"]["sample"] += "; graph " + sample_note
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

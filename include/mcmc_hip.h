@@ -87,9 +87,17 @@ int mcmc_graph_upload(const uint64_t* row_off, const uint32_t* col_idx, uint32_t
  * the n(n+1)/2 glibc draws start at `window` (advanced on return, as the reference's global
  * stream is). Neighbour lists ascending, as the reference's. */
 int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device, mcmc_graph** out);
-/* Fast Erdos-Renyi G(n,p) stand-in (counter-based, geometric skips) for sizes where the
- * reference's O(n^2) generator is infeasible. Not the reference's graph. */
+/* Fast Erdos-Renyi G(n,p) for sizes where the reference's O(n^2) setupRnd2 is infeasible
+ * (not the reference's graph): counter-based Philox4x32-10 streams with
+ * geometric skips, fully defined in mcmc_colorer_amd/csrc/er_gen.h (p is used as (double)(float)).
+ * The graph is written straight into the sweep's tiled layout -- no CSR is materialised (C3's
+ * would be 400 GB) -- so the handle serves mcmc_create and mcmc_graph_info; mcmc_graph_download
+ * reconstructs a CSR (small graphs), mcmc_graph_device_ptrs fails. _part generates only the rows
+ * rank `rank` of `world` owns (mcmc_part_layout), for a partitioned run; its m counts those rows'
+ * arcs. */
 int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out);
+int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t world, uint32_t rank, int device,
+                            mcmc_graph** out);
 int mcmc_graph_info(const mcmc_graph* g, uint32_t* n, uint64_t* m, uint32_t* maxDeg, uint32_t* minDeg);
 /* Device pointers (row_off: uint64[n+1], col_idx: uint32[m]) for zero-copy callers. */
 int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const uint32_t** col_idx);

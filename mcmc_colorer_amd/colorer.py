@@ -99,6 +99,20 @@ class Graph:
         return cls(h, prob=float(np.float32(prob)), device=device)
 
     @classmethod
+    def er_fast(cls, n: int, prob: float, seed: int, device: int = 0, world: int = 1, rank: int = 0) -> "Graph":
+        """The build's counter-based G(n, p) (csrc/er_gen.h) for sizes where setupRnd2 is infeasible
+        (SURVEY.md §8d C3/C4), generated on the GPU straight into the sweep's tiled layout.
+        world > 1: only the rows rank ``rank`` owns (a partitioned run); nEdges then counts those."""
+        h = ctypes.c_void_p()
+        if world == 1:
+            check(lib().mcmc_graph_er_fast(n, float(prob), seed, device, ctypes.byref(h)))
+        else:
+            check(lib().mcmc_graph_er_fast_part(n, float(prob), seed, world, rank, device, ctypes.byref(h)))
+        g = cls(h, prob=float(np.float32(prob)), device=device)
+        g.generated = True
+        return g
+
+    @classmethod
     def from_csr(cls, row_off: np.ndarray, col_idx: np.ndarray, device: int = 0, prob: float = 0.0) -> "Graph":
         """Graph(Graph* host) device copy (graphGPU.cu:210-226) of a host CSR."""
         row_off = np.ascontiguousarray(row_off, dtype=np.uint64)

@@ -320,6 +320,7 @@ int mcmc_graph_info(const mcmc_graph* g, uint32_t* n, uint64_t* m, uint32_t* max
 
 int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const uint32_t** col_idx) {
     if (!g) return fail(MCMC_E_ARG, "NULL graph");
+    if (!g->g.row_off) return fail(MCMC_E_STATE, "generated graph: no device CSR (tiled layout only)");
     if (row_off) *row_off = g->g.row_off;
     if (col_idx) *col_idx = g->g.col_idx;
     return MCMC_OK;
@@ -328,6 +329,10 @@ int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const 
 int mcmc_graph_download(const mcmc_graph* g, uint64_t* row_off, uint32_t* col_idx) {
     if (!g) return fail(MCMC_E_ARG, "NULL graph");
     MCMC_HIP_TRY(hipSetDevice(g->g.device));
+    if (!g->g.row_off) {   // generated graph: rebuild the CSR from its tiled layout
+        if (!row_off || !col_idx) return fail(MCMC_E_ARG, "generated graph: download needs both arrays");
+        return tiled_to_csr(g, row_off, col_idx);
+    }
     if (row_off)
         MCMC_HIP_TRY(hipMemcpy(row_off, g->g.row_off, sizeof(uint64_t) * ((size_t)g->g.n + 1), hipMemcpyDeviceToHost));
     if (col_idx && g->g.m)
@@ -344,10 +349,5 @@ void mcmc_graph_destroy(mcmc_graph* g) {
     delete g;
 }
 
-int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out) {
-    (void)n; (void)prob; (void)seed; (void)device;
-    if (out) *out = nullptr;
-    return fail(MCMC_E_STATE, "mcmc_graph_er_fast: not implemented in this build");
-}
 
 }  // extern "C"

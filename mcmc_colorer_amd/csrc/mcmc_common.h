@@ -39,6 +39,8 @@ int sort_rows_inplace(GraphDev& g);
 
 }  // namespace mcmc
 
+struct mcmc_graph;
+
 namespace mcmc {
 // Tiled copy of a row range of the CSR (sweep variant 3, mcmc_sweep.hip): rows in groups of
 // grp_rows, per group the arcs block-major as 16-bit block-local ids, every (row, block) segment
@@ -46,11 +48,23 @@ namespace mcmc {
 struct TiledLayout {
     uint32_t v_begin = 0, v_end = 0, grp_rows = 0, block_log2 = 0, nblocks = 0, ngroups = 0;
     uint64_t ids = 0;              // padded length of tcol
+    uint64_t arcs = 0;             // arcs of the rows (unpadded)
     uint16_t* tcol = nullptr;
     uint64_t* gbase = nullptr;     // [ngroups + 1]
     uint32_t* tseg = nullptr;      // [ngroups][nblocks][grp_rows + 1]
     ~TiledLayout();
 };
+}  // namespace mcmc
+
+namespace mcmc {
+// Builds (or finds in the graph's cache) the tiled layout of rows [v_begin, v_end) (tiled_layout.hip).
+int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t R, uint32_t block_log2,
+                     hipStream_t s, const TiledLayout** out);
+// Default rows per group of a tiled layout on nloc rows (mcmc_create and the generator agree).
+uint32_t tiled_default_rows(uint32_t nloc, uint32_t cus, uint32_t rmax);
+constexpr uint32_t kTileGenRowsMax = 4095;   // generator layouts: R + 1 <= 4 * 1024 (segment prefetch)
+// CSR (ascending rows) of a generated graph with a full-range layout.
+int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx);
 }  // namespace mcmc
 
 struct mcmc_graph {

@@ -1018,126 +1018,9 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     MCMC_PHASE(a, 4);
 }
 
-// ---- tiled layout construction (once per context) ----------------------------------------------
-// Padded (to 8 ids) total of every group over all blocks.
-__global__ void tile_group_total_kernel(const uint32_t* __restrict__ seg, uint32_t nloc, uint32_t nb, uint32_t R,
-                                        uint32_t G, uint64_t* __restrict__ totals) {
-    __shared__ unsigned long long red[256];
-    for (uint32_t g = blockIdx.x; g < G; g += gridDim.x) {
-        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
-        unsigned long long s = 0;
-        for (uint32_t i = threadIdx.x; i < rows * nb; i += blockDim.x) {
-            const uint32_t b = i / rows, r = i % rows;
-            const uint32_t len = seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r];
-            s += (len + 7u) & ~7u;
-        }
-        red[threadIdx.x] = s;
-        __syncthreads();
-        for (uint32_t k = blockDim.x / 2; k > 0; k >>= 1) {
-            if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) totals[g] = red[0];
-        __syncthreads();
-    }
-}
-
-// tseg[g][b][r] = padded start of row r's block-b segment relative to the group base; entry R of
-// every block = its end (= the next block's start). Block scan over the rows, blocks in order.
-__global__ void tile_seg_kernel(const uint32_t* __restrict__ seg, uint32_t nloc, uint32_t nb, uint32_t R,
-                                uint32_t G, uint32_t* __restrict__ tseg) {
-    __shared__ uint32_t part[256];
-    __shared__ uint32_t run_sh;
-    for (uint32_t g = blockIdx.x; g < G; g += gridDim.x) {
-        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
-        const uint32_t per = (R + blockDim.x - 1) / blockDim.x;   // consecutive rows per thread
-        if (threadIdx.x == 0) run_sh = 0;
-        __syncthreads();
-        for (uint32_t b = 0; b < nb; b++) {
-            const uint32_t ra = threadIdx.x * per, rb = min(R, ra + per);
-            uint32_t local = 0;
-            for (uint32_t r = ra; r < rb; r++) {
-                const uint32_t len = (r < rows) ? seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r] : 0u;
-                local += (len + 7u) & ~7u;
-            }
-            part[threadIdx.x] = local;
-            __syncthreads();
-            if (threadIdx.x == 0) {   // exclusive scan of the per-thread sums (blockDim <= 256)
-                uint32_t acc = 0;
-                for (uint32_t k = 0; k < blockDim.x; k++) { const uint32_t x = part[k]; part[k] = acc; acc += x; }
-            }
-            __syncthreads();
-            const uint32_t run = run_sh;
-            uint32_t* out = tseg + ((size_t)g * nb + b) * (R + 1);
-            uint32_t acc = run + part[threadIdx.x];
-            for (uint32_t r = ra; r < rb; r++) {
-                out[r] = acc;
-                const uint32_t len = (r < rows) ? seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r] : 0u;
-                acc += (len + 7u) & ~7u;
-            }
-            __syncthreads();
-            if (threadIdx.x == blockDim.x - 1) {
-                out[R] = acc;   // the last thread's running value is the block's end
-                run_sh = acc;
-            }
-            __syncthreads();
-        }
-    }
-}
-
-// Scatter: wave per local row; every arc to its padded block segment as a 16-bit local id, then
-// each segment's padding filled with copies of its first id (OR-idempotent).
-__global__ void tile_scatter_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
-                                    const uint32_t* __restrict__ seg, const uint64_t* __restrict__ gbase,
-                                    const uint32_t* __restrict__ tseg, uint32_t nloc, uint32_t nb, uint32_t R,
-                                    uint32_t block_log2, uint16_t* __restrict__ tcol) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t bmask = (1u << block_log2) - 1u;
-    for (uint32_t l = gw; l < nloc; l += nw) {
-        const uint32_t g = l / R, r = l % R;
-        const uint64_t rs = row_off[l], re = row_off[l + 1];
-        const uint64_t base = gbase[g];
-        const uint32_t* ts = tseg + (size_t)g * nb * (R + 1);
-        for (uint64_t k = rs + lane; k < re; k += 64) {
-            const uint32_t c = col_idx[k];
-            const uint32_t b = c >> block_log2;
-            const uint32_t rel = (uint32_t)(k - rs) - seg[(size_t)b * nloc + l];
-            tcol[base + ts[(size_t)b * (R + 1) + r] + rel] = (uint16_t)(c & bmask);
-        }
-        for (uint32_t b = lane; b < nb; b += 64) {
-            const uint32_t s0 = seg[(size_t)b * nloc + l], s1 = seg[(size_t)(b + 1) * nloc + l];
-            const uint32_t len = s1 - s0;
-            if (len & 7u) {
-                const uint16_t first = (uint16_t)(col_idx[rs + s0] & bmask);
-                const uint64_t p0 = base + ts[(size_t)b * (R + 1) + r];
-                for (uint32_t i = len; i < ((len + 7u) & ~7u); i++) tcol[p0 + i] = first;
-            }
-        }
-    }
-}
-
-// Segment offsets of every local row by column block: seg[b][l] = #neighbours of row l with id
-// < b*B (rows ascending), b = 0..nb. Thread per (block boundary, row) binary search.
+// Layout construction lives in tiled_layout.hip.
 __global__ void segment_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
-                               uint32_t nloc, uint32_t nb, uint32_t block_log2, uint32_t* __restrict__ seg) {
-    const uint64_t total = (uint64_t)(nb + 1) * nloc;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t b = (uint32_t)(i / nloc), l = (uint32_t)(i % nloc);
-        const uint64_t rs = row_off[l], re = row_off[l + 1];
-        if (b == 0) { seg[i] = 0; continue; }
-        if (b == nb) { seg[i] = (uint32_t)(re - rs); continue; }
-        const uint64_t key = (uint64_t)b << block_log2;
-        uint64_t lo = rs, hi = re;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (col_idx[mid] < key) lo = mid + 1; else hi = mid;
-        }
-        seg[i] = (uint32_t)(lo - rs);
-    }
-}
+                               uint32_t nloc, uint32_t nb, uint32_t block_log2, uint32_t* __restrict__ seg);
 
 // Arc-balanced static partition of the local rows over W waves: wave w starts at the first row
 // whose offset reaches w*m/W (lower bound), so every wave streams about m/W arcs.
@@ -1199,74 +1082,6 @@ hipError_t allow_lds(size_t bytes) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 constexpr size_t kMaxLdsBytes = 160 * 1024 - 1024;   // leave room for the static shared variables
-
-TiledLayout::~TiledLayout() {
-    (void)hipFree(tcol);
-    (void)hipFree(gbase);
-    (void)hipFree(tseg);
-}
-
-// Builds (or finds in the graph's cache) the tiled layout of rows [v_begin, v_end).
-int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t R, uint32_t block_log2,
-                     hipStream_t s, const TiledLayout** out) {
-    for (auto& t : gh->tiles)
-        if (t->v_begin == v_begin && t->v_end == v_end && t->grp_rows == R && t->block_log2 == block_log2) {
-            *out = t.get();
-            return MCMC_OK;
-        }
-    GraphDev& gd = gh->g;
-    if (!gd.sorted) {   // segments need ascending rows; neighbour order does not affect the sweep
-        int rs = sort_rows_inplace(gd);
-        if (rs) return rs;
-    }
-    auto L = std::make_unique<TiledLayout>();
-    const uint32_t nloc = v_end - v_begin;
-    L->v_begin = v_begin;
-    L->v_end = v_end;
-    L->grp_rows = R;
-    L->block_log2 = block_log2;
-    L->nblocks = (uint32_t)((((uint64_t)gd.n + 15) / 16 * 16 + (1ull << block_log2) - 1) >> block_log2);
-    L->ngroups = (nloc + R - 1) / R;
-    const uint32_t nb = L->nblocks, G = L->ngroups;
-    uint32_t* seg = nullptr;
-    uint64_t* totals = nullptr;
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0;
-    hipError_t e = hipSuccess;
-    auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
-    const size_t segn = (size_t)(nb + 1) * std::max<uint32_t>(nloc, 1);
-    chk(hipMalloc(&seg, sizeof(uint32_t) * segn));
-    chk(hipMalloc(&totals, sizeof(uint64_t) * (G + 1)));
-    chk(hipMalloc(&L->gbase, sizeof(uint64_t) * (G + 1)));
-    chk(hipMalloc(&L->tseg, sizeof(uint32_t) * std::max<size_t>((size_t)G * nb * (R + 1), 1)));
-    if (e == hipSuccess && nloc) {
-        segment_kernel<<<(uint32_t)std::min<size_t>((segn + 255) / 256, 65536), 256, 0, s>>>(
-            gd.row_off + v_begin, gd.col_idx, nloc, nb, block_log2, seg);
-        tile_group_total_kernel<<<std::min<uint32_t>(G, 65535), 256, 0, s>>>(seg, nloc, nb, R, G, totals);
-        chk(hipMemsetAsync(totals + G, 0, sizeof(uint64_t), s));
-        chk(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, totals, L->gbase, G + 1, s));
-        chk(hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16)));
-        if (e == hipSuccess) chk(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, totals, L->gbase, G + 1, s));
-        chk(hipMemcpyAsync(&L->ids, L->gbase + G, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        chk(hipStreamSynchronize(s));
-    }
-    if (e == hipSuccess) chk(hipMalloc(&L->tcol, sizeof(uint16_t) * (L->ids + 64)));
-    if (e == hipSuccess && nloc) {
-        chk(hipMemsetAsync(L->tcol, 0, sizeof(uint16_t) * (L->ids + 64), s));
-        tile_seg_kernel<<<std::min<uint32_t>(G, 65535), 256, 0, s>>>(seg, nloc, nb, R, G, L->tseg);
-        tile_scatter_kernel<<<2048, 256, 0, s>>>(gd.row_off + v_begin, gd.col_idx, seg, L->gbase, L->tseg, nloc, nb,
-                                                 R, block_log2, L->tcol);
-        chk(hipGetLastError());
-        chk(hipStreamSynchronize(s));
-    }
-    (void)hipFree(seg);
-    (void)hipFree(totals);
-    (void)hipFree(tmp);
-    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("tiled layout: ") + hipGetErrorString(e));
-    *out = L.get();
-    gh->tiles.push_back(std::move(L));
-    return MCMC_OK;
-}
 
 static std::once_flag g_const_once;
 static hipError_t g_const_err = hipSuccess;
@@ -1369,7 +1184,7 @@ int download_state(mcmc_ctx* c, DevState* h) {
 
 SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     SweepArgs a{};
-    a.row_off = c->g->row_off + c->v_begin;
+    a.row_off = c->g->row_off ? c->g->row_off + c->v_begin : nullptr;
     a.col_idx = c->g->col_idx;
     a.colors0 = c->colors[0];
     a.colors1 = c->colors[1];
@@ -1508,6 +1323,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     const std::string gsel = gv ? gv : "";
     c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
     if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
+    if (!gd.row_off) c->variant = 3;   // generated graph: tiled layout only
     const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
     hipError_t ea = hipSuccess;
     if (c->variant == 0) {
@@ -1529,7 +1345,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
            : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
     } else if (c->variant == 3) {
         const char* bl = getenv("MCMC_BLOCK_LOG2");
-        c->block_log2 = bl ? (uint32_t)std::max(4, std::min(16, atoi(bl))) : 16u;
+        c->block_log2 = (bl && gd.row_off) ? (uint32_t)std::max(4, std::min(16, atoi(bl))) : 16u;
     } else {
         static const SweepLaunch tab[4] = {launch_sweep<1, false>, launch_sweep<2, false>, launch_sweep<4, false>,
                                            launch_sweep<8, false>};
@@ -1589,12 +1405,16 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         const uint32_t lds_budget = resident ? (uint32_t)(kMaxLdsBytes - rep) : (uint32_t)(kMaxLdsBytes - c->slice_bytes);
         const uint32_t rmax = std::max<uint32_t>(1u, std::min<uint32_t>(kTileSegPer * c->block.x - 1u,
                                                                         (lds_budget - 4u) / ((c->nw + 1) * 4u)));
-        uint32_t R = (nloc + c->grid.x - 1) / std::max<uint32_t>(c->grid.x, 1);
-        R = std::max<uint32_t>(std::min<uint32_t>(32u, rmax), std::min<uint32_t>(rmax, R));
+        uint32_t R = tiled_default_rows(nloc, c->grid.x, rmax);
         if (gr) R = (uint32_t)std::max(1, std::min((int)rmax, atoi(gr)));
         c->variant_res = resident;
         int rs = get_tiled_layout(const_cast<mcmc_graph*>(g), v_begin, v_end, R, c->block_log2, c->stream, &c->tl);
         if (rs) { mcmc_destroy(c); return rs; }
+        R = c->tl->grp_rows;   // a generated graph's layout brings its own group size
+        if (R > rmax) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_ARG, "generated layout's group rows exceed this nCol's LDS budget (nCol > 128)");
+        }
         c->nblocks = c->tl->nblocks;
         // lanes per row segment: the smallest power of two L >= 4 with L * kTileU quads per step
         // covering half a mean segment (measured on C2 / n = 8e5: fewer lanes make the
@@ -1886,7 +1706,9 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
     mcmc_ctx_info i{};
     const uint64_t nloc = c->v_end - c->v_begin;
     uint64_t mloc = 0;
-    {
+    if (c->tl) {
+        mloc = c->tl->arcs;
+    } else {
         uint64_t ends[2];
         MCMC_HIP_TRY(hipMemcpy(&ends[0], c->g->row_off + c->v_begin, sizeof(uint64_t), hipMemcpyDeviceToHost));
         MCMC_HIP_TRY(hipMemcpy(&ends[1], c->g->row_off + c->v_end, sizeof(uint64_t), hipMemcpyDeviceToHost));

@@ -411,6 +411,85 @@ int oracle_setup_rnd2(uint32_t n, float prob, uint64_t** row_off, uint32_t** col
     return 0;
 }
 
+// ---- the build's counter-based G(n, p) (er_gen.h definition, restated) ----------------------------
+namespace {
+
+void philox10(uint32_t ctr[4], uint32_t key0, uint32_t key1) {
+    const uint32_t M[2] = {0xD2511F53u, 0xCD9E8D57u};
+    uint32_t k[2] = {key0, key1};
+    for (int round = 0; round < 10; round++) {
+        const uint64_t p0 = (uint64_t)M[0] * ctr[0];
+        const uint64_t p1 = (uint64_t)M[1] * ctr[2];
+        const uint32_t out[4] = {(uint32_t)(p1 >> 32) ^ ctr[1] ^ k[0], (uint32_t)p1,
+                                 (uint32_t)(p0 >> 32) ^ ctr[3] ^ k[1], (uint32_t)p0};
+        for (int q = 0; q < 4; q++) ctr[q] = out[q];
+        k[0] += 0x9E3779B9u;
+        k[1] += 0xBB67AE85u;
+    }
+}
+
+// ln(u), u in (0, 1]: u = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = 2 s (1 + s^2/3 + ... + s^24/25).
+double series_log(double u) {
+    uint64_t bits;
+    std::memcpy(&bits, &u, 8);
+    int e = (int)((bits >> 52) & 0x7FF) - 1023;
+    bits = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+    double m;
+    std::memcpy(&m, &bits, 8);
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double poly = 1.0 / 25.0;
+    for (int k = 11; k >= 0; k--) poly = poly * s2 + 1.0 / (double)(2 * k + 1);
+    return ((double)e * 6.93147180369123816490e-01 + 2.0 * s * poly) + (double)e * 1.90821492927058770002e-10;
+}
+
+}  // namespace
+
+int oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, uint32_t** col_idx, uint64_t* m) {
+    const double p = (double)(float)prob;
+    const int mode = p >= 1.0 ? 1 : (p <= 0.0 ? 2 : 0);
+    const double inv = mode == 0 ? 1.0 / std::log1p(-p) : 0.0;
+    const uint32_t T = 65536, nb = (uint32_t)(((uint64_t)n + T - 1) / T);
+    std::vector<std::pair<uint32_t, uint32_t>> edges;
+    for (uint32_t i = 0; i < n && mode != 2; i++) {
+        for (uint32_t Y = i / T; Y < nb; Y++) {
+            const uint64_t end = std::min<uint64_t>(n, (uint64_t)(Y + 1) * T);
+            uint64_t j = std::max<uint64_t>((uint64_t)Y * T, (uint64_t)i + 1);
+            if (j >= end) continue;
+            if (mode == 1) {
+                for (; j < end; j++) edges.emplace_back(i, (uint32_t)j);
+                continue;
+            }
+            j -= 1;
+            bool done = false;
+            for (uint32_t k = 0; !done; k++) {
+                uint32_t c[4] = {k, i, Y, 0x45524721u};
+                philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+                for (int q = 0; q < 4 && !done; q++) {
+                    const double t = series_log(((double)c[q] + 1.0) * 2.3283064365386963e-10) * inv;
+                    const uint64_t skip = (t < 2147483647.0) ? 1u + (uint32_t)t : 0x7FFFFFFFu;
+                    j += skip;
+                    if (j >= end) done = true;
+                    else edges.emplace_back(i, (uint32_t)j);
+                }
+            }
+        }
+    }
+    uint64_t* off = (uint64_t*)calloc((size_t)n + 1, sizeof(uint64_t));
+    if (!off) return -1;
+    for (auto& e : edges) { off[e.first + 1]++; off[e.second + 1]++; }
+    for (uint32_t v = 0; v < n; v++) off[v + 1] += off[v];
+    uint32_t* idx = (uint32_t*)malloc(std::max<uint64_t>(off[n], 1) * sizeof(uint32_t));
+    if (!idx) { free(off); return -1; }
+    std::vector<uint64_t> cur(off, off + n);
+    for (auto& e : edges) { idx[cur[e.first]++] = e.second; idx[cur[e.second]++] = e.first; }
+    for (uint32_t v = 0; v < n; v++) std::sort(idx + off[v], idx + off[v + 1]);
+    *row_off = off;
+    *col_idx = idx;
+    *m = off[n];
+    return 0;
+}
+
 // Graph::doStats (graphCPU.cpp:566-583) -> maxDeg, the default nCol (main.cu:162).
 uint32_t oracle_max_deg(uint32_t n, const uint64_t* row_off) {
     uint32_t maxDeg = 0;

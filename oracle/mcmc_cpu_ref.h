@@ -67,6 +67,14 @@ uint64_t oracle_uniform_int_seq(uint32_t seed, uint32_t nCol, uint64_t count, ui
 // Allocates *row_off (n+1) and *col_idx (m) with malloc; free with oracle_free.
 int      oracle_setup_rnd2(uint32_t n, float prob, uint64_t** row_off, uint32_t** col_idx, uint64_t* m);
 uint32_t oracle_max_deg(uint32_t n, const uint64_t* row_off);
+
+// ---- graph: the build's counter-based G(n, p) for C3/C4-scale runs (NOT a reference function;
+// "the build's documented GPU ER generator ... parity is GPU-vs-restatement on the
+// same graph"). Restated from the definition in mcmc_colorer_amd/csrc/er_gen.h: Philox4x32-10
+// streams per (row i, 65536-column block Y >= i's block), geometric skips
+// 1 + floor(ln(u) / log1p(-p)), u = (x + 1) / 2^32, ln by the same +-*/ series.
+// Rows ascending. Allocates like oracle_setup_rnd2.
+int      oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, uint32_t** col_idx, uint64_t* m);
 void     oracle_free(void* p);
 
 // ---- MCMC: ColoringMCMC_CPU(g, params, seed) + run() ----

@@ -166,3 +166,85 @@ def mcmc_run(off, idx, ncol: int, seed: int, glibc: GlibcRand, max_rip: int = 25
             break
     traj.append(cviol)
     return C.astype(np.uint32), traj, it, max_reached, init.astype(np.uint32)
+
+
+# ---- the build's counter-based G(n, p) (mcmc_colorer_amd/csrc/er_gen.h), vectorised over streams --
+# TEST INFRASTRUCTURE: an independent restatement used to pin oracle_er_fast (C) on small graphs.
+_ER_T = 65536
+_ER_TAG = 0x45524721
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _philox4x32_10(c0, c1, c2, c3, k0, k1):
+    c = [np.asarray(x, dtype=np.uint64) & _M32 for x in (c0, c1, c2, c3)]
+    k = [np.uint64(k0), np.uint64(k1)]
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[0]
+        p1 = np.uint64(0xCD9E8D57) * c[2]
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k[0]) & _M32, p1 & _M32,
+             ((p0 >> np.uint64(32)) ^ c[3] ^ k[1]) & _M32, p0 & _M32]
+        k = [(k[0] + np.uint64(0x9E3779B9)) & _M32, (k[1] + np.uint64(0xBB67AE85)) & _M32]
+    return c
+
+
+def _series_log(u):
+    bits = np.asarray(u, dtype=np.float64).view(np.uint64)
+    e = ((bits >> np.uint64(52)) & np.uint64(0x7FF)).astype(np.int64) - 1023
+    m = ((bits & np.uint64(0x000FFFFFFFFFFFFF)) | np.uint64(0x3FF0000000000000)).view(np.float64)
+    big = m > 1.4142135623730951
+    m = np.where(big, m * 0.5, m)
+    e = e + big
+    s = (m - 1.0) / (m + 1.0)
+    s2 = s * s
+    poly = np.full_like(s, 1.0 / 25.0)
+    for k in range(11, -1, -1):
+        poly = poly * s2 + 1.0 / float(2 * k + 1)
+    ef = e.astype(np.float64)
+    return (ef * 6.93147180369123816490e-01 + 2.0 * s * poly) + ef * 1.90821492927058770002e-10
+
+
+def er_fast(n: int, prob: float, seed: int):
+    """Edges (i < j) of the counter-based G(n, p), as an (E, 2) int64 array, streams walked in lock-step."""
+    import math
+
+    p = float(np.float32(prob))
+    if p <= 0.0 or n < 2:
+        return np.zeros((0, 2), dtype=np.int64)
+    ii, yy = [], []
+    nb = (n + _ER_T - 1) // _ER_T
+    for Y in range(nb):
+        rows = np.arange(0, min(n, (Y + 1) * _ER_T), dtype=np.int64)
+        ii.append(rows)
+        yy.append(np.full(len(rows), Y, dtype=np.int64))
+    i = np.concatenate(ii)
+    Y = np.concatenate(yy)
+    end = np.minimum(n, (Y + 1) * _ER_T)
+    j = np.maximum(Y * _ER_T, i + 1)
+    keep = j < end
+    i, Y, end, j = i[keep], Y[keep], end[keep], j[keep]
+    if p >= 1.0:
+        out = [np.stack([np.repeat(i, end - j), np.concatenate([np.arange(a, b) for a, b in zip(j, end)])], 1)]
+        return np.concatenate(out) if len(i) else np.zeros((0, 2), dtype=np.int64)
+    inv = 1.0 / math.log1p(-p)
+    j = j - 1
+    k = 0
+    out = []
+    active = np.ones(len(i), dtype=bool)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    while active.any():
+        idx = np.nonzero(active)[0]
+        r = _philox4x32_10(np.full(len(idx), k, dtype=np.uint64), i[idx].astype(np.uint64),
+                           Y[idx].astype(np.uint64), np.full(len(idx), _ER_TAG, dtype=np.uint64), k0, k1)
+        alive = np.ones(len(idx), dtype=bool)
+        for q in range(4):
+            x = r[q].astype(np.float64)
+            t = _series_log((x + 1.0) * 2.3283064365386963e-10) * inv
+            skip = np.where(t < 2147483647.0, 1 + np.floor(np.minimum(t, 2147483647.0)).astype(np.int64), 0x7FFFFFFF)
+            jj = j[idx] + np.where(alive, skip, 0)
+            j[idx] = jj
+            hit = alive & (jj < end[idx])
+            out.append(np.stack([i[idx][hit], jj[hit]], 1))
+            alive &= hit
+        active[idx[~alive]] = False
+        k += 1
+    return np.concatenate(out) if out else np.zeros((0, 2), dtype=np.int64)

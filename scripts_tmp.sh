@@ -1,7 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x -k "refstruct or golden" > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider -x -k "er_fast" > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py > gpurun_out/b_default.log 2>&1 || { echo "bench FAIL"; tail -5 gpurun_out/b_default.log; exit 1; }
-python -c "
-import json; d=json.loads(open('gpurun_out/b_default.log').read().strip().splitlines()[-1])
-print(d['value'], d['ms_per_step']); print(d['refstruct']); print(d['cpu_baseline'])"
+timeout -k 10 400 python bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-refstruct > gpurun_out/b_c3.log 2>&1; rc=$?
+echo "c3 rc=$rc"; tail -3 gpurun_out/b_c3.log | cut -c1-1500

@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_setup_rnd2.argtypes = [c_uint32, c_float, POINTER(POINTER(c_uint64)), POINTER(POINTER(c_uint32)),
                                         POINTER(c_uint64)]
         L.oracle_max_deg.argtypes = [c_uint32, c_void_p]
+        L.oracle_er_fast.argtypes = [c_uint32, ctypes.c_double, c_uint64, POINTER(POINTER(c_uint64)),
+                                     POINTER(POINTER(c_uint32)), POINTER(c_uint64)]
         L.oracle_max_deg.restype = c_uint32
         L.oracle_free.argtypes = [c_void_p]
         L.oracle_mcmc_run.argtypes = [c_uint32, c_void_p, c_void_p, POINTER(OracleParams), c_uint32, c_void_p,
@@ -81,6 +83,20 @@ def setup_rnd2(n: int, prob: float) -> tuple[np.ndarray, np.ndarray]:
     idx = POINTER(c_uint32)()
     m = c_uint64()
     rc = lib().oracle_setup_rnd2(n, c_float(prob), byref(off), byref(idx), byref(m))
+    assert rc == 0
+    a = np.ctypeslib.as_array(off, (n + 1,)).copy()
+    b = np.ctypeslib.as_array(idx, (max(m.value, 1),))[: m.value].copy()
+    lib().oracle_free(ctypes.cast(off, c_void_p))
+    lib().oracle_free(ctypes.cast(idx, c_void_p))
+    return a, b
+
+
+def er_fast(n: int, prob: float, seed: int) -> tuple[np.ndarray, np.ndarray]:
+    """The build's counter-based G(n, p) (csrc/er_gen.h), restated on the CPU; rows ascending."""
+    off = POINTER(c_uint64)()
+    idx = POINTER(c_uint32)()
+    m = c_uint64()
+    rc = lib().oracle_er_fast(n, prob, seed, byref(off), byref(idx), byref(m))
     assert rc == 0
     a = np.ctypeslib.as_array(off, (n + 1,)).copy()
     b = np.ctypeslib.as_array(idx, (max(m.value, 1),))[: m.value].copy()

@@ -343,3 +343,64 @@ def test_refstruct_baseline_runs(M):
     assert ms.value > 0
     # monochromatic edges of a colouring with 8 colours on ~50 000 edges: some, not all
     assert 0 < conf.value < len(idx) // 2
+
+
+# ---- the build's counter-based G(n, p) (C3/C4 generator), generated into the tiled layout --------
+@pytest.mark.parametrize("n,p,seed", [(1000, 0.05, 7), (70000, 0.0005, 3), (131073, 0.0002, 11), (300, 1.0, 1),
+                                      (500, 0.0, 1), (2, 0.5, 9), (200000, 0.001, 5)])
+def test_er_fast_generator_matches_restatement(M, n, p, seed):
+    """GPU generator (straight into the tiled layout, CSR rebuilt by download) == oracle_er_fast."""
+    off, idx = O.er_fast(n, p, seed)
+    g = M.Graph.er_fast(n, p, seed)
+    assert g.nEdges == len(idx) and g.maxDeg == O.max_deg(off)
+    s = g.getStruct()
+    assert np.array_equal(s.cumulDegs, off) and np.array_equal(s.neighs, idx)
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,stream", [(130000, 0.004, 16, 5, "0"), (200000, 0.003, 32, 6, "0"),
+                                                  (130000, 0.004, 16, 7, "1")])
+def test_er_fast_sweep_matches_oracle(M, monkeypatch, n, p, ncol, seed, stream):
+    """MCMC on a generated graph (resident replica; streamed slices) == the oracle on the restated CSR."""
+    monkeypatch.setenv("MCMC_TILE_STREAM", stream)
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=12, nthreads=8)
+    g = M.Graph.er_fast(n, p, seed)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=12))
+    st = col.run(0)
+    assert_same(col, st, r)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_er_fast_part_lockstep(M, world):
+    """Each rank generates only its rows (mcmc_graph_er_fast_part); the partitioned protocol over
+    those per-rank graphs == the oracle on the whole restated graph."""
+    import torch
+
+    from mcmc_colorer_amd.distributed import HipRank
+
+    n, p, ncol, seed, maxrip = 150000, 0.003, 16, 8, 10
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=maxrip, nthreads=8)
+    params = M.ColoringMCMCParams(nCol=ncol, maxRip=maxrip)
+    graphs = [M.Graph.er_fast(n, p, seed, world=world, rank=k) for k in range(world)]
+    assert sum(gr.nEdges for gr in graphs) == len(idx)
+    ranks = [HipRank(graphs[k], params, seed, world, k, torch.device("cuda", 0)) for k in range(world)]
+    for b in ranks:
+        b.init(seed, M.GlibcRand(1))
+    t = 0
+    while t < maxrip + 2:
+        for b in ranks:
+            b.sweep()
+        gathered = torch.cat([b.region(t)[1] for b in ranks])
+        for b in ranks:
+            b.region(t)[0].copy_(gathered)
+        for b in ranks:
+            b.commit()
+        t += 1
+        if ranks[0].state()[0]:
+            break
+    for b in ranks:
+        assert b.coloring().tolist() == r.colors.tolist()
+        assert b.trajectory().tolist() == r.traj.tolist()
