@@ -1,22 +1,28 @@
 """bench.py -- vertex-updates/s of the MCMC colour-resampling sweep on MI355X.
 
-Workload (BASELINE.json configs[1]): `--mcmcgpu --simulate 0.01 -n 100000`, 16 colours, seed 1.
-The graph is the reference's exact setupRnd2 graph, generated on the GPU (5e9 glibc draws replayed
-by jump-ahead); data = synthetic, as the reference's own --simulate is. A step is one sweep: all
-n vertices resampled (fused sweep kernel + commit kernel). Inputs are resident in HBM before the
-timed region; the timed region is K back-to-back sweeps bracketed by barrier + synchronize.
+Default workload (--config c3): BASELINE.json configs[2], the configuration the north star's target
+is quoted on -- `--mcmcgpu --simulate 0.001 -n 10000000`, 32 colours, one MI355X. setupRnd2 is
+infeasible there (5e13 sequential glibc draws), so the graph is the build's documented counter-based
+G(n, p) (mcmc_colorer_amd/csrc/er_gen.h, seed 1), generated on the GPU straight into
+the sweep's tiled layout (1e11 arcs, 217 GB; no CSR could exist: 400 GB). Under torchrun (N > 1) it
+is configs[3]: the same graph vertex-partitioned over N GPUs (strong scaling), every rank generating
+only its own rows, one RCCL all-gather per sweep (mcmc_colorer_amd/distributed.py).
+`--config c2`: configs[1], `--simulate 0.01 -n 100000 --nCol 16` with the reference's exact setupRnd2
+graph (weak scaling at N > 1: N*1e5 rows, p 0.01/N).
 
-Prints ONE JSON line (rank 0). Besides the driver contract fields it carries
-  roofline     : dominant kernel (sweep_kernel) algorithmic bytes / its average duration, measured
-                 with hipEvents on the kernel's own stream, against the 8 TB/s HBM peak; traffic =
-                 PMC HBM bytes per launch from the committed rocprofv3 summary, when present
-  cpu_baseline : the oracle (faithful single-thread restatement of --mcmccpu, kind "port") timed on
-                 this host on a bounded number of sweeps of the same graph
-Multi-GPU (torchrun, one process per GPU, RCCL): the vertex-partitioned sweep with its per-sweep
-exchange (all-gather of colour slabs + footers, mcmc_colorer_amd/distributed.py). Weak scaling by
-default: N GPUs sweep `--simulate (0.01/N) -n (N*1e5)` -- every GPU owns 1e5 rows of mean degree
-~1000, the configs[1] shape, and N=1 is exactly configs[1]. `--scaling strong` keeps configs[1]
-fixed and splits it.
+A step is one sweep: all n vertices resampled. Inputs are resident in HBM before the timed region;
+the timed region is K back-to-back sweeps (one hipGraph at N = 1) bracketed by barrier + synchronize,
+max over ranks. Prints ONE JSON line (rank 0). Besides the driver contract fields it carries
+  roofline     : the sweep kernel's bytes per launch in its layout (B_fmt; the
+                 reference-layout B_alg beside it) / its average duration, measured with hipEvents on
+                 the kernel's own stream, against the 8 TB/s HBM peak; traffic = PMC HBM bytes per
+                 launch from the committed rocprofv3 summary (profiles/pmc_summary.json)
+  refstruct    : the reference CUDA path's per-sweep structure re-expressed in HIP (the stand-in for
+                 "the reference CUDA path's vertex-updates/sec", which cannot run on MI355X)
+  cpu_baseline : the oracle (faithful single-thread restatement of --mcmccpu, kind "port") on this
+                 host, a bounded number of sweeps
+For c3 the refstruct and CPU legs run on `--simulate 0.1 -n 100000` (C3's mean degree, 1e4): C3's
+CSR cannot exist on the host or one GPU.
 """
 from __future__ import annotations
 
@@ -95,7 +101,7 @@ def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: floa
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3"], default="c3",
                     help="c2: configs[1] (--simulate 0.01 -n 1e5, 16 colours; weak scaling at N > 1); "
                          "c3: configs[2]/[3] (n 1e7, p 0.001, 32 colours, the build's G(n,p) generator; "
                          "N > 1 partitions the same graph: strong scaling)")
@@ -223,7 +229,7 @@ def main() -> int:
         "warmup": a.warmup,
         "ms_per_step": wall * 1e3 / a.steps,
         "higher_is_better": True,
-        "scaling": "weak" if (world == 1 or a.scaling == "weak") else "strong",
+        "scaling": "strong" if a.config == "c3" else ("weak" if (world == 1 or a.scaling == "weak") else "strong"),
         "vs_baseline": None,
         "dtype": "fp32",
         "data": ("synthetic (reference --simulate generator replayed exactly on the GPU)" if a.config == "c2" else
