@@ -116,6 +116,9 @@ def main() -> int:
     ap.add_argument("--refstruct-sweeps", type=int, default=10)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
+    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--variant", default=None,
                     help="sweep kernel: lds | tiled | blocked | global[:block_log2[:lanes_log2[:group_rows"
                          "[:stream]]]] (empty field / default: the library's choice)")
@@ -129,13 +132,18 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.same_device:
+        local = 0
     dist = None
     if world > 1 or a.force_dist:
         import torch
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
 
     import mcmc_colorer_amd.colorer as M
     from mcmc_colorer_amd._lib import check, lib
@@ -201,7 +209,8 @@ def main() -> int:
             raise RuntimeError("device error flag during the partitioned bench")
         kernel_ms = ev0.elapsed_time(ev1) / a.steps   # whole step per rank: sweep + exchange + commit
         info = drv.b.info()
-        w = torch.tensor([wall], dtype=torch.float64, device=f"cuda:{local}")
+        rdev = f"cuda:{local}" if a.backend == "nccl" else "cpu"
+        w = torch.tensor([wall], dtype=torch.float64, device=rdev)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
 
@@ -209,7 +218,7 @@ def main() -> int:
     if dist is not None and a.config == "c3":   # per-rank graphs hold their rows' arcs only
         import torch
 
-        mt = torch.tensor([m], dtype=torch.float64, device=f"cuda:{local}")
+        mt = torch.tensor([m], dtype=torch.float64, device=f"cuda:{local}" if a.backend == "nccl" else "cpu")
         dist.all_reduce(mt)
         m = int(mt.item())
     value = n * a.steps / wall          # all ranks together update n vertices per sweep

@@ -136,6 +136,9 @@ class PartitionedColoringMCMC:
                  backend=None, check_every: int = 8):
         import torch.distributed as dist
 
+        import torch
+
+        self.torch = torch
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
@@ -162,6 +165,10 @@ class PartitionedColoringMCMC:
         regions, mine = b.region(t)
         if self.inplace:
             self.dist.all_gather_into_tensor(regions, mine, group=self.group)   # one collective per sweep
+        elif regions.is_cuda:   # gloo rehearsal of device ranks: through host memory
+            out = self.torch.empty(regions.numel(), dtype=regions.dtype)
+            self.dist.all_gather_into_tensor(out, mine.cpu(), group=self.group)
+            regions.copy_(out)
         else:
             self.dist.all_gather_into_tensor(regions, mine.clone(), group=self.group)
         b.commit()
