@@ -92,6 +92,13 @@ public:
         MCMC_CHECK(mcmc_graph_simulate(nn, prob_, mcmc::glibc_global().w, device, &h_));
         info();
     }
+    // The build's counter-based G(n, p) (csrc/er_gen.h) for sizes where setupRnd2 is infeasible
+    // (C3: n = 1e7): generated straight into the sweep's tiled layout; no CSR is materialised.
+    struct ErFast {};
+    Graph(ErFast, node nn, float prob_, uint64_t seed, int device = 0) : prob(prob_), device_(device) {
+        MCMC_CHECK(mcmc_graph_er_fast(nn, prob_, seed, device, &h_));
+        info();
+    }
     // Host CSR (e.g. from the edge-list importer) -> device copy.
     Graph(const std::vector<uint64_t>& cumulDegs, const std::vector<node>& neighs, float prob_, int device = 0)
         : prob(prob_), device_(device) {

@@ -98,6 +98,9 @@ void help(const char* argv0) {
     std::cout << "Usage: " << argv0 << " [options]\n"
               << "  --graph file.txt     edge list (header line, then 'src dst [weight]' per line)\n"
               << "  --simulate P -n N    Erdos-Renyi graph, the reference's generator replayed on the GPU\n"
+              << "  --simulate-fast P -n N [--er-seed S]\n"
+              << "                       G(n,p) from the build's counter-based generator (csrc/er_gen.h):\n"
+              << "                       for n where the reference's O(n^2) generator is infeasible (1e7)\n"
               << "  --mcmcgpu            MCMC colorer on the MI355X (default)\n"
               << "  --nCol N             number of colours (default maxDeg / numColRatio)\n"
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
@@ -115,7 +118,8 @@ int main(int argc, char** argv) {
     std::string graphFilename, outDir;
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
-    bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false;
+    bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false;
+    uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
         {"graph", required_argument, 0, 'g'},    {"outDir", required_argument, 0, 'o'},
@@ -126,7 +130,8 @@ int main(int argc, char** argv) {
         {"numColRatio", required_argument, 0, 'r'}, {"tabooIteration", required_argument, 0, 't'},
         {"tailcut", no_argument, 0, 'l'},        {"repet", required_argument, 0, 'R'},
         {"seed", required_argument, 0, 'S'},     {"help", no_argument, 0, 'h'},
-        {"device", required_argument, 0, 'D'},   {0, 0, 0, 0}};
+        {"device", required_argument, 0, 'D'},   {"simulate-fast", required_argument, 0, 'F'},
+        {"er-seed", required_argument, 0, 'E'},  {0, 0, 0, 0}};
     int c;
     while ((c = getopt_long(argc, argv, "g:o:s:n:12345k:r:t:lR:S:hD:", longopts, nullptr)) != -1) {
         try {
@@ -147,6 +152,10 @@ int main(int argc, char** argv) {
                 case 'R': if (std::stoi(optarg) < 1) throw 1; repetitions = std::stoi(optarg); break;
                 case 'S': seed = (uint32_t)std::stoi(optarg); break;
                 case 'D': device = std::stoi(optarg); break;
+                case 'F': simulate = fast = true; prob = std::stod(optarg);
+                          if (prob < 0 || prob > 1) { std::cout << "Simulation: probabilty of positive class must be 0 < prob < 1." << std::endl; return 255; }
+                          break;
+                case 'E': erSeed = std::stoull(optarg); break;
                 case 'h': help(argv[0]); return 0;
                 default: break;
             }
@@ -188,6 +197,7 @@ int main(int argc, char** argv) {
         }
     } else {
         graphName = std::to_string(n) + "_" + std::to_string(prob) + "_" + std::to_string(numColRatio);
+        if (fast) graphName += "_er" + std::to_string(erSeed);
     }
     if (outDir.empty()) outDir = graphName + "_out";
     mkdir(outDir.c_str(), 0775);
@@ -195,7 +205,9 @@ int main(int argc, char** argv) {
     const float numColorRatio = 1.0f / (float)numColRatio;        // main.cu:53
     Graph<float, float>* g;
     auto t0 = std::chrono::steady_clock::now();
-    if (simulate) {
+    if (fast) {
+        g = new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device);
+    } else if (simulate) {
         g = new Graph<float, float>(n, (float)prob, seed, device);
     } else {
         std::vector<uint64_t> off;

@@ -62,3 +62,23 @@ def test_cli_graph_file(tmp_path):
     f = tmp_path / "mygraph.edges.txt"
     f.write_text("\n".join(lines) + "\n")
     run_pair(tmp_path, ["--graph", str(f), "--nCol", "24", "--seed", "11", "--repet", "2"], "mygraph.edges", repet=2)
+
+
+@pytest.mark.gpu
+def test_cli_simulate_fast(tmp_path):
+    """--simulate-fast (the build's G(n,p) generator, two column blocks): the colours file equals the
+    oracle's run on the restated graph (seed 5, 16 colours, maxRip 250 -> 251 sweeps)."""
+    import oracle_ref as O
+
+    n, p, seed = 70000, 0.002, 5
+    r1 = subprocess.run([str(CLI), "--mcmcgpu", "--simulate-fast", str(p), "-n", str(n), "--er-seed", "3",
+                         "--nCol", "16", "--seed", str(seed), "--outDir", str(tmp_path)],
+                        capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    name = f"{n}_{p:.6f}_1.000000_er3"
+    got = (tmp_path / f"{name}-MCMC_GPU-0-colors.txt").read_text().split("\n")
+    off, idx = O.er_fast(n, p, 3)
+    O.srand(1)      # --seed S leaves glibc unseeded (ArgHandle.cpp:272-276); the generator draws none
+    r = O.mcmc_run(off, idx, 16, seed, nthreads=8)
+    want = [f"{v} {c}" for v, c in enumerate(r.colors.tolist())]
+    assert [l for l in got if l] == want
