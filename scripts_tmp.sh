@@ -1,5 +1,8 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29551 bench.py --config c2 --steps 20 --warmup 2 --backend gloo --same-device > gpurun_out/b_r2_c2.log 2>&1 || { echo "r2 c2 FAIL"; tail -20 gpurun_out/b_r2_c2.log; exit 1; }
-tail -1 gpurun_out/b_r2_c2.log | cut -c1-700
-timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29552 bench.py --config c3 --steps 5 --warmup 1 --backend gloo --same-device > gpurun_out/b_r2_c3.log 2>&1 || { echo "r2 c3 FAIL"; tail -20 gpurun_out/b_r2_c3.log; exit 1; }
-tail -1 gpurun_out/b_r2_c3.log | cut -c1-900
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
+timeout -k 10 600 python bench.py > gpurun_out/b_default.log 2>&1 || { echo "bench FAIL"; tail -5 gpurun_out/b_default.log; exit 1; }
+python -c "
+import json; d=json.loads(open('gpurun_out/b_default.log').read().strip().splitlines()[-1])
+print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['traffic'], d['refstruct']['speedup'], d['cpu_baseline']['value'])"
