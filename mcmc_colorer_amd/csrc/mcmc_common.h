@@ -42,6 +42,10 @@ int sort_rows_inplace(GraphDev& g);
 struct mcmc_graph;
 
 namespace mcmc {
+// Row stride of a tiled layout's segment table: R + 1 entries rounded up to 4, so every
+// (group, block) table row is 16-byte aligned for LDS-DMA.
+__host__ __device__ inline uint32_t tseg_stride(uint32_t R) { return (R + 4u) & ~3u; }
+
 // Tiled copy of a row range of the CSR (sweep variant 3, mcmc_sweep.hip): rows in groups of
 // grp_rows, per group the arcs block-major as 16-bit block-local ids, every (row, block) segment
 // padded to a multiple of 8 ids. Cached on the graph, so contexts re-created per repetition reuse it.
@@ -51,7 +55,7 @@ struct TiledLayout {
     uint64_t arcs = 0;             // arcs of the rows (unpadded)
     uint16_t* tcol = nullptr;
     uint64_t* gbase = nullptr;     // [ngroups + 1]
-    uint32_t* tseg = nullptr;      // [ngroups][nblocks][grp_rows + 1]
+    uint32_t* tseg = nullptr;      // [ngroups][nblocks][tseg_stride(grp_rows)] (entries 0..grp_rows used)
     ~TiledLayout();
 };
 }  // namespace mcmc
@@ -62,7 +66,7 @@ int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t 
                      hipStream_t s, const TiledLayout** out);
 // Default rows per group of a tiled layout on nloc rows (mcmc_create and the generator agree).
 uint32_t tiled_default_rows(uint32_t nloc, uint32_t cus, uint32_t rmax);
-constexpr uint32_t kTileGenRowsMax = 4095;   // generator layouts: R + 1 <= 4 * 1024 (segment prefetch)
+constexpr uint32_t kTileGenRowsMax = 1792;   // generator layouts: fits the streaming LDS for nCol <= 64
 // CSR (ascending rows) of a generated graph with a full-range layout.
 int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx);
 }  // namespace mcmc

@@ -96,7 +96,8 @@ struct SweepArgs {
     const uint32_t* tseg;       // [ngroups][nblocks][grp_rows + 1] segment start relative to gbase
     uint32_t grp_rows, ngroups;
     uint32_t sub_log2;          // lanes per row segment = 2^sub_log2
-    uint32_t slice_bytes;       // tiled: LDS bytes of the colour slice (masks follow it)
+    uint32_t slice_bytes;       // tiled: colour bytes a pair's slice can hold (resident: the replica)
+    uint32_t seg_buf_bytes;     // tiled: LDS bytes of one segment-table buffer (1 KiB multiple)
     unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
     // partitioned colour buffers: vertex v at byte v + (v / part_S) * part_FB (part_FB = 0: plain)
     uint32_t part_S, part_FB;
@@ -564,6 +565,7 @@ __device__ __forceinline__ void scan_tile(const uint32_t* __restrict__ tcol, con
 // arrives; the workgroup whose arrival is last acquires.
 struct TailShared {
     uint32_t wg_viol, wg_last, t, E, err;
+    uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     unsigned long long viol;
 };
 
@@ -790,79 +792,78 @@ __device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, cons
     }
 }
 
-// RES: the whole replica is LDS-resident; otherwise a 64 KiB slice per (group, block). Both run
-// one 1024-thread workgroup per CU (two smaller workgroups per CU were measured to split the CU's
-// issue unevenly: the younger one finished 30% later and the tail ran at half occupancy). A workgroup walks its (group, block) pairs
-// in order; while it scans pair k, the colour slice (streaming mode) and segment table of pair
-// k+1 are already in flight into registers, and land in LDS after the scan's barrier.
-constexpr uint32_t kTileSegPer = 4;   // segment-table entries per thread per pair: R + 1 <= 4 * blockDim
+// Streaming mode: the colour slice of a pair (2^16 vertices at most) per LDS buffer.
+constexpr uint32_t kSliceBytes = 65536;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable 16 B
-template <bool RES>
-constexpr int kTileSlicePer = RES ? 1 : (65536 / 16) / 1024;   // uint4 of a 64 KiB slice per thread
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
-// Issue the loads of pair (g, b)'s segment table (and streaming: colour slice) into registers.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_u8*)(p); }
+
+// LDS-DMA (global_load_lds_dwordx4): 16 B per lane from `gsrc` to LDS `lds_dst + lane * 16` (`lds_dst`
+// wave-uniform). Inline asm, so hipcc's own vmcnt bookkeeping ignores it (cdna_hip_programming.md
+// "What hipcc does not do"): its completion is awaited by the counted wait at the pair boundary.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// DMA of pair (g, b) into LDS buffer `buf`: its segment-table row (tseg_stride(R) entries, 16-B
+// pieces, 64 per wave-instruction) and, streaming, its colour slice (4096 pieces: 4 per lane).
 template <bool RES>
-__device__ __forceinline__ void tile_prefetch(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
-                                              uint32_t b, uint32_t nloc, uint32_t (&pseg)[kTileSegPer],
-                                              u32x4 (&pslice)[kTileSlicePer<RES>]) {
-    const uint32_t R = a.grp_rows;
-    const uint32_t rows = min(R, nloc - g * R);
-    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * (R + 1);
-#pragma unroll
-    for (uint32_t k = 0; k < kTileSegPer; k++) {
-        const uint32_t i = threadIdx.x + k * blockDim.x;
-        pseg[k] = gs[i <= rows ? i : 0u];
+__device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
+                                              uint32_t b, uint32_t seg_lds, uint32_t slice_lds, uint32_t wid,
+                                              uint32_t nwaves, int lane) {
+    const uint32_t TS = tseg_stride(a.grp_rows);
+    const uint32_t np = TS / 4u;   // 16-B pieces of the table row
+    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * TS;
+    for (uint32_t w = wid; w * 64u < np; w += nwaves) {
+        const uint32_t p = min(w * 64u + (uint32_t)lane, np - 1u);
+        glds16(gs + 4u * p, __builtin_amdgcn_readfirstlane(seg_lds + w * 1024u));
     }
     if (!RES) {
         const uint32_t lo = b << a.block_log2;
         const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
 #pragma unroll
-        for (int k = 0; k < kTileSlicePer<RES>; k++) {
-            const uint32_t i = threadIdx.x + k * blockDim.x;
-            pslice[k] = *reinterpret_cast<const u32x4*>(C + caddr(a, lo + 16u * (i < nq16 ? i : 0u)));
+        for (uint32_t k = 0; k < kSliceBytes / 16u / 64u / 16u; k++) {   // 4 wave-instructions per wave
+            const uint32_t piece = (k * nwaves + wid) * 64u;
+            const uint32_t q = min(piece + (uint32_t)lane, nq16 - 1u);
+            glds16(C + caddr(a, lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
         }
     }
 }
 
-// Segment bounds (ids from the group base) of this lane's first row in pair (g, b): the
-// sub-group's first row of its wave's share, read from the global segment table. Branch-free
-// (idle sub-groups read the empty range [s(wr1), s(wr1)) ), so the loads stay in flight until used.
+// Segment bounds (ids from the group base) of this lane's first row in pair (g, b): sub-group
+// (wave w, s) starts at row w * nsub + s; read from the global segment table. Branch-free (rows
+// beyond the group read the empty range [s(rows), s(rows)) ), so the loads stay in flight.
 __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
                                                uint32_t wid, uint32_t nwaves, uint32_t sub,
                                                uint32_t& s0, uint32_t& s1) {
     const uint32_t R = a.grp_rows;
     const uint32_t rows = min(R, nloc - g * R);
-    const uint32_t q = (rows + nwaves - 1) / nwaves;
-    const uint32_t wr0 = min(rows, wid * q), wr1 = min(rows, wr0 + q);
-    const uint32_t row = wr0 + sub;
-    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * (R + 1);
-    s0 = gs[min(row, wr1)];
-    s1 = gs[min(row + 1, wr1)];
+    const uint32_t row = wid * (64u >> a.sub_log2) + sub;   // the sub-group's static first row
+    const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * tseg_stride(R);
+    s0 = gs[min(row, rows)];
+    s1 = gs[min(row + 1, rows)];
 }
 
-// Store the prefetched pair into LDS (after the barrier that ends the previous pair's scan).
-template <bool RES>
-__device__ __forceinline__ void tile_land(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
-                                          uint32_t* sseg, uint4* lds_raw, const uint32_t (&pseg)[kTileSegPer],
-                                          const u32x4 (&pslice)[kTileSlicePer<RES>]) {
-    const uint32_t R = a.grp_rows;
-    const uint32_t rows = min(R, nloc - g * R);
-#pragma unroll
-    for (uint32_t k = 0; k < kTileSegPer; k++) {
-        const uint32_t i = threadIdx.x + k * blockDim.x;
-        sseg[i <= rows ? i : 0u] = pseg[k];   // out-of-range threads rewrite entry 0 with its value
-    }
-    if (!RES) {
-        const uint32_t lo = b << a.block_log2;
-        const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
-#pragma unroll
-        for (int k = 0; k < kTileSlicePer<RES>; k++) {
-            const uint32_t i = threadIdx.x + k * blockDim.x;
-            reinterpret_cast<u32x4*>(lds_raw)[i < nq16 ? i : 0u] = pslice[k];
-        }
-    }
-}
+// Pair boundary: this lane's LDS-DMA (issued before at least 6 ordinary vector-memory operations:
+// the next pair's 2 first-row bounds and 4 first quads) has landed, this wave's LDS traffic is
+// done, then a raw barrier -- the loads issued after the DMA stay in flight across it (a
+// __syncthreads() would drain them).
+#define MCMC_PAIR_BARRIER() asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#define MCMC_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+// RES: the whole replica is LDS-resident; otherwise the colour slice of each pair. One 1024-thread
+// workgroup per CU (two smaller ones per CU were measured to split the CU's issue unevenly: the
+// younger finished 30% later and the tail ran at half occupancy). A workgroup walks its
+// (group, block) pairs in order. LDS: [replica | slice buffers 0, 1] [segment-table buffers 0, 1]
+// [row masks]. While pair k is scanned from buffer k&1, pair k+1's table (and slice) arrive in
+// buffer (k+1)&1 by LDS-DMA, and pair k+1's first quads are issued before the boundary barrier,
+// so no pair starts from an empty memory pipeline (the register-landing design spent 38% of the
+// C3 sweep at pair boundaries).
 template <int NW, bool RES>
 __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
@@ -875,10 +876,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
-    uint8_t* sc = reinterpret_cast<uint8_t*>(lds_raw);
+    uint8_t* lbase = reinterpret_cast<uint8_t*>(lds_raw);
     const uint32_t R = a.grp_rows, nb = a.nblocks;
-    uint32_t* smask = reinterpret_cast<uint32_t*>(sc + a.slice_bytes);
-    uint32_t* sseg = smask + R * NW;   // [R + 1] segment starts of the pair being scanned
+    const uint32_t SB = RES ? a.slice_bytes : kSliceBytes;             // bytes per colour buffer
+    uint8_t* seg_base = lbase + (RES ? SB : 2u * SB);
+    const uint32_t SEGB = a.seg_buf_bytes;                              // bytes per table buffer
+    uint32_t* smask = reinterpret_cast<uint32_t*>(seg_base + 2u * SEGB);
     const int lane = threadIdx.x & 63;
     const uint32_t wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const uint32_t L = 1u << a.sub_log2, nsub = 64u >> a.sub_log2;
@@ -886,16 +889,17 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t step = 8u * L * kTileU;
     const uint32_t nloc = a.v_end - a.v_begin;
     const uint32_t nbytes16 = (a.n + 15u) & ~15u;
+    const uint32_t lds0 = lds_addr(lbase), seg_lds0 = lds_addr(seg_base);
     uint32_t wave_viol = 0;
+    const bool timing = a.phase_ts != nullptr;
+    uint64_t cyc_wait = 0, cyc_scan = 0, cyc_eval = 0, tmark = 0;
 
-    // prefetch registers: the next pair's segment table and (streaming mode) its colour slice
-    uint32_t pseg[kTileSegPer];
-    u32x4 pslice[kTileSlicePer<RES>];
-    uint32_t g = blockIdx.x, b = 0;
+    uint32_t g = blockIdx.x, b = 0, buf = 0;
     const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
-    // Issue order: the first pair's segment table and first-row bounds, then (once the bounds are
-    // back) its first quads, then the resident replica -- the quads fly across the staging.
-    tile_prefetch<RES>(a, C, gclamp, 0, nloc, pseg, pslice);
+    for (uint32_t i = threadIdx.x; i < R * NW; i += blockDim.x) smask[i] = 0;
+    if (threadIdx.x == 0) sh.cursor[0] = nwaves * nsub;
+    if (g < a.ngroups) tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
+    // the first pair's first quads (bounds from the global table), then the resident replica
     uint32_t fpos, fend;
     tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend);
     fpos += 8u * li;
@@ -922,44 +926,55 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             reinterpret_cast<u32x4*>(lds_raw)[i < nq16 ? i : 0u] = rr[k];   // (src[0] again at 0)
         }
     }
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // DMA + staging landed
+    MCMC_PHASE(a, 1);
+
     while (g < a.ngroups) {
+        if (timing) tmark = __builtin_readcyclecounter();
         const uint32_t r0 = g * R;
         const uint32_t rows = min(R, nloc - r0);
-        const uint32_t q = (rows + nwaves - 1) / nwaves;
-        const uint32_t wr0 = min(rows, wid * q), wr1 = min(rows, wr0 + q);
-        __syncthreads();   // previous pair's scan (or the previous group's evaluation) is done
-        if (b == 0)
-            for (uint32_t i = threadIdx.x; i < rows * NW; i += blockDim.x) smask[i] = 0;
-        tile_land<RES>(a, g, b, nloc, sseg, lds_raw, pseg, pslice);
-        __syncthreads();
+        const uint32_t q = (rows + nwaves - 1) / nwaves;   // evaluation share per wave
+        // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
+        if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
+        // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
         const uint32_t ng = (b + 1 < nb) ? g : g + gridDim.x, nbn = (b + 1 < nb) ? b + 1 : 0u;
-        const uint32_t pg = ng < a.ngroups ? ng : g, pb = ng < a.ngroups ? nbn : b;
-        tile_prefetch<RES>(a, C, pg, pb, nloc, pseg, pslice);
+        const bool nvalid = ng < a.ngroups;
+        if (nvalid)
+            tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane);
+        const uint32_t pg = nvalid ? ng : g, pb = nvalid ? nbn : b;
         uint32_t npos, nend;
         tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
-        if (b == 0 && g == blockIdx.x) MCMC_PHASE(a, 1);
-        const uint8_t* __restrict__ scb = RES ? sc + (b << a.block_log2) : sc;
-        // sub-group state: current row, this lane's next quad, the row's end (ids, from gbase);
-        // the first step's quads are already in v
-        uint32_t row = wr0 + sub, pos = fpos, end = fend;
+        const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + buf * SB;
+        const uint32_t* __restrict__ sseg = reinterpret_cast<const uint32_t*>(seg_base + buf * SEGB);
+        // sub-group state: current row, this lane's next quad, the row's end (ids from the group
+        // base); the first step's quads are already in v. Rows after the first come from the pair's
+        // LDS cursor, claimed one row ahead (dynamic balance across the waves: the static split
+        // left 36% of the C3 sweep waiting at pair barriers for the slowest wave).
+        uint32_t row = wid * nsub + sub, pos = fpos, end = fend;
+        uint32_t claim = 0;
+        if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
         uint32_t m[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) m[i] = 0;
-        while (__ballot(row < wr1)) {
-            const bool act = row < wr1;
-            // next step's position (same row, or the sub-group's next row) and its loads first
-            uint32_t npos = pos + step, nrow = row, nend = end;
-            const bool fin = act && (npos - 8u * li >= end);
-            if (fin) {
-                nrow = row + nsub;
-                if (nrow < wr1) { npos = sseg[nrow] + 8u * li; nend = sseg[nrow + 1]; }
+        while (__ballot(row < rows)) {
+            const bool act = row < rows;
+            // next step's position (same row, or the sub-group's claimed next row) and its loads first
+            uint32_t npos2 = pos + step, nrow = row, nend2 = end;
+            const bool fin = act && (npos2 - 8u * li >= end);
+            if (__ballot(fin)) {
+                const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);
+                if (fin) {
+                    nrow = got;
+                    if (nrow < rows) { npos2 = sseg[nrow] + 8u * li; nend2 = sseg[nrow + 1]; }
+                    if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
+                }
             }
             uint4 vn[kTileU];
 #pragma unroll
             for (int u = 0; u < kTileU; u++) {
-                const uint32_t pu = npos + 8u * L * u;
-                vn[u] = *reinterpret_cast<const uint4*>(gcol + ((nrow < wr1 && pu < nend) ? pu : 0u));
+                const uint32_t pu = npos2 + 8u * L * u;
+                vn[u] = *reinterpret_cast<const uint4*>(gcol + ((nrow < rows && pu < nend2) ? pu : 0u));
             }
 #pragma unroll
             for (int u = 0; u < kTileU; u++)
@@ -984,12 +999,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 }
             }
             row = nrow;
-            pos = npos;
-            end = nend;
+            pos = npos2;
+            end = nend2;
 #pragma unroll
             for (int u = 0; u < kTileU; u++) v[u] = vn[u];
         }
-        // the next pair's first quads: in flight across the barriers, landing and evaluation
+        // the next pair's first quads: in flight across the boundary (and the evaluation)
         gcol = ngcol;
         fpos = npos + 8u * li;
         fend = nend;
@@ -998,21 +1013,35 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             const uint32_t pu = fpos + 8u * L * u;
             v[u] = *reinterpret_cast<const uint4*>(gcol + (pu < fend ? pu : 0u));
         }
+        if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_scan += t1 - tmark; tmark = t1; }
         if (b + 1 == nb) {
-            __syncthreads();   // all blocks scanned: every wave evaluates a share of the group's rows
-            MCMC_PHASE(a, 2);
+            MCMC_LDS_BARRIER();   // every wave's mask ORs of the group are in
+            // every wave evaluates a share of the group's rows and clears their masks for the next group
             for (uint32_t e0 = wid * min(q, 64u); e0 < rows; e0 += nwaves * min(q, 64u)) {
                 const uint32_t cnt = min(min(q, 64u), rows - e0);
                 uint32_t acc[NW];
 #pragma unroll
-                for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
+                for (int i = 0; i < NW; i++) {
+                    const uint32_t idx = (e0 + lane) * NW + i;
+                    acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
+                    if ((uint32_t)lane < cnt) smask[idx] = 0;
+                }
                 wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane);
             }
+            if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         }
+        MCMC_PAIR_BARRIER();   // pair k+1's DMA landed everywhere; buffer k&1 and the masks are free
+        if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_wait += t1 - tmark; }
         g = ng;
         b = nbn;
+        buf ^= 1u;
     }
     MCMC_PHASE(a, 3);
+    if (timing && threadIdx.x == 0) {   // shader-clock cycles per phase kind, wave 0
+        a.phase_ts[blockIdx.x * 8u + 5] = cyc_wait;
+        a.phase_ts[blockIdx.x * 8u + 6] = cyc_scan;
+        a.phase_ts[blockIdx.x * 8u + 7] = cyc_eval;
+    }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
     sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
     MCMC_PHASE(a, 4);
@@ -1228,6 +1257,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.block_log2 = c->tl->block_log2;
         a.sub_log2 = c->sub_log2;
         a.slice_bytes = c->slice_bytes;
+        a.seg_buf_bytes = (tseg_stride(c->tl->grp_rows) * 4u + 1023u) & ~1023u;
     }
     a.phase_ts = c->phase_ts;
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
@@ -1389,22 +1419,33 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     if (c->taboo) (void)hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * nloc, c->stream);
     // persistent grids; rows statically arc-balanced over all waves (blocked: over workgroups)
     if (c->variant == 3) {
-        // Resident (replica + masks + segment table fit one workgroup's LDS): replica staged once.
-        // Otherwise a 2^block_log2-byte colour slice per (group, block). One 1024-thread
-        // workgroup per CU either way. Groups of R rows: one
-        // group per workgroup while the mask LDS allows (fixed per-pair costs paid once), and
-        // R + 1 <= kTileSegPer * blockDim (segment-table prefetch registers).
+        // Resident (replica + two segment-table buffers + masks fit one workgroup's LDS): replica
+        // staged once. Otherwise (streaming) two 64 KiB colour-slice buffers. One 1024-thread
+        // workgroup per CU either way. Groups of R rows: about one group per workgroup, at most
+        // what the LDS holds (rmax) and 4095 (a table row = one DMA instruction per wave).
         const size_t rep = lds_bytes;
         const char* gr = getenv("MCMC_GROUP_ROWS");
-        const bool resident = rep + 256u * (c->nw + 1) * 4u + 4u <= kMaxLdsBytes && rep <= 10u * 16u * 1024u &&
-                              !(getenv("MCMC_TILE_STREAM") && atoi(getenv("MCMC_TILE_STREAM")));
+        auto lds_need = [&](bool res, uint32_t rows) -> size_t {
+            const size_t segb = ((size_t)tseg_stride(rows) * 4u + 1023u) & ~(size_t)1023u;
+            return (res ? rep : 2u * (size_t)kSliceBytes) + 2u * segb + (size_t)rows * c->nw * 4u;
+        };
+        auto rmax_for = [&](bool res) -> uint32_t {
+            uint32_t r = 4095;
+            while (r > 1 && lds_need(res, r) > kMaxLdsBytes) r -= 1;
+            return lds_need(res, r) <= kMaxLdsBytes ? r : 0u;
+        };
+        const bool stream_forced = getenv("MCMC_TILE_STREAM") && atoi(getenv("MCMC_TILE_STREAM"));
+        const uint32_t rmax_res = rep <= 10u * 16u * 1024u ? rmax_for(true) : 0u;
+        const bool resident = !stream_forced && rmax_res >= 64u;
         if (!resident) c->block_log2 = std::min<uint32_t>(c->block_log2, 16u);
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);
         c->slice_bytes = resident ? (uint32_t)rep : (uint32_t)std::min<size_t>(1ull << c->block_log2, rep);
-        const uint32_t lds_budget = resident ? (uint32_t)(kMaxLdsBytes - rep) : (uint32_t)(kMaxLdsBytes - c->slice_bytes);
-        const uint32_t rmax = std::max<uint32_t>(1u, std::min<uint32_t>(kTileSegPer * c->block.x - 1u,
-                                                                        (lds_budget - 4u) / ((c->nw + 1) * 4u)));
+        const uint32_t rmax = resident ? rmax_res : rmax_for(false);
+        if (rmax == 0) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_ARG, "tiled sweep: no group size fits the LDS for this nCol");
+        }
         uint32_t R = tiled_default_rows(nloc, c->grid.x, rmax);
         if (gr) R = (uint32_t)std::max(1, std::min((int)rmax, atoi(gr)));
         c->variant_res = resident;
@@ -1413,7 +1454,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         R = c->tl->grp_rows;   // a generated graph's layout brings its own group size
         if (R > rmax) {
             mcmc_destroy(c);
-            return fail(MCMC_E_ARG, "generated layout's group rows exceed this nCol's LDS budget (nCol > 128)");
+            return fail(MCMC_E_ARG, "generated layout's group rows exceed this nCol's LDS budget (streaming: nCol > 64)");
         }
         c->nblocks = c->tl->nblocks;
         // lanes per row segment: the smallest power of two L >= 4 with L * kTileU quads per step
@@ -1426,7 +1467,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         const char* sv = getenv("MCMC_SUB_LOG2");
         if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));
         c->sub_log2 = sl;
-        c->lds = (size_t)c->slice_bytes + (size_t)R * c->nw * 4u + (size_t)(R + 1) * 4u;
+        c->lds = lds_need(resident, R);
         if (resident) {
             static const SweepLaunch tab[4] = {launch_tiled<1, true>, launch_tiled<2, true>, launch_tiled<4, true>,
                                                launch_tiled<8, true>};
@@ -1728,7 +1769,7 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         i.grp_rows = t.grp_rows;
         i.ngroups = t.ngroups;
         i.sub_log2 = c->sub_log2;
-        const uint64_t segb = 4ull * (t.grp_rows + 1) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
+        const uint64_t segb = 4ull * tseg_stride(t.grp_rows) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
         i.layout_bytes = 2 * t.ids + segb;
         i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;
     } else {

@@ -64,7 +64,7 @@ __global__ void tile_seg_kernel(const uint32_t* __restrict__ seg, uint32_t nloc,
             }
             __syncthreads();
             const uint32_t run = run_sh;
-            uint32_t* out = tseg + ((size_t)g * nb + b) * (R + 1);
+            uint32_t* out = tseg + ((size_t)g * nb + b) * tseg_stride(R);
             uint32_t acc = run + part[threadIdx.x];
             for (uint32_t r = ra; r < rb; r++) {
                 out[r] = acc;
@@ -95,19 +95,19 @@ __global__ void tile_scatter_kernel(const uint64_t* __restrict__ row_off, const 
         const uint32_t g = l / R, r = l % R;
         const uint64_t rs = row_off[l], re = row_off[l + 1];
         const uint64_t base = gbase[g];
-        const uint32_t* ts = tseg + (size_t)g * nb * (R + 1);
+        const uint32_t* ts = tseg + (size_t)g * nb * tseg_stride(R);
         for (uint64_t k = rs + lane; k < re; k += 64) {
             const uint32_t c = col_idx[k];
             const uint32_t b = c >> block_log2;
             const uint32_t rel = (uint32_t)(k - rs) - seg[(size_t)b * nloc + l];
-            tcol[base + ts[(size_t)b * (R + 1) + r] + rel] = (uint16_t)(c & bmask);
+            tcol[base + ts[(size_t)b * tseg_stride(R) + r] + rel] = (uint16_t)(c & bmask);
         }
         for (uint32_t b = lane; b < nb; b += 64) {
             const uint32_t s0 = seg[(size_t)b * nloc + l], s1 = seg[(size_t)(b + 1) * nloc + l];
             const uint32_t len = s1 - s0;
             if (len & 7u) {
                 const uint16_t first = (uint16_t)(col_idx[rs + s0] & bmask);
-                const uint64_t p0 = base + ts[(size_t)b * (R + 1) + r];
+                const uint64_t p0 = base + ts[(size_t)b * tseg_stride(R) + r];
                 for (uint32_t i = len; i < ((len + 7u) & ~7u); i++) tcol[p0 + i] = first;
             }
         }
@@ -154,7 +154,7 @@ int layout_from_seg(TiledLayout& L, const uint32_t* seg, hipStream_t s) {
     auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
     chk(hipMalloc(&totals, sizeof(uint64_t) * (G + 1)));
     chk(hipMalloc(&L.gbase, sizeof(uint64_t) * (G + 1)));
-    chk(hipMalloc(&L.tseg, sizeof(uint32_t) * std::max<size_t>((size_t)G * nb * (R + 1), 1)));
+    chk(hipMalloc(&L.tseg, sizeof(uint32_t) * std::max<size_t>((size_t)G * nb * tseg_stride(R), 4)));
     if (e == hipSuccess && nloc) {
         tile_group_total_kernel<<<std::min<uint32_t>(G, 65535), 256, 0, s>>>(seg, nloc, nb, R, G, totals);
         chk(hipMemsetAsync(totals + G, 0, sizeof(uint64_t), s));
@@ -200,7 +200,7 @@ struct ErArgs {
 __device__ __forceinline__ uint64_t tile_pos(const uint64_t* gbase, const uint32_t* tseg, uint32_t R, uint32_t nb,
                                              uint32_t l, uint32_t b) {
     const uint32_t g = l / R, r = l - g * R;
-    return gbase[g] + tseg[((size_t)g * nb + b) * (R + 1) + r];
+    return gbase[g] + tseg[((size_t)g * nb + b) * tseg_stride(R) + r];
 }
 
 // Streams (i, Y) whose edges touch rows [vb, ve): row i own (any Y >= block(i)), or column block Y
@@ -354,7 +354,7 @@ int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx) {
     const uint32_t n = gh->g.n, R = L->grp_rows, nb = L->nblocks, G = L->ngroups;
     std::vector<uint16_t> tc(L->ids);
     std::vector<uint64_t> gb(G + 1);
-    std::vector<uint32_t> ts((size_t)G * nb * (R + 1));
+    std::vector<uint32_t> ts((size_t)G * nb * tseg_stride(R));
     MCMC_HIP_TRY(hipSetDevice(gh->g.device));
     MCMC_HIP_TRY(hipMemcpy(tc.data(), L->tcol, sizeof(uint16_t) * L->ids, hipMemcpyDeviceToHost));
     MCMC_HIP_TRY(hipMemcpy(gb.data(), L->gbase, sizeof(uint64_t) * (G + 1), hipMemcpyDeviceToHost));
@@ -365,7 +365,7 @@ int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx) {
         const uint32_t g = v / R, r = v % R;
         row.clear();
         for (uint32_t b = 0; b < nb; b++) {
-            const uint32_t* t = ts.data() + ((size_t)g * nb + b) * (R + 1);
+            const uint32_t* t = ts.data() + ((size_t)g * nb + b) * tseg_stride(R);
             for (uint64_t q = gb[g] + t[r]; q < gb[g] + t[r + 1]; q++)
                 row.push_back((b << L->block_log2) | tc[q]);
         }

@@ -16,3 +16,13 @@ for path in sys.argv[1:]:
     d = np.diff(rel[:, :5], axis=1)
     for k, nm in enumerate(["stage", "scan", "evaluate", "tail"]):
         print(f"  d_{nm:9s} min {d[:, k].min():7.2f} med {np.median(d[:, k]):7.2f} max {d[:, k].max():7.2f} us")
+
+# accumulated shader cycles per phase kind (slots 5-7, tiled kernel; wave 0 of each workgroup)
+for path in sys.argv[1:]:
+    t = np.fromfile(path, dtype=np.uint64).reshape(-1, 8).astype(np.float64)
+    t = t[t[:, 0] > 0]
+    if t[:, 5:8].sum() == 0:
+        continue
+    tot = t[:, 5:8].sum(axis=1)
+    for k, nm in zip(range(5, 8), ["land+barriers", "scan", "evaluate"]):
+        print(f"  cycles {nm:14s} median share {np.median(t[:, k] / tot):.3f}  median {np.median(t[:, k]) / 2.4e3:9.1f} us @2.4GHz")
