@@ -770,24 +770,27 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
 constexpr uint32_t kTileU = MCMC_TILE_U;   // quads per lane per step of the tiled scan
 
 template <int NW>
-__device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, const uint4& v, uint32_t okb,
+__device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, const uint4& v, bool ok,
                                             uint32_t (&m)[NW]) {
-    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
-    uint32_t cg[8];
+    // exec-masked: a slot past its segment (about half the slots on C3) issues no LDS reads
+    if (ok) {
+        const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+        uint32_t cg[8];
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-        cg[2 * e] = sc[w8[e] & 0xFFFFu];
-        cg[2 * e + 1] = sc[w8[e] >> 16];
-    }
+        for (int e = 0; e < 4; e++) {
+            cg[2 * e] = sc[w8[e] & 0xFFFFu];
+            cg[2 * e + 1] = sc[w8[e] >> 16];
+        }
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-        if (NW == 1) {
-            m[0] |= okb << cg[e];
-        } else {
-            const uint32_t c = cg[e];
-            const uint32_t bit = okb << (c & 31);
+        for (int e = 0; e < 8; e++) {
+            if (NW == 1) {
+                m[0] |= 1u << cg[e];
+            } else {
+                const uint32_t c = cg[e];
+                const uint32_t bit = 1u << (c & 31);
 #pragma unroll
-            for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
+                for (int w = 0; w < NW; w++) m[w] |= ((c >> 5) == (uint32_t)w) ? bit : 0u;
+            }
         }
     }
 }
@@ -833,6 +836,37 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
             glds16(C + caddr(a, lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
         }
     }
+}
+
+// Buffer descriptor over group g's ids: loads at an offset past its end (idle lanes, slots past a
+// segment) return 0 without a memory request -- a clamped address would still cost a request (C3:
+// 8 lanes/segment 64 ms, 4 lanes 42 ms: the dummy loads were throughput, not free).
+constexpr uint32_t kTileOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_group_rsrc(const SweepArgs& a, uint32_t g) {
+    const uint64_t p = (uint64_t)(uintptr_t)(a.tcol + a.gbase[g]);
+    const uint64_t bytes = 2ull * (a.gbase[g + 1] - a.gbase[g]);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const uint32_t nb = __builtin_amdgcn_readfirstlane((uint32_t)min<uint64_t>(bytes, 0xFFFFFFF0ull));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, (int)nb,
+                                             0x00020000);
+}
+#ifndef MCMC_TILE_BUFLOAD
+#define MCMC_TILE_BUFLOAD 0
+#endif
+// One quad of ids at byte offset `byte_off` of the group. MCMC_TILE_BUFLOAD=1: buffer load, slots
+// past the end return 0 without a request; 0 (default, measured faster on C3): a plain load
+// clamped to the group base.
+__device__ __forceinline__ uint4 tile_load(__amdgpu_buffer_rsrc_t r, const uint16_t* gbase_ptr, uint32_t byte_off) {
+#if MCMC_TILE_BUFLOAD
+    (void)gbase_ptr;
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    (void)r;
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(gbase_ptr) +
+                                           (byte_off == kTileOOB ? 0u : byte_off));
+#endif
 }
 
 // Segment bounds (ids from the group base) of this lane's first row in pair (g, b): sub-group
@@ -903,12 +937,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint32_t fpos, fend;
     tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend);
     fpos += 8u * li;
+    __amdgpu_buffer_rsrc_t gr = tile_group_rsrc(a, gclamp);
     const uint16_t* __restrict__ gcol = a.tcol + a.gbase[gclamp];
     uint4 v[kTileU];
 #pragma unroll
     for (int u = 0; u < kTileU; u++) {
         const uint32_t pu = fpos + 8u * L * u;
-        v[u] = *reinterpret_cast<const uint4*>(gcol + (pu < fend ? pu : 0u));
+        v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the staging below the first quads
     if (RES) {
@@ -944,6 +979,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         const uint32_t pg = nvalid ? ng : g, pb = nvalid ? nbn : b;
         uint32_t npos, nend;
         tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend);
+        const __amdgpu_buffer_rsrc_t ngr = tile_group_rsrc(a, pg);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
         const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + buf * SB;
         const uint32_t* __restrict__ sseg = reinterpret_cast<const uint32_t*>(seg_base + buf * SEGB);
@@ -957,9 +993,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         uint32_t m[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) m[i] = 0;
-        while (__ballot(row < rows)) {
+        // One step: gathers of `cur` (this step's quads), loads of the next step into `nxt`.
+        // Unrolled by two over ping-pong register sets: a `v = vn` copy at the back-edge made the
+        // compiler wait vmcnt(0) before the copy, i.e. a one-step-deep pipeline.
+        auto step_fn = [&](const uint4 (&cur)[kTileU], uint4 (&nxt)[kTileU]) -> bool {
             const bool act = row < rows;
-            // next step's position (same row, or the sub-group's claimed next row) and its loads first
+            // next step's position (same row, or the sub-group's claimed next row)
             uint32_t npos2 = pos + step, nrow = row, nend2 = end;
             const bool fin = act && (npos2 - 8u * li >= end);
             if (__ballot(fin)) {
@@ -970,15 +1009,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
                 }
             }
-            uint4 vn[kTileU];
 #pragma unroll
             for (int u = 0; u < kTileU; u++) {
                 const uint32_t pu = npos2 + 8u * L * u;
-                vn[u] = *reinterpret_cast<const uint4*>(gcol + ((nrow < rows && pu < nend2) ? pu : 0u));
+                nxt[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);
             }
 #pragma unroll
-            for (int u = 0; u < kTileU; u++)
-                tile_gather<NW>(scb, v[u], (act && pos + 8u * L * u < end) ? 1u : 0u, m);
+            for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
             if (__ballot(fin)) {
                 // OR over the L lanes of every sub-group (all lanes take part; only finished
                 // sub-groups use the result)
@@ -1001,17 +1038,24 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             row = nrow;
             pos = npos2;
             end = nend2;
-#pragma unroll
-            for (int u = 0; u < kTileU; u++) v[u] = vn[u];
+            return __ballot(row < rows) != 0;
+        };
+        uint4 v1[kTileU];
+        if (__ballot(row < rows)) {
+            for (;;) {
+                if (!step_fn(v, v1)) break;
+                if (!step_fn(v1, v)) break;
+            }
         }
         // the next pair's first quads: in flight across the boundary (and the evaluation)
+        gr = ngr;
         gcol = ngcol;
         fpos = npos + 8u * li;
         fend = nend;
 #pragma unroll
         for (int u = 0; u < kTileU; u++) {
             const uint32_t pu = fpos + 8u * L * u;
-            v[u] = *reinterpret_cast<const uint4*>(gcol + (pu < fend ? pu : 0u));
+            v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
         }
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_scan += t1 - tmark; tmark = t1; }
         if (b + 1 == nb) {

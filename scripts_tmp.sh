@@ -1,9 +1,11 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x -k "tiled or gather or lockstep or golden or unsorted or er_fast or grid" > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x -k "tiled or gather or lockstep or golden or er_fast" > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-ph() { name=$1; shift; MCMC_PHASE_DUMP=gpurun_out/ph_$name.bin timeout -k 10 400 python bench.py --warmup 2 --no-cpu-baseline --no-refstruct "$@" > gpurun_out/b_$name.log 2>&1 || { tail -5 gpurun_out/b_$name.log; exit 1; }
-python -c "import json; d=json.loads(open('gpurun_out/b_$name.log').read().strip().splitlines()[-1]); print('$name', '%.4f ms'%d['roofline']['kernel_ms'], '%.3e'%d['value'], 'frac %.3f'%d['roofline']['frac'], 'R', d['roofline']['layout']['grp_rows'])"
-python scripts_phase.py gpurun_out/ph_$name.bin | tail -7; }
-ph c3 --steps 10
-ph c2 --steps 50 --config c2
-ph c2s --steps 50 --config c2 --variant tiled::::1
+for v in tiled:16:1 tiled:16:2 tiled:16:3; do
+timeout -k 10 400 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-refstruct --variant $v > gpurun_out/b_c3v.log 2>&1 || { tail -5 gpurun_out/b_c3v.log; exit 1; }
+python -c "import json; d=json.loads(open('gpurun_out/b_c3v.log').read().strip().splitlines()[-1]); print('c3 $v', '%.3f ms'%d['roofline']['kernel_ms'], 'frac %.3f'%d['roofline']['frac'])"
+done
+for v in tiled tiled::::1; do
+timeout -k 10 400 python bench.py --config c2 --steps 50 --warmup 5 --no-cpu-baseline --no-refstruct --variant $v > gpurun_out/b_c2v.log 2>&1 || { tail -5 gpurun_out/b_c2v.log; exit 1; }
+python -c "import json; d=json.loads(open('gpurun_out/b_c2v.log').read().strip().splitlines()[-1]); print('c2 $v', '%.4f ms'%d['roofline']['kernel_ms'], '%.3e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+done
