@@ -1009,13 +1009,22 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
                 }
             }
+            // the wave's last step issues no loads, so no load is pending into either register set
+            // when the loop ends (a pending one made hipcc wait vmcnt(0) at the next loop entry);
+            // the gathers sit in both branches so each path keeps an exact vmcnt
+            const bool cont = __ballot(nrow < rows) != 0;
+            if (cont) {
 #pragma unroll
-            for (int u = 0; u < kTileU; u++) {
-                const uint32_t pu = npos2 + 8u * L * u;
-                nxt[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);
+                for (int u = 0; u < kTileU; u++) {
+                    const uint32_t pu = npos2 + 8u * L * u;
+                    nxt[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);
+                }
+#pragma unroll
+                for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
+            } else {
+#pragma unroll
+                for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
             }
-#pragma unroll
-            for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
             if (__ballot(fin)) {
                 // OR over the L lanes of every sub-group (all lanes take part; only finished
                 // sub-groups use the result)
@@ -1038,7 +1047,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             row = nrow;
             pos = npos2;
             end = nend2;
-            return __ballot(row < rows) != 0;
+            return cont;
         };
         uint4 v1[kTileU];
         if (__ballot(row < rows)) {
