@@ -993,69 +993,65 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         uint32_t m[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) m[i] = 0;
-        // One step: gathers of `cur` (this step's quads), loads of the next step into `nxt`.
-        // Unrolled by two over ping-pong register sets: a `v = vn` copy at the back-edge made the
-        // compiler wait vmcnt(0) before the copy, i.e. a one-step-deep pipeline.
-        auto step_fn = [&](const uint4 (&cur)[kTileU], uint4 (&nxt)[kTileU]) -> bool {
-            const bool act = row < rows;
-            // next step's position (same row, or the sub-group's claimed next row)
-            uint32_t npos2 = pos + step, nrow = row, nend2 = end;
-            const bool fin = act && (npos2 - 8u * li >= end);
-            if (__ballot(fin)) {
-                const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);
-                if (fin) {
-                    nrow = got;
-                    if (nrow < rows) { npos2 = sseg[nrow] + 8u * li; nend2 = sseg[nrow + 1]; }
-                    if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
-                }
-            }
-            // the wave's last step issues no loads, so no load is pending into either register set
-            // when the loop ends (a pending one made hipcc wait vmcnt(0) at the next loop entry);
-            // the gathers sit in both branches so each path keeps an exact vmcnt
-            const bool cont = __ballot(nrow < rows) != 0;
-            if (cont) {
-#pragma unroll
-                for (int u = 0; u < kTileU; u++) {
-                    const uint32_t pu = npos2 + 8u * L * u;
-                    nxt[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);
-                }
-#pragma unroll
-                for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
-            } else {
-#pragma unroll
-                for (int u = 0; u < kTileU; u++) tile_gather<NW>(scb, cur[u], act && pos + 8u * L * u < end, m);
-            }
-            if (__ballot(fin)) {
-                // OR over the L lanes of every sub-group (all lanes take part; only finished
-                // sub-groups use the result)
-                uint32_t red[NW];
-#pragma unroll
-                for (int i = 0; i < NW; i++) {
-                    uint32_t x = m[i];
-                    for (uint32_t off = 1; off < L; off <<= 1) x |= __shfl_xor(x, (int)off, 64);
-                    red[i] = x;
-                }
-                if (fin) {
-                    if (li == 0) {
-#pragma unroll
-                        for (int i = 0; i < NW; i++) atomicOr(&smask[row * NW + i], red[i]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < NW; i++) m[i] = 0;
-                }
-            }
-            row = nrow;
-            pos = npos2;
-            end = nend2;
-            return cont;
-        };
+        // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
+        // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
+        // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
+        // loads, so nothing is pending into either set when the loop ends; the gathers sit in both
+        // branches so each path keeps an exact vmcnt.
+#define MCMC_TILE_STEP(CUR, NXT, CONT)                                                                  \
+    {                                                                                                   \
+        const bool act = row < rows;                                                                    \
+        uint32_t npos2 = pos + step, nrow = row, nend2 = end;                                           \
+        const bool fin = act && (npos2 - 8u * li >= end);                                               \
+        if (__ballot(fin)) {                                                                            \
+            const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
+            if (fin) {                                                                                  \
+                nrow = got;                                                                             \
+                if (nrow < rows) { npos2 = sseg[nrow] + 8u * li; nend2 = sseg[nrow + 1]; }              \
+                if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);                                    \
+            }                                                                                           \
+        }                                                                                               \
+        CONT = __ballot(nrow < rows) != 0;                                                              \
+        if (CONT) {                                                                                     \
+            _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                        \
+                const uint32_t pu = npos2 + 8u * L * u;                                                 \
+                NXT[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);         \
+            }                                                                                           \
+            _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
+                tile_gather<NW>(scb, CUR[u], act && pos + 8u * L * u < end, m);                         \
+        } else {                                                                                        \
+            _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
+                tile_gather<NW>(scb, CUR[u], act && pos + 8u * L * u < end, m);                         \
+        }                                                                                               \
+        if (__ballot(fin)) {                                                                            \
+            uint32_t red[NW];                                                                           \
+            _Pragma("unroll") for (int i = 0; i < NW; i++) {                                            \
+                uint32_t x = m[i];                                                                      \
+                for (uint32_t off = 1; off < L; off <<= 1) x |= __shfl_xor(x, (int)off, 64);            \
+                red[i] = x;                                                                             \
+            }                                                                                           \
+            if (fin) {                                                                                  \
+                if (li == 0) {                                                                          \
+                    _Pragma("unroll") for (int i = 0; i < NW; i++) atomicOr(&smask[row * NW + i], red[i]); \
+                }                                                                                       \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) m[i] = 0;                                \
+            }                                                                                           \
+        }                                                                                               \
+        row = nrow;                                                                                     \
+        pos = npos2;                                                                                    \
+        end = nend2;                                                                                    \
+    }
         uint4 v1[kTileU];
         if (__ballot(row < rows)) {
             for (;;) {
-                if (!step_fn(v, v1)) break;
-                if (!step_fn(v1, v)) break;
+                bool c0, c1;
+                MCMC_TILE_STEP(v, v1, c0)
+                if (!c0) break;
+                MCMC_TILE_STEP(v1, v, c1)
+                if (!c1) break;
             }
         }
+#undef MCMC_TILE_STEP
         // the next pair's first quads: in flight across the boundary (and the evaluation)
         gr = ngr;
         gcol = ngcol;
@@ -1487,9 +1483,13 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
             while (r > 1 && lds_need(res, r) > kMaxLdsBytes) r -= 1;
             return lds_need(res, r) <= kMaxLdsBytes ? r : 0u;
         };
-        const bool stream_forced = getenv("MCMC_TILE_STREAM") && atoi(getenv("MCMC_TILE_STREAM"));
+        // Streaming is the default: with the slices double-buffered by LDS-DMA it measured faster
+        // than the resident replica even where the replica fits (C2: 44.3 vs 45.4 us).
+        // MCMC_TILE_STREAM=0 selects the resident replica when it fits.
+        const char* ts_env = getenv("MCMC_TILE_STREAM");
+        const bool want_resident = ts_env && atoi(ts_env) == 0;
         const uint32_t rmax_res = rep <= 10u * 16u * 1024u ? rmax_for(true) : 0u;
-        const bool resident = !stream_forced && rmax_res >= 64u;
+        const bool resident = want_resident && rmax_res >= 64u;
         if (!resident) c->block_log2 = std::min<uint32_t>(c->block_log2, 16u);
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);

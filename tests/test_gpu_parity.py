@@ -148,15 +148,16 @@ def circulant(n, K):
 
 @pytest.mark.parametrize("gather", ["lds", "global", "blocked:17", "blocked:8", "blocked:6", "tiled",
                                     "tiled:8", "tiled:6:0:7", "tiled:7:3:1", "tiled:4:6:33", "tiled:9:2:100",
-                                    "tiled::::1", "tiled:8:1:50:1", "tiled:6:2:7:1", "tiled:10:5:1:1"])
+                                    "tiled::::0", "tiled:8:1:50:0", "tiled:6:2:7:0", "tiled:10:5:1:0"])
 @pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip", [(3000, 0.02, 16, 31, 1e-8, 0, 60),
                                                             (2000, 0.05, 100, 32, 1e-8, 2, 20),
                                                             (1500, 0.3, 5, 33, 3.3e6, 1, 15),
                                                             (2500, 0.1, 200, 34, 1e-8, 0, 10)])
 def test_all_gather_variants(M, monkeypatch, gather, n, p, ncol, seed, eps, taboo, maxrip):
     """LDS-staged, L2-gather, column-blocked (down to 64-vertex blocks, i.e. dozens of column
-    blocks and many chunks) and tiled sweeps (spec tiled:block_log2:lanes_log2:group_rows -- 16-vertex
-    blocks, 1..64 lanes per row segment, odd group sizes) give the same bit-exact results."""
+    blocks and many chunks) and tiled sweeps (spec tiled:block_log2:lanes_log2:group_rows:stream --
+    16-vertex blocks, 1..64 lanes per row segment, odd group sizes; streamed slices by default,
+    stream=0 the LDS-resident replica) give the same bit-exact results."""
     set_gather(monkeypatch, gather)
     off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
     col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo)
@@ -288,7 +289,7 @@ def test_partitioned_driver_nccl_world1(M):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("gather", ["blocked:7", "tiled:7", "tiled:7:::1"])
+@pytest.mark.parametrize("gather", ["blocked:7", "tiled:7", "tiled:7:::0"])
 def test_blocked_unsorted_upload(M, monkeypatch, gather):
     """Uploaded rows in arbitrary order (as --graph produces) are sorted once for the blocked and
     tiled variants; the result is unchanged (the sweep is order-independent)."""
@@ -304,10 +305,10 @@ def test_blocked_unsorted_upload(M, monkeypatch, gather):
     assert_same(col, st, r)
 
 
-@pytest.mark.parametrize("gather", ["blocked:15", "blocked:12", "tiled", "tiled:12", "tiled::::1", "tiled:14:2::1"])
+@pytest.mark.parametrize("gather", ["blocked:15", "blocked:12", "tiled", "tiled:12", "tiled::::0", "tiled:14:2::0"])
 def test_c2_blocked_matches_golden(M, monkeypatch, gather):
     """configs[1] full run through the column-blocked kernel (4 and 25 column blocks) and the tiled
-    kernel (resident replica with 2 and 25 column blocks; streamed 64 KiB / 16 KiB slices)."""
+    kernel (streamed slices with 2 and 25 column blocks; LDS-resident replica with 2 and 7)."""
     set_gather(monkeypatch, gather)
     d = json.loads((GOLDEN / "c2.json").read_text())
     rng = M.GlibcRand(1)
@@ -319,7 +320,7 @@ def test_c2_blocked_matches_golden(M, monkeypatch, gather):
 
 
 @pytest.mark.parametrize("world", [2, 5])
-@pytest.mark.parametrize("gather", ["tiled:9", "tiled:9:::1", "tiled:6:1:5:1"])
+@pytest.mark.parametrize("gather", ["tiled:9", "tiled:9:::0", "tiled:6:1:5:0"])
 def test_partitioned_lockstep_tiled(M, monkeypatch, world, gather):
     set_gather(monkeypatch, gather)
     off, idx, nc, r = oracle_case(3000, 0.03, 20, 61, maxRip=30)
@@ -357,7 +358,7 @@ def test_er_fast_generator_matches_restatement(M, n, p, seed):
     assert np.array_equal(s.cumulDegs, off) and np.array_equal(s.neighs, idx)
 
 
-@pytest.mark.parametrize("n,p,ncol,seed,stream", [(130000, 0.004, 16, 5, "0"), (200000, 0.003, 32, 6, "0"),
+@pytest.mark.parametrize("n,p,ncol,seed,stream", [(130000, 0.004, 16, 5, "0"), (200000, 0.003, 32, 6, "1"),
                                                   (130000, 0.004, 16, 7, "1")])
 def test_er_fast_sweep_matches_oracle(M, monkeypatch, n, p, ncol, seed, stream):
     """MCMC on a generated graph (resident replica; streamed slices) == the oracle on the restated CSR."""
