@@ -337,10 +337,15 @@ int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t 
     return MCMC_OK;
 }
 
-// Group rows of the tiled layout a context on `nloc` rows picks by default (mcmc_create): about one
-// group per CU, at least 32, at most `rmax`.
+// Group rows of the tiled layout a context on `nloc` rows picks by default (mcmc_create and the
+// generator agree): the group count a multiple of the CU count (k groups per workgroup, so no
+// workgroup finishes a group later than the others: C4's 1.25e6 rows per rank at R = 1792 were 698
+// groups = 2 or 3 per workgroup), R at most `rmax`, at least 32.
 uint32_t tiled_default_rows(uint32_t nloc, uint32_t cus, uint32_t rmax) {
-    uint32_t R = (nloc + cus - 1) / std::max<uint32_t>(cus, 1);
+    cus = std::max<uint32_t>(cus, 1);
+    rmax = std::max<uint32_t>(rmax, 1);
+    const uint64_t k = std::max<uint64_t>(1, ((uint64_t)nloc + (uint64_t)cus * rmax - 1) / ((uint64_t)cus * rmax));
+    const uint32_t R = (uint32_t)(((uint64_t)nloc + k * cus - 1) / (k * cus));
     return std::max<uint32_t>(std::min<uint32_t>(32u, rmax), std::min<uint32_t>(rmax, R));
 }
 

@@ -1,4 +1,4 @@
-"""Folds rocprofv3 PMC passes (scripts_gpu_prof.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE) into
+"""Folds rocprofv3 PMC passes (scripts/gpu_prof.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE) into
 profiles/pmc_summary.json, which bench.py reads for roofline.traffic.
 
   python profiles/make_pmc_summary.py <prof_dir> <key> [kernel-substring]

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel trace + stats of a short bench, then PMC HBM counters in separate passes
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950). Extra args go to bench.py.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 OUT=gpurun_out/prof_$TAG
