@@ -53,6 +53,8 @@ struct DevState {
     unsigned long long viol;    // sum of viol_v over the swept rows (Cviol_t)
     uint32_t ev_count;          // overflow events this sweep
     uint32_t arrive;            // workgroups finished with the running sweep (fused commit)
+    unsigned long long arrive_viol;   // packed fused arrival: [63:48] workgroups arrived,
+                                      // [47:32] workgroups that appended events, [31:0] Cviol
     uint32_t glibc_head;        // ring head of the glibc window
     uint32_t glibc_ring[31];
     uint32_t init_rejections;
@@ -239,6 +241,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         st->viol = 0;
         st->ev_count = 0;
         st->arrive = 0;
+        st->arrive_viol = 0;
     }
 }
 
@@ -258,6 +261,7 @@ __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long lon
             st->maxIterReached = stop_cap;
             st->finalViol = viol;
             st->arrive = 0;
+            st->arrive_viol = 0;
         }
         return;
     }
@@ -320,6 +324,7 @@ __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long v
         st->viol = 0;
         st->ev_count = 0;
         st->arrive = 0;
+        st->arrive_viol = 0;
     }
 }
 
@@ -370,7 +375,7 @@ template <int NW>
 __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* __restrict__ st,
                                               const uint8_t* __restrict__ Cown, uint8_t* __restrict__ Cs,
                                               uint32_t x_t, uint32_t l0, uint32_t cnt, const uint32_t (&acc)[NW],
-                                              int lane) {
+                                              int lane, uint32_t& ev_flag) {
     const bool valid = (uint32_t)lane < cnt;
     const uint32_t l = l0 + lane;
     const uint32_t v = a.v_begin + l;
@@ -435,6 +440,7 @@ __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* 
     const uint32_t nviol = (uint32_t)__popcll(__ballot(viol));
     const uint64_t eb = __ballot(event);
     if (eb) {
+        ev_flag = 1u;
         uint32_t basei = 0;
         if (lane == 0) basei = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
         basei = __shfl(basei, 0, 64);
@@ -564,34 +570,50 @@ __device__ __forceinline__ void scan_tile(const uint32_t* __restrict__ tcol, con
 // drains its stores, the workgroup meets, lane 0 publishes Cviol, releases at agent scope and
 // arrives; the workgroup whose arrival is last acquires.
 struct TailShared {
-    uint32_t wg_viol, wg_last, t, E, err;
+    uint32_t wg_viol, wg_ev, wg_last, t, E, err;
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     unsigned long long viol;
 };
 
 __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, TailShared& sh, uint32_t wave_viol,
-                                           int lane, uint32_t* lds, uint32_t cap) {
-    if (lane == 0 && wave_viol) atomicAdd(&sh.wg_viol, wave_viol);
+                                           uint32_t wave_ev, int lane, uint32_t* lds, uint32_t cap) {
+    if (lane == 0) {
+        if (wave_viol) atomicAdd(&sh.wg_viol, wave_viol);
+        if (wave_ev) sh.wg_ev = 1u;
+    }
     if (!a.fused) {
         __syncthreads();
         if (threadIdx.x == 0 && sh.wg_viol) atomicAdd(&st->viol, (unsigned long long)sh.wg_viol);
         return;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (sh.wg_viol) atomicAdd(&st->viol, (unsigned long long)sh.wg_viol);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t prev = atomicAdd(&st->arrive, 1u);
-        sh.wg_last = (prev == gridDim.x - 1) ? 1u : 0u;
-        if (sh.wg_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // One packed arrival: [63:48] +1 workgroup, [47:32] +1 if it appended overflow events,
+        // [31:0] its Cviol. The events are the only plain stores the committing workgroup reads, so
+        // only a workgroup that appended some releases (and the last one acquires only if the
+        // packed count says any did): the per-workgroup release fence and second atomic of every
+        // sweep are gone.
+        const bool ev = sh.wg_ev != 0;
+        if (ev) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const unsigned long long mine = (1ull << 48) | (ev ? (1ull << 32) : 0ull) | (unsigned long long)sh.wg_viol;
+        const unsigned long long prev = atomicAdd(&st->arrive_viol, mine);
+        sh.wg_last = ((prev >> 48) == gridDim.x - 1) ? 1u : 0u;
+        if (sh.wg_last) {
+            const unsigned long long tot = prev + mine;
+            sh.viol = tot & 0xFFFFFFFFull;
+            if ((tot >> 32) & 0xFFFFull) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                sh.E = __hip_atomic_load(&st->ev_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                sh.E = 0;
+            }
             sh.t = st->t;
-            sh.viol = st->viol;
-            sh.E = st->ev_count;
-            sh.err = st->err;
+            sh.err = __hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
@@ -611,7 +633,7 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     __shared__ uint32_t sort_static[LDSC ? 1 : 2048];
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
-    if (threadIdx.x == 0) sh.wg_viol = 0;
+    if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
@@ -641,7 +663,7 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t wbeg = a.wave_start[gw], wend = a.wave_start[gw + 1];
-    uint32_t wave_viol = 0;   // Cviol of this wave's rows
+    uint32_t wave_viol = 0, wave_ev = 0;   // Cviol of this wave's rows; overflow events appended
 
     for (uint32_t l0 = wbeg; l0 < wend; l0 += a.tile) {
         const uint32_t cnt = min(a.tile, wend - l0);
@@ -653,9 +675,9 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
         const uint64_t tb = readlane64(ob, 0) & ~3ull;   // tile-relative 32-bit arc positions
         uint32_t acc[NW];
         scan_tile<NW>(a.col_idx + tb, Cg, 0u, 0xFFFFFFFFu, (uint32_t)(ob - tb), (uint32_t)(oe - tb), cnt, lane, acc);
-        wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane);
+        wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane, wave_ev);
     }
-    sweep_tail(a, st, sh, wave_viol, lane, LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static,
+    sweep_tail(a, st, sh, wave_viol, wave_ev, lane, LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static,
                LDSC ? a.lds_sort_cap : 2048u);
 }
 
@@ -675,7 +697,7 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
     __shared__ uint32_t tile_ctr;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
-    if (threadIdx.x == 0) sh.wg_viol = 0;
+    if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
@@ -689,7 +711,7 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
     const uint32_t nb = a.nblocks;
     const uint32_t nloc = a.v_end - a.v_begin;
     const uint32_t gbeg = a.wave_start[blockIdx.x], gend = a.wave_start[blockIdx.x + 1];
-    uint32_t wave_viol = 0;
+    uint32_t wave_viol = 0, wave_ev = 0;
 
     for (uint32_t c0 = gbeg; c0 < gend; c0 += R) {
         const uint32_t cn = min(R, gend - c0);
@@ -748,11 +770,11 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
             uint32_t acc[NW];
 #pragma unroll
             for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
-            wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, c0 + e0, cnt, acc, lane);
+            wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, c0 + e0, cnt, acc, lane, wave_ev);
         }
     }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
-    sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), B / 4u);
+    sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), B / 4u);
 }
 
 // Tiled sweep (variant 3). Group g = local rows [g*R, (g+1)*R); for every column block b the group's
@@ -905,7 +927,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
     MCMC_PHASE(a, 0);
-    if (threadIdx.x == 0) sh.wg_viol = 0;
+    if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
@@ -924,7 +946,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t nloc = a.v_end - a.v_begin;
     const uint32_t nbytes16 = (a.n + 15u) & ~15u;
     const uint32_t lds0 = lds_addr(lbase), seg_lds0 = lds_addr(seg_base);
-    uint32_t wave_viol = 0;
+    uint32_t wave_viol = 0, wave_ev = 0;
     const bool timing = a.phase_ts != nullptr;
     uint64_t cyc_wait = 0, cyc_scan = 0, cyc_eval = 0, tmark = 0;
 
@@ -1075,7 +1097,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
                     if ((uint32_t)lane < cnt) smask[idx] = 0;
                 }
-                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane);
+                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane, wave_ev);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         }
@@ -1092,7 +1114,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         a.phase_ts[blockIdx.x * 8u + 7] = cyc_eval;
     }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
-    sweep_tail(a, st, sh, wave_viol, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+    sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
     MCMC_PHASE(a, 4);
 }
 
