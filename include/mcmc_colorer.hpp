@@ -70,6 +70,7 @@ struct ColoringMCMCParams {
     float ratioFreezed;
     uint32_t tabooIteration;
     bool tailcut;
+    uint32_t tailcutRepair = 0;   // extension: corrected tail-cut pass cap (mcmc_set_tailcut_repair), 0 = off
 };
 
 // GraphStruct (graph.h:37-79) -- host view; cumulDegs widened to uint64.
@@ -179,6 +180,7 @@ public:
         p.seed = seed + (uint32_t)iteration;
         MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
         MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));
+        if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(ctx, param.tailcutRepair));
         MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
         MCMC_CHECK(mcmc_run(ctx, 0, &stats));
         MCMC_CHECK(mcmc_get_glibc_window(ctx, mcmc::glibc_global().w));

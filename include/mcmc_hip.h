@@ -64,7 +64,7 @@ typedef struct {
     uint64_t initDraws;        /* engine draws of the initial coloring (n + rejections)          */
     double   loopMs;           /* device time of the sweep loop (hipEvent)                       */
     uint32_t sweepsRun;        /* sweeps executed (= iter, plus the final count-only pass)       */
-    uint32_t reserved;
+    uint32_t tailcutPasses;    /* tail-cut passes run after the loop (mcmc_set_tailcut_repair)   */
 } mcmc_run_stats;
 
 const char* mcmc_last_error(void);
@@ -119,6 +119,15 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0);
 /* run() main loop (coloringMCMC_CPU.cpp:127-270) on the device: sweeps until Cviol <= z or the
  * maxRip cap. max_sweeps > 0 stops early after that many sweeps (bounded samples). */
 int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats);
+/* Tail cutting after the loop (coloringMCMC_CPU.cpp:272-311) with the inner loop's k++ fix (the
+ * reference increments i at :289 and never returns): colorIdx sorted by ascending colour histogram
+ * when z > 0; then, while Cviol > 0 and at most max_passes times, every flagged vertex in ascending
+ * order takes the first colour of colorIdx free among its neighbours, and Cviol is recounted. The
+ * first pass visits the vertices flagged in the colouring before the last accepted sweep, as the
+ * reference's (unswapped) Cviols does. Call before mcmc_run; mcmc_run then reports the repaired
+ * Cviol in finalViol and the passes in tailcutPasses (the trajectory is the loop's). 0 disables.
+ * Whole-graph contexts only; costs n bytes of flag writes per sweep while enabled. */
+int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes);
 int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out /* n */);
 int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 /* Timed throughput mode for benchmarks: exactly `sweeps` sweeps of the loop body (no

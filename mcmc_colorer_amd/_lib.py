@@ -36,6 +36,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_init_coloring": (c_int, [c_void_p, _u32p]),
     "mcmc_run": (c_int, [c_void_p, c_uint32, c_void_p]),
     "mcmc_get_coloring": (c_int, [c_void_p, _u32p]),
+    "mcmc_set_tailcut_repair": (c_int, [c_void_p, c_uint32]),
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
@@ -76,7 +77,7 @@ class MCMCRunStats(ctypes.Structure):
         ("initDraws", c_uint64),
         ("loopMs", c_double),
         ("sweepsRun", c_uint32),
-        ("reserved", c_uint32),
+        ("tailcutPasses", c_uint32),
     ]
 
 

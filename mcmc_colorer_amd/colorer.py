@@ -39,6 +39,9 @@ class ColoringMCMCParams:
     maxRip: int = 250
     tabooIteration: int = 0
     tailcut: bool = False
+    # extension: corrected tail cut after the loop (coloringMCMC_CPU.cpp:272-311 with k++), at
+    # most this many passes; 0 = off (the reference's tail cut never returns, see tailcut.hip)
+    tailcutRepair: int = 0
 
     def to_c(self, seed: int) -> MCMCParams:
         return MCMCParams(self.nCol, self.epsilon, self.lambda_, self.ratioFreezed, self.numColorRatio,
@@ -212,6 +215,8 @@ class ColoringMCMC:
         check(lib().mcmc_create(self.graph.handle, ctypes.byref(self._cparams), self.v_begin, self.v_end,
                                 ctypes.byref(self._ctx)))
         check(lib().mcmc_set_glibc_window(self._ctx, u32ptr(self.rand.glibc.window)))
+        if self.param.tailcutRepair:
+            check(lib().mcmc_set_tailcut_repair(self._ctx, int(self.param.tailcutRepair)))
         c0 = None if C0 is None else u32ptr(np.ascontiguousarray(C0, dtype=np.uint32))
         check(lib().mcmc_init_coloring(self._ctx, c0))
 

@@ -4,6 +4,8 @@
 // Same options, defaults and output naming as the reference:
 //   --graph FILE | --simulate P -n N, --mcmcgpu, --nCol N, --numColRatio R, --tabooIteration N,
 //   --tailcut, --repet N, --seed N, --outDir D
+//   --tailcutRepair: after the loop, run the reference's tail cut (coloringMCMC_CPU.cpp:272-311)
+//   with its inner loop fixed (k++; the reference's never returns), at most 1000 passes
 // Outputs <outDir>/<graphName>-MCMC_GPU-<i>.log and -colors.txt per repetition.
 // --mcmccpu is served by the test-infrastructure oracle (oracle/build/mcmc_cpu_ref, same flags);
 // --lubygpu/--grdffgpu/--vffgpu are other colorers, outside this build's scope.
@@ -106,6 +108,7 @@ void help(const char* argv0) {
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
               << "  --tabooIteration N   taboo iterations (default 0)\n"
               << "  --tailcut            stop at Cviol <= max(50, n/2000)\n"
+              << "  --tailcutRepair      then repair the remaining conflicts (corrected tail cut, <= 1000 passes)\n"
               << "  --repet N            repetitions, seeds seed+i (default 1)\n"
               << "  --seed N             seed (default: time, which also srand()s glibc)\n"
               << "  --outDir D           output directory\n"
@@ -118,7 +121,8 @@ int main(int argc, char** argv) {
     std::string graphFilename, outDir;
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
-    bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false;
+    bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false,
+         tailcutRepair = false;
     uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
@@ -131,7 +135,8 @@ int main(int argc, char** argv) {
         {"tailcut", no_argument, 0, 'l'},        {"repet", required_argument, 0, 'R'},
         {"seed", required_argument, 0, 'S'},     {"help", no_argument, 0, 'h'},
         {"device", required_argument, 0, 'D'},   {"simulate-fast", required_argument, 0, 'F'},
-        {"er-seed", required_argument, 0, 'E'},  {0, 0, 0, 0}};
+        {"er-seed", required_argument, 0, 'E'},  {"tailcutRepair", no_argument, 0, 'X'},
+        {0, 0, 0, 0}};
     int c;
     while ((c = getopt_long(argc, argv, "g:o:s:n:12345k:r:t:lR:S:hD:", longopts, nullptr)) != -1) {
         try {
@@ -156,6 +161,7 @@ int main(int argc, char** argv) {
                           if (prob < 0 || prob > 1) { std::cout << "Simulation: probabilty of positive class must be 0 < prob < 1." << std::endl; return 255; }
                           break;
                 case 'E': erSeed = std::stoull(optarg); break;
+                case 'X': tailcutRepair = true; break;
                 case 'h': help(argv[0]); return 0;
                 default: break;
             }
@@ -234,12 +240,15 @@ int main(int argc, char** argv) {
         params.maxRip = 250;
         params.tabooIteration = tabooIteration;
         params.tailcut = tailcut;
+        params.tailcutRepair = tailcutRepair ? 1000u : 0u;
         ColoringMCMC<float, float> colMCMC(g, GPURandGen.randStates, params);
         colMCMC.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));
         colMCMC.run((int)i);
         const auto& st = colMCMC.getStats();
         std::cout << "MCMC GPU elapsed time: " << st.loopMs / 1000.0 << " (" << st.iter << " sweeps, final conflicts "
-                  << st.finalViol << (st.maxIterReached ? ", max iteration reached" : "") << ")" << std::endl
+                  << st.finalViol << (st.maxIterReached ? ", max iteration reached" : "");
+        if (tailcutRepair) std::cout << ", " << st.tailcutPasses << " tail-cut passes";
+        std::cout << ")" << std::endl
                   << std::endl;
     }
     delete g;

@@ -71,6 +71,27 @@ constexpr uint32_t kTileGenRowsMax = 1792;   // generator layouts: fits the stre
 int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx);
 }  // namespace mcmc
 
+namespace mcmc {
+// Row access for the tail cut (tailcut.hip): the CSR when the graph has one, else the tiled layout.
+struct TailView {
+    uint32_t n = 0;
+    const uint64_t* row_off = nullptr;
+    const uint32_t* col_idx = nullptr;
+    const uint16_t* tcol = nullptr;
+    const uint64_t* gbase = nullptr;
+    const uint32_t* tseg = nullptr;
+    uint32_t R = 0, nb = 0, block_log2 = 0;
+};
+// flags[v] = colour of v used by a neighbour (violation_count, coloringMCMC_CPU.cpp:329-350); *count = sum.
+int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s);
+// Ascending list of the flagged vertices; *list_len on the device. tmp: scratch, grown on demand.
+int tail_select(const uint8_t* flags, uint32_t n, uint32_t* list, uint32_t* list_len, void** tmp, size_t* tmp_bytes,
+                hipStream_t s);
+// One corrected tail-cut pass (coloringMCMC_CPU.cpp:281-305, k++) over the listed vertices, in order.
+int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint32_t* list_len,
+                const uint32_t* colorIdx, uint32_t nCol, hipStream_t s);
+}  // namespace mcmc
+
 struct mcmc_graph {
     mcmc::GraphDev g;
     std::vector<std::unique_ptr<mcmc::TiledLayout>> tiles;   // freed with the graph

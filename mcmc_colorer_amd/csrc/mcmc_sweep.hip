@@ -105,6 +105,9 @@ struct SweepArgs {
     uint32_t part_S, part_FB;
     uint32_t own_off;           // rank * part_FB: byte offset of this rank's own vertices
     uint64_t footer_off;        // rank * (part_S + part_FB) + part_S: this rank's footer slot
+    // tail cutting enabled (mcmc_set_tailcut_repair): sweep t stores the violation flags of C_t at
+    // vflags[(t & 1) * nloc + l] -- the tail cut's first pass needs those of the previous sweep
+    uint8_t* vflags;
 };
 
 // Byte address of vertex v in a colour buffer (partitioned buffers interleave per-rank footers).
@@ -375,7 +378,7 @@ template <int NW>
 __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* __restrict__ st,
                                               const uint8_t* __restrict__ Cown, uint8_t* __restrict__ Cs,
                                               uint32_t x_t, uint32_t l0, uint32_t cnt, const uint32_t (&acc)[NW],
-                                              int lane, uint32_t& ev_flag) {
+                                              int lane, uint32_t& ev_flag, uint8_t* __restrict__ vf) {
     const bool valid = (uint32_t)lane < cnt;
     const uint32_t l = l0 + lane;
     const uint32_t v = a.v_begin + l;
@@ -385,6 +388,7 @@ __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* 
     for (int i = 0; i < NW; i++) pop += __popc(acc[i]);
     const bool viol = valid && get_color_bit<NW>(acc, cv);
     const uint32_t Zvcomp = a.nCol - pop;
+    if (vf != nullptr && valid) vf[l] = viol;   // Cviols of C_t (coloringMCMC_CPU.cpp:152)
 
     uint32_t tab = 0;
     if (a.taboo != nullptr && valid) tab = a.taboo[l];
@@ -636,6 +640,7 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
     if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
+    uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * (a.v_end - a.v_begin) : nullptr;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     const uint8_t* __restrict__ Cg = C;
@@ -675,7 +680,7 @@ __global__ __launch_bounds__(1024) void sweep_kernel(SweepArgs a) {
         const uint64_t tb = readlane64(ob, 0) & ~3ull;   // tile-relative 32-bit arc positions
         uint32_t acc[NW];
         scan_tile<NW>(a.col_idx + tb, Cg, 0u, 0xFFFFFFFFu, (uint32_t)(ob - tb), (uint32_t)(oe - tb), cnt, lane, acc);
-        wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane, wave_ev);
+        wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, l0, cnt, acc, lane, wave_ev, vf);
     }
     sweep_tail(a, st, sh, wave_viol, wave_ev, lane, LDSC ? reinterpret_cast<uint32_t*>(sc_raw) : sort_static,
                LDSC ? a.lds_sort_cap : 2048u);
@@ -700,6 +705,7 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
     if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
+    uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * (a.v_end - a.v_begin) : nullptr;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     const uint32_t B = 1u << a.block_log2;
@@ -770,7 +776,7 @@ __global__ __launch_bounds__(1024) void sweep_blocked_kernel(SweepArgs a) {
             uint32_t acc[NW];
 #pragma unroll
             for (int i = 0; i < NW; i++) acc[i] = ((uint32_t)lane < cnt) ? smask[(e0 + lane) * NW + i] : 0u;
-            wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, c0 + e0, cnt, acc, lane, wave_ev);
+            wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, c0 + e0, cnt, acc, lane, wave_ev, vf);
         }
     }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
@@ -930,6 +936,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
+    uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * (a.v_end - a.v_begin) : nullptr;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     uint8_t* lbase = reinterpret_cast<uint8_t*>(lds_raw);
@@ -1097,7 +1104,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
                     if ((uint32_t)lane < cnt) smask[idx] = 0;
                 }
-                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane, wave_ev);
+                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane, wave_ev, vf);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         }
@@ -1233,6 +1240,15 @@ struct mcmc_ctx {
     uint32_t part_S = 0;                     // partitioned: slab stride (vertices), multiple of 16
     uint8_t* own_colors[2] = {nullptr, nullptr};   // the context's own replicas (freed at destroy)
     std::vector<uint32_t> host_events;
+    // tail cutting (mcmc_set_tailcut_repair, tailcut.hip)
+    uint32_t tailcut_max = 0;   // pass cap; 0 = off
+    uint8_t* vflags = nullptr;  // 2 x n violation flags kept by the sweeps
+    uint32_t* tc_list = nullptr;
+    uint32_t* tc_len = nullptr;
+    uint32_t* tc_colorIdx = nullptr;
+    unsigned long long* tc_count = nullptr;
+    void* tc_tmp = nullptr;
+    size_t tc_tmp_bytes = 0;
 };
 
 namespace {
@@ -1318,6 +1334,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     }
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
+    a.vflags = c->tailcut_max ? c->vflags : nullptr;
     if (c->tl) {
         a.tcol = c->tl->tcol;
         a.gbase = c->tl->gbase;
@@ -1368,6 +1385,63 @@ int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
     c->batch = batch;
+    return MCMC_OK;
+}
+
+// Tail cutting after the loop (coloringMCMC_CPU.cpp:272-311, corrected: k++, at most
+// c->tailcut_max passes; tailcut.hip). h: the device state at loop exit (done, no error).
+int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* passes) {
+    const uint32_t n = c->n, nCol = c->p.nCol;
+    uint8_t* C = c->colors[h.t & 1u];
+    *passes = 0;
+    *finalViol = h.finalViol;
+    // colorIdx: identity (:131-132), sorted by ascending colour histogram when z > 0 (:272-278);
+    // std::sort with the reference's comparator, so ties resolve as the reference's do
+    std::vector<size_t> colorIdx(nCol);
+    for (uint32_t i = 0; i < nCol; i++) colorIdx[i] = i;
+    if (c->z > 0) {
+        std::vector<uint8_t> hc(n);
+        int rc = download_colors(c, C, hc.data());
+        if (rc) return rc;
+        std::vector<size_t> histBins(nCol, 0);
+        for (uint8_t v : hc) histBins[v]++;
+        std::sort(colorIdx.begin(), colorIdx.end(), [&](int i, int j) { return histBins[i] < histBins[j]; });
+    }
+    if (*finalViol == 0) return MCMC_OK;
+    std::vector<uint32_t> ci(colorIdx.begin(), colorIdx.end());
+    MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ci.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice, c->stream));
+    TailView tv;
+    tv.n = n;
+    if (c->g->row_off) {
+        tv.row_off = c->g->row_off;
+        tv.col_idx = c->g->col_idx;
+    } else {
+        tv.tcol = c->tl->tcol;
+        tv.gbase = c->tl->gbase;
+        tv.tseg = c->tl->tseg;
+        tv.R = c->tl->grp_rows;
+        tv.nb = c->tl->nblocks;
+        tv.block_log2 = c->tl->block_log2;
+    }
+    // first pass: the flags of the colouring before the last accepted sweep (run() never swaps
+    // Cviols with Cstarviols, :259-260); sweep t kept those of C_t at parity t & 1
+    const uint8_t* flags = c->vflags + (size_t)(h.t >= 1 ? (h.t - 1u) & 1u : 0u) * n;
+    uint64_t cviol = *finalViol;
+    while (cviol > 0 && *passes < c->tailcut_max) {
+        int rc = tail_select(flags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
+        if (rc) return rc;
+        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream);
+        if (rc) return rc;
+        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream);   // :308
+        if (rc) return rc;
+        unsigned long long hv = 0;
+        MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        cviol = hv;
+        flags = c->vflags;
+        (*passes)++;
+    }
+    *finalViol = cviol;
     return MCMC_OK;
 }
 
@@ -1724,10 +1798,40 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     s.glibcDraws = h.glibc_draws;
     s.initDraws = c->initDraws;
     s.loopMs = ms;
+    if (h.done && c->tailcut_max) {
+        rc = run_tailcut(c, h, &s.finalViol, &s.tailcutPasses);
+        if (rc) return rc;
+    }
     c->last = s;
     // keep the host copy of the glibc window in step with the device stream
     for (int i = 0; i < 31; i++) c->glibc.r[i] = h.glibc_ring[(h.glibc_head + i) % 31];
     if (stats) *stats = s;
+    return MCMC_OK;
+}
+
+int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (c->part || c->v_begin != 0 || c->v_end != c->n)
+        return fail(MCMC_E_STATE, "tail cutting runs on whole-graph contexts (mcmc_run)");
+    if (c->p.nCol > 256) return fail(MCMC_E_ARG, "nCol > 256");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (max_passes && !c->vflags) {
+        const size_t n = std::max<uint32_t>(c->n, 1u);
+        MCMC_HIP_TRY(hipMalloc(&c->vflags, 2 * n));
+        MCMC_HIP_TRY(hipMalloc(&c->tc_list, sizeof(uint32_t) * n));
+        MCMC_HIP_TRY(hipMalloc(&c->tc_len, sizeof(uint32_t)));
+        MCMC_HIP_TRY(hipMalloc(&c->tc_colorIdx, sizeof(uint32_t) * 256));
+        MCMC_HIP_TRY(hipMalloc(&c->tc_count, sizeof(unsigned long long)));
+        MCMC_HIP_TRY(hipMemsetAsync(c->vflags, 0, 2 * n, c->stream));
+    }
+    if ((max_passes != 0) != (c->tailcut_max != 0)) {
+        // captured sweeps carry the flag pointer: re-capture with the new setting
+        if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }
+        if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
+        c->batch = 0;
+        c->bench_n = 0;
+    }
+    c->tailcut_max = max_passes;
     return MCMC_OK;
 }
 
@@ -1870,6 +1974,12 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wave_start);
     (void)hipFree(c->seg);
     (void)hipFree(c->phase_ts);
+    (void)hipFree(c->vflags);
+    (void)hipFree(c->tc_list);
+    (void)hipFree(c->tc_len);
+    (void)hipFree(c->tc_colorIdx);
+    (void)hipFree(c->tc_count);
+    (void)hipFree(c->tc_tmp);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -43,6 +43,13 @@ def test_cli_simulate_c1(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_tailcut_repair(tmp_path):
+    """--tailcut --tailcutRepair: the loop stops within z, the corrected tail cut repairs the rest."""
+    run_pair(tmp_path, ["--simulate", "0.02", "-n", "2500", "--nCol", "24", "--tailcut", "--tailcutRepair",
+                        "--seed", "1"], "2500_0.020000_1.000000")
+
+
+@pytest.mark.gpu
 def test_cli_simulate_repetitions_taboo_ratio(tmp_path):
     run_pair(tmp_path, ["--simulate", "0.05", "-n", "1500", "--numColRatio", "2.5", "--tabooIteration", "2",
                         "--repet", "3", "--seed", "7"], "1500_0.050000_2.500000", repet=3)

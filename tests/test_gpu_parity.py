@@ -405,3 +405,77 @@ def test_er_fast_part_lockstep(M, world):
     for b in ranks:
         assert b.coloring().tolist() == r.colors.tolist()
         assert b.trajectory().tolist() == r.traj.tolist()
+
+
+def test_gpu_generator_exact_at_1e6(M):
+    """the reference's exact setupRnd2 graph at n = 1e6 (5e11 glibc draws,
+    far beyond a CPU replay). Size-independent checks: the stream advances n(n+1)/2 draws; the CSR
+    is symmetric, loop-free and sorted; and sampled rows' upper neighbours equal the REAL glibc
+    rand() draws (the oracle's libc, positioned at row v's first draw v*n - v(v-1)/2 by the
+    jump-ahead that test_capi pins against glibc), thresholded as graphCPU.cpp:308 does."""
+    n, p = 1_000_000, 1e-4
+    rng = M.GlibcRand(1)
+    g = M.Graph.simulate(n, p, rng)
+    assert np.array_equal(rng.window, M.GlibcRand(1, n * (n + 1) // 2).window)
+    s = g.getStruct()
+    off, idx = s.cumulDegs.astype(np.int64), s.neighs.astype(np.int64)
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(off))
+    assert not np.any(rows == idx)
+    fwd = rows * n + idx
+    assert np.all(np.diff(fwd) > 0)                       # rows ascending, no duplicates
+    assert np.array_equal(np.sort(idx * n + rows), fwd)   # symmetric
+    assert abs(len(idx) - p * n * (n - 1)) < 6 * np.sqrt(p * n * n)
+    pf = float(np.float32(p))
+    for v in (0, 1, 4567, 500000, 999_998):
+        k0 = v * n - v * (v - 1) // 2                     # draws before row v of the upper triangle
+        O.set_glibc_window(M.GlibcRand(1, k0).window)
+        draws = np.asarray(O.rand(n - v), dtype=np.float64)
+        upper = v + np.nonzero(draws / 2147483647.0 < pf)[0]
+        upper = upper[upper > v]                          # the diagonal draw is consumed, then cleared
+        got = idx[off[v]:off[v + 1]]
+        assert np.array_equal(got[got > v], upper), v
+
+
+TAILCUT = [
+    # n, p, nCol, seed, maxRip, tailcut
+    (1000, 0.1, 0, 1, 250, True),     # configs[0] with --tailcut: one pass repairs the rest
+    (2500, 0.02, 24, 1, 250, True),   # nCol > 16: histogram order by libstdc++'s introsort
+    (600, 0.03, 10, 1, 250, True),    # the repair oscillates: runs to the 1000-pass bound
+    (500, 0.02, 7, 1, 250, True),
+    (250, 0.2, 5, 3, 30, False),      # too few colours: loop cap, then 1000 passes
+    (200, 0.01, 16, 4, 250, True),    # initial colouring within z: no accepted sweep
+    (300, 0.1, 40, 5, 3, False),      # z = 0: identity colour order
+]
+
+
+@pytest.mark.parametrize("gather", ["tiled", "tiled::::0", "tiled:6:2:7", "lds", "global", "blocked:8"])
+@pytest.mark.parametrize("n,p,ncol,seed,maxrip,tailcut", TAILCUT)
+def test_tailcut_repair_matches_oracle(M, monkeypatch, gather, n, p, ncol, seed, maxrip, tailcut):
+    """Corrected tail cut (coloringMCMC_CPU.cpp:272-311, k++) after the device loop == the oracle's
+    tail_cut(): colouring, repaired Cviol and pass count; the trajectory stays the loop's. Every
+    sweep kernel keeps the violation flags the first pass needs (those of the colouring before the
+    last accepted sweep)."""
+    set_gather(monkeypatch, gather)
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, maxRip=maxrip, tailcut=tailcut, tailcutRepair=True)
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=nc, maxRip=maxrip, tailcut=tailcut, tailcutRepair=1000)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1, n * (n + 1) // 2)), params)
+    st = col.run(0)
+    assert_same(col, st, r)
+    assert st.tailcutPasses == r.res.tailcutPasses
+
+
+def test_tailcut_repair_generated_graph(M):
+    """Tail cut on a generated graph (no CSR on the device: rows read through the tiled layout,
+    several 2^16-column blocks) == the oracle on the restated CSR."""
+    n, p, ncol, seed = 140000, 0.0004, 120, 9
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, tailcut=True, tailcutRepair=True, nthreads=8)
+    assert r.res.tailcutPasses >= 1
+    g = M.Graph.er_fast(n, p, seed)
+    params = M.ColoringMCMCParams(nCol=ncol, tailcut=True, tailcutRepair=1000)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), params)
+    st = col.run(0)
+    assert_same(col, st, r)
+    assert st.tailcutPasses == r.res.tailcutPasses

@@ -110,3 +110,66 @@ def test_openmp_variant_bit_identical(threads):
         assert np.array_equal(a.colors, b.colors)
         assert a.traj.tolist() == b.traj.tolist()
         assert a.res.glibcDraws == b.res.glibcDraws
+
+
+def _viol_flags(off, idx, C):
+    return np.array([bool(np.any(C[idx[off[i]:off[i + 1]]] == C[i])) for i in range(len(off) - 1)])
+
+
+def _py_tail_cut(off, idx, C, flags, ncol, z, cap=1000):
+    """coloringMCMC_CPU.cpp:272-311 with k++ (the reference increments i and never returns),
+    restated in Python: colorIdx by ascending histogram when z > 0 (a stable sort equals libstdc++'s
+    std::sort for nCol <= 16, a plain insertion sort), then Gauss-Seidel passes over the flagged
+    vertices, first free colour in colorIdx order, recount."""
+    C = C.copy()
+    order = list(range(ncol))
+    if z > 0:
+        hist = np.bincount(C, minlength=ncol)
+        order = sorted(order, key=lambda c: hist[c])
+    cviol, passes = int(_viol_flags(off, idx, C).sum()), 0
+    while cviol > 0 and passes < cap:
+        for i in np.flatnonzero(flags):
+            used = set(C[idx[off[i]:off[i + 1]]].tolist())
+            for c in order:
+                if c not in used:
+                    C[i] = c
+                    break
+        flags = _viol_flags(off, idx, C)
+        cviol, passes = int(flags.sum()), passes + 1
+    return C, cviol, passes
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,maxrip,tailcut", [
+    (400, 0.05, 12, 2, 250, True),   # loop stops at Cviol <= 50, one pass repairs the rest
+    (500, 0.02, 7, 1, 250, True),    # stops within z, the repair oscillates: runs to the pass bound
+    (250, 0.2, 5, 3, 30, False),     # too few colours: cap reached, passes hit the bound
+    (200, 0.01, 16, 4, 250, True),   # initial colouring already within z: no accepted sweep
+    (300, 0.1, 40, 5, 3, False),     # nCol > 16, identity colorIdx
+])
+def test_oracle_tail_cut_equals_python_restatement(n, p, ncol, seed, maxrip, tailcut):
+    """Pins the oracle's corrected tail cut, including the reference's quirk that the first pass
+    visits the vertices flagged in the colouring BEFORE the last accepted sweep (run() swaps C and
+    Cstar but not Cviols, coloringMCMC_CPU.cpp:259-260). The reference itself never returns from
+    its tail cut (:289 increments i), so this restatement is the pin (parity unpinned against the
+    reference's own output: there is none)."""
+    O.srand(1)
+    off, idx = O.setup_rnd2(n, p)
+    O.srand(1)
+    O.setup_rnd2(n, p)
+    base = O.mcmc_run(off, idx, ncol, seed, maxRip=maxrip, tailcut=tailcut)
+    O.srand(1)
+    O.setup_rnd2(n, p)
+    rep = O.mcmc_run(off, idx, ncol, seed, maxRip=maxrip, tailcut=tailcut, tailcutRepair=True)
+    K = base.res.iter
+    if K >= 1:
+        O.srand(1)
+        O.setup_rnd2(n, p)
+        prev = O.mcmc_run(off, idx, ncol, seed, maxRip=maxrip, tailcut=tailcut, sweep_limit=K - 1).colors
+    else:
+        prev = base.colors
+    z = max(50, n // 2000) if tailcut else 0
+    C, cviol, passes = _py_tail_cut(off, idx, base.colors, _viol_flags(off, idx, prev), ncol, z)
+    assert rep.traj.tolist() == base.traj.tolist()
+    assert rep.colors.tolist() == C.tolist()
+    assert (rep.res.finalViol, rep.res.tailcutPasses) == (cviol, passes)
+    assert passes > 0 or base.res.finalViol == 0
