@@ -39,6 +39,7 @@ extern "C" {
 
 typedef struct mcmc_ctx mcmc_ctx;
 typedef struct mcmc_graph mcmc_graph;
+typedef struct mcmc_gpurand mcmc_gpurand;
 
 /* Mirrors ColoringMCMCParams (graph_coloring/coloring.h:65-74) plus the colorer seed, which the
  * reference passes separately (ColoringMCMC_CPU ctor, coloringMCMC_CPU.h:15; main.cu:171 seed+i). */
@@ -196,6 +197,16 @@ int mcmc_part_sweep_async(mcmc_ctx* c);
 int mcmc_part_commit_async(mcmc_ctx* c);
 /* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final). */
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
+
+/* ---- reference-GPU-semantics mode ------------------------------------
+ * The per-vertex cuRAND XORWOW states of the reference's GPURand (GPUutils/GPURandomizer.cu:8-13,
+ * 85-101: curand_init(seed, v, 0) for every vertex v), shared by all repetitions (main.cu:80,193).
+ * mcmc_xorwow_state: host probe of one state, {v0..v4, d}; flavor 0 = cuRAND's salts, 1 = rocRAND's
+ * (the tests pin the transition and the 2^67 subsequence jump against rocRAND's engine). */
+int mcmc_xorwow_state(uint64_t seed, uint64_t subsequence, int flavor, uint32_t out[6]);
+int mcmc_gpurand_create(uint32_t n, uint32_t seed, int device, mcmc_gpurand** out);
+int mcmc_gpurand_states(const mcmc_gpurand* r, uint32_t* out /* [n][6] */);
+void mcmc_gpurand_destroy(mcmc_gpurand* r);
 
 #ifdef __cplusplus
 }

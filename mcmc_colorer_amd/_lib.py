@@ -48,6 +48,10 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_part_sweep_async": (c_int, [c_void_p]),
     "mcmc_part_commit_async": (c_int, [c_void_p]),
     "mcmc_part_state": (c_int, [c_void_p, POINTER(c_int32), _u32p, _u32p]),
+    "mcmc_xorwow_state": (c_int, [c_uint64, c_uint64, c_int, _u32p]),
+    "mcmc_gpurand_create": (c_int, [c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
+    "mcmc_gpurand_states": (c_int, [c_void_p, _u32p]),
+    "mcmc_gpurand_destroy": (None, [c_void_p]),
 }
 
 

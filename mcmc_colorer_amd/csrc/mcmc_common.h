@@ -96,3 +96,12 @@ struct mcmc_graph {
     mcmc::GraphDev g;
     std::vector<std::unique_ptr<mcmc::TiledLayout>> tiles;   // freed with the graph
 };
+
+// Per-vertex cuRAND XORWOW states of the reference-GPU-semantics mode (refmode.hip).
+struct mcmc_gpurand {
+    int device = 0;
+    uint32_t n = 0;
+    uint32_t seed = 0;
+    uint32_t* states[2] = {nullptr, nullptr};   // SoA {v0..v4, d} x n words, double-buffered
+    uint32_t cur = 0;                            // parity holding the current states
+};

@@ -89,6 +89,32 @@ int      oracle_mcmc_run(uint32_t n, const uint64_t* row_off, const uint32_t* co
                          uint64_t* traj, uint64_t traj_cap,
                          uint32_t sweep_limit, int nthreads, oracle_result* res);
 
+// ---- reference-GPU-semantics mode (oracle/mcmc_gpu_ref.cpp) ----
+typedef struct {
+    uint32_t rip;               // ColoringMCMC::rip after the loop (coloringMCMC_main.cu:160-269)
+    int32_t  maxIterReached;    // rip == maxRip (:294-295)
+    uint32_t sweeps;            // sweeps executed
+    uint32_t tailcutPasses;     // passes of the GPU tail cut (:279-289), bounded by tail_max_passes
+    uint64_t conflictCounter;   // the host's conflictCounter at loop exit (tail-cut entry value)
+    uint64_t finalConflicts;    // conflicting edges of the returned colouring
+    uint64_t trajLen;           // conflicting-edge counts written: C_0 .. C_last
+} oracle_gpu_result;
+
+// cuRAND XORWOW (flavor 0; 1 = rocRAND's salts): state after curand_init(seed, subsequence, 0),
+// out = {v0..v4, d}; _next advances a state and returns `count` outputs.
+void     oracle_xorwow_init(uint64_t seed, uint64_t subsequence, int flavor, uint32_t out[6]);
+void     oracle_xorwow_next(uint32_t st[6], uint32_t count, uint32_t* out);
+// GPURand(n, seed) (GPURandomizer.cu:85-101): states [n][6].
+void     oracle_gpurand_init(uint32_t n, uint32_t seed, uint32_t* states);
+// ColoringMCMC::run() with the default build's kernels. states: in/out [n][6] (the per-vertex
+// curandStates shared by all repetitions, main.cu:80,193). traj: conflicting-edge count of every
+// colouring the loop counted, plus the last sweep's when the loop ran out. The tail cut runs when
+// prm->tailcut (as the reference's), at most tail_max_passes passes; tail_traj: optional
+// [tail_max_passes] counts after each pass.
+int      oracle_mcmc_gpu_run(uint32_t n, const uint64_t* row_off, const uint32_t* col_idx, const oracle_params* prm,
+                             uint32_t* states, uint32_t* out_colors, uint64_t* traj, uint64_t traj_cap,
+                             uint32_t tail_max_passes, uint64_t* tail_traj, oracle_gpu_result* res);
+
 // Writes the reference's saveStats / saveColor text outputs (coloringMCMC_CPUutils.cpp:177-217).
 int      oracle_save_outputs(const char* log_path, const char* colors_path, uint32_t n, uint64_t nEdges,
                              uint32_t maxDeg, uint32_t minDeg, float meanDeg, float prob, uint32_t seed,

@@ -30,6 +30,11 @@ class OracleResult(ctypes.Structure):
                 ("sweepsRun", c_uint32), ("tailcutPasses", c_uint32)]
 
 
+class OracleGpuResult(ctypes.Structure):
+    _fields_ = [("rip", c_uint32), ("maxIterReached", c_int32), ("sweeps", c_uint32), ("tailcutPasses", c_uint32),
+                ("conflictCounter", c_uint64), ("finalConflicts", c_uint64), ("trajLen", c_uint64)]
+
+
 _lib = None
 
 
@@ -56,6 +61,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_free.argtypes = [c_void_p]
         L.oracle_mcmc_run.argtypes = [c_uint32, c_void_p, c_void_p, POINTER(OracleParams), c_uint32, c_void_p,
                                       c_void_p, c_void_p, c_uint64, c_uint32, c_int, POINTER(OracleResult)]
+        L.oracle_xorwow_init.argtypes = [c_uint64, c_uint64, c_int, c_void_p]
+        L.oracle_xorwow_next.argtypes = [c_void_p, c_uint32, c_void_p]
+        L.oracle_gpurand_init.argtypes = [c_uint32, c_uint32, c_void_p]
+        L.oracle_mcmc_gpu_run.argtypes = [c_uint32, c_void_p, c_void_p, POINTER(OracleParams), c_void_p, c_void_p,
+                                          c_void_p, c_uint64, c_uint32, c_void_p, POINTER(OracleGpuResult)]
         _lib = L
     return _lib
 
@@ -133,3 +143,51 @@ def mcmc_run(row_off: np.ndarray, col_idx: np.ndarray, nCol: int, seed: int, *, 
                                _p(init), _p(colors), _p(traj), len(traj), sweep_limit, nthreads, byref(res))
     assert rc == 0
     return OracleRun(colors, init, traj[: res.trajLen].copy(), res)
+
+
+# ---- reference-GPU-semantics mode (oracle/mcmc_gpu_ref.cpp) ----------------------------------
+def xorwow_init(seed: int, subsequence: int, flavor: int = 0) -> np.ndarray:
+    out = np.zeros(6, dtype=np.uint32)
+    lib().oracle_xorwow_init(seed, subsequence, flavor, _p(out))
+    return out
+
+
+def xorwow_next(state: np.ndarray, count: int) -> np.ndarray:
+    """Advances `state` (6 words, in place) and returns `count` outputs."""
+    out = np.zeros(count, dtype=np.uint32)
+    lib().oracle_xorwow_next(_p(state), count, _p(out))
+    return out
+
+
+def gpurand_init(n: int, seed: int) -> np.ndarray:
+    """GPURand(n, seed) -> [n][6] states."""
+    st = np.zeros((n, 6), dtype=np.uint32)
+    lib().oracle_gpurand_init(n, seed & 0xFFFFFFFF, _p(st))
+    return st
+
+
+@dataclass
+class OracleGpuRun:
+    colors: np.ndarray
+    traj: np.ndarray
+    tail_traj: np.ndarray
+    res: OracleGpuResult
+
+
+def mcmc_gpu_run(row_off: np.ndarray, col_idx: np.ndarray, nCol: int, states: np.ndarray, *,
+                 epsilon: float = 1e-8, maxRip: int = 250, tabooIteration: int = 0, tailcut: bool = False,
+                 tail_max_passes: int = 1000) -> OracleGpuRun:
+    """ColoringMCMC (GPU, default build) run() from per-vertex XORWOW `states` ([n][6], advanced in place)."""
+    row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+    col_idx = np.ascontiguousarray(col_idx, dtype=np.uint32)
+    n = len(row_off) - 1
+    assert states.shape == (n, 6) and states.dtype == np.uint32 and states.flags.c_contiguous
+    prm = OracleParams(nCol, epsilon, 1.0, 0.01, 1.0, maxRip, tabooIteration, int(tailcut), 0)
+    colors = np.zeros(n, dtype=np.uint32)
+    traj = np.zeros(maxRip + 2, dtype=np.uint64)
+    tail = np.zeros(max(tail_max_passes, 1), dtype=np.uint64)
+    res = OracleGpuResult()
+    rc = lib().oracle_mcmc_gpu_run(n, _p(row_off), _p(col_idx) if len(col_idx) else None, byref(prm), _p(states),
+                                   _p(colors), _p(traj), len(traj), tail_max_passes, _p(tail), byref(res))
+    assert rc == 0
+    return OracleGpuRun(colors, traj[: res.trajLen].copy(), tail[: res.tailcutPasses].copy(), res)
