@@ -207,6 +207,22 @@ int mcmc_xorwow_state(uint64_t seed, uint64_t subsequence, int flavor, uint32_t 
 int mcmc_gpurand_create(uint32_t n, uint32_t seed, int device, mcmc_gpurand** out);
 int mcmc_gpurand_states(const mcmc_gpurand* r, uint32_t* out /* [n][6] */);
 void mcmc_gpurand_destroy(mcmc_gpurand* r);
+/* The reference's own --mcmcgpu colorer: ColoringMCMC as built by default (coloringMCMC.h:22-41:
+ * COLOR_BALANCE_DYNAMIC_DISTR, STANDARD_INIT, TABOO), on the tiled sweep. Per sweep: conflicts
+ * counted as edges (conflictCounter + calcConflicts, coloringMCMC_utils.cu:103-119,184-198), the
+ * loop stops when they are <= z (do/while, coloringMCMC_main.cu:160-269, at most maxRip sweeps),
+ * proposal selectStarColoringBalanceDynamic (coloringMCMC_balance.cu:79-143) with one XORWOW
+ * draw per updated vertex. mcmc_ref_run initialises the colouring from `rand` (initColoring,
+ * coloringMCMC_utils.cu:24-33), runs, then -- if params.tailcut -- the GPU tail cut
+ * (coloringMCMC_main.cu:271-290) for at most tail_max_passes passes (the reference's is unbounded).
+ * Stats: iter = rip, maxIterReached = (rip == maxRip), finalViol = conflicting EDGES of the
+ * returned colouring, sweepsRun = sweeps, trajLen = counts of C_0 .. C_last (mcmc_get_trajectory).
+ * The states advance as the reference's do; repetitions pass the same `rand`. 2 <= nCol <= 255.
+ * Parity unpinned against CUDA. */
+int mcmc_ref_create(const mcmc_graph* g, const mcmc_params* p, mcmc_gpurand* rand, mcmc_ctx** out);
+int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats);
+/* Cviol (REF: conflicting edges) after each tail-cut pass of the last run. */
+int mcmc_get_tail_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,9 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_gpurand_create": (c_int, [c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "mcmc_gpurand_states": (c_int, [c_void_p, _u32p]),
     "mcmc_gpurand_destroy": (None, [c_void_p]),
+    "mcmc_ref_create": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_void_p)]),
+    "mcmc_ref_run": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "mcmc_get_tail_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
 }
 
 

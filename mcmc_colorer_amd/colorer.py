@@ -275,6 +275,104 @@ class ColoringMCMC:
             pass
 
 
+class CurandStates:
+    """GPURand's per-vertex curandState array (GPURandomizer.cu:85-101: curand_init(seed, v, 0) for
+    every vertex v) for the reference-GPU-semantics mode: cuRAND XORWOW states on the device, shared
+    by every repetition (main.cu:80, 193) and advanced as the reference's are."""
+
+    def __init__(self, n: int, seed: int, device: int = 0):
+        self.n = n
+        self.seed = seed & 0xFFFFFFFF
+        self.device = device
+        self._h = ctypes.c_void_p()
+        check(lib().mcmc_gpurand_create(n, self.seed, device, ctypes.byref(self._h)))
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def states(self) -> np.ndarray:
+        """[n][6] = {v0..v4, d} per vertex."""
+        out = np.zeros((self.n, 6), dtype=np.uint32)
+        check(lib().mcmc_gpurand_states(self._h, u32ptr(out)))
+        return out
+
+    def close(self) -> None:
+        if self._h:
+            lib().mcmc_gpurand_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ColoringMCMCGpuRef:
+    """The reference's own --mcmcgpu colorer, semantics included: ColoringMCMC
+    as built by default (coloringMCMC.h:22-41 -- balance-dynamic proposal, cuRAND XORWOW per vertex,
+    conflicts counted as edges, the GPU tail cut), run on the MI355X tiled sweep. ``run()`` returns
+    MCMCRunStats with iter = rip, finalViol = conflicting edges of the returned colouring; the
+    trajectory holds the conflicting-edge count of every colouring the loop counted. Parity is
+    unpinned against CUDA (none here): pinned pieces and the oracle are listed in DESIGN.md."""
+
+    def __init__(self, graph_d: Graph, states: CurandStates, params: ColoringMCMCParams):
+        if params.nCol == 0:
+            params = ColoringMCMCParams(**{**params.__dict__, "nCol": default_ncol(graph_d, params)})
+        self.graph = graph_d
+        self.rand = states
+        self.param = params
+        self._cparams = params.to_c(states.seed)
+        self._ctx = ctypes.c_void_p()
+        check(lib().mcmc_ref_create(graph_d.handle, ctypes.byref(self._cparams), states.handle,
+                                    ctypes.byref(self._ctx)))
+        self.stats: Optional[MCMCRunStats] = None
+
+    def run(self, tail_max_passes: int = 1000) -> MCMCRunStats:
+        st = MCMCRunStats()
+        check(lib().mcmc_ref_run(self._ctx, tail_max_passes, ctypes.byref(st)))
+        self.stats = st
+        return st
+
+    def coloring(self) -> np.ndarray:
+        out = np.zeros(self.graph.nNodes, dtype=np.uint32)
+        check(lib().mcmc_get_coloring(self._ctx, u32ptr(out)))
+        return out
+
+    def trajectory(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        check(lib().mcmc_get_trajectory(self._ctx, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            check(lib().mcmc_get_trajectory(self._ctx, u64ptr(out), n.value, ctypes.byref(n)))
+        return out
+
+    def tail_trajectory(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        check(lib().mcmc_get_tail_trajectory(self._ctx, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            check(lib().mcmc_get_tail_trajectory(self._ctx, u64ptr(out), n.value, ctypes.byref(n)))
+        return out
+
+    def info(self) -> dict:
+        i = MCMCCtxInfo()
+        check(lib().mcmc_get_info(self._ctx, ctypes.byref(i)))
+        return i.as_dict()
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().mcmc_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def write_report(path: str, flavour: str, graph: Graph, p: ColoringMCMCParams, seed: int, rep: int,
                  duration: float, st: MCMCRunStats, C: np.ndarray) -> None:
     """The .log block of saveStats (coloringMCMC_CPUutils.cpp:177-210), parseable by the

@@ -45,6 +45,8 @@ namespace mcmc {
 // Row stride of a tiled layout's segment table: R + 1 entries rounded up to 4, so every
 // (group, block) table row is 16-byte aligned for LDS-DMA.
 __host__ __device__ inline uint32_t tseg_stride(uint32_t R) { return (R + 4u) & ~3u; }
+// A segment-table entry: padded start (multiple of 8) | padding count of the segment (low 3 bits).
+constexpr uint32_t kTsegPos = ~7u;
 
 // Tiled copy of a row range of the CSR (sweep variant 3, mcmc_sweep.hip): rows in groups of
 // grp_rows, per group the arcs block-major as 16-bit block-local ids, every (row, block) segment
@@ -83,13 +85,16 @@ struct TailView {
     uint32_t R = 0, nb = 0, block_log2 = 0;
 };
 // flags[v] = colour of v used by a neighbour (violation_count, coloringMCMC_CPU.cpp:329-350); *count = sum.
-int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s);
+// edges: the reference GPU colorer's conflictCounter (same-colour neighbours with a larger id, counted).
+int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s,
+               bool edges);
 // Ascending list of the flagged vertices; *list_len on the device. tmp: scratch, grown on demand.
 int tail_select(const uint8_t* flags, uint32_t n, uint32_t* list, uint32_t* list_len, void** tmp, size_t* tmp_bytes,
                 hipStream_t s);
 // One corrected tail-cut pass (coloringMCMC_CPU.cpp:281-305, k++) over the listed vertices, in order.
+// ref: the GPU colorer's tailCutting rule over at most `limit` listed vertices.
 int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint32_t* list_len,
-                const uint32_t* colorIdx, uint32_t nCol, hipStream_t s);
+                const uint32_t* colorIdx, uint32_t nCol, hipStream_t s, bool ref, unsigned long long limit);
 }  // namespace mcmc
 
 struct mcmc_graph {

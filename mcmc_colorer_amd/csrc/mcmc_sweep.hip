@@ -33,6 +33,7 @@
 
 #include "mcmc_common.h"
 #include "rng.h"
+#include "xorwow.h"
 
 namespace mcmc {
 
@@ -108,7 +109,14 @@ struct SweepArgs {
     // tail cutting enabled (mcmc_set_tailcut_repair): sweep t stores the violation flags of C_t at
     // vflags[(t & 1) * nloc + l] -- the tail cut's first pass needs those of the previous sweep
     uint8_t* vflags;
+    // reference-GPU-semantics mode (REF instantiations of the tiled sweep, refmode.hip)
+    uint32_t* xw0;              // XORWOW states of sweep parity 0 / 1: SoA {v0..v4, d} x nloc
+    uint32_t* xw1;
+    uint32_t* hist;             // [2][kHistWords] colour histograms of C_t by parity (C_t[v] <= nCol)
+    float ref_hi;               // 1 - (nCol - 1) * eps (coloringMCMC_balance.cu:132)
+    uint32_t own_buf_bytes;     // streaming REF: LDS bytes of one own-colour buffer
 };
+constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
 
 // Byte address of vertex v in a colour buffer (partitioned buffers interleave per-rank footers).
 __device__ __forceinline__ uint32_t caddr(const SweepArgs& a, uint32_t v) {
@@ -273,6 +281,37 @@ __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long lon
         return;
     }
     commit_accept(a, t, a.events, E, lds, lds_cap);
+}
+
+// Loop control of the reference's GPU run() (coloringMCMC_main.cu:160-269), fused into the last
+// workgroup of sweep t: `ecnt` = C_t's arcs (v, w) with w > v and equal colours, summed over the
+// rows by the scan -- the conflictCounter kernel + calcConflicts (coloringMCMC_utils.cu:103-119,
+// 184-198). Iteration rip = t + 1 counts C_t and stops at <= z; after maxRip
+// iterations (maxRip sweeps) the loop ends without that test, and this sweep is the count-only
+// pass whose count is the last sweep's "nuovi conflitti" (:229). Accepting flips the parity of
+// the colours, XORWOW states and histograms, and clears the histogram sweep t+1 accumulates into.
+__device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long long ecnt) {
+    DevState* st = a.st;
+    const unsigned long long c = ecnt;
+    if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = c;
+    const uint32_t cap = a.maxRip > 0 ? a.maxRip : 1u;   // do { ... } while (rip < maxRip): >= 1 sweep
+    if (t == cap || c <= a.z) {
+        if (threadIdx.x == 0) {
+            const uint32_t rip = (t == cap) ? cap : t + 1u;
+            st->done = 1;
+            st->iter = rip;
+            st->maxIterReached = rip == a.maxRip;   // :294-295
+            st->finalViol = c;
+            st->arrive_viol = 0;
+        }
+        return;
+    }
+    uint32_t* h = a.hist + (t & 1u) * kHistWords;
+    for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x) h[i] = 0;
+    if (threadIdx.x == 0) {
+        st->t = t + 1;
+        st->arrive_viol = 0;
+    }
 }
 
 // Stand-alone commit (MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
@@ -626,6 +665,26 @@ __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, Tai
     else pack_footer(a, sh.t, sh.viol, sh.E, sh.err, lds, cap);
 }
 
+// REF tail: the packed arrival carries the workgroup's same-colour arc count in [47:0] (REF sweeps
+// append no overflow events); the last workgroup runs the reference's loop control.
+__device__ __forceinline__ void sweep_tail_ref(const SweepArgs& a, DevState* st, TailShared& sh,
+                                               unsigned long long wave_cnt, int lane) {
+    if (lane == 0 && wave_cnt) atomicAdd(&sh.viol, wave_cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long mine = (1ull << 48) | sh.viol;
+        const unsigned long long prev = atomicAdd(&st->arrive_viol, mine);
+        sh.wg_last = ((prev >> 48) == gridDim.x - 1) ? 1u : 0u;
+        if (sh.wg_last) {
+            sh.viol = (prev + mine) & ((1ull << 48) - 1ull);
+            sh.t = st->t;
+        }
+    }
+    __syncthreads();
+    if (!sh.wg_last) return;
+    commit_control_ref(a, sh.t, sh.viol);
+}
+
 // The fused sweep (n fits LDS, or the L2-gather variant). Every wave owns a contiguous,
 // arc-balanced range of rows (wave_start, computed once per context) and walks it in tiles.
 // LDSC: the whole colour replica (n bytes) is first staged in LDS so the byte gathers never pull
@@ -823,6 +882,109 @@ __device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, cons
     }
 }
 
+// REF scan: the occupancy masks plus the arcs the reference's conflictCounter counts
+// (coloringMCMC_utils.cu:115): same colour as the row's (oc) and a larger id (vertex vrow, the
+// pair's block starts at whi), not padding (the quad starts at id position q of the group, the
+// row's real ids end at tend).
+template <int NW>
+__device__ __forceinline__ void tile_gather_ref(const uint8_t* __restrict__ sc, const uint4& v, bool ok,
+                                                uint32_t (&m)[NW], uint32_t oc, uint32_t q, uint32_t tend,
+                                                uint32_t whi, uint32_t vrow, uint32_t& ecnt) {
+    if (ok) {
+        const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+        uint32_t id[8], cg[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            id[2 * e] = w8[e] & 0xFFFFu;
+            id[2 * e + 1] = w8[e] >> 16;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) cg[e] = sc[id[e]];
+        uint32_t c = 0;
+#pragma unroll
+        for (int e = 0; e < 8; e++) c += (cg[e] == oc && q + (uint32_t)e < tend && (whi | id[e]) > vrow) ? 1u : 0u;
+        ecnt += c;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const uint32_t cc = cg[e];
+            const uint32_t bit = 1u << (cc & 31);
+#pragma unroll
+            for (int w = 0; w < NW; w++) m[w] |= ((cc >> 5) == (uint32_t)w) ? bit : 0u;
+        }
+    }
+}
+
+// REF evaluation of one tile (selectStarColoringBalanceDynamic, coloringMCMC_balance.cu:79-143):
+// lane j < cnt, vertex l0 + j, occupancy `acc`. Taboo'd: count down, keep the colour (the
+// reference leaves the star slot unwritten; it holds the colour of two sweeps before, which equals
+// the current one whenever a vertex is taboo'd). No free colour: keep, no draw. Otherwise one
+// curand_uniform and the proposal walk: occupied own colour -> free colours p[i] + r with
+// r = (sum over occupied of p - eps) / Zp, occupied eps; free own colour -> hi at the own colour,
+// eps elsewhere; stop at threshold >= u or i = nCol. A colour >= nCol (initColoring at u = 1.0f)
+// occupies nothing (the reference writes it into the next vertex's checker row: a data race).
+// States: read at parity t & 1, written (advanced or not) at the other parity.
+template <int NW>
+__device__ __forceinline__ void evaluate_ref_tile(const SweepArgs& a, const uint8_t* __restrict__ Cown,
+                                                  uint8_t* __restrict__ Cs, uint32_t t, uint32_t l0, uint32_t cnt,
+                                                  const uint32_t (&acc)[NW], int lane, const float* __restrict__ p,
+                                                  uint32_t* hist_lds) {
+    if ((uint32_t)lane >= cnt) return;
+    const uint32_t l = l0 + (uint32_t)lane, v = a.v_begin + l;
+    const size_t nloc = a.v_end - a.v_begin;
+    const uint32_t* __restrict__ X = (t & 1u) ? a.xw1 : a.xw0;
+    uint32_t* __restrict__ Y = (t & 1u) ? a.xw0 : a.xw1;
+    xw::State s;
+#pragma unroll
+    for (int k = 0; k < xw::kWords; k++) s.v[k] = X[k * nloc + l];
+    s.d = X[xw::kWords * nloc + l];
+    const uint32_t nodeCol = Cown[v];
+    uint32_t star = nodeCol;
+    const uint32_t tab = a.taboo ? a.taboo[l] : 0u;
+    if (tab > 0) {
+        a.taboo[l] = tab - 1u;
+    } else {
+        uint32_t occ[NW];
+        uint32_t Zn = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t lo = 32u * i;
+            const uint32_t valid = a.nCol >= lo + 32u ? ~0u : (a.nCol > lo ? (1u << (a.nCol - lo)) - 1u : 0u);
+            occ[i] = acc[i] & valid;
+            Zn += __popc(occ[i]);
+        }
+        const uint32_t Zp = a.nCol - Zn;
+        if (Zp != 0) {
+            float reminder = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                uint32_t bits = occ[i];
+                while (bits) {
+                    const uint32_t b = __builtin_ctz(bits);
+                    bits &= bits - 1u;
+                    reminder += p[32u * i + b] - a.eps;
+                }
+            }
+            const float u = xw::uniform(xw::next(s));
+            const bool own = nodeCol < a.nCol && get_color_bit<NW>(occ, nodeCol);
+            const float r = reminder / (float)Zp;
+            uint32_t i = 0;
+            float thr = 0.0f;
+            do {
+                const float q = own ? (get_color_bit<NW>(occ, i) ? a.eps : p[i] + r) : (i == nodeCol ? a.ref_hi : a.eps);
+                thr += q;
+                i++;
+            } while (thr < u && i < a.nCol);
+            star = i - 1u;
+            if (a.taboo) a.taboo[l] = (star == nodeCol) ? a.tabooIteration : 0u;
+        }
+    }
+    Cs[v] = (uint8_t)star;
+#pragma unroll
+    for (int k = 0; k < xw::kWords; k++) Y[k * nloc + l] = s.v[k];
+    Y[xw::kWords * nloc + l] = s.d;
+    atomicAdd(&hist_lds[star], 1u);
+}
+
 // Streaming mode: the colour slice of a pair (2^16 vertices at most) per LDS buffer.
 constexpr uint32_t kSliceBytes = 65536;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable 16 B
@@ -866,6 +1028,21 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
     }
 }
 
+// REF, streaming: DMA of group g's own colours (the rows' bytes, from the 16-byte boundary at or
+// below the group's first vertex) into an own-colour buffer (a multiple of 1 KiB: every wave
+// instruction lands 64 x 16 B). Single context: colour buffers are plain (caddr = identity).
+__device__ __forceinline__ void tile_dma_own(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
+                                             uint32_t own_lds, uint32_t wid, uint32_t nwaves, int lane) {
+    const uint32_t R = a.grp_rows, nloc = a.v_end - a.v_begin;
+    const uint32_t v0 = a.v_begin + g * R, rows = min(R, nloc - g * R);
+    const uint32_t base = v0 & ~15u;
+    const uint32_t np = (v0 + rows - base + 15u) >> 4;
+    for (uint32_t w = wid; w * 64u < np; w += nwaves) {
+        const uint32_t q = min(w * 64u + (uint32_t)lane, np - 1u);
+        glds16(C + base + 16u * q, __builtin_amdgcn_readfirstlane(own_lds + w * 1024u));
+    }
+}
+
 // Buffer descriptor over group g's ids: loads at an offset past its end (idle lanes, slots past a
 // segment) return 0 without a memory request -- a clamped address would still cost a request (C3:
 // 8 lanes/segment 64 ms, 4 lanes 42 ms: the dummy loads were throughput, not free).
@@ -902,13 +1079,15 @@ __device__ __forceinline__ uint4 tile_load(__amdgpu_buffer_rsrc_t r, const uint1
 // beyond the group read the empty range [s(rows), s(rows)) ), so the loads stay in flight.
 __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, uint32_t b, uint32_t nloc,
                                                uint32_t wid, uint32_t nwaves, uint32_t sub,
-                                               uint32_t& s0, uint32_t& s1) {
+                                               uint32_t& s0, uint32_t& s1, uint32_t& pads) {
     const uint32_t R = a.grp_rows;
     const uint32_t rows = min(R, nloc - g * R);
     const uint32_t row = wid * (64u >> a.sub_log2) + sub;   // the sub-group's static first row
     const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * tseg_stride(R);
-    s0 = gs[min(row, rows)];
-    s1 = gs[min(row + 1, rows)];
+    const uint32_t raw = gs[min(row, rows)];
+    s0 = raw & kTsegPos;
+    s1 = gs[min(row + 1, rows)] & kTsegPos;
+    pads = raw & 7u;
 }
 
 // Pair boundary: this lane's LDS-DMA (issued before at least 6 ordinary vector-memory operations:
@@ -926,14 +1105,17 @@ __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, u
 // buffer (k+1)&1 by LDS-DMA, and pair k+1's first quads are issued before the boundary barrier,
 // so no pair starts from an empty memory pipeline (the register-landing design spent 38% of the
 // C3 sweep at pair boundaries).
-template <int NW, bool RES>
+// REF: the reference-GPU-semantics sweep on the same pipeline -- the scan also counts the rows'
+// same-colour arcs (own colours from the replica, or streamed per group into LDS), the evaluation
+// is evaluate_ref_tile, the arrival carries the count (sweep_tail_ref).
+template <int NW, bool RES, bool REF>
 __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
     __shared__ TailShared sh;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
     MCMC_PHASE(a, 0);
-    if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; }
+    if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; sh.viol = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
     uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * (a.v_end - a.v_begin) : nullptr;
@@ -945,6 +1127,19 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint8_t* seg_base = lbase + (RES ? SB : 2u * SB);
     const uint32_t SEGB = a.seg_buf_bytes;                              // bytes per table buffer
     uint32_t* smask = reinterpret_cast<uint32_t*>(seg_base + 2u * SEGB);
+    // REF: [dynamic distribution p (256 floats)][new-colour histogram][2 own-colour buffers]
+    float* p_lds = reinterpret_cast<float*>(seg_base + 2u * SEGB + ((R * NW * 4u + 15u) & ~15u));
+    uint32_t* hist_lds = reinterpret_cast<uint32_t*>(p_lds + 256);
+    uint8_t* own_base = reinterpret_cast<uint8_t*>(hist_lds + kHistWords);
+    if (REF) {
+        // genDynamicDistribution (coloringMCMC_utils.cu:64-70) from C_t's histogram
+        const uint32_t* __restrict__ H = a.hist + (t & 1u) * kHistWords;
+        for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x) hist_lds[i] = 0;
+        for (uint32_t c = threadIdx.x; c < a.nCol; c += blockDim.x)
+            p_lds[c] = (1.0f - ((float)H[c] / (float)a.n)) / (float)(a.nCol - 1u);
+    }
+    uint32_t ecnt = 0;      // REF: same-colour arcs scanned by this lane
+    uint32_t gpar = 0;      // REF streaming: own-colour buffer of the current group
     const int lane = threadIdx.x & 63;
     const uint32_t wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const uint32_t L = 1u << a.sub_log2, nsub = 64u >> a.sub_log2;
@@ -961,10 +1156,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
     for (uint32_t i = threadIdx.x; i < R * NW; i += blockDim.x) smask[i] = 0;
     if (threadIdx.x == 0) sh.cursor[0] = nwaves * nsub;
-    if (g < a.ngroups) tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
+    if (g < a.ngroups) {
+        tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
+        if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
+    }
     // the first pair's first quads (bounds from the global table), then the resident replica
-    uint32_t fpos, fend;
-    tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend);
+    uint32_t fpos, fend, fpads;
+    tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend, fpads);
     fpos += 8u * li;
     __amdgpu_buffer_rsrc_t gr = tile_group_rsrc(a, gclamp);
     const uint16_t* __restrict__ gcol = a.tcol + a.gbase[gclamp];
@@ -1003,11 +1201,14 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
         const uint32_t ng = (b + 1 < nb) ? g : g + gridDim.x, nbn = (b + 1 < nb) ? b + 1 : 0u;
         const bool nvalid = ng < a.ngroups;
-        if (nvalid)
+        if (nvalid) {
             tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane);
+            if (REF && !RES && nbn == 0)
+                tile_dma_own(a, C, ng, lds_addr(own_base) + (gpar ^ 1u) * a.own_buf_bytes, wid, nwaves, lane);
+        }
         const uint32_t pg = nvalid ? ng : g, pb = nvalid ? nbn : b;
-        uint32_t npos, nend;
-        tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend);
+        uint32_t npos, nend, npads;
+        tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend, npads);
         const __amdgpu_buffer_rsrc_t ngr = tile_group_rsrc(a, pg);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
         const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + buf * SB;
@@ -1017,6 +1218,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // LDS cursor, claimed one row ahead (dynamic balance across the waves: the static split
         // left 36% of the C3 sweep waiting at pair barriers for the slowest wave).
         uint32_t row = wid * nsub + sub, pos = fpos, end = fend;
+        uint32_t tend = fend - fpads;                 // REF: the row's real ids end here
+        const uint32_t whi = b << a.block_log2;       // REF: vertex id of the pair's block start
+        // REF: the own colour of a row of this group (0 past the group: such rows gather nothing)
+        const uint8_t* ownp = RES ? lbase + a.v_begin + r0
+                                  : own_base + gpar * a.own_buf_bytes + ((a.v_begin + r0) & 15u);
+        auto own_of = [&](uint32_t r) -> uint32_t { return r < rows ? (uint32_t)ownp[r] : 0u; };
+        uint32_t oc = REF ? own_of(row) : 0u;
         uint32_t claim = 0;
         if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
         uint32_t m[NW];
@@ -1030,13 +1238,19 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
 #define MCMC_TILE_STEP(CUR, NXT, CONT)                                                                  \
     {                                                                                                   \
         const bool act = row < rows;                                                                    \
-        uint32_t npos2 = pos + step, nrow = row, nend2 = end;                                           \
+        uint32_t npos2 = pos + step, nrow = row, nend2 = end, noc = oc, ntend = tend;                   \
         const bool fin = act && (npos2 - 8u * li >= end);                                               \
         if (__ballot(fin)) {                                                                            \
             const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
             if (fin) {                                                                                  \
                 nrow = got;                                                                             \
-                if (nrow < rows) { npos2 = sseg[nrow] + 8u * li; nend2 = sseg[nrow + 1]; }              \
+                if (nrow < rows) {                                                                      \
+                    const uint32_t sraw = sseg[nrow];                                                   \
+                    npos2 = (sraw & kTsegPos) + 8u * li;                                                \
+                    nend2 = sseg[nrow + 1] & kTsegPos;                                                  \
+                    ntend = nend2 - (sraw & 7u);                                                        \
+                }                                                                                       \
+                if (REF) noc = own_of(nrow);                                                            \
                 if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);                                    \
             }                                                                                           \
         }                                                                                               \
@@ -1047,10 +1261,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 NXT[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);         \
             }                                                                                           \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
-                tile_gather<NW>(scb, CUR[u], act && pos + 8u * L * u < end, m);                         \
+                MCMC_TILE_GATHER(CUR[u], act && pos + 8u * L * u < end, pos + 8u * L * u);              \
         } else {                                                                                        \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
-                tile_gather<NW>(scb, CUR[u], act && pos + 8u * L * u < end, m);                         \
+                MCMC_TILE_GATHER(CUR[u], act && pos + 8u * L * u < end, pos + 8u * L * u);              \
         }                                                                                               \
         if (__ballot(fin)) {                                                                            \
             uint32_t red[NW];                                                                           \
@@ -1069,7 +1283,14 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         row = nrow;                                                                                     \
         pos = npos2;                                                                                    \
         end = nend2;                                                                                    \
+        oc = noc;                                                                                       \
+        tend = ntend;                                                                                   \
     }
+#define MCMC_TILE_GATHER(Q, OK, QPOS)                                                                   \
+    do {                                                                                                \
+        if (REF) tile_gather_ref<NW>(scb, Q, OK, m, oc, QPOS, tend, whi, a.v_begin + r0 + row, ecnt);   \
+        else tile_gather<NW>(scb, Q, OK, m);                                                            \
+    } while (0)
         uint4 v1[kTileU];
         if (__ballot(row < rows)) {
             for (;;) {
@@ -1081,11 +1302,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             }
         }
 #undef MCMC_TILE_STEP
+#undef MCMC_TILE_GATHER
         // the next pair's first quads: in flight across the boundary (and the evaluation)
         gr = ngr;
         gcol = ngcol;
         fpos = npos + 8u * li;
         fend = nend;
+        fpads = npads;
 #pragma unroll
         for (int u = 0; u < kTileU; u++) {
             const uint32_t pu = fpos + 8u * L * u;
@@ -1104,12 +1327,17 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
                     if ((uint32_t)lane < cnt) smask[idx] = 0;
                 }
-                wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc, lane, wave_ev, vf);
+                if (REF)
+                    evaluate_ref_tile<NW>(a, C, Cs, t, r0 + e0, cnt, acc, lane, p_lds, hist_lds);
+                else
+                    wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc,
+                                                   lane, wave_ev, vf);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         }
         MCMC_PAIR_BARRIER();   // pair k+1's DMA landed everywhere; buffer k&1 and the masks are free
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_wait += t1 - tmark; }
+        if (REF && !RES && nbn == 0) gpar ^= 1u;   // the next pair starts a new group
         g = ng;
         b = nbn;
         buf ^= 1u;
@@ -1121,7 +1349,17 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         a.phase_ts[blockIdx.x * 8u + 7] = cyc_eval;
     }
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
-    sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+    if (REF) {
+        // C_(t+1)'s histogram: this workgroup's counts; its same-colour arcs ride the arrival
+        uint32_t* __restrict__ Hn = a.hist + ((t + 1u) & 1u) * kHistWords;
+        for (uint32_t c = threadIdx.x; c <= a.nCol; c += blockDim.x)
+            if (hist_lds[c]) atomicAdd(&Hn[c], hist_lds[c]);
+        uint32_t x = ecnt;
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        sweep_tail_ref(a, st, sh, (unsigned long long)x, lane);
+    } else {
+        sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+    }
     MCMC_PHASE(a, 4);
 }
 
@@ -1149,6 +1387,29 @@ __global__ void partition_kernel(const uint64_t* __restrict__ row_off, uint32_t 
 // ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61): vertex v uses engine draw v + 1 when
 // no earlier draw was rejected by uniform_int_distribution; rejections (P ~ nCol/2^31 each) are
 // counted and handed to the exact sequential host path.
+// REF initColoring (coloringMCMC_utils.cu:24-33): colour (int)(curand_uniform * nCol) -- nCol
+// when u == 1.0f, as in the reference -- from each vertex's XORWOW state (advanced in place), and
+// C_0's histogram.
+__global__ void ref_init_kernel(uint8_t* __restrict__ C, uint32_t* __restrict__ X, uint32_t n, uint32_t nCol,
+                                uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kHistWords];
+    for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+        xw::State s;
+        for (int k = 0; k < xw::kWords; k++) s.v[k] = X[(size_t)k * n + v];
+        s.d = X[(size_t)xw::kWords * n + v];
+        const uint32_t c = (uint32_t)(int)(xw::uniform(xw::next(s)) * (float)nCol);
+        C[v] = (uint8_t)c;
+        for (int k = 0; k < xw::kWords; k++) X[(size_t)k * n + v] = s.v[k];
+        X[(size_t)xw::kWords * n + v] = s.d;
+        atomicAdd(&h[c], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i <= nCol; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
 __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st,
                                      uint32_t part_S, uint32_t part_FB) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
@@ -1174,13 +1435,13 @@ hipError_t allow_lds_blocked(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_blocked_kernel<NW>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-template <int NW, bool RES>
+template <int NW, bool RES, bool REF = false>
 void launch_tiled(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
-    sweep_tiled_kernel<NW, RES><<<g, b, lds, s>>>(a);
+    sweep_tiled_kernel<NW, RES, REF><<<g, b, lds, s>>>(a);
 }
-template <int NW, bool RES>
+template <int NW, bool RES, bool REF = false>
 hipError_t allow_lds_tiled(size_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES, REF>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 template <int NW, bool LDSC>
@@ -1249,6 +1510,13 @@ struct mcmc_ctx {
     unsigned long long* tc_count = nullptr;
     void* tc_tmp = nullptr;
     size_t tc_tmp_bytes = 0;
+    std::vector<unsigned long long> tail_traj;   // Cviol (conflicting edges, REF) after each pass
+    // reference-GPU-semantics mode (mcmc_ref_create)
+    bool ref = false;
+    mcmc_gpurand* rand = nullptr;   // caller-owned per-vertex XORWOW states
+    uint32_t rand_base = 0;         // the states' parity when the run started
+    uint32_t* hist = nullptr;       // [2][kHistWords]
+    uint32_t own_buf_bytes = 0;
 };
 
 namespace {
@@ -1335,6 +1603,15 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
     a.vflags = c->tailcut_max ? c->vflags : nullptr;
+    if (c->ref) {
+        a.vflags = nullptr;
+        a.xw0 = c->rand->states[c->rand_base];
+        a.xw1 = c->rand->states[c->rand_base ^ 1u];
+        a.hist = c->hist;
+        // nvcc contracts 1.0f - (nCol - 1) * eps into one fma (coloringMCMC_balance.cu:132)
+        a.ref_hi = std::fma(-(float)(c->p.nCol - 1u), c->p.epsilon, 1.0f);
+        a.own_buf_bytes = c->own_buf_bytes;
+    }
     if (c->tl) {
         a.tcol = c->tl->tcol;
         a.gbase = c->tl->gbase;
@@ -1388,6 +1665,77 @@ int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
     return MCMC_OK;
 }
 
+int ensure_tail_buffers(mcmc_ctx* c) {
+    if (c->vflags) return MCMC_OK;
+    const size_t n = std::max<uint32_t>(c->n, 1u);
+    MCMC_HIP_TRY(hipMalloc(&c->vflags, 2 * n));
+    MCMC_HIP_TRY(hipMalloc(&c->tc_list, sizeof(uint32_t) * n));
+    MCMC_HIP_TRY(hipMalloc(&c->tc_len, sizeof(uint32_t)));
+    MCMC_HIP_TRY(hipMalloc(&c->tc_colorIdx, sizeof(uint32_t) * 256));
+    MCMC_HIP_TRY(hipMalloc(&c->tc_count, sizeof(unsigned long long)));
+    MCMC_HIP_TRY(hipMemsetAsync(c->vflags, 0, 2 * n, c->stream));
+    return MCMC_OK;
+}
+
+TailView tail_view(const mcmc_ctx* c) {
+    TailView tv;
+    tv.n = c->n;
+    if (c->g->row_off) {
+        tv.row_off = c->g->row_off;
+        tv.col_idx = c->g->col_idx;
+    } else {
+        tv.tcol = c->tl->tcol;
+        tv.gbase = c->tl->gbase;
+        tv.tseg = c->tl->tseg;
+        tv.R = c->tl->grp_rows;
+        tv.nb = c->tl->nblocks;
+        tv.block_log2 = c->tl->block_log2;
+    }
+    return tv;
+}
+
+// The reference GPU colorer's tail cut (coloringMCMC_main.cu:271-290): orderedIndex by ascending
+// histogram of the final colouring (std::sort with the reference's comparator), then while
+// conflictCounter > 0 (at most c->tailcut_max passes; the reference loops until resolved):
+// per-vertex edge counts (conflictCounter kernel), tailCutting over the first conflictCounter
+// flagged vertices in order (own colour occupied -> first free colour of orderedIndex, the last
+// one if none), recount. cc: the host's conflictCounter at loop exit.
+int run_tailcut_ref(mcmc_ctx* c, const DevState& h, uint64_t cc, uint64_t* finalConf, uint32_t* passes) {
+    const uint32_t n = c->n, nCol = c->p.nCol;
+    uint8_t* C = c->colors[h.t & 1u];
+    *passes = 0;
+    *finalConf = h.finalViol;
+    std::vector<uint8_t> hc(n);
+    int rc = download_colors(c, C, hc.data());
+    if (rc) return rc;
+    std::vector<uint32_t> stats(std::max(n, nCol) + 1u, 0u);
+    for (uint8_t v : hc) stats[v]++;
+    std::vector<uint32_t> ordered(nCol);
+    for (uint32_t i = 0; i < nCol; i++) ordered[i] = i;
+    std::sort(&ordered[0], &ordered[0] + nCol, [&](int i, int j) { return stats[i] < stats[j]; });
+    MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ordered.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice,
+                                c->stream));
+    const TailView tv = tail_view(c);
+    rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, true);
+    if (rc) return rc;
+    while (cc > 0 && *passes < c->tailcut_max) {
+        rc = tail_select(c->vflags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
+        if (rc) return rc;
+        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, true, cc);
+        if (rc) return rc;
+        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, true);
+        if (rc) return rc;
+        unsigned long long hv = 0;
+        MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        cc = hv;
+        c->tail_traj.push_back(hv);
+        (*passes)++;
+        *finalConf = hv;
+    }
+    return MCMC_OK;
+}
+
 // Tail cutting after the loop (coloringMCMC_CPU.cpp:272-311, corrected: k++, at most
 // c->tailcut_max passes; tailcut.hip). h: the device state at loop exit (done, no error).
 int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* passes) {
@@ -1410,19 +1758,7 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
     if (*finalViol == 0) return MCMC_OK;
     std::vector<uint32_t> ci(colorIdx.begin(), colorIdx.end());
     MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ci.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice, c->stream));
-    TailView tv;
-    tv.n = n;
-    if (c->g->row_off) {
-        tv.row_off = c->g->row_off;
-        tv.col_idx = c->g->col_idx;
-    } else {
-        tv.tcol = c->tl->tcol;
-        tv.gbase = c->tl->gbase;
-        tv.tseg = c->tl->tseg;
-        tv.R = c->tl->grp_rows;
-        tv.nb = c->tl->nblocks;
-        tv.block_log2 = c->tl->block_log2;
-    }
+    const TailView tv = tail_view(c);
     // first pass: the flags of the colouring before the last accepted sweep (run() never swaps
     // Cviols with Cstarviols, :259-260); sweep t kept those of C_t at parity t & 1
     const uint8_t* flags = c->vflags + (size_t)(h.t >= 1 ? (h.t - 1u) & 1u : 0u) * n;
@@ -1430,14 +1766,15 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
     while (cviol > 0 && *passes < c->tailcut_max) {
         int rc = tail_select(flags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
         if (rc) return rc;
-        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream);
+        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, false, ~0ull);
         if (rc) return rc;
-        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream);   // :308
+        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, false);   // :308
         if (rc) return rc;
         unsigned long long hv = 0;
         MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
         MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
         cviol = hv;
+        c->tail_traj.push_back(hv);
         flags = c->vflags;
         (*passes)++;
     }
@@ -1470,7 +1807,9 @@ int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out) {
     return MCMC_OK;
 }
 
-int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end, mcmc_ctx** out) {
+// ref != nullptr: a reference-GPU-semantics context (tiled REF sweep) over ref's XORWOW states.
+static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end,
+                       mcmc_gpurand* ref, mcmc_ctx** out) {
     if (!g || !p || !out) return fail(MCMC_E_ARG, "NULL argument");
     *out = nullptr;
     const GraphDev& gd = g->g;
@@ -1478,6 +1817,13 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     if (p->nCol > 256)
         return fail(MCMC_E_ARG, "nCol > 256 is not supported by this build (uint8 colour replicas)");
     if (v_begin > v_end || v_end > gd.n) return fail(MCMC_E_ARG, "bad vertex range");
+    if (ref) {
+        // a colour may equal nCol (initColoring at u = 1.0f): it must fit the uint8 replicas
+        if (p->nCol < 2 || p->nCol > 255) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
+        if (v_begin != 0 || v_end != gd.n) return fail(MCMC_E_ARG, "reference-GPU mode: whole-graph contexts");
+        if (ref->n != gd.n || ref->device != gd.device)
+            return fail(MCMC_E_ARG, "reference-GPU mode: the XORWOW states do not match the graph");
+    }
     int rc = ensure_constants();
     if (rc) return rc;
     MCMC_HIP_TRY(hipSetDevice(gd.device));
@@ -1488,7 +1834,11 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     c->v_begin = v_begin;
     c->v_end = v_end;
     c->z = p->tailcut ? std::max<uint32_t>(50u, gd.n / 2000u) : 0u;   // :89-97
+    // (REF: a colour equal to nCol sets no mask bit -- tile_gather_ref selects words by c >> 5)
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
+    c->ref = ref != nullptr;
+    c->rand = ref;
+    if (ref) c->fused = 1;
     // Variant: the tiled layout (16-bit block-local ids, replica LDS-resident when it fits, else
     // streamed 64 KiB slices) -- fastest on every measured shape. The CSR variants stay selectable
     // for A/B runs and parity tests. Knobs: MCMC_GATHER=tiled|lds|blocked|global, MCMC_BLOCK_LOG2,
@@ -1498,7 +1848,7 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
     const std::string gsel = gv ? gv : "";
     c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
     if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
-    if (!gd.row_off) c->variant = 3;   // generated graph: tiled layout only
+    if (!gd.row_off || ref) c->variant = 3;   // generated graph / REF: tiled layout only
     const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
     hipError_t ea = hipSuccess;
     if (c->variant == 0) {
@@ -1570,9 +1920,14 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         // what the LDS holds (rmax) and 4095 (a table row = one DMA instruction per wave).
         const size_t rep = lds_bytes;
         const char* gr = getenv("MCMC_GROUP_ROWS");
+        // REF adds [p: 1 KiB][histogram][2 own-colour buffers of own_bytes(rows) (streaming)]
+        auto own_bytes = [](uint32_t rows) -> size_t { return ((size_t)rows + 47u + 1023u) & ~(size_t)1023u; };
         auto lds_need = [&](bool res, uint32_t rows) -> size_t {
             const size_t segb = ((size_t)tseg_stride(rows) * 4u + 1023u) & ~(size_t)1023u;
-            return (res ? rep : 2u * (size_t)kSliceBytes) + 2u * segb + (size_t)rows * c->nw * 4u;
+            const size_t base = (res ? rep : 2u * (size_t)kSliceBytes) + 2u * segb;
+            if (!ref) return base + (size_t)rows * c->nw * 4u;
+            return base + (((size_t)rows * c->nw * 4u + 15u) & ~(size_t)15u) + 1024u + 4u * kHistWords +
+                   (res ? 0u : 2u * own_bytes(rows));
         };
         auto rmax_for = [&](bool res) -> uint32_t {
             uint32_t r = 4095;
@@ -1617,7 +1972,22 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
         if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));
         c->sub_log2 = sl;
         c->lds = lds_need(resident, R);
-        if (resident) {
+        c->own_buf_bytes = resident ? 0u : (uint32_t)own_bytes(R);
+        if (ref) {
+            if (resident) {
+                static const SweepLaunch tab[4] = {launch_tiled<1, true, true>, launch_tiled<2, true, true>,
+                                                   launch_tiled<4, true, true>, launch_tiled<8, true, true>};
+                c->sweep = tab[wi];
+                ea = wi == 0 ? allow_lds_tiled<1, true, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, true, true>(c->lds)
+                   : wi == 2 ? allow_lds_tiled<4, true, true>(c->lds) : allow_lds_tiled<8, true, true>(c->lds);
+            } else {
+                static const SweepLaunch tab[4] = {launch_tiled<1, false, true>, launch_tiled<2, false, true>,
+                                                   launch_tiled<4, false, true>, launch_tiled<8, false, true>};
+                c->sweep = tab[wi];
+                ea = wi == 0 ? allow_lds_tiled<1, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, false, true>(c->lds)
+                   : wi == 2 ? allow_lds_tiled<4, false, true>(c->lds) : allow_lds_tiled<8, false, true>(c->lds);
+            }
+        } else if (resident) {
             static const SweepLaunch tab[4] = {launch_tiled<1, true>, launch_tiled<2, true>, launch_tiled<4, true>,
                                                launch_tiled<8, true>};
             c->sweep = tab[wi];
@@ -1675,8 +2045,21 @@ int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uin
             return fail(MCMC_E_HIP, std::string("segments: ") + hipGetErrorString(es));
         }
     }
+    if (ref && hipMalloc(&c->hist, sizeof(uint32_t) * 2u * kHistWords) != hipSuccess) {
+        mcmc_destroy(c);
+        return fail(MCMC_E_NOMEM, "histogram allocation");
+    }
     *out = c;
     return MCMC_OK;
+}
+
+int mcmc_create(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end, mcmc_ctx** out) {
+    return create_impl(g, p, v_begin, v_end, nullptr, out);
+}
+
+int mcmc_ref_create(const mcmc_graph* g, const mcmc_params* p, mcmc_gpurand* rand, mcmc_ctx** out) {
+    if (!rand) return fail(MCMC_E_ARG, "NULL XORWOW states");
+    return create_impl(g, p, 0, g ? g->g.n : 0, rand, out);
 }
 
 int mcmc_set_glibc_window(mcmc_ctx* c, const uint32_t window[31]) {
@@ -1700,6 +2083,7 @@ int mcmc_get_glibc_window(mcmc_ctx* c, uint32_t window[31]) {
 
 int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (c->ref) return fail(MCMC_E_STATE, "reference-GPU contexts initialise in mcmc_ref_run");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     const uint32_t n = c->n;
     const uint32_t s0 = minstd_seed_state(c->p.seed);
@@ -1750,6 +2134,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
 
 int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (c->ref) return fail(MCMC_E_STATE, "reference-GPU contexts run with mcmc_ref_run");
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_run");
     if (c->v_begin != 0 || c->v_end != c->n)
         return fail(MCMC_E_STATE, "mcmc_run drives whole-graph contexts; use mcmc_part_* for partitions");
@@ -1798,6 +2183,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     s.glibcDraws = h.glibc_draws;
     s.initDraws = c->initDraws;
     s.loopMs = ms;
+    c->tail_traj.clear();
     if (h.done && c->tailcut_max) {
         rc = run_tailcut(c, h, &s.finalViol, &s.tailcutPasses);
         if (rc) return rc;
@@ -1815,14 +2201,9 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
         return fail(MCMC_E_STATE, "tail cutting runs on whole-graph contexts (mcmc_run)");
     if (c->p.nCol > 256) return fail(MCMC_E_ARG, "nCol > 256");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    if (max_passes && !c->vflags) {
-        const size_t n = std::max<uint32_t>(c->n, 1u);
-        MCMC_HIP_TRY(hipMalloc(&c->vflags, 2 * n));
-        MCMC_HIP_TRY(hipMalloc(&c->tc_list, sizeof(uint32_t) * n));
-        MCMC_HIP_TRY(hipMalloc(&c->tc_len, sizeof(uint32_t)));
-        MCMC_HIP_TRY(hipMalloc(&c->tc_colorIdx, sizeof(uint32_t) * 256));
-        MCMC_HIP_TRY(hipMalloc(&c->tc_count, sizeof(unsigned long long)));
-        MCMC_HIP_TRY(hipMemsetAsync(c->vflags, 0, 2 * n, c->stream));
+    if (max_passes) {
+        int rc = ensure_tail_buffers(c);
+        if (rc) return rc;
     }
     if ((max_passes != 0) != (c->tailcut_max != 0)) {
         // captured sweeps carry the flag pointer: re-capture with the new setting
@@ -1832,6 +2213,90 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
         c->bench_n = 0;
     }
     c->tailcut_max = max_passes;
+    return MCMC_OK;
+}
+
+int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (!c->ref) return fail(MCMC_E_STATE, "mcmc_ref_run needs a context from mcmc_ref_create");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    const uint32_t n = c->n, nCol = c->p.nCol;
+    // run() (coloringMCMC_main.cu:101-158): taboo cleared, colours from the states' next draw
+    c->rand_base = c->rand->cur;
+    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }   // states moved
+    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
+    c->batch = c->bench_n = 0;
+    c->tailcut_max = tail_max_passes;
+    if (c->p.tailcut && tail_max_passes) {
+        int rc = ensure_tail_buffers(c);
+        if (rc) return rc;
+    }
+    MCMC_HIP_TRY(hipMemsetAsync(c->hist, 0, sizeof(uint32_t) * 2u * kHistWords, c->stream));
+    if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * n, c->stream));
+    int rc = upload_state(c, 0);
+    if (rc) return rc;
+    {
+        const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 2048u));
+        ref_init_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], c->rand->states[c->rand_base], n, nCol, c->hist);
+        MCMC_HIP_TRY(hipGetLastError());
+    }
+    c->initialized = true;
+    c->ran = true;
+    const uint32_t cap = c->p.maxRip > 0 ? c->p.maxRip : 1u;
+    const uint32_t total = cap + 1u;   // cap sweeps + the count-only pass
+    const uint32_t batch = std::min<uint32_t>(16u, total);
+    rc = build_batch_graph(c, batch);
+    if (rc) return rc;
+    MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    uint32_t launched = 0;
+    DevState h{};
+    while (launched < total) {
+        if (total - launched >= batch) {
+            MCMC_HIP_TRY(hipGraphLaunch(c->batch_exec, c->stream));
+            launched += batch;
+        } else {
+            SweepArgs a = make_args(c, 1);
+            for (; launched < total; launched++) launch_pair(c, a);
+            MCMC_HIP_TRY(hipGetLastError());
+        }
+        rc = download_state(c, &h);
+        if (rc) return rc;
+        if (h.done) break;
+    }
+    MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
+    float ms = 0;
+    MCMC_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (!h.done) return fail(MCMC_E_DEVICE, "reference-GPU loop did not finish");
+    c->rand->cur = (c->rand_base + h.t) & 1u;   // sweep t's own state writes were discarded
+    mcmc_run_stats st{};
+    st.iter = h.iter;                             // rip
+    st.maxIterReached = (int32_t)h.maxIterReached;
+    st.finalViol = h.finalViol;                   // conflicting edges of the returned colouring
+    st.trajLen = (uint64_t)h.t + 1;
+    st.sweepsRun = (h.t == cap) ? cap : h.t;      // selectStar launches of the reference
+    st.initDraws = n;
+    st.loopMs = ms;
+    c->last = st;
+    c->tail_traj.clear();
+    if (c->p.tailcut && tail_max_passes) {
+        // the host's conflictCounter: C_t's count, or C_(cap-1)'s when the loop ran out (:163, :229)
+        unsigned long long cc = 0;
+        const uint32_t idx = (h.t == cap) ? h.t - 1u : h.t;
+        MCMC_HIP_TRY(hipMemcpyAsync(&cc, c->traj + idx, sizeof(cc), hipMemcpyDeviceToHost, c->stream));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        rc = run_tailcut_ref(c, h, cc, &st.finalViol, &st.tailcutPasses);
+        if (rc) return rc;
+        c->last = st;
+    }
+    if (stats) *stats = st;
+    return MCMC_OK;
+}
+
+int mcmc_get_tail_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    if (len) *len = c->tail_traj.size();
+    for (uint64_t i = 0; out && i < std::min<uint64_t>(cap, c->tail_traj.size()); i++) out[i] = c->tail_traj[i];
     return MCMC_OK;
 }
 
@@ -1980,6 +2445,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->tc_colorIdx);
     (void)hipFree(c->tc_count);
     (void)hipFree(c->tc_tmp);
+    (void)hipFree(c->hist);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -61,6 +61,7 @@ __global__ void gpurand_init_kernel(uint32_t n, uint64_t seed, const uint32_t* _
 }
 
 }  // namespace
+
 }  // namespace mcmc
 
 using namespace mcmc;

@@ -13,6 +13,12 @@
 // initial colouring when no sweep was accepted). The sweep kernels keep those flags when a
 // context has tail cutting enabled (SweepArgs::vflags, mcmc_sweep.hip).
 //
+// The reference GPU colorer's tail cut (coloringMCMC_main.cu:271-290, coloringMCMC_utils.cu:73-119;
+// reference-GPU-semantics mode) shares the kernels: conflicts are counted as edges (a flagged vertex
+// has a same-colour neighbour with a larger id), the repair keeps a free own colour and otherwise
+// takes the first free colour of orderedIndex (the last one when none is free), and a pass stops
+// after conflictCounter flagged vertices.
+//
 // Kernels (one context, whole graph):
 //   tail_count_kernel   one wave per row: flag = any neighbour with the row's colour; Cviol.
 //   rocprim::select     flagged rows -> ascending list (order-preserving compaction).
@@ -34,7 +40,8 @@ namespace {
 // Neighbours of local row l, from the CSR (global ids) or the tiled layout (block-local 16-bit
 // ids, segments padded with copies of a real neighbour -- harmless for occupancy and conflicts).
 // Calls f(w) for every neighbour at positions part, part + parts, ... of the row's arc stream.
-template <class F>
+// SKIP_PADS: leave out the padding (a segment's padding count is in its table entry's low bits).
+template <bool SKIP_PADS = false, class F>
 __device__ __forceinline__ void for_neighbours(const TailView& g, uint32_t l, uint32_t part, uint32_t parts, F&& f) {
     if (g.row_off) {
         const uint64_t rs = g.row_off[l], re = g.row_off[l + 1];
@@ -46,41 +53,57 @@ __device__ __forceinline__ void for_neighbours(const TailView& g, uint32_t l, ui
     const uint32_t stride = tseg_stride(g.R);
     const uint32_t* ts = g.tseg + (size_t)grp * g.nb * stride;
     for (uint32_t b = 0; b < g.nb; b++) {
-        const uint32_t s0 = ts[(size_t)b * stride + r], s1 = ts[(size_t)b * stride + r + 1];
+        const uint32_t raw = ts[(size_t)b * stride + r];
+        const uint32_t s0 = raw & kTsegPos, s1 = (ts[(size_t)b * stride + r + 1] & kTsegPos) - (SKIP_PADS ? raw & 7u : 0u);
         const uint32_t hi = b << g.block_log2;
         for (uint32_t k = s0 + part; k < s1; k += parts) f(hi | ids[k]);
     }
 }
 
+// EDGES = false: flag = any same-colour neighbour (violation_count), count = flagged vertices.
+// EDGES = true: per-vertex same-colour neighbours with a larger id (conflictCounter kernel),
+// flag = nonzero, count = their sum (calcConflicts).
+template <bool EDGES>
 __global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const uint8_t* __restrict__ C,
                                                          uint8_t* __restrict__ flags,
                                                          unsigned long long* __restrict__ count) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-    uint32_t wave_viol = 0;
+    unsigned long long wave_total = 0;
     for (uint32_t l = gw; l < g.n; l += nw) {
         const uint8_t cv = C[l];
-        bool hit = false;
-        for_neighbours(g, l, lane, 64u, [&](uint32_t w) { hit |= C[w] == cv; });
-        const bool viol = __ballot(hit) != 0;
-        if (lane == 0) flags[l] = viol;
-        wave_viol += viol;
+        uint32_t hits = 0;
+        if (EDGES) {
+            for_neighbours<true>(g, l, lane, 64u, [&](uint32_t w) { hits += (C[w] == cv && w > l) ? 1u : 0u; });
+            for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
+        } else {
+            bool hit = false;
+            for_neighbours(g, l, lane, 64u, [&](uint32_t w) { hit |= C[w] == cv; });
+            hits = __ballot(hit) != 0 ? 1u : 0u;
+        }
+        if (lane == 0) flags[l] = hits != 0;
+        wave_total += hits;
     }
-    if (lane == 0 && wave_viol) atomicAdd(count, (unsigned long long)wave_viol);
+    if (lane == 0 && wave_total) atomicAdd(count, wave_total);
 }
 
 constexpr uint32_t kRepairThreads = 1024;
 constexpr int kMaskWords = 8;   // nCol <= 256 (uint8 colours)
 
+// REF = false: the corrected CPU rule (first free colour of colorIdx, unchanged when none is free).
+// REF = true: tailCutting (coloringMCMC_utils.cu:73-101): an own colour that is free (or >= nCol)
+// stays; otherwise the first free colour of orderedIndex, the last one when none is free. At most
+// `limit` listed vertices (resolved < conflictCounter).
+template <bool REF>
 __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g, uint8_t* C,
                                                                      const uint32_t* __restrict__ list,
                                                                      const uint32_t* __restrict__ list_len,
                                                                      const uint32_t* __restrict__ colorIdx,
-                                                                     uint32_t nCol) {
+                                                                     uint32_t nCol, unsigned long long limit) {
     __shared__ uint32_t mask[kMaskWords];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t L = *list_len;
+    const uint32_t L = (uint32_t)min((unsigned long long)*list_len, limit);
     // colours of this pass are read with volatile (L1-bypassing) loads: vertex k must see the
     // colour thread 0 stored for an earlier vertex of the list
     const volatile uint8_t* Cv = C;
@@ -102,9 +125,16 @@ __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g,
         }
         __syncthreads();
         if (tid == 0) {
-            for (uint32_t j = 0; j < nCol; j++) {          // first free colour in colorIdx order
-                const uint32_t c = colorIdx[j];
-                if (!((mask[c >> 5] >> (c & 31)) & 1u)) { C[i] = (uint8_t)c; break; }
+            auto used = [&](uint32_t c) { return c < nCol && ((mask[c >> 5] >> (c & 31)) & 1u); };
+            if (REF) {
+                uint32_t c = Cv[i];
+                for (uint32_t j = 0; used(c) && j < nCol; j++) c = colorIdx[j];
+                C[i] = (uint8_t)c;
+            } else {
+                for (uint32_t j = 0; j < nCol; j++) {      // first free colour in colorIdx order
+                    const uint32_t c = colorIdx[j];
+                    if (!used(c)) { C[i] = (uint8_t)c; break; }
+                }
             }
             __threadfence();
         }
@@ -114,11 +144,13 @@ __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g,
 
 }  // namespace
 
-int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s) {
+int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s,
+               bool edges) {
     MCMC_HIP_TRY(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
     if (g.n == 0) return MCMC_OK;
     const uint32_t blocks = std::min<uint32_t>((g.n + 3) / 4, 8192u);   // 4 rows (waves) per block
-    tail_count_kernel<<<blocks, 256, 0, s>>>(g, C, flags, count);
+    if (edges) tail_count_kernel<true><<<blocks, 256, 0, s>>>(g, C, flags, count);
+    else tail_count_kernel<false><<<blocks, 256, 0, s>>>(g, C, flags, count);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }
@@ -139,9 +171,10 @@ int tail_select(const uint8_t* flags, uint32_t n, uint32_t* list, uint32_t* list
 }
 
 int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint32_t* list_len,
-                const uint32_t* colorIdx, uint32_t nCol, hipStream_t s) {
+                const uint32_t* colorIdx, uint32_t nCol, hipStream_t s, bool ref, unsigned long long limit) {
     if (nCol > 32u * kMaskWords) return MCMC_E_ARG;
-    tail_repair_kernel<<<1, kRepairThreads, 0, s>>>(g, C, list, list_len, colorIdx, nCol);
+    if (ref) tail_repair_kernel<true><<<1, kRepairThreads, 0, s>>>(g, C, list, list_len, colorIdx, nCol, limit);
+    else tail_repair_kernel<false><<<1, kRepairThreads, 0, s>>>(g, C, list, list_len, colorIdx, nCol, limit);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }

@@ -38,8 +38,10 @@ __global__ void tile_group_total_kernel(const uint32_t* __restrict__ seg, uint32
     }
 }
 
-// tseg[g][b][r] = padded start of row r's block-b segment relative to the group base; entry R of
-// every block = its end (= the next block's start). Block scan over the rows, blocks in order.
+// tseg[g][b][r] = padded start of row r's block-b segment relative to the group base (a multiple
+// of 8) | the segment's padding count (0..7) in the low 3 bits; entry R of every block = its end
+// (= the next block's start). Readers mask with ~7 (kTsegPos); the padding count gives the true end
+// (the reference-GPU-semantics scan counts arcs exactly). Block scan over the rows, blocks in order.
 __global__ void tile_seg_kernel(const uint32_t* __restrict__ seg, uint32_t nloc, uint32_t nb, uint32_t R,
                                 uint32_t G, uint32_t* __restrict__ tseg) {
     __shared__ uint32_t part[256];
@@ -67,8 +69,8 @@ __global__ void tile_seg_kernel(const uint32_t* __restrict__ seg, uint32_t nloc,
             uint32_t* out = tseg + ((size_t)g * nb + b) * tseg_stride(R);
             uint32_t acc = run + part[threadIdx.x];
             for (uint32_t r = ra; r < rb; r++) {
-                out[r] = acc;
                 const uint32_t len = (r < rows) ? seg[(size_t)(b + 1) * nloc + r0 + r] - seg[(size_t)b * nloc + r0 + r] : 0u;
+                out[r] = acc | (((len + 7u) & ~7u) - len);
                 acc += (len + 7u) & ~7u;
             }
             __syncthreads();
@@ -100,14 +102,14 @@ __global__ void tile_scatter_kernel(const uint64_t* __restrict__ row_off, const 
             const uint32_t c = col_idx[k];
             const uint32_t b = c >> block_log2;
             const uint32_t rel = (uint32_t)(k - rs) - seg[(size_t)b * nloc + l];
-            tcol[base + ts[(size_t)b * tseg_stride(R) + r] + rel] = (uint16_t)(c & bmask);
+            tcol[base + (ts[(size_t)b * tseg_stride(R) + r] & kTsegPos) + rel] = (uint16_t)(c & bmask);
         }
         for (uint32_t b = lane; b < nb; b += 64) {
             const uint32_t s0 = seg[(size_t)b * nloc + l], s1 = seg[(size_t)(b + 1) * nloc + l];
             const uint32_t len = s1 - s0;
             if (len & 7u) {
                 const uint16_t first = (uint16_t)(col_idx[rs + s0] & bmask);
-                const uint64_t p0 = base + ts[(size_t)b * tseg_stride(R) + r];
+                const uint64_t p0 = base + (ts[(size_t)b * tseg_stride(R) + r] & kTsegPos);
                 for (uint32_t i = len; i < ((len + 7u) & ~7u); i++) tcol[p0 + i] = first;
             }
         }
@@ -200,7 +202,7 @@ struct ErArgs {
 __device__ __forceinline__ uint64_t tile_pos(const uint64_t* gbase, const uint32_t* tseg, uint32_t R, uint32_t nb,
                                              uint32_t l, uint32_t b) {
     const uint32_t g = l / R, r = l - g * R;
-    return gbase[g] + tseg[((size_t)g * nb + b) * tseg_stride(R) + r];
+    return gbase[g] + (tseg[((size_t)g * nb + b) * tseg_stride(R) + r] & kTsegPos);
 }
 
 // Streams (i, Y) whose edges touch rows [vb, ve): row i own (any Y >= block(i)), or column block Y
@@ -371,11 +373,10 @@ int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx) {
         row.clear();
         for (uint32_t b = 0; b < nb; b++) {
             const uint32_t* t = ts.data() + ((size_t)g * nb + b) * tseg_stride(R);
-            for (uint64_t q = gb[g] + t[r]; q < gb[g] + t[r + 1]; q++)
-                row.push_back((b << L->block_log2) | tc[q]);
+            const uint64_t q0 = gb[g] + (t[r] & kTsegPos), q1 = gb[g] + (t[r + 1] & kTsegPos) - (t[r] & 7u);
+            for (uint64_t q = q0; q < q1; q++) row.push_back((b << L->block_log2) | tc[q]);
         }
         std::sort(row.begin(), row.end());
-        row.erase(std::unique(row.begin(), row.end()), row.end());
         row_off[v] = k;
         for (uint32_t w : row) {
             if (k >= gh->g.m) return fail(MCMC_E_STATE, "tiled layout holds more arcs than the graph's m");
