@@ -9,6 +9,9 @@ is configs[3]: the same graph vertex-partitioned over N GPUs (strong scaling), e
 only its own rows, one RCCL all-gather per sweep (mcmc_colorer_amd/distributed.py).
 `--config c2`: configs[1], `--simulate 0.01 -n 100000 --nCol 16` with the reference's exact setupRnd2
 graph (weak scaling at N > 1: N*1e5 rows, p 0.01/N).
+`--semantics ref` (one GPU): the same sweep with the reference GPU colorer's own semantics
+(--mcmcgpu-ref: balance-dynamic proposal, per-vertex cuRAND XORWOW, conflicts counted as edges);
+its CPU leg times the oracle's restatement of those semantics.
 
 A step is one sweep: all n vertices resampled. Inputs are resident in HBM before the timed region;
 the timed region is K back-to-back sweeps (one hipGraph at N = 1) bracketed by barrier + synchronize,
@@ -82,6 +85,34 @@ def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window:
     }
 
 
+def cpu_baseline_ref(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, n: int, max_seconds: float = 20.0):
+    """Oracle restatement of the reference GPU colorer (oracle/mcmc_gpu_ref.cpp), single thread, a
+    bounded number of sweeps (maxRip = k: k sweeps, a conflict count before each and after the last)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as O
+
+    st0 = O.gpurand_init(n, seed)
+    t0 = time.perf_counter()
+    st = st0.copy()
+    t = time.perf_counter()
+    O.mcmc_gpu_run(off, idx, ncol, st, maxRip=1)
+    one = time.perf_counter() - t
+    k = max(1, min(30, int(max_seconds / max(one, 1e-3))))
+    st = st0.copy()
+    t = time.perf_counter()
+    r = O.mcmc_gpu_run(off, idx, ncol, st, maxRip=k)
+    loop = time.perf_counter() - t
+    return {
+        "value": n * r.res.sweeps / loop,
+        "unit": "vertex-updates/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{r.res.sweeps} sweeps of the same graph/seed (oracle single-thread restatement of the "
+                  f"reference GPU colorer: conflict count + balance-dynamic selection per sweep); "
+                  f"{time.perf_counter() - t0:.1f} s wall",
+    }
+
+
 def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: float) -> dict:
     """The reference CUDA path's per-sweep structure re-expressed in HIP (mcmc_refstruct_bench):
     the stand-in for 'the reference CUDA path's vertex-updates/sec', which cannot run on MI355X."""
@@ -119,6 +150,9 @@ def main() -> int:
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
     ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--semantics", choices=["cpu", "ref"], default="cpu",
+                    help="cpu: --mcmccpu semantics (the north-star path); ref: the reference GPU colorer's own "
+                         "semantics (--mcmcgpu-ref), one GPU")
     ap.add_argument("--variant", default=None,
                     help="sweep kernel: lds | tiled | blocked | global[:block_log2[:lanes_log2[:group_rows"
                          "[:stream]]]] (empty field / default: the library's choice)")
@@ -175,9 +209,17 @@ def main() -> int:
             torch.cuda.synchronize()
             dist.barrier()
 
+    ref = a.semantics == "ref"
+    if ref and dist is not None:
+        raise SystemExit("--semantics ref runs on one GPU")
     if dist is None:
-        col = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
-        col.init(0)
+        if ref:
+            states = M.CurandStates(g.nNodes, a.seed, dev)
+            col = M.ColoringMCMCGpuRef(g, states, params)
+            col.init()
+        else:
+            col = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
+            col.init(0)
         if a.warmup:
             check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
         check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
@@ -229,6 +271,8 @@ def main() -> int:
     achieved = b_fmt / (kernel_ms * 1e-3) / 1e9
     variant = info["variant"]
     key = f"{a.config}/{variant}" if (world == 1 and (a.config == "c3" or n_req == 100000)) else None
+    if key and ref:
+        key += "-ref"
     out = {
         "metric": "vertex-updates/sec per MCMC sweep",
         "value": value,
@@ -243,14 +287,17 @@ def main() -> int:
         "dtype": "fp32",
         "data": ("synthetic (reference --simulate generator replayed exactly on the GPU)" if a.config == "c2" else
                  "synthetic G(n,p) (the build's counter-based generator, er_gen.h, seed 1; setupRnd2 infeasible at n=1e7)"),
-        "config": {"workload": f"--mcmcgpu --simulate {p_req:g} -n {n_req} --nCol {a.ncol} --seed {a.seed}",
+        "config": {"workload": f"--mcmcgpu{'-ref' if ref else ''} --simulate {p_req:g} -n {n_req} "
+                               f"--nCol {a.ncol} --seed {a.seed}",
                    "config": a.config,
+                   "semantics": "reference GPU colorer (--mcmcgpu-ref)" if ref else "--mcmccpu (north star)",
                    "n": n, "arcs": m, "nCol": a.ncol,
                    "parallelism": f"vertex-partitioned x{world} (RCCL all-gather per sweep)" if world > 1 else "single",
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,
-                     "kernel": KERNELS.get(variant, variant) + ("" if world == 1 else " + exchange (per-rank step)"),
+                     "kernel": KERNELS.get(variant, variant) + ("<REF>" if ref else "")
+                               + ("" if world == 1 else " + exchange (per-rank step)"),
                      "kernel_ms": kernel_ms, "algorithmic_bytes": b_fmt,
                      "ref_layout_bytes": b_ref, "ref_layout_equiv_GBs": b_ref / (kernel_ms * 1e-3) / 1e9,
                      "layout": info},
@@ -274,7 +321,10 @@ def main() -> int:
             out["refstruct"]["graph"] = sample_note
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         s = sample.getStruct()
-        out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed, sample_window, sample_n)
+        if ref:
+            out["cpu_baseline"] = cpu_baseline_ref(s.cumulDegs, s.neighs, a.ncol, a.seed, sample_n)
+        else:
+            out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, a.ncol, a.seed, sample_window, sample_n)
         if sample_note:
             out["cpu_baseline"]["sample"] += "; graph " + sample_note
     if rank == 0:

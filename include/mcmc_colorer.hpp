@@ -17,6 +17,7 @@
 // CDF-overflow draws) is a process-global glibc window here (mcmc::glibc_global()). Like the
 // reference (GPUutils/GPUutils.h:20-26), errors print and abort.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -252,4 +253,141 @@ private:
     std::vector<uint64_t> trajectory;
     uint32_t lastSeed{0};
     int lastRepetition{0};
+};
+
+// ---- reference-GPU-semantics mode -------------------------------------
+// GPURand's per-vertex curandStates (GPURandomizer.cu:85-101), shared by every repetition.
+class CurandStates {
+public:
+    CurandStates(uint32_t n, long seed, int device = 0) : num(n) {
+        MCMC_CHECK(mcmc_gpurand_create(n, (uint32_t)seed, device, &h_));
+    }
+    ~CurandStates() { mcmc_gpurand_destroy(h_); }
+    CurandStates(const CurandStates&) = delete;
+    CurandStates& operator=(const CurandStates&) = delete;
+    mcmc_gpurand* handle() const { return h_; }
+    uint32_t num;
+
+private:
+    mcmc_gpurand* h_{nullptr};
+};
+
+// The reference's own ColoringMCMC (coloringMCMC.h:44-140 as built by default: balance-dynamic
+// proposal, XORWOW per vertex, conflicts counted as edges, the GPU tail cut) on the MI355X sweep.
+// run() writes <dir>.log in the layout of coloringMCMC_prints.cu and <dir>-colors.txt.
+template <typename nodeW, typename edgeW>
+class ColoringMCMCGpuRef {
+public:
+    ColoringMCMCGpuRef(Graph<nodeW, edgeW>* inGraph_d, CurandStates* randStates, ColoringMCMCParams params,
+                       uint32_t tailMaxPasses = 1000)
+        : graph(inGraph_d), states(randStates), param(params), tailMax(tailMaxPasses) {}
+    ~ColoringMCMCGpuRef() { if (ctx) mcmc_destroy(ctx); }
+    void setDirectoryPath(std::string directory) { this->directory = directory; }
+
+    void run(int /*iteration*/) {
+        if (ctx) mcmc_destroy(ctx);
+        mcmc_params p{};
+        p.nCol = param.nCol;
+        p.epsilon = param.epsilon;
+        p.lambda = param.lambda;
+        p.ratioFreezed = param.ratioFreezed;
+        p.numColorRatio = param.numColorRatio;
+        p.maxRip = param.maxRip;
+        p.tabooIteration = param.tabooIteration;
+        p.tailcut = param.tailcut;
+        MCMC_CHECK(mcmc_ref_create(graph->handle(), &p, states->handle(), &ctx));
+        MCMC_CHECK(mcmc_ref_run(ctx, tailMax, &stats));
+        coloring.resize(graph->getNNodes());
+        MCMC_CHECK(mcmc_get_coloring(ctx, coloring.data()));
+        uint64_t len = 0;
+        trajectory.resize(stats.trajLen);
+        MCMC_CHECK(mcmc_get_trajectory(ctx, trajectory.data(), trajectory.size(), &len));
+        MCMC_CHECK(mcmc_get_tail_trajectory(ctx, nullptr, 0, &len));
+        tail.resize(len);
+        MCMC_CHECK(mcmc_get_tail_trajectory(ctx, tail.data(), tail.size(), &len));
+        if (!directory.empty()) save();
+    }
+
+    // coloringMCMC_prints.cu: __customPrintRun0_start (:20-36), per iteration Run2/Run3 (:55-75),
+    // the tail cut's (Run2 with "---> TailCutting"; its "nuovi conflitti" is the last sweep's
+    // count, conflictCounterStar is not updated there), Run7_end (:95-110) + getStatsNumColors.
+    void save() const {
+        std::ofstream log(directory + ".log");
+        uint64_t fr = 0, tot = 0;
+        (void)mcmc_device_mem_info(0, &fr, &tot);
+        log << "total memory: " << tot << " free memory:" << fr << std::endl;
+        log << "numCol: " << param.nCol << std::endl;
+        log << "epsilon: " << param.epsilon << std::endl;
+        log << "lambda: " << param.lambda << std::endl;
+        log << "ratioFreezed: " << param.ratioFreezed << std::endl;
+        log << "maxRip: " << param.maxRip << std::endl << std::endl;
+        log << "numColorRatio: " << param.numColorRatio << std::endl;
+        const uint32_t sweeps = stats.sweepsRun;
+        for (uint32_t k = 1; k <= sweeps; k++) {
+            log << "***** Tentativo numero: " << k << std::endl;
+            log << "conflitti rilevati: " << trajectory[k - 1] << std::endl;
+            log << "nuovi conflitti rilevati: " << trajectory[k] << std::endl;
+        }
+        uint64_t cc = sweeps == param.maxRip && sweeps > 0 ? trajectory[sweeps - 1] : trajectory[stats.trajLen - 1];
+        const uint64_t star = sweeps ? trajectory[sweeps] : 0;
+        for (uint64_t x : tail) {
+            log << "***** Tentativo numero: " << stats.iter << std::endl << "---> TailCutting" << std::endl;
+            log << "conflitti rilevati: " << cc << std::endl;
+            log << "nuovi conflitti rilevati: " << star << std::endl;
+            cc = x;
+        }
+        log << "COLORAZIONE FINALE" << std::endl;
+        log << "Time " << stats.loopMs / 1000.0 << std::endl;
+        log << "Max iteration reached " << (stats.maxIterReached ? "yes" : "no") << std::endl;
+        // getStatsNumColors("end_") (:123-218)
+        const uint32_t n = graph->getNNodes(), nCol = param.nCol;
+        std::vector<uint32_t> h(std::max(n, nCol) + 1, 0);
+        for (uint32_t c : coloring) h[c]++;
+        int counter = 0, max_i = 0, min_i = (int)n, max_c = 0, min_c = (int)n;
+        const float average = (float)n / (float)nCol;
+        float variance = 0, balancingIndex = 0;
+        for (uint32_t i = 0; i < nCol; i++) {
+            if (h[i] > 0) {
+                counter++;
+                if ((int)h[i] > max_c) { max_i = (int)i; max_c = (int)h[i]; }
+                if ((int)h[i] < min_c) { min_i = (int)i; min_c = (int)h[i]; }
+                const float d = (float)h[i] - average;
+                balancingIndex += d * d;
+            }
+        }
+        balancingIndex /= ((float)n * graph->prob);
+        balancingIndex = std::sqrt(balancingIndex);
+        for (uint32_t i = 0; i < nCol; i++) {
+            const float d = (float)h[i] - average;
+            variance += d * d;
+        }
+        variance /= (float)nCol;
+        log << "Number of used colors is " << counter << " on " << nCol << " available" << std::endl;
+        log << "Most used colors is " << max_i << " used " << max_c << " times" << std::endl;
+        log << "Least used colors is " << min_i << " used " << min_c << " times" << std::endl << std::endl;
+        log << "Average " << average << std::endl;
+        log << "Variance " << variance << std::endl;
+        log << "StandardDeviation " << std::sqrt(variance) << std::endl;
+        log << "BalancingIndex " << balancingIndex << std::endl << std::endl;
+        log << std::endl << "end colorazione finale -------------------------------------------------------------------"
+            << std::endl << std::endl;
+        std::ofstream cf(directory + "-colors.txt");
+        for (size_t i = 0; i < coloring.size(); i++) cf << i << " " << coloring[i] << "\n";
+    }
+
+    const std::vector<uint32_t>& getColoring() const { return coloring; }
+    const std::vector<uint64_t>& getTrajectory() const { return trajectory; }
+    const std::vector<uint64_t>& getTailTrajectory() const { return tail; }
+    const mcmc_run_stats& getStats() const { return stats; }
+
+private:
+    Graph<nodeW, edgeW>* graph;
+    CurandStates* states;
+    ColoringMCMCParams param;
+    uint32_t tailMax;
+    std::string directory;
+    mcmc_ctx* ctx{nullptr};
+    mcmc_run_stats stats{};
+    std::vector<uint32_t> coloring;
+    std::vector<uint64_t> trajectory, tail;
 };

@@ -221,6 +221,11 @@ void mcmc_gpurand_destroy(mcmc_gpurand* r);
  * Parity unpinned against CUDA. */
 int mcmc_ref_create(const mcmc_graph* g, const mcmc_params* p, mcmc_gpurand* rand, mcmc_ctx** out);
 int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats);
+/* The run's initialisation alone (initial colouring from `rand`, cleared taboo and histograms):
+ * then mcmc_bench_sweeps times sweeps of this semantics. */
+int mcmc_ref_init(mcmc_ctx* c);
+/* cudaMemGetInfo's pair for the GPU colorer's log header (coloringMCMC_prints.cu:20-22). */
+int mcmc_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes);
 /* Cviol (REF: conflicting edges) after each tail-cut pass of the last run. */
 int mcmc_get_tail_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 

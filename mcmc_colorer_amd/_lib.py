@@ -54,7 +54,9 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_gpurand_destroy": (None, [c_void_p]),
     "mcmc_ref_create": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_void_p)]),
     "mcmc_ref_run": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "mcmc_ref_init": (c_int, [c_void_p]),
     "mcmc_get_tail_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
+    "mcmc_device_mem_info": (c_int, [c_int, _u64p, _u64p]),
 }
 
 

@@ -329,6 +329,10 @@ class ColoringMCMCGpuRef:
                                     ctypes.byref(self._ctx)))
         self.stats: Optional[MCMCRunStats] = None
 
+    def init(self) -> None:
+        """The run's initialisation alone (throughput benchmarks time mcmc_bench_sweeps after it)."""
+        check(lib().mcmc_ref_init(self._ctx))
+
     def run(self, tail_max_passes: int = 1000) -> MCMCRunStats:
         st = MCMCRunStats()
         check(lib().mcmc_ref_run(self._ctx, tail_max_passes, ctypes.byref(st)))

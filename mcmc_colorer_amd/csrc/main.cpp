@@ -4,6 +4,9 @@
 // Same options, defaults and output naming as the reference:
 //   --graph FILE | --simulate P -n N, --mcmcgpu, --nCol N, --numColRatio R, --tabooIteration N,
 //   --tailcut, --repet N, --seed N, --outDir D
+//   --mcmcgpu-ref: the reference's own GPU colorer semantics (ColoringMCMC as built by default:
+//   balance-dynamic proposal, cuRAND XORWOW per vertex, conflicts as edges, the GPU tail cut) on the
+//   same sweep; outputs <graph>-MCMC_GPU-<i>.log in coloringMCMC_prints.cu's layout
 //   --tailcutRepair: after the loop, run the reference's tail cut (coloringMCMC_CPU.cpp:272-311)
 //   with its inner loop fixed (k++; the reference's never returns), at most 1000 passes
 // Outputs <outDir>/<graphName>-MCMC_GPU-<i>.log and -colors.txt per repetition.
@@ -104,6 +107,7 @@ void help(const char* argv0) {
               << "                       G(n,p) from the build's counter-based generator (csrc/er_gen.h):\n"
               << "                       for n where the reference's O(n^2) generator is infeasible (1e7)\n"
               << "  --mcmcgpu            MCMC colorer on the MI355X (default)\n"
+              << "  --mcmcgpu-ref        the reference's GPU colorer semantics (XORWOW, balance-dynamic)\n"
               << "  --nCol N             number of colours (default maxDeg / numColRatio)\n"
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
               << "  --tabooIteration N   taboo iterations (default 0)\n"
@@ -122,7 +126,7 @@ int main(int argc, char** argv) {
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
     bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false,
-         tailcutRepair = false;
+         tailcutRepair = false, mcmcgpuref = false;
     uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
@@ -136,6 +140,7 @@ int main(int argc, char** argv) {
         {"seed", required_argument, 0, 'S'},     {"help", no_argument, 0, 'h'},
         {"device", required_argument, 0, 'D'},   {"simulate-fast", required_argument, 0, 'F'},
         {"er-seed", required_argument, 0, 'E'},  {"tailcutRepair", no_argument, 0, 'X'},
+        {"mcmcgpu-ref", no_argument, 0, 'G'},
         {0, 0, 0, 0}};
     int c;
     while ((c = getopt_long(argc, argv, "g:o:s:n:12345k:r:t:lR:S:hD:", longopts, nullptr)) != -1) {
@@ -162,6 +167,7 @@ int main(int argc, char** argv) {
                           break;
                 case 'E': erSeed = std::stoull(optarg); break;
                 case 'X': tailcutRepair = true; break;
+                case 'G': mcmcgpuref = true; break;
                 case 'h': help(argv[0]); return 0;
                 default: break;
             }
@@ -183,7 +189,12 @@ int main(int argc, char** argv) {
         std::cout << "--lubygpu / --grdffgpu / --vffgpu are outside this build (see DESIGN.md)" << std::endl;
         return 255;
     }
-    if (!mcmcgpu) std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
+    if (mcmcgpu && mcmcgpuref) {
+        std::cout << "--mcmcgpu and --mcmcgpu-ref write the same files: choose one" << std::endl;
+        return 255;
+    }
+    if (!mcmcgpu && !mcmcgpuref)
+        std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
     if (simulate && n == 0) { std::cout << "Simualtion enabled: specify the number of nodes (-n)." << std::endl; return 255; }
     if (numColRatio == 0.0) numColRatio = 1.0;
     if (seed == 0) {                                              // ArgHandle.cpp:272-276
@@ -229,6 +240,7 @@ int main(int argc, char** argv) {
               << " - Mean Degree: " << g->getMeanNodeDeg() << "  (graph ready in " << tgen << " s)" << std::endl;
 
     GPURand GPURandGen(g->getNNodes(), (long)seed);
+    CurandStates* curand = mcmcgpuref ? new CurandStates(g->getNNodes(), (long)seed, device) : nullptr;   // main.cu:80
     for (uint32_t i = 0; i < repetitions; i++) {
         std::cout << "Repetition: " << i << std::endl;
         ColoringMCMCParams params;                                   // main.cu:160-168
@@ -241,6 +253,16 @@ int main(int argc, char** argv) {
         params.tabooIteration = tabooIteration;
         params.tailcut = tailcut;
         params.tailcutRepair = tailcutRepair ? 1000u : 0u;
+        if (curand) {
+            ColoringMCMCGpuRef<float, float> colRef(g, curand, params);
+            colRef.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));
+            colRef.run((int)i);
+            const auto& st = colRef.getStats();
+            std::cout << "MCMC GPU elapsed time: " << st.loopMs / 1000.0 << " (" << st.sweepsRun
+                      << " sweeps, final conflicting edges " << st.finalViol
+                      << (st.maxIterReached ? ", max iteration reached" : "") << ")" << std::endl << std::endl;
+            continue;
+        }
         ColoringMCMC<float, float> colMCMC(g, GPURandGen.randStates, params);
         colMCMC.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));
         colMCMC.run((int)i);
@@ -251,6 +273,7 @@ int main(int argc, char** argv) {
         std::cout << ")" << std::endl
                   << std::endl;
     }
+    delete curand;
     delete g;
     return EXIT_SUCCESS;
 }

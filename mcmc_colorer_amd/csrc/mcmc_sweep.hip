@@ -2216,9 +2216,9 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     return MCMC_OK;
 }
 
-int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
+int mcmc_ref_init(mcmc_ctx* c) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
-    if (!c->ref) return fail(MCMC_E_STATE, "mcmc_ref_run needs a context from mcmc_ref_create");
+    if (!c->ref) return fail(MCMC_E_STATE, "mcmc_ref_init needs a context from mcmc_ref_create");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     const uint32_t n = c->n, nCol = c->p.nCol;
     // run() (coloringMCMC_main.cu:101-158): taboo cleared, colours from the states' next draw
@@ -2226,22 +2226,27 @@ int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }   // states moved
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
     c->batch = c->bench_n = 0;
-    c->tailcut_max = tail_max_passes;
-    if (c->p.tailcut && tail_max_passes) {
-        int rc = ensure_tail_buffers(c);
-        if (rc) return rc;
-    }
     MCMC_HIP_TRY(hipMemsetAsync(c->hist, 0, sizeof(uint32_t) * 2u * kHistWords, c->stream));
     if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * n, c->stream));
     int rc = upload_state(c, 0);
     if (rc) return rc;
-    {
-        const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 2048u));
-        ref_init_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], c->rand->states[c->rand_base], n, nCol, c->hist);
-        MCMC_HIP_TRY(hipGetLastError());
-    }
+    const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 2048u));
+    ref_init_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], c->rand->states[c->rand_base], n, nCol, c->hist);
+    MCMC_HIP_TRY(hipGetLastError());
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     c->initialized = true;
     c->ran = true;
+    return MCMC_OK;
+}
+
+int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
+    int rc = mcmc_ref_init(c);
+    if (rc) return rc;
+    c->tailcut_max = tail_max_passes;
+    if (c->p.tailcut && tail_max_passes) {
+        rc = ensure_tail_buffers(c);
+        if (rc) return rc;
+    }
     const uint32_t cap = c->p.maxRip > 0 ? c->p.maxRip : 1u;
     const uint32_t total = cap + 1u;   // cap sweeps + the count-only pass
     const uint32_t batch = std::min<uint32_t>(16u, total);
@@ -2275,7 +2280,7 @@ int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
     st.finalViol = h.finalViol;                   // conflicting edges of the returned colouring
     st.trajLen = (uint64_t)h.t + 1;
     st.sweepsRun = (h.t == cap) ? cap : h.t;      // selectStar launches of the reference
-    st.initDraws = n;
+    st.initDraws = c->n;
     st.loopMs = ms;
     c->last = st;
     c->tail_traj.clear();
@@ -2400,6 +2405,10 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         mloc = ends[1] - ends[0];
     }
     const uint64_t taboo = c->p.tabooIteration > 0 ? 8 * nloc : 0;
+    // REF: XORWOW states read and written (24 + 24 B per vertex), the rows' own colours (streamed
+    // per group), both histograms; the reference's B_alg adds the same states plus its n*nCol
+    // colorsChecker memset and row writes it does not model here
+    const uint64_t ref_extra = c->ref ? 48 * nloc + nloc + 8ull * kHistWords : 0;
     i.variant = c->variant;
     i.resident = c->variant_res ? 1 : 0;
     i.block_log2 = c->block_log2;
@@ -2407,7 +2416,7 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
     i.grid = c->grid.x;
     i.block = c->block.x;
     i.lds_bytes = c->lds;
-    i.ref_bytes = 4 * (nloc + 1) + 4 * mloc + 4 * (uint64_t)c->n + 4 * nloc + taboo;
+    i.ref_bytes = 4 * (nloc + 1) + 4 * mloc + 4 * (uint64_t)c->n + 4 * nloc + taboo + (c->ref ? 48 * nloc : 0);
     if (c->tl) {
         const TiledLayout& t = *c->tl;
         i.grp_rows = t.grp_rows;
@@ -2415,7 +2424,7 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         i.sub_log2 = c->sub_log2;
         const uint64_t segb = 4ull * tseg_stride(t.grp_rows) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
         i.layout_bytes = 2 * t.ids + segb;
-        i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;
+        i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo + ref_extra;
     } else {
         i.layout_bytes = 8 * (nloc + 1) + 4 * mloc;
         i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;

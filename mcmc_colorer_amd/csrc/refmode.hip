@@ -76,6 +76,16 @@ int mcmc_xorwow_state(uint64_t seed, uint64_t subsequence, int flavor, uint32_t 
     return MCMC_OK;
 }
 
+int mcmc_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
+    if (!free_bytes || !total_bytes) return fail(MCMC_E_ARG, "NULL argument");
+    MCMC_HIP_TRY(hipSetDevice(device));
+    size_t f = 0, t = 0;
+    MCMC_HIP_TRY(hipMemGetInfo(&f, &t));
+    *free_bytes = f;
+    *total_bytes = t;
+    return MCMC_OK;
+}
+
 int mcmc_gpurand_create(uint32_t n, uint32_t seed, int device, mcmc_gpurand** out) {
     if (!out || n == 0) return fail(MCMC_E_ARG, "bad argument");
     MCMC_HIP_TRY(hipSetDevice(device));

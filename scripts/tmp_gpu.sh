@@ -1,8 +1,11 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-for v in tiled tiled::::0; do
-timeout -k 10 400 python bench.py --config c2 --steps 100 --warmup 5 --no-cpu-baseline --no-refstruct --variant $v > gpurun_out/b_c2v.log 2>&1 || { tail -5 gpurun_out/b_c2v.log; exit 1; }
-python -c "import json; d=json.loads(open('gpurun_out/b_c2v.log').read().strip().splitlines()[-1]); print('c2 $v', '%.4f ms'%d['roofline']['kernel_ms'], '%.3e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
-done
-timeout -k 10 400 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-refstruct > gpurun_out/b_c3v.log 2>&1 && python -c "import json; d=json.loads(open('gpurun_out/b_c3v.log').read().strip().splitlines()[-1]); print('c3', '%.3f ms'%d['roofline']['kernel_ms'], '%.3e'%d['value'], 'frac %.3f'%d['roofline']['frac'])"
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests/test_cli.py -m gpu -q -p no:cacheprovider > gpurun_out/pytest_cli.log 2>&1
+rc=$?; echo "cli rc=$rc"; tail -3 gpurun_out/pytest_cli.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python bench.py --config c2 --semantics ref --steps 200 --warmup 20 > gpurun_out/bench_ref_c2.log 2>&1
+rc=$?; echo "ref c2 rc=$rc"; tail -1 gpurun_out/bench_ref_c2.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python bench.py --semantics ref --steps 20 --warmup 3 > gpurun_out/bench_ref_c3.log 2>&1
+rc=$?; echo "ref c3 rc=$rc"; tail -1 gpurun_out/bench_ref_c3.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
+bash scripts/gpu_prof.sh r01ref_c2 --config c2 --semantics ref --no-refstruct || exit $?
+bash scripts/gpu_prof.sh r01ref_c3 --semantics ref --no-refstruct || exit $?

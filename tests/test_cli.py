@@ -89,3 +89,32 @@ def test_cli_simulate_fast(tmp_path):
     r = O.mcmc_run(off, idx, 16, seed, nthreads=8)
     want = [f"{v} {c}" for v, c in enumerate(r.colors.tolist())]
     assert [l for l in got if l] == want
+
+
+@pytest.mark.gpu
+def test_cli_mcmcgpu_ref(tmp_path):
+    """--mcmcgpu-ref: the reference's GPU colorer semantics, two repetitions sharing the XORWOW
+    states (main.cu:80,193), with the GPU tail cut; colours against the oracle's restatement, the
+    log in coloringMCMC_prints.cu's layout."""
+    import numpy as np
+
+    import oracle_ref as O
+
+    out = tmp_path / "o"
+    r = subprocess.run([str(CLI), "--mcmcgpu-ref", "--simulate", "0.1", "-n", "1000", "--seed", "1", "--repet", "2",
+                        "--tailcut", "--outDir", str(out)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    O.srand(1)
+    off, idx = O.setup_rnd2(1000, 0.1)
+    st = O.gpurand_init(1000, 1)
+    name = "1000_0.100000_1.000000"
+    for i in range(2):
+        res = O.mcmc_gpu_run(off, idx, O.max_deg(off), st, tailcut=True)
+        got = (out / f"{name}-MCMC_GPU-{i}-colors.txt").read_text().split("\n")
+        assert [int(x.split()[1]) for x in got if x] == res.colors.tolist()
+        log = (out / f"{name}-MCMC_GPU-{i}.log").read_text()
+        assert f"numCol: {O.max_deg(off)}" in log and "COLORAZIONE FINALE" in log
+        assert f"conflitti rilevati: {res.traj[0]}" in log
+        assert log.count("***** Tentativo numero:") == res.res.sweeps + res.res.tailcutPasses
+        assert ("---> TailCutting" in log) == (res.res.tailcutPasses > 0)
+        assert f"Max iteration reached {'yes' if res.res.maxIterReached else 'no'}" in log
