@@ -885,11 +885,14 @@ __device__ __forceinline__ void tile_gather(const uint8_t* __restrict__ sc, cons
 // REF scan: the occupancy masks plus the arcs the reference's conflictCounter counts
 // (coloringMCMC_utils.cu:115): same colour as the row's (oc) and a larger id (vertex vrow, the
 // pair's block starts at whi), not padding (the quad starts at id position q of the group, the
-// row's real ids end at tend).
+// row's real ids end at tend). cmode (pair-uniform): 0 the block lies below every row of the
+// group (no arc counts), 1 above them all (no id test), 2 the diagonal block (id test). Padding
+// fills the tail of a segment's last quad with copies of one id, so the count of the 8 ids is
+// corrected by (pads) x [element 7 counts] instead of a position test per id.
 template <int NW>
 __device__ __forceinline__ void tile_gather_ref(const uint8_t* __restrict__ sc, const uint4& v, bool ok,
                                                 uint32_t (&m)[NW], uint32_t oc, uint32_t q, uint32_t tend,
-                                                uint32_t whi, uint32_t vrow, uint32_t& ecnt) {
+                                                uint32_t whi, uint32_t vrow, uint32_t cmode, uint32_t& ecnt) {
     if (ok) {
         const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
         uint32_t id[8], cg[8];
@@ -900,10 +903,19 @@ __device__ __forceinline__ void tile_gather_ref(const uint8_t* __restrict__ sc, 
         }
 #pragma unroll
         for (int e = 0; e < 8; e++) cg[e] = sc[id[e]];
-        uint32_t c = 0;
+        if (cmode == 1) {
+            uint32_t c = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++) c += (cg[e] == oc && q + (uint32_t)e < tend && (whi | id[e]) > vrow) ? 1u : 0u;
-        ecnt += c;
+            for (int e = 0; e < 8; e++) c += cg[e] == oc ? 1u : 0u;
+            const uint32_t nv = tend - q;   // >= 1: a quad starts before its segment's real end
+            ecnt += c - ((nv < 8u && cg[7] == oc) ? 8u - nv : 0u);
+        } else if (cmode == 2) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) c += (cg[e] == oc && (whi | id[e]) > vrow) ? 1u : 0u;
+            const uint32_t nv = tend - q;
+            ecnt += c - ((nv < 8u && cg[7] == oc && (whi | id[7]) > vrow) ? 8u - nv : 0u);
+        }
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             const uint32_t cc = cg[e];
@@ -1220,6 +1232,8 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         uint32_t row = wid * nsub + sub, pos = fpos, end = fend;
         uint32_t tend = fend - fpads;                 // REF: the row's real ids end here
         const uint32_t whi = b << a.block_log2;       // REF: vertex id of the pair's block start
+        const uint32_t vlo = a.v_begin + r0;
+        const uint32_t cmode = (whi + (1u << a.block_log2) - 1u < vlo) ? 0u : (whi > vlo + rows - 1u) ? 1u : 2u;
         // REF: the own colour of a row of this group (0 past the group: such rows gather nothing)
         const uint8_t* ownp = RES ? lbase + a.v_begin + r0
                                   : own_base + gpar * a.own_buf_bytes + ((a.v_begin + r0) & 15u);
@@ -1288,7 +1302,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     }
 #define MCMC_TILE_GATHER(Q, OK, QPOS)                                                                   \
     do {                                                                                                \
-        if (REF) tile_gather_ref<NW>(scb, Q, OK, m, oc, QPOS, tend, whi, a.v_begin + r0 + row, ecnt);   \
+        if (REF) tile_gather_ref<NW>(scb, Q, OK, m, oc, QPOS, tend, whi, a.v_begin + r0 + row, cmode, ecnt); \
         else tile_gather<NW>(scb, Q, OK, m);                                                            \
     } while (0)
         uint4 v1[kTileU];
