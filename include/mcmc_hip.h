@@ -140,13 +140,21 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
  * instantiation out of a host-timed region). */
 int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps);
 
+/* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
+ * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.
+ * mask == NULL: fill_p's own-colour distribution (cases (i)/(iii): p[cv] = p, eps elsewhere);
+ * else case (ii): eps where a bit of mask (nCol bits, 32 per word) is set, p where clear.
+ * Returns the drawn colour, or nCol for a CDF overflow. */
+uint32_t mcmc_cdf_walk(const uint32_t* mask, uint32_t nCol, uint32_t cv, float eps, float p, float u);
+
 /* Sweep kernel and adjacency layout a context chose (no reference counterpart: the reference's
  * sweep has one fixed CSR layout). sweep_bytes = B_fmt of SURVEY.md §8d, the HBM bytes one sweep
  * of this context's rows must move in its layout (adjacency + offsets/segment tables + colour
  * replica read once + local colour write [+ taboo r/w]); ref_bytes = the same rows' B_alg in the
  * reference's uint32 layout (4(n+1) + 4m + 4n + 4n [+ 8n]). */
 typedef struct mcmc_ctx_info {
-    int32_t variant;          /* 0 LDS-staged CSR, 1 column-blocked CSR, 2 L2-gather CSR, 3 tiled */
+    int32_t variant;          /* 0 LDS-staged CSR, 1 column-blocked CSR, 2 L2-gather CSR, 3 tiled,
+                                 4 wide (nCol > 256: uint16 replicas, CSR) */
     int32_t resident;         /* tiled: whole colour replica LDS-resident (else streamed slices) */
     uint32_t block_log2;      /* tiled / blocked: column block = 2^block_log2 vertices */
     uint32_t nblocks;

@@ -41,6 +41,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
+    "mcmc_cdf_walk": (c_uint32, [_u32p, c_uint32, c_uint32, c_float, c_float, c_float]),
     "mcmc_refstruct_bench": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_double), _u64p]),
     "mcmc_destroy": (None, [c_void_p]),
     "mcmc_part_layout": (c_int, [c_uint32, c_uint32, _u64p, _u64p]),
@@ -108,7 +109,7 @@ class MCMCCtxInfo(ctypes.Structure):
         ("ref_bytes", c_uint64),
     ]
 
-    VARIANTS = {0: "lds", 1: "blocked", 2: "global", 3: "tiled"}
+    VARIANTS = {0: "lds", 1: "blocked", 2: "global", 3: "tiled", 4: "wide"}
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}

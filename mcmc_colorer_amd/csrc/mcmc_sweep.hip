@@ -31,6 +31,7 @@
 #include <mutex>
 #include <vector>
 
+#include "cdf_walk.h"
 #include "mcmc_common.h"
 #include "rng.h"
 #include "xorwow.h"
@@ -115,6 +116,13 @@ struct SweepArgs {
     uint32_t* hist;             // [2][kHistWords] colour histograms of C_t by parity (C_t[v] <= nCol)
     float ref_hi;               // 1 - (nCol - 1) * eps (coloringMCMC_balance.cu:132)
     uint32_t own_buf_bytes;     // streaming REF: LDS bytes of one own-colour buffer
+    // wide sweep (nCol > 256, uint16 replicas; sweep_wide.h)
+    uint64_t arc_begin, arc_count;   // the local rows' arcs: col_idx[arc_begin, arc_begin + arc_count)
+    const uint32_t* chunk_row;  // [nchunks + 1] first local row of every 256-arc chunk
+    uint32_t nchunks;
+    uint8_t* wflag;             // [nloc] viol flags of the running sweep (cleared by the evaluation)
+    uint32_t* wlist;            // [nloc] violating, untaboo'd vertices (global ids)
+    uint32_t* wcount;           // their number
 };
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
 
@@ -213,11 +221,13 @@ __device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
 
 // Applies the accepted sweep: replays E sorted events, advances the RNG, flips buffers.
 // `ev` holds the events (global ids, any order) and is sorted in place (via LDS when small).
+// CT: the colour replica's element type (uint8_t; uint16_t for the wide sweep, nCol > 256).
+template <typename CT = uint8_t>
 __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
                               uint32_t lds_cap) {
     DevState* st = a.st;
-    const uint8_t* C = (t & 1) ? a.colors1 : a.colors0;
-    uint8_t* Cs = (t & 1) ? a.colors0 : a.colors1;
+    const CT* C = reinterpret_cast<const CT*>((t & 1) ? a.colors1 : a.colors0);
+    CT* Cs = reinterpret_cast<CT*>((t & 1) ? a.colors0 : a.colors1);
     if (E > 0) {
         uint32_t P = 1;
         while (P < E) P <<= 1;
@@ -237,7 +247,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
                 const uint32_t v = s[i];
                 const uint32_t r = glibc_next(ring, head);
                 const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
-                Cs[caddr(a, v)] = (uint8_t)c;
+                Cs[caddr(a, v)] = (CT)c;
                 if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                     a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
             }
@@ -259,6 +269,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
 // Loop control of run() (coloringMCMC_CPU.cpp:136, :259-269): records Cviol_t, stops on the cap or
 // on Cviol_t <= z, otherwise accepts the sweep. All threads of one workgroup call it with the same
 // state values; thread 0 writes the state.
+template <typename CT = uint8_t>
 __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
                                uint32_t* lds, uint32_t lds_cap) {
     DevState* st = a.st;
@@ -280,7 +291,7 @@ __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long lon
         if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
         return;
     }
-    commit_accept(a, t, a.events, E, lds, lds_cap);
+    commit_accept<CT>(a, t, a.events, E, lds, lds_cap);
 }
 
 // Loop control of the reference's GPU run() (coloringMCMC_main.cu:160-269), fused into the last
@@ -315,6 +326,7 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
 }
 
 // Stand-alone commit (MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
+template <typename CT>
 __global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
     __shared__ uint32_t lds[kLdsSortCap];
     __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
@@ -329,7 +341,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
     }
     __syncthreads();
     if (sh_done) return;
-    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+    commit_control<CT>(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
 }
 
 // ---- vertex-partitioned sweep: footer exchange ------------------------------------------------
@@ -1434,8 +1446,16 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
     }
 }
 
+#include "sweep_wide.h"
+
 // ----------------------------------------------------------------------------------------------
 using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
+// wide sweep: grid = CUs (g.x); scan 8 x 256-thread workgroups per CU, evaluation 4, walk 16
+void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
+    wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
+    wide_eval_kernel<<<g.x * 4u, 256, 0, s>>>(a);
+    wide_walk_kernel<<<g.x * 8u, kWideWalkThreads, 0, s>>>(a);
+}
 template <int NW, bool LDSC>
 void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
     sweep_kernel<NW, LDSC><<<g, b, lds, s>>>(a);
@@ -1531,6 +1551,15 @@ struct mcmc_ctx {
     uint32_t rand_base = 0;         // the states' parity when the run started
     uint32_t* hist = nullptr;       // [2][kHistWords]
     uint32_t own_buf_bytes = 0;
+    // wide sweep (variant 4: nCol > 256, uint16 colour replicas; sweep_wide.h)
+    bool wide = false;
+    uint32_t cbytes = 1;            // bytes per colour in the replicas
+    uint32_t* chunk_row = nullptr;
+    uint32_t nchunks = 0;
+    uint64_t arc_begin = 0, arc_count = 0;
+    uint8_t* wflag = nullptr;
+    uint32_t* wlist = nullptr;
+    uint32_t* wcount = nullptr;
 };
 
 namespace {
@@ -1539,7 +1568,7 @@ namespace {
 // regions of S colours followed by a footer.
 int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
     if (!c->part) {
-        MCMC_HIP_TRY(hipMemcpyAsync(dst, h, c->n, hipMemcpyHostToDevice, c->stream));
+        MCMC_HIP_TRY(hipMemcpyAsync(dst, h, (size_t)c->n * c->cbytes, hipMemcpyHostToDevice, c->stream));
     } else {
         const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
         for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
@@ -1552,7 +1581,7 @@ int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
 
 int download_colors(mcmc_ctx* c, const uint8_t* src, uint8_t* h) {
     if (!c->part) {
-        MCMC_HIP_TRY(hipMemcpyAsync(h, src, c->n, hipMemcpyDeviceToHost, c->stream));
+        MCMC_HIP_TRY(hipMemcpyAsync(h, src, (size_t)c->n * c->cbytes, hipMemcpyDeviceToHost, c->stream));
     } else {
         const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
         for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
@@ -1638,6 +1667,16 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.slice_bytes = c->slice_bytes;
         a.seg_buf_bytes = (tseg_stride(c->tl->grp_rows) * 4u + 1023u) & ~1023u;
     }
+    if (c->wide) {
+        a.arc_begin = c->arc_begin;
+        a.arc_count = c->arc_count;
+        a.chunk_row = c->chunk_row;
+        a.nchunks = c->nchunks;
+        a.wflag = c->wflag;
+        a.wlist = c->wlist;
+        a.wcount = c->wcount;
+        a.fused = 0;
+    }
     a.phase_ts = c->phase_ts;
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
@@ -1661,7 +1700,9 @@ int ensure_constants() {
 // Host launch of one (sweep, commit) pair on the context stream.
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     c->sweep(a, c->grid, c->block, c->lds, c->stream);
-    if (!a.fused) commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (a.fused) return;
+    if (c->wide) commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+    else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
 int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
@@ -1828,9 +1869,17 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     *out = nullptr;
     const GraphDev& gd = g->g;
     if (p->nCol == 0) return fail(MCMC_E_ARG, "nCol must be >= 1");
-    if (p->nCol > 256)
-        return fail(MCMC_E_ARG, "nCol > 256 is not supported by this build (uint8 colour replicas)");
     if (v_begin > v_end || v_end > gd.n) return fail(MCMC_E_ARG, "bad vertex range");
+    // nCol > 256: the wide sweep (uint16 replicas, sweep_wide.h); MCMC_GATHER=wide forces it
+    const char* gv = getenv("MCMC_GATHER");
+    const std::string gsel = gv ? gv : "";
+    const bool wide = p->nCol > 256 || (gsel == "wide" && !ref);
+    if (wide) {
+        if (p->nCol > kWideMaxCol) return fail(MCMC_E_ARG, "nCol > 65535 is not supported (uint16 colour replicas)");
+        if (ref) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
+        if (!gd.row_off) return fail(MCMC_E_ARG, "nCol > 256 needs a CSR graph (mcmc_graph_upload / _simulate)");
+        if (v_begin != 0 || v_end != gd.n) return fail(MCMC_E_ARG, "nCol > 256: whole-graph contexts only");
+    }
     if (ref) {
         // a colour may equal nCol (initColoring at u = 1.0f): it must fit the uint8 replicas
         if (p->nCol < 2 || p->nCol > 255) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
@@ -1858,11 +1907,16 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     // for A/B runs and parity tests. Knobs: MCMC_GATHER=tiled|lds|blocked|global, MCMC_BLOCK_LOG2,
     // MCMC_SUB_LOG2, MCMC_GROUP_ROWS, MCMC_TILE_STREAM.
     const size_t lds_bytes = (((size_t)gd.n + 15) / 16) * 16;
-    const char* gv = getenv("MCMC_GATHER");
-    const std::string gsel = gv ? gv : "";
     c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
     if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
     if (!gd.row_off || ref) c->variant = 3;   // generated graph / REF: tiled layout only
+    if (wide) {
+        c->variant = 4;
+        c->wide = true;
+        c->cbytes = 2;
+        c->fused = 0;
+        c->sweep = launch_wide;
+    }
     const int wi = c->nw == 1 ? 0 : c->nw == 2 ? 1 : c->nw == 4 ? 2 : 3;
     hipError_t ea = hipSuccess;
     if (c->variant == 0) {
@@ -1906,8 +1960,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     chk(hipEventCreate(&c->ev0));
     chk(hipEventCreate(&c->ev1));
     // colour replicas carry 256 B of slack so equal-size partition slabs can be all-gathered in place
-    chk(hipMalloc(&c->colors[0], (size_t)gd.n + 256));
-    chk(hipMalloc(&c->colors[1], (size_t)gd.n + 256));
+    chk(hipMalloc(&c->colors[0], ((size_t)gd.n + 256) * c->cbytes));
+    chk(hipMalloc(&c->colors[1], ((size_t)gd.n + 256) * c->cbytes));
     c->own_colors[0] = c->colors[0];
     c->own_colors[1] = c->colors[1];
     if (p->tabooIteration > 0) chk(hipMalloc(&c->taboo, sizeof(uint32_t) * std::max<uint32_t>(nloc, 1)));
@@ -2018,6 +2072,31 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
         }
+    } else if (c->variant == 4) {
+        c->grid = dim3((uint32_t)cus);   // launch_wide scales it per kernel
+        c->block = dim3(256);
+        uint64_t ends[2];
+        hipError_t ew = hipMemcpy(&ends[0], gd.row_off + v_begin, sizeof(uint64_t), hipMemcpyDeviceToHost);
+        if (ew == hipSuccess) ew = hipMemcpy(&ends[1], gd.row_off + v_end, sizeof(uint64_t), hipMemcpyDeviceToHost);
+        c->arc_begin = ends[0];
+        c->arc_count = ends[1] - ends[0];
+        c->nchunks = (uint32_t)((c->arc_count + kWideChunk - 1) / kWideChunk);
+        if (ew == hipSuccess) ew = hipMalloc(&c->chunk_row, sizeof(uint32_t) * ((size_t)c->nchunks + 1));
+        if (ew == hipSuccess) ew = hipMalloc(&c->wflag, std::max<size_t>(nloc, 1));
+        if (ew == hipSuccess) ew = hipMalloc(&c->wlist, sizeof(uint32_t) * std::max<size_t>(nloc, 1));
+        if (ew == hipSuccess) ew = hipMalloc(&c->wcount, sizeof(uint32_t));
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, std::max<size_t>(nloc, 1), c->stream);
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, sizeof(uint32_t), c->stream);
+        if (ew == hipSuccess) {
+            const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((c->nchunks + 256) / 256, 4096u));
+            wide_chunk_row_kernel<<<blocks, 256, 0, c->stream>>>(gd.row_off + v_begin, nloc, c->arc_begin,
+                                                                 c->arc_count, c->nchunks, c->chunk_row);
+            ew = hipStreamSynchronize(c->stream);
+        }
+        if (ew != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("wide sweep setup: ") + hipGetErrorString(ew));
+        }
     } else if (c->variant != 2) {
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);
@@ -2025,7 +2104,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->block = dim3(256);
         c->grid = dim3((uint32_t)cus * 8u);
     }
-    if (c->variant != 3) {
+    if (c->variant != 3 && c->variant != 4) {
         const uint32_t W = c->variant == 1 ? c->grid.x : c->grid.x * (c->block.x / 64);
         hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
         if (ew != hipSuccess) {
@@ -2101,11 +2180,14 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     const uint32_t n = c->n;
     const uint32_t s0 = minstd_seed_state(c->p.seed);
+    if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(n, 1u), c->stream));
     if (C0) {
-        std::vector<uint8_t> h(n);
-        for (uint32_t v = 0; v < n; v++) {
+        for (uint32_t v = 0; v < n; v++)
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
-            h[v] = (uint8_t)C0[v];
+        std::vector<uint8_t> h((size_t)n * c->cbytes);
+        for (uint32_t v = 0; v < n; v++) {
+            if (c->wide) reinterpret_cast<uint16_t*>(h.data())[v] = (uint16_t)C0[v];
+            else h[v] = (uint8_t)C0[v];
         }
         int rc = upload_colors(c, c->colors[0], h.data());
         if (rc) return rc;
@@ -2115,8 +2197,13 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
         MCMC_HIP_TRY(hipMemcpyAsync(c->st, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
         const UniformIntConst k = uniform_int_const(c->p.nCol);
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
-        init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st, c->part ? c->part_S : 0u,
-                                                             c->part ? 4u * kFooterWords : 0u);
+        if (c->wide)
+            init_coloring_wide_kernel<<<blocks, 256, 0, c->stream>>>(reinterpret_cast<uint16_t*>(c->colors[0]), n, s0,
+                                                                     k, c->st);
+        else
+            init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st,
+                                                                 c->part ? c->part_S : 0u,
+                                                                 c->part ? 4u * kFooterWords : 0u);
         MCMC_HIP_TRY(hipGetLastError());
         DevState h;
         int rc = download_state(c, &h);
@@ -2124,13 +2211,14 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
         uint64_t draws = n;
         if (h.init_rejections > 0) {
             // Exact sequential replay of uniform_int_distribution's rejection loop.
-            std::vector<uint8_t> hc(n);
+            std::vector<uint8_t> hc((size_t)n * c->cbytes);
             uint32_t x = s0;
             draws = 0;
             for (uint32_t v = 0; v < n; v++) {
                 uint32_t r;
                 do { x = minstd_mulmod(x, kMinstdA); r = x - 1u; draws++; } while (r >= k.past);
-                hc[v] = (uint8_t)(r / k.scaling);
+                if (c->wide) reinterpret_cast<uint16_t*>(hc.data())[v] = (uint16_t)(r / k.scaling);
+                else hc[v] = (uint8_t)(r / k.scaling);
             }
             rc = upload_colors(c, c->colors[0], hc.data());
             if (rc) return rc;
@@ -2213,7 +2301,7 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (c->part || c->v_begin != 0 || c->v_end != c->n)
         return fail(MCMC_E_STATE, "tail cutting runs on whole-graph contexts (mcmc_run)");
-    if (c->p.nCol > 256) return fail(MCMC_E_ARG, "nCol > 256");
+    if (c->wide) return fail(MCMC_E_ARG, "tail cutting: nCol <= 256 (uint8 replicas) only");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (max_passes) {
         int rc = ensure_tail_buffers(c);
@@ -2328,10 +2416,13 @@ int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out) {
         if (rc) return rc;
         which = h.t & 1;
     }
-    std::vector<uint8_t> tmp(c->n);
+    std::vector<uint8_t> tmp((size_t)c->n * c->cbytes);
     int rc = download_colors(c, c->colors[which], tmp.data());
     if (rc) return rc;
-    for (uint32_t v = 0; v < c->n; v++) out[v] = tmp[v];
+    if (c->wide)
+        for (uint32_t v = 0; v < c->n; v++) out[v] = reinterpret_cast<const uint16_t*>(tmp.data())[v];
+    else
+        for (uint32_t v = 0; v < c->n; v++) out[v] = tmp[v];
     return MCMC_OK;
 }
 
@@ -2405,6 +2496,12 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     return MCMC_OK;
 }
 
+uint32_t mcmc_cdf_walk(const uint32_t* mask, uint32_t nCol, uint32_t cv, float eps, float p, float u) {
+    if (nCol == 0) return 0;
+    if (!mask) return walk_own(nCol, cv < nCol ? cv : nCol - 1u, eps, p, u);
+    return walk_mask(mask, nCol, eps, p, u);
+}
+
 int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
     if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
     mcmc_ctx_info i{};
@@ -2439,6 +2536,10 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         const uint64_t segb = 4ull * tseg_stride(t.grp_rows) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
         i.layout_bytes = 2 * t.ids + segb;
         i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo + ref_extra;
+    } else if (c->wide) {
+        // CSR + per-chunk row table; colour replica read once + own colours + write (2 B each)
+        i.layout_bytes = 8 * (nloc + 1) + 4 * mloc + 4ull * (c->nchunks + 1);
+        i.sweep_bytes = i.layout_bytes + 2 * (uint64_t)c->n + 4 * nloc + taboo;
     } else {
         i.layout_bytes = 8 * (nloc + 1) + 4 * mloc;
         i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo;
@@ -2469,6 +2570,10 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->tc_count);
     (void)hipFree(c->tc_tmp);
     (void)hipFree(c->hist);
+    (void)hipFree(c->chunk_row);
+    (void)hipFree(c->wflag);
+    (void)hipFree(c->wlist);
+    (void)hipFree(c->wcount);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -1,0 +1,157 @@
+"""The wide sweep (nCol > 256: uint16 colour replicas, csrc/sweep_wide.h).
+
+The reference's default colour count is maxDeg (main.cu:53,162), so power-law and dense graphs run
+with hundreds to thousands of colours. The wide sweep keeps the --mcmccpu semantics
+(coloringMCMC_CPU.cpp:115-270) bit-exactly; its CDF walk jumps over runs of equal probabilities
+(csrc/cdf_walk.h), which the CPU tests pin against a plain float32 step-by-step walk, and the GPU
+tests pin against the oracle (final colouring, trajectory, iter, glibc draws).
+"""
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from mcmc_colorer_amd import _lib
+
+
+def naive_walk(mask_bits, ncol, eps, p, u):
+    """extract_new_color (:505-520) literally: cdf += p[c] in float32, stop on cdf > u."""
+    eps, p, u = np.float32(eps), np.float32(p), np.float32(u)
+    cdf = np.float32(0.0)
+    for c in range(ncol):
+        cdf = np.float32(cdf + (eps if mask_bits[c] else p))
+        if cdf > u:
+            return c
+    return ncol
+
+
+def lib_walk(mask_bits, ncol, cv, eps, p, u):
+    L = _lib.lib()
+    if mask_bits is None:
+        return L.mcmc_cdf_walk(None, ncol, cv, eps, p, u)
+    words = np.zeros((ncol + 31) // 32, dtype=np.uint32)
+    for c in np.nonzero(mask_bits)[0]:
+        words[c >> 5] |= np.uint32(1 << (int(c) & 31))
+    return L.mcmc_cdf_walk(_lib.u32ptr(words), ncol, cv, eps, p, u)
+
+
+def canon(x):
+    """generate_canonical<float,24> of a minstd draw."""
+    u = np.float32(np.float32(x - 1) / np.float32(2147483648.0))
+    return u if u < 1 else np.float32(np.nextafter(np.float32(1), np.float32(0)))
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_cdf_walk_matches_stepwise_float32(case):
+    rng = np.random.default_rng(100 + case)
+    eps = [1e-8, 1e-8, 1e-3, 3e-5, 2.0 ** -30 * 77, 1e-8][case]
+    mism = []
+    for it in range(40):
+        ncol = int(rng.integers(2, 1500 if case < 5 else 4000))
+        dens = rng.random() ** 3
+        bits = rng.random(ncol) < dens
+        pop = int(bits.sum())
+        if it % 4 == 0:
+            u = np.float32(1.0) - np.float32(int(rng.integers(0, 4096))) * np.float32(2.0 ** -24)
+        elif it % 4 == 1:
+            u = np.float32(int(rng.integers(0, 100000)) * 1e-12)
+        else:
+            u = canon(int(rng.integers(1, 2**31 - 1)))
+        u = np.float32(min(u, np.float32(np.nextafter(np.float32(1), np.float32(0)))))
+        if 0 < pop < ncol:
+            pf = np.float32((np.float32(1.0) - np.float32(eps) * np.float32(pop)) / np.float32(ncol - pop))
+            a, b = lib_walk(bits, ncol, 0, eps, pf, u), naive_walk(bits, ncol, eps, pf, u)
+            if a != b:
+                mism.append(("mask", ncol, pop, float(u), a, b))
+        cv = int(rng.integers(0, ncol))
+        hi = np.float32(np.float32(1.0) - np.float32(ncol - 1) * np.float32(eps))
+        own = np.zeros(ncol, dtype=bool)
+        own[:] = True
+        own[cv] = False   # naive_walk: eps where the bit is set, p (= hi) where clear
+        a, b = lib_walk(None, ncol, cv, eps, hi, u), naive_walk(own, ncol, eps, hi, u)
+        if a != b:
+            mism.append(("own", ncol, cv, float(u), a, b))
+    assert not mism, mism[:5]
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU parity
+
+
+@pytest.fixture(scope="module")
+def M(hip_lib):
+    import mcmc_colorer_amd.colorer as M
+
+    return M
+
+
+def run_both(M, off, idx, ncol, seed=1, **kw):
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, epsilon=kw.get("epsilon", 1e-8), maxRip=kw.get("maxRip", 250),
+                                  tabooIteration=kw.get("tabooIteration", 0), tailcut=kw.get("tailcut", False))
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, seed, M.GlibcRand(1)), params)
+    st = col.run(0)
+    O.srand(1)   # both glibc streams at srand(1), no draws
+    r = O.mcmc_run(off, idx, ncol, seed, **kw)
+    assert col.info()["variant"] == "wide"
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws, st.initDraws) == (
+        r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws, r.res.initDraws)
+    return st, r
+
+
+@pytest.mark.gpu
+def test_wide_default_ncol_maxdeg_dense():
+    """nCol = maxDeg > 256 by default (main.cu:162) on an exact --simulate graph."""
+    import mcmc_colorer_amd.colorer as M
+
+    O.srand(1)
+    off, idx = O.setup_rnd2(1200, 0.3)
+    ncol = O.max_deg(off)
+    assert ncol > 256
+    run_both(M, off, idx, ncol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncol,eps,taboo,tailcut", [(300, 1e-8, 0, False), (1000, 1e-8, 2, False),
+                                                     (700, 1e-3, 0, False), (4000, 1e-8, 0, True),
+                                                     (65535, 1e-8, 0, False)])
+def test_wide_sparse(M, ncol, eps, taboo, tailcut):
+    O.srand(1)
+    off, idx = O.setup_rnd2(3000, 0.01)
+    run_both(M, off, idx, ncol, epsilon=eps, tabooIteration=taboo, tailcut=tailcut)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncol,eps,taboo", [(16, 1e-8, 0), (16, 1e-3, 0), (7, 1e-8, 3), (256, 1e-2, 0)])
+def test_wide_forced_small_ncol(M, monkeypatch, ncol, eps, taboo):
+    """MCMC_GATHER=wide on nCol <= 256: every vertex violates (C2-like), events, taboo."""
+    monkeypatch.setenv("MCMC_GATHER", "wide")
+    O.srand(1)
+    off, idx = O.setup_rnd2(2000, 0.05)
+    run_both(M, off, idx, ncol, epsilon=eps, tabooIteration=taboo, maxRip=60)
+
+
+@pytest.mark.gpu
+def test_wide_skewed_degrees(M):
+    """A hub joined to every vertex plus a sparse remainder: one long row, many empty/short ones."""
+    rng = np.random.default_rng(5)
+    n = 5000
+    E = set()
+    for v in range(1, n):
+        E.add((0, v))
+    for _ in range(8000):
+        a, b = rng.integers(1, n, 2)
+        if a != b:
+            E.add((min(a, b), max(a, b)))
+    for v in range(4000, n):   # isolated tail: drop the hub arcs too
+        E.discard((0, v))
+    arcs = sorted([(a, b) for a, b in E] + [(b, a) for a, b in E])
+    src = np.array([a for a, _ in arcs], dtype=np.int64)
+    idx = np.array([b for _, b in arcs], dtype=np.uint32)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.add.at(off, src + 1, 1)
+    off = np.cumsum(off).astype(np.uint64)
+    ncol = O.max_deg(off)
+    run_both(M, off, idx, ncol)
+    run_both(M, off, idx, 300, maxRip=30)
