@@ -1936,6 +1936,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->lds = (size_t)(1u << c->block_log2) + (size_t)c->chunk_rows * c->nw * 4u;
         ea = wi == 0 ? allow_lds_blocked<1>(c->lds) : wi == 1 ? allow_lds_blocked<2>(c->lds)
            : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
+    } else if (c->variant == 4) {
+        c->sweep = launch_wide;   // geometry and tables below
     } else if (c->variant == 3) {
         const char* bl = getenv("MCMC_BLOCK_LOG2");
         c->block_log2 = (bl && gd.row_off) ? (uint32_t)std::max(4, std::min(16, atoi(bl))) : 16u;
