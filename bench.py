@@ -9,6 +9,11 @@ is configs[3]: the same graph vertex-partitioned over N GPUs (strong scaling), e
 only its own rows, one RCCL all-gather per sweep (mcmc_colorer_amd/distributed.py).
 `--config c2`: configs[1], `--simulate 0.01 -n 100000 --nCol 16` with the reference's exact setupRnd2
 graph (weak scaling at N > 1: N*1e5 rows, p 0.01/N).
+`--config c5`: configs[4] (power-law, nCol = maxDeg). SNAP LiveJournal / Reddit are not available, so
+the graph is the build's R-MAT stand-in of LiveJournal's size and skew (csrc/er_gen.h rmat_edge: scale
+22 = 4.19M vertices, edge factor 10, (a,b,c) = (0.5,0.2,0.2), seed 1; about 82M arcs, maxDeg about 26K),
+one GPU, the wide sweep (uint16 colours). The run converges, so the line also carries the full
+--mcmcgpu run from the initial colouring: sweeps-to-zero-conflict and its wall time.
 `--semantics ref` (one GPU): the same sweep with the reference GPU colorer's own semantics
 (--mcmcgpu-ref: balance-dynamic proposal, per-vertex cuRAND XORWOW, conflicts counted as edges);
 its CPU leg times the oracle's restatement of those semantics.
@@ -46,7 +51,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 KERNELS = {"lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
-           "tiled": "sweep_tiled_kernel"}
+           "tiled": "sweep_tiled_kernel", "wide": "wide_scan+wide_eval+wide_walk+commit (one sweep)"}
 
 
 def load_traffic(key: str):
@@ -132,7 +137,7 @@ def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: floa
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["c2", "c3"], default="c3",
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3",
                     help="c2: configs[1] (--simulate 0.01 -n 1e5, 16 colours; weak scaling at N > 1); "
                          "c3: configs[2]/[3] (n 1e7, p 0.001, 32 colours, the build's G(n,p) generator; "
                          "N > 1 partitions the same graph: strong scaling)")
@@ -186,6 +191,10 @@ def main() -> int:
     n_req, p_req = a.vertices, a.prob
     if a.config == "c3":
         n_req, p_req, a.ncol, a.scaling = 10_000_000, 0.001, 32, "strong"
+    elif a.config == "c5":
+        if world > 1:
+            raise SystemExit("--config c5 runs on one GPU (the wide sweep has no partitioned driver yet)")
+        n_req, p_req = 1 << 22, 0.0
     elif world > 1 and a.scaling == "weak":
         n_req, p_req = a.vertices * world, a.prob / world
     t_gen = time.perf_counter()
@@ -195,6 +204,9 @@ def main() -> int:
         # written straight into the tiled layout; under torchrun each rank generates only its rows
         g = M.Graph.er_fast(n_req, p_req, 1, device=dev, world=world if dist is not None else 1,
                             rank=rank if dist is not None else 0)
+    elif a.config == "c5":
+        g = M.Graph.rmat(22, 10, 0.5, 0.2, 0.2, 1, device=dev)
+        a.ncol = g.getMaxNodeDeg()   # main.cu:162 default: maxDeg * numColRatio (1)
     else:
         g = M.Graph.simulate(n_req, p_req, rng, device=dev)
     t_gen = time.perf_counter() - t_gen
@@ -210,6 +222,18 @@ def main() -> int:
             dist.barrier()
 
     ref = a.semantics == "ref"
+    conv = None
+    if a.config == "c5" and dist is None:
+        # the reference loop itself (run(), coloringMCMC_CPU.cpp:115-270): until Cviol == 0 or the cap
+        cr = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=a.ncol))
+        t0 = time.perf_counter()
+        st = cr.run(0)
+        cw = time.perf_counter() - t0
+        conv = {"sweeps_to_zero_conflict": int(st.iter) if st.finalViol == 0 else None,
+                "converged": bool(st.finalViol == 0), "final_Cviol": int(st.finalViol),
+                "loop_ms": st.loopMs, "wall_s": round(cw, 4), "glibc_draws": int(st.glibcDraws),
+                "trajectory": [int(x) for x in cr.trajectory()[:64]]}
+        cr.close()
     if ref and dist is not None:
         raise SystemExit("--semantics ref runs on one GPU")
     if dist is None:
@@ -273,6 +297,13 @@ def main() -> int:
     key = f"{a.config}/{variant}" if (world == 1 and (a.config == "c3" or n_req == 100000)) else None
     if key and ref:
         key += "-ref"
+    data = {"c2": "synthetic (reference --simulate generator replayed exactly on the GPU)",
+            "c3": "synthetic G(n,p) (the build's counter-based generator, er_gen.h, seed 1; setupRnd2 infeasible at n=1e7)",
+            "c5": "synthetic R-MAT power-law stand-in for SNAP LiveJournal (er_gen.h rmat_edge, scale 22, edge factor "
+                  "10, a/b/c 0.5/0.2/0.2, seed 1; the SNAP graphs are not available)"}[a.config]
+    workload = (f"--mcmcgpu{'-ref' if ref else ''} --simulate {p_req:g} -n {n_req} --nCol {a.ncol} --seed {a.seed}"
+                if a.config != "c5" else
+                f"--mcmcgpu --graph <R-MAT scale 22 ef 10, LiveJournal stand-in> (nCol = maxDeg = {a.ncol}) --seed {a.seed}")
     out = {
         "metric": "vertex-updates/sec per MCMC sweep",
         "value": value,
@@ -285,10 +316,8 @@ def main() -> int:
         "scaling": "strong" if a.config == "c3" else ("weak" if (world == 1 or a.scaling == "weak") else "strong"),
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": ("synthetic (reference --simulate generator replayed exactly on the GPU)" if a.config == "c2" else
-                 "synthetic G(n,p) (the build's counter-based generator, er_gen.h, seed 1; setupRnd2 infeasible at n=1e7)"),
-        "config": {"workload": f"--mcmcgpu{'-ref' if ref else ''} --simulate {p_req:g} -n {n_req} "
-                               f"--nCol {a.ncol} --seed {a.seed}",
+        "data": data,
+        "config": {"workload": workload,
                    "config": a.config,
                    "semantics": "reference GPU colorer (--mcmcgpu-ref)" if ref else "--mcmccpu (north star)",
                    "n": n, "arcs": m, "nCol": a.ncol,
@@ -303,9 +332,22 @@ def main() -> int:
                      "layout": info},
         "cpu_baseline": None,
     }
+    if conv is not None:
+        out["convergence"] = conv
     # CPU and refstruct legs: on the benchmarked graph for c2; for c3 (no CSR can exist: 400 GB) on
     # --simulate 0.1 -n 100000, which has C3's mean degree 1e4 (per-vertex work is per-degree)
     sample, sample_n, sample_window, sample_note = g, n, None, None
+    cpu_ncol = a.ncol
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.config == "c5":
+        # the oracle's fill_p / extract_new_color are O(nCol) per vertex (26K colours here): one sweep
+        # of the full graph takes minutes, so the CPU leg runs on the same generator at scale 18
+        cs = M.Graph.rmat(18, 10, 0.5, 0.2, 0.2, 1, device=dev)
+        s = cs.getStruct()
+        cpu_ncol = cs.getMaxNodeDeg()
+        out["cpu_baseline"] = cpu_baseline(s.cumulDegs, s.neighs, cpu_ncol, a.seed, M.GlibcRand(1).window, cs.nNodes)
+        out["cpu_baseline"]["sample"] += (f"; graph R-MAT scale 18 (same generator and seed, n = {cs.nNodes}, "
+                                          f"nCol = maxDeg = {cpu_ncol}; the oracle is O(nCol) per vertex)")
+        cs.close()
     if rank == 0 and world == 1 and not (a.no_refstruct and a.no_cpu_baseline):
         if a.config == "c3":
             g.close()
@@ -319,7 +361,7 @@ def main() -> int:
         out["refstruct"] = refstruct_baseline(sample, a.ncol, a.refstruct_sweeps, a.seed, sample_n, value)
         if sample_note:
             out["refstruct"]["graph"] = sample_note
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.config != "c5":
         s = sample.getStruct()
         if ref:
             out["cpu_baseline"] = cpu_baseline_ref(s.cumulDegs, s.neighs, a.ncol, a.seed, sample_n)

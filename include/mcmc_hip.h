@@ -99,6 +99,13 @@ int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device,
 int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out);
 int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t world, uint32_t rank, int device,
                             mcmc_graph** out);
+/* R-MAT power-law graph (configs[4] stand-in: SNAP LiveJournal / Reddit are not available; SURVEY.md
+ * §8d C5), generated on the device as a CSR with ascending neighbour lists: 2^scale vertices,
+ * edge_factor * 2^scale Philox-driven quadrant draws with probabilities (a, b, c, 1-a-b-c), ids
+ * scrambled by a fixed bijection, self-loops dropped, both arcs kept, duplicates merged. Fully
+ * defined in mcmc_colorer_amd/csrc/er_gen.h (rmat_edge). Not a reference graph. */
+int mcmc_graph_rmat(uint32_t scale, uint32_t edge_factor, double a, double b, double c, uint64_t seed, int device,
+                    mcmc_graph** out);
 int mcmc_graph_info(const mcmc_graph* g, uint32_t* n, uint64_t* m, uint32_t* maxDeg, uint32_t* minDeg);
 /* Device pointers (row_off: uint64[n+1], col_idx: uint32[m]) for zero-copy callers. */
 int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const uint32_t** col_idx);

@@ -116,6 +116,19 @@ class Graph:
         return g
 
     @classmethod
+    def rmat(cls, scale: int, edge_factor: int, a: float = 0.5, b: float = 0.2, c: float = 0.2, seed: int = 1,
+             device: int = 0) -> "Graph":
+        """R-MAT power-law stand-in for configs[4] (csrc/er_gen.h rmat_edge; SURVEY.md §8d C5: the SNAP
+        graphs are not available), generated on the GPU as a CSR with ascending neighbour lists."""
+        h = ctypes.c_void_p()
+        check(lib().mcmc_graph_rmat(scale, edge_factor, a, b, c, seed, device, ctypes.byref(h)))
+        n = 1 << scale
+        g = cls(h, device=device)
+        if n > 0:
+            g.prob = g.nEdges / float(np.float32(n) * np.float32(n))
+        return g
+
+    @classmethod
     def from_csr(cls, row_off: np.ndarray, col_idx: np.ndarray, device: int = 0, prob: float = 0.0) -> "Graph":
         """Graph(Graph* host) device copy (graphGPU.cu:210-226) of a host CSR."""
         row_off = np.ascontiguousarray(row_off, dtype=np.uint64)

@@ -121,4 +121,47 @@ ER_HD uint32_t walk_stream(uint64_t seed, double inv_l1p, int p_mode, uint32_t n
     }
 }
 
+// ---- R-MAT (Kronecker) stand-in for configs[4] ------------------------------
+// SNAP LiveJournal / Reddit are not available here, so C5 runs on a synthetic power-law graph of
+// similar size and skew. Definition (mcmc_graph_rmat):
+//   n = 2^scale vertices, E = edge_factor * n edge draws e = 0 .. E-1. Draw e picks one quadrant
+//   per level l = 0 .. scale-1, most significant bit first, from x = word (l % 4) of
+//   Philox4x32-10(counter {e_lo, e_hi, l / 4, 0x524D4154}, key {seed_lo, seed_hi}):
+//   x < tA -> (0,0), x < tAB -> (0,1), x < tABC -> (1,0), else (1,1), with the uint32 thresholds
+//   tA = floor(a 2^32), tAB = floor((a+b) 2^32), tABC = floor((a+b+c) 2^32) (double, clamped).
+//   Both endpoints go through rmat_scramble (a fixed bijection of [0, 2^scale), so the hubs are
+//   not the low ids). Self-loops are dropped, both arcs of every other draw kept, duplicates
+//   merged; neighbour lists ascending.
+constexpr uint32_t kRmatTag = 0x524D4154u;
+
+struct RmatConst {
+    uint32_t scale, mask, tA, tAB, tABC, k0, k1;
+};
+
+ER_HD uint32_t rmat_scramble(uint32_t x, const RmatConst& k) {
+    const uint32_t h = (k.scale + 1u) / 2u;
+    x = (x * 0x9E3779B1u) & k.mask;   // odd multiplier: a bijection mod 2^scale
+    x ^= x >> h;
+    x = (x * 0x85EBCA6Bu) & k.mask;
+    x ^= x >> h;
+    return (x ^ (k.k0 * 0xC2B2AE35u)) & k.mask;
+}
+
+ER_HD void rmat_edge(uint64_t e, const RmatConst& k, uint32_t& i, uint32_t& j) {
+    i = 0;
+    j = 0;
+    for (uint32_t l = 0; l < k.scale; l += 4) {
+        const Philox4 r = philox4x32_10((uint32_t)e, (uint32_t)(e >> 32), l >> 2, kRmatTag, k.k0, k.k1);
+        for (uint32_t q = 0; q < 4 && l + q < k.scale; q++) {
+            const uint32_t x = r.v[q];
+            const uint32_t ib = x >= k.tAB ? 1u : 0u;
+            const uint32_t jb = ((x >= k.tA && x < k.tAB) || x >= k.tABC) ? 1u : 0u;
+            i = (i << 1) | ib;
+            j = (j << 1) | jb;
+        }
+    }
+    i = rmat_scramble(i, k);
+    j = rmat_scramble(j, k);
+}
+
 }  // namespace er

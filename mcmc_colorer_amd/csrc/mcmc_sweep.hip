@@ -73,6 +73,7 @@ struct SweepArgs {
     uint8_t* colors1;
     uint32_t* taboo;            // local rows, nullptr when tabooIteration == 0
     uint32_t* events;           // overflow event list (global vertex ids)
+    uint32_t* evdraw;           // the events' rand() draws (commit scratch, ev_cap entries)
     DevState* st;
     unsigned long long* traj;   // per-sweep Cviol, traj_cap entries
     uint32_t traj_cap;
@@ -123,6 +124,8 @@ struct SweepArgs {
     uint8_t* wflag;             // [nloc] viol flags of the running sweep (cleared by the evaluation)
     uint32_t* wlist;            // [nloc] violating, untaboo'd vertices (global ids)
     uint32_t* wcount;           // their number
+    int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
+    const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
 };
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
 
@@ -239,21 +242,34 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         }
         __syncthreads();
         bitonic_sort_block(s, P);
+        // The events' rand() draws in ascending vertex order: one thread steps the TYPE_3
+        // recurrence with the window in registers -- rounds of 31 unrolled steps, so the ring
+        // indices are static -- into a.evdraw; then every thread applies its share.
         if (threadIdx.x == 0) {
-            uint32_t ring[31];
-            for (int i = 0; i < 31; i++) ring[i] = st->glibc_ring[i];
-            uint32_t head = st->glibc_head;
-            for (uint32_t i = 0; i < E; i++) {
-                const uint32_t v = s[i];
-                const uint32_t r = glibc_next(ring, head);
-                const uint32_t c = r % (a.nCol - 1u);   // rand() % (nCol - 1), :518
-                Cs[caddr(a, v)] = (CT)c;
-                if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
-                    a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
+            uint32_t r[31];
+            const uint32_t h0 = st->glibc_head;
+            for (int i = 0; i < 31; i++) r[i] = st->glibc_ring[(h0 + i) % 31u];
+            for (uint32_t b = 0; b < E; b += 31) {
+#pragma unroll
+                for (int j = 0; j < 31; j++) {
+                    if (b + j < E) {
+                        r[j] += r[(j + 28) % 31];
+                        a.evdraw[b + j] = r[j] >> 1;
+                    }
+                }
             }
-            for (int i = 0; i < 31; i++) st->glibc_ring[i] = ring[i];
-            st->glibc_head = head;
+            for (int i = 0; i < 31; i++) st->glibc_ring[i] = r[i];
+            st->glibc_head = E % 31u;
         }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
+            const uint32_t v = s[i];
+            const uint32_t c = a.evdraw[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+            Cs[caddr(a, v)] = (CT)c;
+            if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
+                a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
+        }
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
         st->glibc_draws += E;
@@ -275,7 +291,7 @@ __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long lon
     DevState* st = a.st;
     if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
     const bool stop_cap = t == a.maxRip + 1;     // iter > maxiter after sweep maxRip
-    const bool stop_conv = viol <= a.z;          // while (Cviol > z)
+    const bool stop_conv = !a.bench && viol <= a.z;   // while (Cviol > z)
     if (stop_cap || stop_conv) {
         if (threadIdx.x == 0) {
             st->done = 1;
@@ -1501,6 +1517,7 @@ struct mcmc_ctx {
     uint8_t* colors[2] = {nullptr, nullptr};
     uint32_t* taboo = nullptr;
     uint32_t* events = nullptr;
+    uint32_t* evdraw = nullptr;
     uint32_t ev_cap = 0;
     DevState* st = nullptr;
     unsigned long long* traj = nullptr;
@@ -1560,6 +1577,7 @@ struct mcmc_ctx {
     uint8_t* wflag = nullptr;
     uint32_t* wlist = nullptr;
     uint32_t* wcount = nullptr;
+    float* etab = nullptr;
 };
 
 namespace {
@@ -1617,6 +1635,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.colors1 = c->colors[1];
     a.taboo = c->taboo;
     a.events = c->events;
+    a.evdraw = c->evdraw;
     a.st = c->st;
     a.traj = c->traj;
     a.traj_cap = c->traj_cap;
@@ -1675,6 +1694,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.wflag = c->wflag;
         a.wlist = c->wlist;
         a.wcount = c->wcount;
+        a.etab = c->etab;
         a.fused = 0;
     }
     a.phase_ts = c->phase_ts;
@@ -1971,6 +1991,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     uint32_t pcap = 1;
     while (pcap < c->ev_cap) pcap <<= 1;
     chk(hipMalloc(&c->events, sizeof(uint32_t) * pcap));
+    chk(hipMalloc(&c->evdraw, sizeof(uint32_t) * pcap));
     chk(hipMalloc(&c->st, sizeof(DevState)));
     chk(hipMalloc(&c->traj, sizeof(unsigned long long) * c->traj_cap));
     if (getenv("MCMC_PHASE_DUMP")) {
@@ -2087,6 +2108,10 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMalloc(&c->wflag, std::max<size_t>(nloc, 1));
         if (ew == hipSuccess) ew = hipMalloc(&c->wlist, sizeof(uint32_t) * std::max<size_t>(nloc, 1));
         if (ew == hipSuccess) ew = hipMalloc(&c->wcount, sizeof(uint32_t));
+        std::vector<float> et((size_t)p->nCol + 1);
+        eps_table(p->epsilon, p->nCol, et.data());
+        if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
+        if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, std::max<size_t>(nloc, 1), c->stream);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, sizeof(uint32_t), c->stream);
         if (ew == hipSuccess) {
@@ -2449,11 +2474,13 @@ int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
     if (c->bench_exec && c->bench_n == sweeps) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
-    // Throughput mode: the loop body with the stop tests disabled (no cap; z = 0 stops only on a
-    // proper colouring), `sweeps` launches captured into one hipGraph.
+    // Throughput mode: the loop body with the stop tests disabled (no cap, no convergence stop:
+    // a sweep from a proper colouring still resamples every vertex), `sweeps` launches captured
+    // into one hipGraph.
     SweepArgs a = make_args(c, 1);
     a.maxRip = 0xFFFFFFF0u;
     a.traj_cap = 0;
+    a.bench = 1;   // a convergent run (C5) keeps sweeping from its proper colouring
     hipGraph_t graph;
     MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     for (uint32_t i = 0; i < sweeps; i++) launch_pair(c, a);
@@ -2500,7 +2527,11 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
 
 uint32_t mcmc_cdf_walk(const uint32_t* mask, uint32_t nCol, uint32_t cv, float eps, float p, float u) {
     if (nCol == 0) return 0;
-    if (!mask) return walk_own(nCol, cv < nCol ? cv : nCol - 1u, eps, p, u);
+    if (!mask) {
+        std::vector<float> E((size_t)nCol + 1);
+        eps_table(eps, nCol, E.data());
+        return walk_own_tab(E.data(), nCol, cv < nCol ? cv : nCol - 1u, eps, p, u);
+    }
     return walk_mask(mask, nCol, eps, p, u);
 }
 
@@ -2560,6 +2591,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->own_colors[1]);
     (void)hipFree(c->taboo);
     (void)hipFree(c->events);
+    (void)hipFree(c->evdraw);
     (void)hipFree(c->st);
     (void)hipFree(c->traj);
     (void)hipFree(c->wave_start);
@@ -2576,6 +2608,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wflag);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
+    (void)hipFree(c->etab);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

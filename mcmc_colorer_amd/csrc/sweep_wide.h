@@ -79,13 +79,17 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     const uint32_t nloc = a.v_end - a.v_begin;
     const int lane = threadIdx.x & 63;
     uint32_t cviol = 0;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += gridDim.x * blockDim.x) {
+    // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139); the
+    // grid-stride loop advances every lane's draw by 16807^stride, one mulmod per vertex
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t a_stride = minstd_pow_tab(stride);
+    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + blockIdx.x * blockDim.x +
+                                                                 (threadIdx.x & ~63u) + 1)),
+                               kMinstdLanePow[lane]);
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += stride, x = minstd_mulmod(x, a_stride)) {
         const uint32_t l = base + threadIdx.x;
         const bool valid = l < nloc;
         const uint32_t v = a.v_begin + l;
-        // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
-        const uint32_t w0 = a.v_begin + base + (threadIdx.x & ~63u);
-        const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)w0 + 1)), kMinstdLanePow[lane]);
         const float u = minstd_canonical(x);
         uint32_t viol = 0, cv = 0, tab = 0;
         if (valid) {
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
             } else if (viol) {
                 walk = true;   // case (i) or (ii): needs the occupancy set
             } else {           // case (iii)
-                const uint32_t nc = walk_own(a.nCol, cv, a.eps, a.hi, u);
+                const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
                 event = nc == a.nCol;
                 Cs[v] = (uint16_t)(event ? cv : nc);   // an event's colour is the commit's replay
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(kWideWalkThreads) void wide_walk_kernel(SweepArgs a
                 const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
                 nc = walk_mask(mask, a.nCol, a.eps, pf, u);
             } else {            // case (i)
-                nc = walk_own(a.nCol, cv, a.eps, a.hi, u);
+                nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
             }
             const bool event = nc == a.nCol;
             Cs[v] = (uint16_t)(event ? cv : nc);

@@ -248,3 +248,56 @@ def er_fast(n: int, prob: float, seed: int):
         active[idx[~alive]] = False
         k += 1
     return np.concatenate(out) if out else np.zeros((0, 2), dtype=np.int64)
+
+
+# ---- R-MAT stand-in for configs[4] (mcmc_colorer_amd/csrc/er_gen.h rmat_edge), vectorised ----------
+# TEST INFRASTRUCTURE: an independent restatement pinning mcmc_graph_rmat on small graphs.
+_RMAT_TAG = 0x524D4154
+
+
+def _rmat_threshold(x: float) -> int:
+    import math
+
+    return int(min(4294967295.0, math.floor(max(0.0, x) * 4294967296.0)))
+
+
+def _rmat_scramble(x, scale: int, k0: int):
+    M = np.uint64((1 << scale) - 1)
+    h = np.uint64((scale + 1) // 2)
+    x = np.asarray(x, dtype=np.uint64)
+    x = (x * np.uint64(0x9E3779B1)) & _M32 & M
+    x = x ^ (x >> h)
+    x = (x * np.uint64(0x85EBCA6B)) & _M32 & M
+    x = x ^ (x >> h)
+    return (x ^ np.uint64((k0 * 0xC2B2AE35) & 0xFFFFFFFF)) & M
+
+
+def rmat(scale: int, edge_factor: int, a: float, b: float, c: float, seed: int):
+    """CSR (row_off uint64, col_idx uint32) of mcmc_graph_rmat(scale, edge_factor, a, b, c, seed)."""
+    n = 1 << scale
+    E = edge_factor * n
+    tA, tAB, tABC = _rmat_threshold(a), _rmat_threshold(a + b), _rmat_threshold(a + b + c)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    e = np.arange(E, dtype=np.uint64)
+    i = np.zeros(E, dtype=np.uint64)
+    j = np.zeros(E, dtype=np.uint64)
+    for l0 in range(0, scale, 4):
+        r = _philox4x32_10(e & _M32, e >> np.uint64(32), np.full(E, l0 >> 2, dtype=np.uint64),
+                           np.full(E, _RMAT_TAG, dtype=np.uint64), k0, k1)
+        for q in range(4):
+            if l0 + q >= scale:
+                break
+            x = r[q]
+            ib = (x >= np.uint64(tAB)).astype(np.uint64)
+            jb = (((x >= np.uint64(tA)) & (x < np.uint64(tAB))) | (x >= np.uint64(tABC))).astype(np.uint64)
+            i = (i << np.uint64(1)) | ib
+            j = (j << np.uint64(1)) | jb
+    i = _rmat_scramble(i, scale, k0)
+    j = _rmat_scramble(j, scale, k0)
+    keep = i != j
+    i, j = i[keep], j[keep]
+    keys = np.unique(np.concatenate([(i << np.uint64(32)) | j, (j << np.uint64(32)) | i]))
+    rows = (keys >> np.uint64(32)).astype(np.int64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.add.at(off, rows + 1, 1)
+    return np.cumsum(off).astype(np.uint64), (keys & _M32).astype(np.uint32)
