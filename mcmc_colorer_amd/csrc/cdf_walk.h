@@ -164,11 +164,95 @@ MCMC_HD uint32_t walk_mask(const MaskT* mask, uint32_t nCol, float eps, float pf
     return nCol;
 }
 
+// First of 64 candidates (0..63) whose predicate holds, -1 if none. On the device every lane of
+// the wave evaluates its own candidate and a ballot picks the first (all 64 lanes must be active
+// and call it together); the host build loops.
+template <typename Pred>
+MCMC_HD int first_of_64(Pred pred) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const unsigned long long b = __ballot(pred((int)__lane_id()));
+    return b ? __ffsll(b) - 1 : -1;
+#else
+    for (int l = 0; l < 64; l++)
+        if (pred(l)) return l;
+    return -1;
+#endif
+}
+
+// walk_mask with word prefix counts pre[w] = occupied colours in words < w (NWW + 1 entries),
+// for a whole wave. Inside a binade with non-tying increments dE, dP the mantissa integer after
+// colour x is k0 + occ(c..x) dE + free(c..x) dP: monotone, so the first colour whose sum passes
+// T (u's mantissa when u is in this binade, else the binade's top) is found by testing 64 word
+// ends at once, then the 32 colours of the hit word at once. At T = u that colour is the stop;
+// at the binade's top it takes one explicit fp32 step (the rounding changes there) and the walk
+// continues in the next binade. Binades whose increments tie (or cdf = 0) step one colour at a
+// time. Cost: O(binades + nCol / 2048) wave steps instead of O(nCol / 32) serial ones.
+MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32_t nCol, float eps, float pf,
+                               float u) {
+    if (!pos_normal(eps) || !pos_normal(pf)) return walk_mask(mask, nCol, eps, pf, u);
+    const uint32_t NWW = (nCol + 31u) >> 5;
+    const uint32_t bu = f32_bits(u);
+    float cdf = 0.0f;
+    uint32_t c = 0;
+    while (c < nCol) {
+        const uint32_t bc = f32_bits(cdf);
+        const uint32_t E = bc >> 23;
+        uint32_t dE = 0, dP = 0;
+        if (E == 0u || !binade_inc(eps, E, dE) || !binade_inc(pf, E, dP)) {   // one exact step
+            cdf += ((mask[c >> 5] >> (c & 31u)) & 1u) ? eps : pf;
+            if (cdf > u) return c;
+            c++;
+            continue;
+        }
+        if (dE == 0u && dP == 0u) return nCol;   // every further sum rounds back to cdf (<= u)
+        const uint64_t k0 = (bc & 0x7FFFFFu) | 0x800000u;
+        const uint64_t T = ((bu >> 23) == E) ? (uint64_t)((bu & 0x7FFFFFu) | 0x800000u) : 0xFFFFFFull;
+        const uint32_t w0 = c >> 5;
+        const uint32_t occ0 = pre[w0] + (uint32_t)__builtin_popcount(mask[w0] & ((1u << (c & 31u)) - 1u));
+        // the mantissa integer after the last colour of word w >= w0 (colours [c, min(32(w+1), nCol)))
+        auto kend = [&](uint32_t w) -> uint64_t {
+            const uint32_t x = 32u * (w + 1u) < nCol ? 32u * (w + 1u) : nCol;
+            const uint32_t occ = pre[w + 1u] - occ0;
+            return k0 + (uint64_t)occ * dE + (uint64_t)(x - c - occ) * dP;
+        };
+        uint32_t wf = NWW;   // the word holding the first colour whose sum passes T
+        for (uint32_t wb = w0; wb < NWW; wb += 64u) {
+            const int f = first_of_64([&](int l) {
+                const uint32_t w = wb + (uint32_t)l;
+                return w < NWW && kend(w) > T;
+            });
+            if (f >= 0) {
+                wf = wb + (uint32_t)f;
+                break;
+            }
+        }
+        if (wf == NWW) return nCol;   // the rest of the walk stays in the binade at or below u
+        const uint32_t b0 = wf == w0 ? (c & 31u) : 0u;
+        const uint64_t ks = wf == w0 ? k0 : kend(wf - 1u);   // before colour 32 wf + b0
+        const uint32_t word = mask[wf] >> b0;
+        const uint32_t nb = (nCol - 32u * wf < 32u ? nCol - 32u * wf : 32u) - b0;
+        auto kat = [&](uint32_t i) -> uint64_t {   // after the first i colours from b0
+            const uint32_t occ = (uint32_t)__builtin_popcount(i >= 32u ? word : word & ((1u << i) - 1u));
+            return ks + (uint64_t)occ * dE + (uint64_t)(i - occ) * dP;
+        };
+        const int fb = first_of_64([&](int l) { return (uint32_t)l < nb && kat((uint32_t)l + 1u) > T; });
+        const uint32_t i = (uint32_t)fb;   // kend(wf) > T, so fb >= 0
+        const uint32_t y = 32u * wf + b0 + i;
+        if (T < 0xFFFFFFu) return y;   // u is in this binade: the sum passes it at y (in or above the binade)
+        const uint64_t kb = kat(i);     // the sum leaves the binade at y: one exact fp32 step
+        cdf = f32_from((E << 23) | ((uint32_t)kb & 0x7FFFFFu));
+        cdf += ((word >> i) & 1u) ? eps : pf;
+        if (cdf > u) return y;
+        c = y + 1u;
+    }
+    return nCol;
+}
+
 // walk_own with the table E[k] = fl(...fl(eps + eps)... + eps) (k terms, E[0] = 0): the cdf before
 // colour cv is E[cv], so a stop before cv is a binary search and the rest is two steps.
-MCMC_HD uint32_t walk_own_tab(const float* E, uint32_t nCol, uint32_t cv, float eps, float hi, float u) {
+// ecv = E[cv], loaded by the caller (the evaluation issues it with its other loads).
+MCMC_HD uint32_t walk_own_tab_e(const float* E, float ecv, uint32_t nCol, uint32_t cv, float eps, float hi, float u) {
     if (!(eps > 0.0f)) return walk_own(nCol, cv, eps, hi, u);   // E is monotone only for eps > 0
-    const float ecv = E[cv];
     if (ecv > u) {   // the first k in [1, cv] with E[k] > u stops at colour k - 1
         uint32_t lo = 1, up = cv;
         while (lo < up) {
@@ -181,6 +265,10 @@ MCMC_HD uint32_t walk_own_tab(const float* E, uint32_t nCol, uint32_t cv, float 
     if (cdf > u) return cv;
     const uint32_t s = cdf_run(cdf, eps, nCol - cv - 1u, u);
     return s ? cv + s : nCol;
+}
+
+MCMC_HD uint32_t walk_own_tab(const float* E, uint32_t nCol, uint32_t cv, float eps, float hi, float u) {
+    return walk_own_tab_e(E, eps > 0.0f ? E[cv] : 0.0f, nCol, cv, eps, hi, u);
 }
 
 // The table of walk_own_tab, host side (nCol + 1 entries).

@@ -97,9 +97,36 @@ int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint3
                 const uint32_t* colorIdx, uint32_t nCol, hipStream_t s, bool ref, unsigned long long limit);
 }  // namespace mcmc
 
+namespace mcmc {
+constexpr uint32_t kXSlabs = 8;   // L2 mode: column slabs of the wide sweep's edge layout, one per XCD
+// Slab edge layout of a row range for the wide sweep (sweep_wide.h, get_xslab): slab s holds the
+// kept arcs whose column lies in [s S, (s+1) S), row-sorted, as 256-entry chunks of 32-bit entries
+// (row delta from the chunk's base row << cbits | slab-local column), padded with 0xFFFFFFFF.
+//   mode 0 (L2): 8 slabs, one per XCD, colours gathered through that XCD's L2;
+//   mode 1 (LDS): slabs of 2^17 vertices whose colour fingerprints a workgroup stages in LDS, each
+//                 slab's chunks cut into pieces, pieces assigned to workgroups on the host.
+struct XSlabLayout {
+    uint32_t v_begin = 0, v_end = 0;
+    uint32_t mode = 0;
+    uint32_t S = 0, cbits = 0;
+    uint32_t sym = 0;                  // 1: one entry per local edge (symmetric CSR); 0: every arc
+    uint32_t nslabs = 0, chunks = 0;
+    std::vector<uint32_t> chunk0_h;    // first chunk of every slab (nslabs + 1)
+    uint64_t entries = 0;              // kept arcs (unpadded)
+    uint32_t* ent = nullptr;           // [chunks * 256]; nullptr: the layout does not apply
+    uint32_t* base = nullptr;          // [chunks]
+    uint32_t* chunk0 = nullptr;        // device copy of chunk0_h
+    uint32_t nwg = 0, npieces = 0;     // LDS mode: workgroups, pieces
+    uint32_t* pieces = nullptr;        // [npieces][3] {slab, first chunk, end chunk}, grouped by workgroup
+    uint32_t* wg_piece = nullptr;      // [nwg + 1] first piece of every workgroup
+    ~XSlabLayout();
+};
+}  // namespace mcmc
+
 struct mcmc_graph {
     mcmc::GraphDev g;
     std::vector<std::unique_ptr<mcmc::TiledLayout>> tiles;   // freed with the graph
+    std::vector<std::unique_ptr<mcmc::XSlabLayout>> xslabs;
 };
 
 // Per-vertex cuRAND XORWOW states of the reference-GPU-semantics mode (refmode.hip).

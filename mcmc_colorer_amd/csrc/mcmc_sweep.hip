@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -85,6 +86,7 @@ struct SweepArgs {
                                 // [wave_start[w], wave_start[w+1])
     uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
     float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
+    float emax;                 // wide: E[nCol - 1], the largest eps prefix (walk_own_tab_e fast path)
     int check_done;             // device-resident loop: exit immediately once done
     int fused;                  // last-arriving workgroup: 1 = runs the commit (single-context loop),
                                 //                          2 = packs this rank's footer (partitioned)
@@ -122,10 +124,22 @@ struct SweepArgs {
     const uint32_t* chunk_row;  // [nchunks + 1] first local row of every 256-arc chunk
     uint32_t nchunks;
     uint8_t* wflag;             // [nloc] viol flags of the running sweep (cleared by the evaluation)
+    uint8_t* wfp;               // wide LDS scan: [n] colour fingerprints (low byte) of C_t
     uint32_t* wlist;            // [nloc] violating, untaboo'd vertices (global ids)
     uint32_t* wcount;           // their number
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
+    // wide: XCD-slab edge layout of the violation scan (sweep_wide.h, get_xslab); xs_ent == nullptr
+    // -> the CSR arc scan
+    const uint32_t* xs_ent;     // [xs_chunk0[8] * 256] entries (row delta << cbits | slab-local column)
+    const uint32_t* xs_base;    // [xs_chunk0[8]] first local row of every chunk
+    const uint32_t* xs_chunk0;  // [nslabs + 1] first chunk of every slab
+    const uint32_t* xs_pieces;  // LDS mode: [npieces][3] {slab, c0, c1} grouped by workgroup
+    const uint32_t* xs_wgp;     // LDS mode: [workgroups + 1] first piece of every workgroup
+    uint32_t xs_mode;           // 0: L2 slabs (wide_xscan_kernel), 1: LDS tiles (wide_tscan_kernel)
+    uint32_t xs_S, xs_cbits;    // slab width (vertices), bits of the slab-local column
+    uint32_t xs_nwg;            // LDS mode: workgroups of the scan launch
+    uint32_t xs_sym;            // 1: one entry per local edge, flags both ends; 0: every arc, flags its row
 };
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
 
@@ -205,6 +219,7 @@ __device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
 // Commit: loop control + ordered glibc replay. One workgroup.
 constexpr int kCommitThreads = 256;
 constexpr uint32_t kLdsSortCap = 8192;
+constexpr uint32_t kRankSortMax = 1024;   // commit: rank-sort event lists up to this length
 
 __device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
     for (uint32_t k = 2; k <= P; k <<= 1) {
@@ -232,39 +247,63 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
     const CT* C = reinterpret_cast<const CT*>((t & 1) ? a.colors1 : a.colors0);
     CT* Cs = reinterpret_cast<CT*>((t & 1) ? a.colors0 : a.colors1);
     if (E > 0) {
-        uint32_t P = 1;
-        while (P < E) P <<= 1;
-        uint32_t* s = (P <= lds_cap) ? lds : ev;
-        if (s == ev) {
-            for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
+        // Ascending vertex order. Events are distinct vertices, so a short list is ranked directly
+        // (each event counts the smaller ids: all threads, LDS broadcast reads); longer ones take
+        // the bitonic sort.
+        const uint32_t E4 = (E + 3u) & ~3u;
+        uint32_t* s;
+        uint32_t* draws = a.evdraw;
+        if (E <= kRankSortMax && 2u * E4 <= lds_cap) {
+            for (uint32_t i = threadIdx.x; i < E4; i += blockDim.x) lds[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
+            __syncthreads();
+            s = lds + E4;
+            for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
+                const uint32_t v = lds[i];
+                uint32_t r = 0;
+#pragma unroll 4
+                for (uint32_t j = 0; j < E4; j++) r += (lds[j] < v) ? 1u : 0u;
+                s[r] = v;
+            }
+            __syncthreads();
+            draws = lds;   // the unsorted copy is dead: the draws go there
         } else {
-            for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
+            uint32_t P = 1;
+            while (P < E) P <<= 1;
+            s = (P <= lds_cap) ? lds : ev;
+            if (s == ev) {
+                for (uint32_t i = E + threadIdx.x; i < P; i += blockDim.x) s[i] = 0xFFFFFFFFu;
+            } else {
+                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
+            }
+            __syncthreads();
+            bitonic_sort_block(s, P);
         }
-        __syncthreads();
-        bitonic_sort_block(s, P);
-        // The events' rand() draws in ascending vertex order: one thread steps the TYPE_3
-        // recurrence with the window in registers -- rounds of 31 unrolled steps, so the ring
-        // indices are static -- into a.evdraw; then every thread applies its share.
-        if (threadIdx.x == 0) {
-            uint32_t r[31];
+        // The events' rand() draws in ascending vertex order, by wave 0: lane j < 31 holds the TYPE_3
+        // window word r[n-31+j]; a round makes the next 31 draws x_j = r[n-31+j] + x_{j-3} (x_{-3..-1}
+        // = the window's last three words), three lanes per step, 11 steps.
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x;
             const uint32_t h0 = st->glibc_head;
-            for (int i = 0; i < 31; i++) r[i] = st->glibc_ring[(h0 + i) % 31u];
-            for (uint32_t b = 0; b < E; b += 31) {
-#pragma unroll
-                for (int j = 0; j < 31; j++) {
-                    if (b + j < E) {
-                        r[j] += r[(j + 28) % 31];
-                        a.evdraw[b + j] = r[j] >> 1;
-                    }
+            uint32_t w = lane < 31u ? st->glibc_ring[(h0 + lane) % 31u] : 0u;
+            for (uint32_t b = 0; b < E; b += 31u) {
+                uint32_t x = w + (uint32_t)__shfl((int)w, (int)((lane + 28u) & 63u), 64);   // lanes 0..2
+                for (uint32_t k = 1; k < 11; k++) {
+                    const uint32_t y = (uint32_t)__shfl((int)x, (int)(lane >= 3u ? lane - 3u : lane), 64);
+                    if (lane >= 3u * k && lane < 3u * k + 3u) x = w + y;
+                }
+                if (lane < 31u && b + lane < E) {
+                    draws[b + lane] = x >> 1;
+                    w = x;   // a partial last round leaves lanes >= E - b as they were (ring head E % 31)
                 }
             }
-            for (int i = 0; i < 31; i++) st->glibc_ring[i] = r[i];
-            st->glibc_head = E % 31u;
+            if (lane < 31u) st->glibc_ring[lane] = w;
+            if (lane == 0) st->glibc_head = E % 31u;
         }
+        __threadfence_block();
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
             const uint32_t v = s[i];
-            const uint32_t c = a.evdraw[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+            const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
             Cs[caddr(a, v)] = (CT)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                 a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
@@ -341,9 +380,10 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
     }
 }
 
-// Stand-alone commit (MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
-template <typename CT>
-__global__ __launch_bounds__(kCommitThreads) void commit_kernel(SweepArgs a) {
+// Stand-alone commit (the wide sweep; MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
+// NT threads: the wide sweep's hundreds of events per sweep rank-sort faster on 1024.
+template <typename CT, int NT = kCommitThreads>
+__global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
     __shared__ uint32_t lds[kLdsSortCap];
     __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
     __shared__ unsigned long long sh_viol;
@@ -1466,10 +1506,17 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
 
 // ----------------------------------------------------------------------------------------------
 using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
-// wide sweep: grid = CUs (g.x); scan 8 x 256-thread workgroups per CU, evaluation 4, walk 16
+// wide sweep: grid = CUs (g.x); scan 8 x 256-thread workgroups per CU (a multiple of the 8 slabs),
+// evaluation one workgroup per 2048 vertices, walk 8 per CU
 void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
-    wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
-    wide_eval_kernel<<<g.x * 4u, 256, 0, s>>>(a);
+    if (a.xs_ent && a.xs_mode == 1) {
+        wide_fp_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 2047u) / 2048u, 4096u)), 256, 0, s>>>(a);
+        wide_tscan_kernel<<<a.xs_nwg, kTscanThreads, kTscanLds, s>>>(a);
+    }
+    else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
+    else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
+    const uint32_t nloc = a.v_end - a.v_begin;
+    wide_eval_kernel<<<std::max<uint32_t>(1u, (nloc + 256u * kWideEvalPer - 1u) / (256u * kWideEvalPer)), 256, 0, s>>>(a);
     wide_walk_kernel<<<g.x * 8u, kWideWalkThreads, 0, s>>>(a);
 }
 template <int NW, bool LDSC>
@@ -1575,9 +1622,12 @@ struct mcmc_ctx {
     uint32_t nchunks = 0;
     uint64_t arc_begin = 0, arc_count = 0;
     uint8_t* wflag = nullptr;
+    uint8_t* wfp = nullptr;       // wide LDS scan: colour fingerprints, n (+16) bytes
     uint32_t* wlist = nullptr;
     uint32_t* wcount = nullptr;
     float* etab = nullptr;
+    float emax = 0.0f;
+    const XSlabLayout* xs = nullptr;   // wide: XCD-slab edge layout (graph-owned; nullptr: CSR arc scan)
 };
 
 namespace {
@@ -1692,10 +1742,24 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.chunk_row = c->chunk_row;
         a.nchunks = c->nchunks;
         a.wflag = c->wflag;
+        a.wfp = c->wfp;
         a.wlist = c->wlist;
         a.wcount = c->wcount;
         a.etab = c->etab;
+        a.emax = c->emax;
         a.fused = 0;
+        if (c->xs) {
+            a.xs_ent = c->xs->ent;
+            a.xs_base = c->xs->base;
+            a.xs_chunk0 = c->xs->chunk0;
+            a.xs_pieces = c->xs->pieces;
+            a.xs_wgp = c->xs->wg_piece;
+            a.xs_mode = c->xs->mode;
+            a.xs_nwg = c->xs->nwg;
+            a.xs_S = c->xs->S;
+            a.xs_cbits = c->xs->cbits;
+            a.xs_sym = c->xs->sym;
+        }
     }
     a.phase_ts = c->phase_ts;
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
@@ -1721,7 +1785,7 @@ int ensure_constants() {
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     c->sweep(a, c->grid, c->block, c->lds, c->stream);
     if (a.fused) return;
-    if (c->wide) commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (c->wide) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
@@ -2110,6 +2174,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMalloc(&c->wcount, sizeof(uint32_t));
         std::vector<float> et((size_t)p->nCol + 1);
         eps_table(p->epsilon, p->nCol, et.data());
+        c->emax = et[p->nCol - 1];
         if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
         if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, std::max<size_t>(nloc, 1), c->stream);
@@ -2119,6 +2184,24 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             wide_chunk_row_kernel<<<blocks, 256, 0, c->stream>>>(gd.row_off + v_begin, nloc, c->arc_begin,
                                                                  c->arc_count, c->nchunks, c->chunk_row);
             ew = hipStreamSynchronize(c->stream);
+        }
+        // the violation scan: MCMC_WIDE_SCAN = lds (default: LDS-staged colour tiles) | l2 (8 XCD
+        // slabs through L2) | csr (the CSR arc scan; A/B runs, tests)
+        const char* wsv = getenv("MCMC_WIDE_SCAN");
+        const std::string wsel = wsv ? wsv : "lds";
+        if (ew == hipSuccess && wsel != "csr") {
+            int rx = get_xslab(const_cast<mcmc_graph*>(g), v_begin, v_end, wsel == "l2" ? 0u : 1u,
+                                     (uint32_t)cus, c->stream, &c->xs);
+            if (!rx && !c->xs && wsel != "l2")   // row deltas beyond the LDS tiles' field: the L2 slabs
+                rx = get_xslab(const_cast<mcmc_graph*>(g), v_begin, v_end, 0u, (uint32_t)cus, c->stream, &c->xs);
+            if (rx) {
+                mcmc_destroy(c);
+                return rx;
+            }
+            if (c->xs && c->xs->mode == 1) {
+                ew = hipMalloc(&c->wfp, (size_t)gd.n + 16);
+                if (ew == hipSuccess) ew = hipMemset(c->wfp, 0, (size_t)gd.n + 16);
+            }
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);
@@ -2207,7 +2290,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     const uint32_t n = c->n;
     const uint32_t s0 = minstd_seed_state(c->p.seed);
-    if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(n, 1u), c->stream));
+    if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(c->v_end - c->v_begin, 1u), c->stream));
     if (C0) {
         for (uint32_t v = 0; v < n; v++)
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
@@ -2226,7 +2309,8 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
         if (c->wide)
             init_coloring_wide_kernel<<<blocks, 256, 0, c->stream>>>(reinterpret_cast<uint16_t*>(c->colors[0]), n, s0,
-                                                                     k, c->st);
+                                                                     k, c->st, c->part ? c->part_S : 0u,
+                                                                     c->part ? 4u * kFooterWords / 2u : 0u);
         else
             init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st,
                                                                  c->part ? c->part_S : 0u,
@@ -2532,7 +2616,13 @@ uint32_t mcmc_cdf_walk(const uint32_t* mask, uint32_t nCol, uint32_t cv, float e
         eps_table(eps, nCol, E.data());
         return walk_own_tab(E.data(), nCol, cv < nCol ? cv : nCol - 1u, eps, p, u);
     }
-    return walk_mask(mask, nCol, eps, p, u);
+    // the wave walk of wide_walk_kernel (host build: the 64 lanes as a loop); the per-word serial
+    // walk must agree, else the hook reports 0xFFFFFFFF
+    const uint32_t NWW = (nCol + 31u) >> 5;
+    std::vector<uint32_t> pre((size_t)NWW + 1, 0u);
+    for (uint32_t w = 0; w < NWW; w++) pre[w + 1] = pre[w] + (uint32_t)__builtin_popcount(mask[w]);
+    const uint32_t r = walk_mask_pre(mask, pre.data(), nCol, eps, p, u);
+    return r == walk_mask(mask, nCol, eps, p, u) ? r : 0xFFFFFFFFu;
 }
 
 int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
@@ -2569,6 +2659,12 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         const uint64_t segb = 4ull * tseg_stride(t.grp_rows) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
         i.layout_bytes = 2 * t.ids + segb;
         i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo + ref_extra;
+    } else if (c->wide && c->xs) {
+        // slab entries + chunk base rows; colour replica read once; per own vertex the flag, the
+        // colour read and the colour write (1 + 2 + 2 B)
+        i.layout_bytes = 4ull * kWideChunk * c->xs->chunks + 4ull * c->xs->chunks;
+        i.sweep_bytes = i.layout_bytes + 2 * (uint64_t)c->n + 5 * nloc + taboo +
+                        (c->xs->mode == 1 ? (uint64_t)c->n : 0);   // LDS mode: the fingerprint array
     } else if (c->wide) {
         // CSR + per-chunk row table; colour replica read once + own colours + write (2 B each)
         i.layout_bytes = 8 * (nloc + 1) + 4 * mloc + 4ull * (c->nchunks + 1);
@@ -2606,6 +2702,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->hist);
     (void)hipFree(c->chunk_row);
     (void)hipFree(c->wflag);
+    (void)hipFree(c->wfp);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
     (void)hipFree(c->etab);

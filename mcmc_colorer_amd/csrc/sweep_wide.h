@@ -9,20 +9,183 @@
 //     (i)/(iii), :402-412, :471-479) whose walk needs only C[v] and u_v -- no occupancy set;
 //   * only violating vertices need the occupancy set and pf (case (ii), :414-420).
 // So a sweep is three launches plus the commit (commit_kernel<uint16_t>):
-//   wide_scan_kernel  arc-parallel pass over the CSR in 256-arc chunks (64 lanes x one dwordx4 of
-//                     ids): neighbour colour == own colour -> viol flag of the row (plain byte
-//                     store; conflicts are rare, so the flags cost almost no traffic). The row of
-//                     an arc comes from a per-chunk first-row table and a short binary search.
-//   wide_eval_kernel  lane per vertex: viol -> Cviol and, untaboo'd, the violator list;
-//                     otherwise u_v, walk_own (cdf_walk.h), Cstar / taboo / overflow event.
-//   wide_walk_kernel  one 256-thread workgroup per violator: occupancy mask of nCol bits in LDS
-//                     (ds_or), Zvcomp by popcount, pf, walk_mask over runs of equal p.
-// All three are persistent (grid-stride) and exit at once when the loop is done.
+//   wide_xscan_kernel  violation flags (violation_count, :329-351) from the XCD-slab edge layout
+//                      (get_xslab below). The column space is cut into 8 slabs of S vertices;
+//                      slab s's entries are read only by workgroups b with b % 8 == s, which share
+//                      one XCD under round-robin dispatch, so the slab's colours (2 S bytes: 1 MiB at
+//                      C5) stay in that XCD's 4 MiB L2 while the entries stream past (placement only
+//                      changes speed). Every local edge is stored ONCE (in the slab of one end,
+//                      picked by the parity of i + j) and a monochromatic edge flags both ends; an
+//                      arc to another rank's row is kept and flags its own row. Entries are 32-bit:
+//                      row delta from the 256-entry chunk's base row | slab-local column.
+//   wide_scan_kernel   fallback (MCMC_WIDE_SCAN=csr, or no layout): arc-parallel pass over the CSR
+//                      in 256-arc chunks, the row of an arc found by binary search.
+//   wide_eval_kernel   lane per vertex, 8 vertices per lane with every load issued up front: viol ->
+//                      Cviol and, untaboo'd, the violator list; otherwise u_v, walk_own_tab_e
+//                      (cdf_walk.h), Cstar / taboo / overflow event.
+//   wide_walk_kernel   one 256-thread workgroup per violator: occupancy mask of nCol bits in LDS
+//                      (ds_or), word prefix counts, then one wave walks it (walk_mask_pre: the
+//                      first colour passing u found 64 words / 32 colours at a time).
+// All are grid-stride or one-shot and exit at once when the loop is done.
 
-constexpr uint32_t kWideChunk = 256;      // arcs per wave chunk: 64 lanes x 4 ids
+constexpr uint32_t kWideChunk = 256;      // entries (arcs) per wave chunk: 64 lanes x 4
 constexpr uint32_t kWideMaskWords = 2048; // nCol <= 65536
 constexpr uint32_t kWideMaxCol = 65535;
 constexpr int kWideWalkThreads = 256;
+constexpr int kWideEvalPer = 8;           // vertices per evaluation lane
+constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
+
+__global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    const uint32_t t = st->t;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    const uint32_t s = blockIdx.x & (kXSlabs - 1u);   // blocks b, b + 8, ... share an XCD: one slab
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t stride = (gridDim.x / kXSlabs) * wpb;
+    const uint32_t c1 = a.xs_chunk0[s + 1];
+    uint32_t ch = a.xs_chunk0[s] + (blockIdx.x / kXSlabs) * wpb + (threadIdx.x >> 6);
+    if (ch >= c1) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cb = a.xs_cbits, cmask = (1u << cb) - 1u, colbase = s * a.xs_S;
+    const uint32_t vb = a.v_begin, nloc = a.v_end - a.v_begin;
+    const uint32_t* __restrict__ ent = a.xs_ent + 4u * lane;
+    uint4 q = *reinterpret_cast<const uint4*>(ent + (size_t)ch * kWideChunk);
+    uint32_t base = a.xs_base[ch];
+    for (;;) {
+        const uint32_t nx = ch + stride;
+        const bool more = nx < c1;
+        uint4 qn = make_uint4(kXsPad, kXsPad, kXsPad, kXsPad);
+        uint32_t bn = 0;
+        if (more) {   // the next chunk's entries are in flight while this one's colours are gathered
+            qn = *reinterpret_cast<const uint4*>(ent + (size_t)nx * kWideChunk);
+            bn = a.xs_base[nx];
+        }
+        const uint32_t e[4] = {q.x, q.y, q.z, q.w};
+        uint32_t r[4], j[4], cr[4], cc[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            r[i] = base + (e[i] >> cb);
+            j[i] = colbase + (e[i] & cmask);
+            cr[i] = 0;
+            cc[i] = 1;
+            if (e[i] != kXsPad) {
+                cr[i] = C[caddr(a, vb + r[i])];
+                cc[i] = C[caddr(a, j[i])];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (e[i] != kXsPad && cr[i] == cc[i]) {   // rare: a monochromatic edge
+                a.wflag[r[i]] = 1;
+                if (a.xs_sym && j[i] - vb < nloc) a.wflag[j[i] - vb] = 1;
+            }
+        }
+        if (!more) break;
+        ch = nx;
+        q = qn;
+        base = bn;
+    }
+}
+
+// LDS mode (default). The colours gathered per arc are replaced by 8-bit fingerprints (the
+// colour's low byte): equal colours have equal fingerprints, so an arc whose fingerprints differ
+// is not monochromatic, and the rare match is settled on the full colours. wide_fp_kernel writes
+// the fingerprints of C_t (n bytes); one 1024-thread workgroup per CU then, for each piece dealt to
+// it (slab s, chunks [c0, c1)), stages the fingerprints of vertices [s 2^17, (s+1) 2^17) in LDS
+// (128 KiB) and streams the piece's chunks, every wave with the next chunk in flight: the column
+// fingerprint is a random LDS read, the row fingerprint a byte gather from the fingerprint array
+// (rows ascend through a chunk), so a sweep moves the entries, one fingerprint pass per slab and
+// no per-arc L2 request.
+constexpr uint32_t kTsLog = 17;                                  // 2^17 vertices per LDS tile
+constexpr int kTscanThreads = 1024;
+constexpr size_t kTscanLds = (size_t)1 << kTsLog;                // 128 KiB of fingerprints
+
+__global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    const uint32_t t = st->t;
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    const uint32_t n = a.n;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; 8u * k < n; k += gridDim.x * blockDim.x) {
+        const uint32_t v = 8u * k;   // caddr keeps 8-aligned groups contiguous (part_S % 16 == 0)
+        uint32_t w[2] = {0, 0};
+        if (v + 8u <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(C + caddr(a, v));
+            const uint32_t c[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) w[i >> 1] |= ((c[i] & 0xFFu) | ((c[i] >> 8) & 0xFF00u)) << (16u * (i & 1));
+        } else {
+            for (uint32_t i = 0; v + i < n; i++) w[i >> 2] |= ((uint32_t)C[caddr(a, v + i)] & 0xFFu) << (8u * (i & 3u));
+        }
+        *reinterpret_cast<uint2*>(a.wfp + v) = make_uint2(w[0], w[1]);
+    }
+}
+
+__global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lfp[];
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    const uint32_t t = st->t;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    const uint8_t* __restrict__ fp = a.wfp;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+    const uint32_t vb = a.v_begin, nloc = a.v_end - a.v_begin, n = a.n;
+    const uint32_t p1 = a.xs_wgp[blockIdx.x + 1];
+    const uint32_t* __restrict__ ent = a.xs_ent + 4u * lane;
+    constexpr uint32_t cmask = (1u << kTsLog) - 1u;
+    for (uint32_t p = a.xs_wgp[blockIdx.x]; p < p1; p++) {
+        const uint32_t s = a.xs_pieces[3 * p], c0 = a.xs_pieces[3 * p + 1], c1 = a.xs_pieces[3 * p + 2];
+        const uint32_t v0 = s << kTsLog;
+        const uint32_t nv = min(1u << kTsLog, n - v0);
+        __syncthreads();   // the previous piece's reads are done with the tile
+        for (uint32_t k = threadIdx.x; 16u * k < nv; k += blockDim.x)   // fp has 16 bytes of slack
+            *reinterpret_cast<uint4*>(lfp + 16u * k) = *reinterpret_cast<const uint4*>(fp + v0 + 16u * k);
+        __syncthreads();
+        uint32_t ch = c0 + wave;
+        if (ch >= c1) continue;
+        uint4 q = *reinterpret_cast<const uint4*>(ent + (size_t)ch * kWideChunk);
+        uint32_t base = a.xs_base[ch];
+        for (;;) {
+            const uint32_t nx = ch + nwave;
+            const bool more = nx < c1;
+            uint4 qn = make_uint4(kXsPad, kXsPad, kXsPad, kXsPad);
+            uint32_t bn = 0;
+            if (more) {
+                qn = *reinterpret_cast<const uint4*>(ent + (size_t)nx * kWideChunk);
+                bn = a.xs_base[nx];
+            }
+            const uint32_t e[4] = {q.x, q.y, q.z, q.w};
+            uint32_t r[4], fr[4], fc[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                r[i] = base + (e[i] >> kTsLog);
+                fr[i] = 0;
+                fc[i] = 1;
+                if (e[i] != kXsPad) {
+                    fr[i] = fp[vb + r[i]];
+                    fc[i] = lfp[e[i] & cmask];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (e[i] != kXsPad && fr[i] == fc[i]) {   // fingerprints match (1 in 256 at random): compare colours
+                    const uint32_t j = v0 + (e[i] & cmask);
+                    if (C[caddr(a, vb + r[i])] == C[caddr(a, j)]) {
+                        a.wflag[r[i]] = 1;
+                        if (a.xs_sym && j - vb < nloc) a.wflag[j - vb] = 1;
+                    }
+                }
+            }
+            if (!more) break;
+            ch = nx;
+            q = qn;
+            base = bn;
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
     DevState* st = a.st;
@@ -45,7 +208,7 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
             if (k0 + i >= m) id[i] = 0u;   // slack past m: gather a valid address, ignore below
         uint32_t nc[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) nc[i] = C[id[i]];
+        for (int i = 0; i < 4; i++) nc[i] = C[caddr(a, id[i])];
         // row of arc k0: the largest r in [lo, hi] with ro[r] - a0 <= k0
         uint32_t lo = a.chunk_row[ch], hi = a.chunk_row[ch + 1];
         while (lo < hi) {
@@ -54,20 +217,22 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
         }
         uint32_t r = lo;
         uint64_t rend = ro[r + 1] - a0;
-        uint32_t own = C[a.v_begin + r];
+        uint32_t own = C[caddr(a, a.v_begin + r)];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint64_t k = k0 + i;
             if (k >= m) break;
             if (rend <= k) {
                 do { r++; rend = ro[r + 1] - a0; } while (rend <= k);
-                own = C[a.v_begin + r];
+                own = C[caddr(a, a.v_begin + r)];
             }
             if (nc[i] == own) a.wflag[r] = 1;
         }
     }
 }
 
+// Grid: ceil(nloc / (256 * kWideEvalPer)) workgroups of 256; lane `tid` of workgroup b takes the
+// vertices b * 2048 + j * 256 + tid, j < 8 (coalesced per j).
 __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol;
     DevState* st = a.st;
@@ -78,39 +243,64 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t nloc = a.v_end - a.v_begin;
     const int lane = threadIdx.x & 63;
-    uint32_t cviol = 0;
+    const uint32_t l0 = blockIdx.x * (256u * kWideEvalPer) + threadIdx.x;
+    uint32_t viol[kWideEvalPer], cv[kWideEvalPer], tab[kWideEvalPer];
+    float ecv[kWideEvalPer];
+#pragma unroll
+    for (int j = 0; j < kWideEvalPer; j++) {
+        const uint32_t l = l0 + 256u * j;
+        viol[j] = 0;
+        cv[j] = 0;
+        tab[j] = 0;
+        if (l < nloc) {
+            viol[j] = a.wflag[l];
+            cv[j] = C[caddr(a, a.v_begin + l)];
+            if (a.taboo != nullptr) tab[j] = a.taboo[l];
+        }
+    }
     // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139); the
-    // grid-stride loop advances every lane's draw by 16807^stride, one mulmod per vertex
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const uint32_t a_stride = minstd_pow_tab(stride);
-    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + blockIdx.x * blockDim.x +
+    // lane's draw moves by 16807^256 from one j to the next
+    const uint32_t a256 = minstd_pow_tab(256);
+    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + blockIdx.x * (256u * kWideEvalPer) +
                                                                  (threadIdx.x & ~63u) + 1)),
                                kMinstdLanePow[lane]);
-    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += stride, x = minstd_mulmod(x, a_stride)) {
-        const uint32_t l = base + threadIdx.x;
+    float u[kWideEvalPer];
+#pragma unroll
+    for (int j = 0; j < kWideEvalPer; j++) {
+        u[j] = minstd_canonical(x);
+        x = minstd_mulmod(x, a256);
+    }
+    // E[cv] decides the walk only when u < E[nCol-1] or u >= hi (probability about (nCol-1) eps);
+    // otherwise no prefix passes u and the own colour's step does: the result is cv, no lookup
+    const bool tabled = a.eps > 0.0f;   // walk_own_tab_e reads E only for eps > 0
+#pragma unroll
+    for (int j = 0; j < kWideEvalPer; j++) {
+        ecv[j] = 0.0f;
+        if (l0 + 256u * j < nloc && !viol[j] && tab[j] == 0 && tabled && !(a.emax <= u[j] && u[j] < a.hi))
+            ecv[j] = a.etab[cv[j]];
+    }
+    uint32_t cviol = 0;
+#pragma unroll
+    for (int j = 0; j < kWideEvalPer; j++) {
+        const uint32_t l = l0 + 256u * j;
         const bool valid = l < nloc;
         const uint32_t v = a.v_begin + l;
-        const float u = minstd_canonical(x);
-        uint32_t viol = 0, cv = 0, tab = 0;
-        if (valid) {
-            viol = a.wflag[l];
-            if (viol) a.wflag[l] = 0;
-            cv = C[v];
-            if (a.taboo != nullptr) tab = a.taboo[l];
-        }
-        cviol += viol;
+        cviol += viol[j];
         bool event = false, walk = false;
         if (valid) {
-            if (tab > 0) {   // :496-501
-                Cs[v] = (uint16_t)cv;
-                a.taboo[l] = tab - 1;
-            } else if (viol) {
+            if (viol[j]) a.wflag[l] = 0;
+            if (tab[j] > 0) {   // :496-501
+                Cs[caddr(a, v)] = (uint16_t)cv[j];
+                a.taboo[l] = tab[j] - 1;
+            } else if (viol[j]) {
                 walk = true;   // case (i) or (ii): needs the occupancy set
             } else {           // case (iii)
-                const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+                const uint32_t nc = (tabled && a.emax <= u[j] && u[j] < a.hi)
+                                        ? cv[j]
+                                        : walk_own_tab_e(a.etab, ecv[j], a.nCol, cv[j], a.eps, a.hi, u[j]);
                 event = nc == a.nCol;
-                Cs[v] = (uint16_t)(event ? cv : nc);   // an event's colour is the commit's replay
-                if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+                Cs[caddr(a, v)] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
+                if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
             }
         }
         const uint64_t wb = __ballot(walk);
@@ -141,7 +331,8 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
 
 __global__ __launch_bounds__(kWideWalkThreads) void wide_walk_kernel(SweepArgs a) {
     __shared__ uint32_t mask[kWideMaskWords];
-    __shared__ uint32_t sh_pop;
+    __shared__ uint32_t pre[kWideMaskWords + 1];
+    __shared__ uint32_t wsum[kWideWalkThreads / 64];
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     const uint32_t t = st->t, x_t = st->x_t;
@@ -149,11 +340,12 @@ __global__ __launch_bounds__(kWideWalkThreads) void wide_walk_kernel(SweepArgs a
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t cnt = *a.wcount;
     const uint32_t NWW = (a.nCol + 31u) >> 5;
+    const uint32_t per = (NWW + kWideWalkThreads - 1u) / kWideWalkThreads;   // words per thread (prefix)
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
         const uint32_t v = a.wlist[i];
         const uint32_t l = v - a.v_begin;
         for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
-        if (threadIdx.x == 0) sh_pop = 0;
         __syncthreads();
         // count_free_colors (:362-383): occupancy of N(v), 4 independent gathers per thread in flight
         const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
@@ -162,37 +354,57 @@ __global__ __launch_bounds__(kWideWalkThreads) void wide_walk_kernel(SweepArgs a
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint64_t kk = k + (uint64_t)j * blockDim.x;
-                c[j] = kk < re ? (uint32_t)C[a.col_idx[kk]] : 0xFFFFFFFFu;
+                c[j] = kk < re ? (uint32_t)C[caddr(a, a.col_idx[kk])] : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
         }
         __syncthreads();
-        uint32_t pop = 0;
-        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) pop += __popc(mask[w]);
-        for (int off = 32; off >= 1; off >>= 1) pop += __shfl_xor(pop, off, 64);
-        if ((threadIdx.x & 63) == 0 && pop) atomicAdd(&sh_pop, pop);
+        // pre[w] = occupied colours in words < w: per-thread word runs, wave scan, workgroup offsets
+        const uint32_t w0 = threadIdx.x * per;
+        uint32_t s = 0;
+        for (uint32_t w = w0; w < w0 + per && w < NWW; w++) s += __popc(mask[w]);
+        uint32_t inc = s;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        if (lane == 63u) wsum[wave] = inc;
         __syncthreads();
+        uint32_t run = inc - s;
+        for (uint32_t k = 0; k < wave; k++) run += wsum[k];
+        for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
+            pre[w] = run;
+            run += __popc(mask[w]);
+        }
         if (threadIdx.x == 0) {
-            const uint32_t P = sh_pop, Zvcomp = a.nCol - P;
-            const uint32_t cv = C[v];
+            uint32_t T = 0;
+            for (uint32_t k = 0; k < kWideWalkThreads / 64; k++) T += wsum[k];
+            pre[NWW] = T;
+        }
+        __syncthreads();
+        if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
+            const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
+            const uint32_t cv = C[caddr(a, v)];
             const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1));
             const float u = minstd_canonical(x);
             uint32_t nc;
             if (Zvcomp > 0) {   // case (ii)
                 const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
-                nc = walk_mask(mask, a.nCol, a.eps, pf, u);
+                nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
             } else {            // case (i)
                 nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
             }
-            const bool event = nc == a.nCol;
-            Cs[v] = (uint16_t)(event ? cv : nc);
-            if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
-            if (event) {
-                const uint32_t idx = atomicAdd(&st->ev_count, 1u);
-                if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
+            if (lane == 0) {
+                const bool event = nc == a.nCol;
+                Cs[caddr(a, v)] = (uint16_t)(event ? cv : nc);
+                if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+                if (event) {
+                    const uint32_t idx = atomicAdd(&st->ev_count, 1u);
+                    if (idx < a.ev_cap) a.events[idx] = v;
+                    else atomicOr(&st->err, 1u);
+                }
             }
         }
         __syncthreads();
@@ -216,11 +428,335 @@ __global__ void wide_chunk_row_kernel(const uint64_t* __restrict__ row_off, uint
 }
 
 // ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61) into a uint16 replica.
-__global__ void init_coloring_wide_kernel(uint16_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st) {
+__global__ void init_coloring_wide_kernel(uint16_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st,
+                                          uint32_t part_S, uint32_t part_FB) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         const uint32_t x = minstd_mulmod(x0, minstd_pow_tab((uint64_t)v + 1));
         const uint32_t r = x - 1u;
         if (r >= k.past) atomicAdd(&st->init_rejections, 1u);
-        C[v] = (uint16_t)min(r / k.scaling, 65535u);
+        C[part_FB ? v + (v / part_S) * part_FB : v] = (uint16_t)min(r / k.scaling, 65535u);
     }
+}
+
+// ---- slab edge layout (built once per graph, row range and mode; cached on the graph) ------------
+// Local rows [vb, vb + nloc). Arc (i, j) of row i = vb + l is kept iff the layout is asymmetric
+// (every arc, flags its row only), or j is another rank's row, or ((i + j) & 1) == (i < j): of the
+// two arcs of a local edge exactly one survives.
+__device__ __forceinline__ bool xs_keep(uint32_t i, uint32_t j, uint32_t vb, uint32_t nloc, uint32_t sym) {
+    return !sym || j - vb >= nloc || ((i + j) & 1u) == (i < j ? 1u : 0u);
+}
+
+// bad |= 1 unless every local arc (i, j) with j local has its reverse (rows ascending): the
+// one-entry-per-edge layout needs a symmetric CSR (--simulate, R-MAT and --graph imports are).
+// One wave per row: hub rows are tens of thousands of arcs.
+__global__ __launch_bounds__(256) void xs_symcheck_kernel(const uint64_t* __restrict__ row_off,
+                                                          const uint32_t* __restrict__ col, uint32_t vb, uint32_t nloc,
+                                                          uint32_t* bad) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
+        const uint32_t i = vb + l;
+        const uint64_t e = row_off[i + 1];
+        bool ok = true;
+        for (uint64_t k = row_off[i] + lane; k < e; k += 64) {
+            const uint32_t j = col[k];
+            if (j - vb >= nloc) continue;
+            uint64_t lo = row_off[j], hi = row_off[j + 1];
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (col[mid] < i) lo = mid + 1; else hi = mid;
+            }
+            if (lo == row_off[j + 1] || col[lo] != i) ok = false;
+        }
+        if (!ok) atomicOr(bad, 1u);
+    }
+}
+
+// cnt[l] = kept arcs of local row l. One wave per row.
+__global__ __launch_bounds__(256) void xs_rowcount_kernel(const uint64_t* __restrict__ ro,
+                                                          const uint32_t* __restrict__ col, uint32_t nloc, uint32_t vb,
+                                                          uint32_t sym, uint32_t* __restrict__ cnt) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
+        uint32_t k8 = 0;
+        for (uint64_t k = ro[l] + lane; k < ro[l + 1]; k += 64) k8 += xs_keep(vb + l, col[k], vb, nloc, sym) ? 1u : 0u;
+        for (int o = 32; o >= 1; o >>= 1) k8 += __shfl_xor(k8, o, 64);
+        if (lane == 0) cnt[l] = k8;
+    }
+}
+
+// key = slab << 32 | local row, val = slab-local column, for every kept arc in CSR order (pos = the
+// exclusive scan of xs_rowcount_kernel). One wave per row, ballot ranks.
+__global__ __launch_bounds__(256) void xs_keys_kernel(const uint64_t* __restrict__ ro, const uint32_t* __restrict__ col,
+                                                      uint32_t nloc, uint32_t vb, uint32_t S, uint32_t sym,
+                                                      const uint32_t* __restrict__ pos, uint64_t* __restrict__ key,
+                                                      uint32_t* __restrict__ val) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
+        uint32_t run = pos[l];
+        const uint64_t e = ro[l + 1];
+        for (uint64_t kb = ro[l]; kb < e; kb += 64) {
+            const uint64_t k = kb + lane;
+            const uint32_t j = k < e ? col[k] : 0u;
+            const bool keep = k < e && xs_keep(vb + l, j, vb, nloc, sym);
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const uint32_t idx = run + (uint32_t)__popcll(m & lt);
+                const uint32_t s = j / S;
+                key[idx] = ((uint64_t)s << 32) | l;
+                val[idx] = j - s * S;
+            }
+            run += (uint32_t)__popcll(m);
+        }
+    }
+}
+
+// start[s] = first sorted index whose slab is >= s, s = 0..nslabs.
+__global__ void xs_slab_start_kernel(const uint64_t* __restrict__ key, uint32_t total, uint32_t nslabs,
+                                     uint32_t* __restrict__ start) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s <= nslabs; s += gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = total;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)(key[mid] >> 32) < s) lo = mid + 1; else hi = mid;
+        }
+        start[s] = lo;
+    }
+}
+
+// base[g] = local row of chunk g's first entry; ent = every sorted arc's entry.
+__global__ void xs_base_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ start,
+                               const uint32_t* __restrict__ chunk0, uint32_t nslabs, uint32_t chunks,
+                               uint32_t* __restrict__ base) {
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < chunks; g += gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nslabs - 1u;   // the slab s with chunk0[s] <= g < chunk0[s + 1]
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1u) >> 1;
+            if (chunk0[mid] <= g) lo = mid; else hi = mid - 1u;
+        }
+        base[g] = (uint32_t)key[start[lo] + (g - chunk0[lo]) * kWideChunk];
+    }
+}
+
+__global__ void xs_fill_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val, uint32_t total,
+                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ chunk0,
+                               const uint32_t* __restrict__ base, uint32_t cbits, uint32_t* __restrict__ ent,
+                               uint32_t* err) {
+    const uint32_t dmax = (1u << (32u - cbits)) - 2u;   // all-ones stays the padding value
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        const uint64_t k = key[i];
+        const uint32_t s = (uint32_t)(k >> 32), l = (uint32_t)k;
+        const uint32_t rel = i - start[s];
+        const uint32_t g = chunk0[s] + rel / kWideChunk;
+        const uint32_t d = l - base[g];
+        if (d > dmax) atomicOr(err, 1u);
+        ent[(size_t)g * kWideChunk + rel % kWideChunk] = (d << cbits) | val[i];
+    }
+}
+
+XSlabLayout::~XSlabLayout() {
+    (void)hipFree(ent);
+    (void)hipFree(base);
+    (void)hipFree(chunk0);
+    (void)hipFree(pieces);
+    (void)hipFree(wg_piece);
+}
+
+// LDS mode: cut every slab's chunks into pieces of about chunks / nwg (at least one per non-empty
+// slab) and deal them to the nwg workgroups, largest first to the least loaded (LPT).
+static void plan_pieces(const std::vector<uint32_t>& chunk0, uint32_t nwg, std::vector<uint32_t>& pieces,
+                        std::vector<uint32_t>& wgp) {
+    const uint32_t ns = (uint32_t)chunk0.size() - 1u;
+    const double T = std::max(1.0, (double)chunk0[ns] / nwg);
+    std::vector<std::array<uint32_t, 3>> pc;
+    for (uint32_t s = 0; s < ns; s++) {
+        const uint32_t c0 = chunk0[s], cs = chunk0[s + 1] - c0;
+        if (!cs) continue;
+        const uint32_t p = std::max<uint32_t>(1u, (uint32_t)std::llround(cs / T));
+        for (uint32_t k = 0; k < p; k++) {
+            const uint32_t a = c0 + (uint32_t)((uint64_t)cs * k / p), b = c0 + (uint32_t)((uint64_t)cs * (k + 1) / p);
+            if (b > a) pc.push_back({s, a, b});
+        }
+    }
+    std::stable_sort(pc.begin(), pc.end(), [](const std::array<uint32_t, 3>& x, const std::array<uint32_t, 3>& y) {
+        return x[2] - x[1] > y[2] - y[1];
+    });
+    std::vector<std::vector<uint32_t>> per(nwg);
+    std::vector<std::pair<uint64_t, uint32_t>> heap;   // (load, workgroup), min-heap
+    for (uint32_t w = 0; w < nwg; w++) heap.push_back({0, w});
+    auto cmp = [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) { return x > y; };
+    std::make_heap(heap.begin(), heap.end(), cmp);
+    for (uint32_t i = 0; i < (uint32_t)pc.size(); i++) {
+        std::pop_heap(heap.begin(), heap.end(), cmp);
+        auto& h = heap.back();
+        per[h.second].push_back(i);
+        h.first += pc[i][2] - pc[i][1];
+        std::push_heap(heap.begin(), heap.end(), cmp);
+    }
+    pieces.clear();
+    wgp.assign(nwg + 1, 0);
+    for (uint32_t w = 0; w < nwg; w++) {
+        wgp[w] = (uint32_t)(pieces.size() / 3);
+        for (uint32_t i : per[w]) pieces.insert(pieces.end(), pc[i].begin(), pc[i].end());
+    }
+    wgp[nwg] = (uint32_t)(pieces.size() / 3);
+}
+
+// The slab layout of rows [vb, ve) in `mode` (0: 8 L2 slabs, 1: 2^17-vertex LDS tiles over `nwg`
+// workgroups), built on first use and cached on the graph. *out stays nullptr (and MCMC_OK is
+// returned) when the layout does not apply: no CSR, no arcs, uint32 entry positions or row deltas
+// would overflow, or it does not fit in free device memory -- the sweep then scans the CSR.
+int get_xslab(mcmc_graph* gh, uint32_t vb, uint32_t ve, uint32_t mode, uint32_t nwg, hipStream_t st,
+              const XSlabLayout** out) {
+    *out = nullptr;
+    for (auto& x : gh->xslabs)
+        if (x->v_begin == vb && x->v_end == ve && x->mode == mode && (mode == 0 || x->nwg == nwg)) {
+            *out = x->ent ? x.get() : nullptr;
+            return MCMC_OK;
+        }
+    GraphDev& gd = gh->g;
+    const uint32_t nloc = ve - vb;
+    if (!gd.row_off || nloc == 0) return MCMC_OK;
+    uint64_t ends[2];
+    MCMC_HIP_TRY(hipMemcpy(&ends[0], gd.row_off + vb, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    MCMC_HIP_TRY(hipMemcpy(&ends[1], gd.row_off + ve, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    const uint64_t mloc = ends[1] - ends[0];
+    if (mloc == 0 || mloc >= 0x7FF00000ull) return MCMC_OK;
+    const uint32_t S = mode == 1 ? (1u << kTsLog)
+                                 : std::max<uint32_t>(1u, (uint32_t)(((uint64_t)gd.n + kXSlabs - 1) / kXSlabs));
+    const uint32_t nslabs = (uint32_t)(((uint64_t)gd.n + S - 1) / S);
+    uint32_t cbits = 1;
+    while ((1ull << cbits) < S) cbits++;
+    if (cbits > 26) return MCMC_OK;
+    size_t fr = 0, tot = 0;
+    MCMC_HIP_TRY(hipMemGetInfo(&fr, &tot));
+    const uint64_t need = 28ull * mloc + 4ull * kWideChunk * nslabs + 8ull * nloc + (256ull << 20);
+    if (need > fr) return MCMC_OK;
+    if (!gd.sorted) {   // the symmetry check searches rows; neighbour order does not affect the sweep
+        int rs = sort_rows_inplace(gd);
+        if (rs) return rs;
+    }
+    std::unique_ptr<XSlabLayout> L(new XSlabLayout());
+    L->v_begin = vb;
+    L->v_end = ve;
+    L->mode = mode;
+    L->S = S;
+    L->cbits = cbits;
+    L->nslabs = nslabs;
+    uint32_t *flag = nullptr, *cnt = nullptr, *pos = nullptr, *val = nullptr, *val2 = nullptr, *start = nullptr;
+    uint64_t *key = nullptr, *key2 = nullptr;
+    void* tmp = nullptr;
+    auto cleanup = [&]() {
+        (void)hipFree(flag);
+        (void)hipFree(cnt);
+        (void)hipFree(pos);
+        (void)hipFree(val);
+        (void)hipFree(val2);
+        (void)hipFree(start);
+        (void)hipFree(key);
+        (void)hipFree(key2);
+        (void)hipFree(tmp);
+    };
+#define XTRY(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess) {                                                                     \
+            cleanup();                                                                              \
+            return fail(MCMC_E_HIP, std::string("slab layout: " #expr ": ") + hipGetErrorString(_e)); \
+        }                                                                                           \
+    } while (0)
+    const uint32_t wblocks = std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 3u) / 4u, 65535u));   // 4 rows per block
+    uint32_t h[2] = {0, 0};
+    XTRY(hipMalloc(&flag, 2 * sizeof(uint32_t)));
+    XTRY(hipMemsetAsync(flag, 0, 2 * sizeof(uint32_t), st));
+    xs_symcheck_kernel<<<wblocks, 256, 0, st>>>(gd.row_off, gd.col_idx, vb, nloc, flag);
+    XTRY(hipGetLastError());
+    XTRY(hipMemcpyAsync(h, flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    XTRY(hipStreamSynchronize(st));
+    L->sym = h[0] ? 0u : 1u;
+    // kept arcs per row -> positions -> (slab, row) keys in CSR order -> stable sort by key
+    XTRY(hipMalloc(&cnt, sizeof(uint32_t) * ((size_t)nloc + 1)));
+    XTRY(hipMalloc(&pos, sizeof(uint32_t) * ((size_t)nloc + 1)));
+    XTRY(hipMemsetAsync(cnt + nloc, 0, sizeof(uint32_t), st));
+    xs_rowcount_kernel<<<wblocks, 256, 0, st>>>(gd.row_off + vb, gd.col_idx, nloc, vb, L->sym, cnt);
+    XTRY(hipGetLastError());
+    size_t tb = 0, tb2 = 0;
+    XTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, pos, (int)nloc + 1, st));
+    XTRY(hipMalloc(&tmp, std::max<size_t>(tb, 1)));
+    XTRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, pos, (int)nloc + 1, st));
+    uint32_t total = 0;
+    XTRY(hipMemcpyAsync(&total, pos + nloc, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    XTRY(hipStreamSynchronize(st));
+    L->entries = total;
+    if (total == 0) {
+        cleanup();
+        gh->xslabs.push_back(std::move(L));   // remembered as "not applicable"
+        return MCMC_OK;
+    }
+    XTRY(hipMalloc(&key, sizeof(uint64_t) * total));
+    XTRY(hipMalloc(&key2, sizeof(uint64_t) * total));
+    XTRY(hipMalloc(&val, sizeof(uint32_t) * total));
+    XTRY(hipMalloc(&val2, sizeof(uint32_t) * total));
+    xs_keys_kernel<<<wblocks, 256, 0, st>>>(gd.row_off + vb, gd.col_idx, nloc, vb, S, L->sym, pos, key, val);
+    XTRY(hipGetLastError());
+    uint32_t kbits = 32;
+    while ((1ull << (kbits - 32)) < nslabs) kbits++;
+    XTRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, key, key2, val, val2, (int)total, 0, (int)kbits, st));
+    if (tb2 > tb) {
+        (void)hipFree(tmp);
+        tmp = nullptr;
+        XTRY(hipMalloc(&tmp, tb2));
+        tb = tb2;
+    }
+    XTRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, key, key2, val, val2, (int)total, 0, (int)kbits, st));
+    XTRY(hipMalloc(&start, sizeof(uint32_t) * ((size_t)nslabs + 1)));
+    xs_slab_start_kernel<<<(nslabs + 256) / 256, 256, 0, st>>>(key2, total, nslabs, start);
+    XTRY(hipGetLastError());
+    std::vector<uint32_t> sh((size_t)nslabs + 1);
+    XTRY(hipMemcpyAsync(sh.data(), start, sizeof(uint32_t) * sh.size(), hipMemcpyDeviceToHost, st));
+    XTRY(hipStreamSynchronize(st));
+    L->chunk0_h.assign((size_t)nslabs + 1, 0u);
+    for (uint32_t s = 0; s < nslabs; s++)
+        L->chunk0_h[s + 1] = L->chunk0_h[s] + (sh[s + 1] - sh[s] + kWideChunk - 1) / kWideChunk;
+    L->chunks = L->chunk0_h[nslabs];
+    XTRY(hipMalloc(&L->chunk0, sizeof(uint32_t) * L->chunk0_h.size()));
+    XTRY(hipMemcpyAsync(L->chunk0, L->chunk0_h.data(), sizeof(uint32_t) * L->chunk0_h.size(), hipMemcpyHostToDevice, st));
+    XTRY(hipMalloc(&L->ent, sizeof(uint32_t) * kWideChunk * (size_t)L->chunks));
+    XTRY(hipMalloc(&L->base, sizeof(uint32_t) * (size_t)L->chunks));
+    XTRY(hipMemsetAsync(L->ent, 0xFF, sizeof(uint32_t) * kWideChunk * (size_t)L->chunks, st));
+    xs_base_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((L->chunks + 255u) / 256u, 65535u)), 256, 0, st>>>(
+        key2, start, L->chunk0, nslabs, L->chunks, L->base);
+    XTRY(hipGetLastError());
+    xs_fill_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((total + 255u) / 256u, 65535u)), 256, 0, st>>>(
+        key2, val2, total, start, L->chunk0, L->base, cbits, L->ent, flag + 1);
+    XTRY(hipGetLastError());
+    XTRY(hipMemcpyAsync(&h[1], flag + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    XTRY(hipStreamSynchronize(st));
+    if (!h[1] && mode == 1) {
+        std::vector<uint32_t> pc, wgp;
+        plan_pieces(L->chunk0_h, nwg, pc, wgp);
+        L->nwg = nwg;
+        L->npieces = (uint32_t)(pc.size() / 3);
+        XTRY(hipMalloc(&L->pieces, sizeof(uint32_t) * std::max<size_t>(pc.size(), 3)));
+        XTRY(hipMalloc(&L->wg_piece, sizeof(uint32_t) * wgp.size()));
+        if (!pc.empty())
+            XTRY(hipMemcpy(L->pieces, pc.data(), sizeof(uint32_t) * pc.size(), hipMemcpyHostToDevice));
+        XTRY(hipMemcpy(L->wg_piece, wgp.data(), sizeof(uint32_t) * wgp.size(), hipMemcpyHostToDevice));
+        XTRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&wide_tscan_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTscanLds));
+    }
+#undef XTRY
+    cleanup();
+    if (h[1]) {   // a row delta beyond the entry's field: scan the CSR instead
+        (void)hipFree(L->ent);
+        L->ent = nullptr;
+        gh->xslabs.push_back(std::move(L));
+        return MCMC_OK;
+    }
+    *out = L.get();
+    gh->xslabs.push_back(std::move(L));
+    return MCMC_OK;
 }

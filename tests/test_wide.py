@@ -9,6 +9,7 @@ tests pin against the oracle (final colouring, trajectory, iter, glibc draws).
 import numpy as np
 import pytest
 
+import oracle_np as NP
 import oracle_ref as O
 from mcmc_colorer_amd import _lib
 
@@ -70,6 +71,33 @@ def test_cdf_walk_matches_stepwise_float32(case):
         a, b = lib_walk(None, ncol, cv, eps, hi, u), naive_walk(own, ncol, eps, hi, u)
         if a != b:
             mism.append(("own", ncol, cv, float(u), a, b))
+    assert not mism, mism[:5]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_cdf_walk_prefix_wave_large_ncol(case):
+    """walk_mask_pre (the wide walk's 64-lane binade search, host build) at nCol up to 65535 and
+    hub-like occupancies; the hook also checks it against the per-word serial walk (0xFFFFFFFF on
+    disagreement), and both against the literal float32 walk."""
+    rng = np.random.default_rng(700 + case)
+    eps = [1e-8, 1e-8, 2e-6, 1e-4][case]
+    mism = []
+    for it in range(12):
+        ncol = int(rng.integers(3000, 65536))
+        dens = [0.02, 0.5, 0.97, rng.random()][it % 4]
+        bits = rng.random(ncol) < dens
+        if it % 3 == 0:   # long runs of occupied / free colours
+            bits[: ncol // 3] = True
+            bits[ncol // 3: ncol // 2] = False
+        pop = int(bits.sum())
+        if not 0 < pop < ncol:
+            continue
+        u = [canon(int(rng.integers(1, 2**31 - 1))), np.float32(1.0) - np.float32(2.0 ** -24),
+             np.float32(int(rng.integers(0, 1000)) * 1e-9)][it % 3]
+        pf = np.float32((np.float32(1.0) - np.float32(eps) * np.float32(pop)) / np.float32(ncol - pop))
+        a, b = lib_walk(bits, ncol, 0, eps, pf, u), naive_walk(bits, ncol, eps, pf, u)
+        if a != b:
+            mism.append((ncol, pop, float(u), a, b))
     assert not mism, mism[:5]
 
 
@@ -155,3 +183,38 @@ def test_wide_skewed_degrees(M):
     ncol = O.max_deg(off)
     run_both(M, off, idx, ncol)
     run_both(M, off, idx, 300, maxRip=30)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scan", ["lds", "l2", "csr"])
+def test_wide_rmat_both_scans(M, monkeypatch, scan):
+    """Power-law graph (R-MAT): the slab edge layouts (one entry per edge, both ends flagged; LDS
+    colour tiles or 8 XCD slabs through L2) and the CSR arc scan give the oracle's run, at nCol = maxDeg and at a smaller nCol whose
+    sweeps keep hundreds of violators (the workgroup-per-violator walk)."""
+    monkeypatch.setenv("MCMC_WIDE_SCAN", scan)
+    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    ncol = O.max_deg(off)
+    assert ncol > 256
+    run_both(M, off, idx, ncol)
+    run_both(M, off, idx, 300, maxRip=25)
+
+
+@pytest.mark.gpu
+def test_wide_asymmetric_csr(M):
+    """Directed arcs without their reverse (mcmc_graph_upload accepts any CSR): the slab layout
+    must keep every arc and flag only its row (violation_count reads N(v) only, :329-351)."""
+    rng = np.random.default_rng(9)
+    n = 3000
+    E = set()
+    for _ in range(30000):
+        a, b = rng.integers(0, n, 2)
+        if a != b:
+            E.add((int(a), int(b)))
+    arcs = sorted(E)
+    src = np.array([a for a, _ in arcs], dtype=np.int64)
+    idx = np.array([b for _, b in arcs], dtype=np.uint32)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.add.at(off, src + 1, 1)
+    off = np.cumsum(off).astype(np.uint64)
+    run_both(M, off, idx, 300, maxRip=30)
+    run_both(M, off, idx, 20000, maxRip=10)
