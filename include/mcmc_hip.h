@@ -203,9 +203,14 @@ int mcmc_refstruct_bench(const mcmc_graph* g, uint32_t nCol, uint32_t sweeps, ui
  *                          every replica -- RNG advance, buffer flip
  * The colour buffers (>= world*P bytes each) are caller-owned device memory (e.g. torch tensors);
  * `stream` is the caller's hipStream_t, used as given (0 = the legacy null stream, torch's default
- * current stream). Partitioned contexts need the tiled sweep (the default variant). */
+ * current stream). Partitioned contexts need the tiled sweep (nCol <= 256, the default variant) or
+ * the wide sweep (nCol > 256: uint16 colours, so a region is 2 S colour bytes + the footer).
+ * mcmc_part_layout is the uint8 layout; mcmc_part_layout2 takes the colour size in bytes
+ * (mcmc_color_bytes(nCol): 1, or 2 for the wide sweep) and gives P = bytes * S + 4*MCMC_FOOTER_WORDS. */
 #define MCMC_FOOTER_WORDS 1024
 int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P);
+int mcmc_part_layout2(uint32_t n, uint32_t world, uint32_t color_bytes, uint64_t* S, uint64_t* P);
+uint32_t mcmc_color_bytes(uint32_t nCol);
 int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
                      uint64_t colors_bytes, void* stream);
 int mcmc_part_sweep_async(mcmc_ctx* c);

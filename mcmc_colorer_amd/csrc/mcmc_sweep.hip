@@ -106,10 +106,11 @@ struct SweepArgs {
     uint32_t slice_bytes;       // tiled: colour bytes a pair's slice can hold (resident: the replica)
     uint32_t seg_buf_bytes;     // tiled: LDS bytes of one segment-table buffer (1 KiB multiple)
     unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
-    // partitioned colour buffers: vertex v at byte v + (v / part_S) * part_FB (part_FB = 0: plain)
+    // partitioned colour buffers: vertex v at element v + (v / part_S) * part_FB (part_FB = 0: plain;
+    // elements of the replica's colour type: a region is part_S colours + a 4 KiB footer)
     uint32_t part_S, part_FB;
     uint32_t own_off;           // rank * part_FB: byte offset of this rank's own vertices
-    uint64_t footer_off;        // rank * (part_S + part_FB) + part_S: this rank's footer slot
+    uint64_t footer_off;        // bytes: colour size * (rank * (part_S + part_FB) + part_S): this rank's footer
     // tail cutting enabled (mcmc_set_tailcut_repair): sweep t stores the violation flags of C_t at
     // vflags[(t & 1) * nloc + l] -- the tail cut's first pass needs those of the previous sweep
     uint8_t* vflags;
@@ -441,6 +442,7 @@ __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long v
 // Every rank, after the all-gathers: global Cviol = sum of the footers, events = rank-ordered
 // concatenation (ranks own ascending vertex ranges, so it is ascending), then the same commit as
 // the single-context loop -- identical glibc replay on every replica.
+template <typename CT>
 __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a) {
     __shared__ uint32_t lds[kLdsSortCap];
     __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
@@ -449,14 +451,14 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
     DevState* st = a.st;
     const uint32_t t0 = st->t;
     const uint8_t* nxt = (t0 & 1) ? a.colors0 : a.colors1;
-    const size_t P = (size_t)a.part_S + a.part_FB;
+    const size_t P = sizeof(CT) * ((size_t)a.part_S + a.part_FB);   // region bytes
     if (threadIdx.x == 0) {
         sh_done = st->done;
         sh_t = t0;
         unsigned long long v = 0;
         uint32_t E = 0, err = st->err;
         for (uint32_t r = 0; r < a.world; r++) {
-            const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + a.part_S);
+            const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + sizeof(CT) * a.part_S);
             v += (unsigned long long)f[0] | ((unsigned long long)f[1] << 32);
             sh_off[r] = E;
             E += min(f[2], kFooterEvents);
@@ -469,12 +471,31 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
     __syncthreads();
     if (sh_done) return;
     for (uint32_t r = 0; r < a.world; r++) {
-        const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + a.part_S);
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + sizeof(CT) * a.part_S);
         const uint32_t Er = min(f[2], kFooterEvents);
         for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = f[4 + i];
     }
     __syncthreads();
-    commit_control(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+    commit_control<CT>(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+}
+
+// The wide sweep's partitioned footer (its kernels have no fused last-workgroup step): this
+// rank's Cviol, sorted events and flags into its region of the next-colour buffer.
+__global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a) {
+    __shared__ uint32_t lds[kLdsSortCap];
+    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
+    __shared__ unsigned long long sh_viol;
+    DevState* st = a.st;
+    if (threadIdx.x == 0) {
+        sh_done = st->done;
+        sh_t = st->t;
+        sh_viol = st->viol;
+        sh_E = st->ev_count;
+        sh_err = st->err;
+    }
+    __syncthreads();
+    if (sh_done) return;
+    pack_footer(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1638,9 +1659,9 @@ int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
     if (!c->part) {
         MCMC_HIP_TRY(hipMemcpyAsync(dst, h, (size_t)c->n * c->cbytes, hipMemcpyHostToDevice, c->stream));
     } else {
-        const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
+        const uint64_t P = (uint64_t)c->cbytes * c->part_S + 4u * kFooterWords;
         for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
-            MCMC_HIP_TRY(hipMemcpyAsync(dst + r * P, h + v, std::min<uint64_t>(c->part_S, c->n - v),
+            MCMC_HIP_TRY(hipMemcpyAsync(dst + r * P, h + v * c->cbytes, c->cbytes * std::min<uint64_t>(c->part_S, c->n - v),
                                         hipMemcpyHostToDevice, c->stream));
     }
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1651,9 +1672,9 @@ int download_colors(mcmc_ctx* c, const uint8_t* src, uint8_t* h) {
     if (!c->part) {
         MCMC_HIP_TRY(hipMemcpyAsync(h, src, (size_t)c->n * c->cbytes, hipMemcpyDeviceToHost, c->stream));
     } else {
-        const uint64_t P = (uint64_t)c->part_S + 4u * kFooterWords;
+        const uint64_t P = (uint64_t)c->cbytes * c->part_S + 4u * kFooterWords;
         for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
-            MCMC_HIP_TRY(hipMemcpyAsync(h + v, src + r * P, std::min<uint64_t>(c->part_S, c->n - v),
+            MCMC_HIP_TRY(hipMemcpyAsync(h + v * c->cbytes, src + r * P, c->cbytes * std::min<uint64_t>(c->part_S, c->n - v),
                                         hipMemcpyDeviceToHost, c->stream));
     }
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1708,9 +1729,9 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.chunk_rows = c->chunk_rows;
     if (c->part) {
         a.part_S = c->part_S;
-        a.part_FB = 4u * kFooterWords;
+        a.part_FB = 4u * kFooterWords / c->cbytes;   // the footer in colour elements
         a.own_off = c->rank * a.part_FB;
-        a.footer_off = (uint64_t)c->rank * (c->part_S + a.part_FB) + c->part_S;
+        a.footer_off = (uint64_t)c->cbytes * ((uint64_t)c->rank * (c->part_S + a.part_FB) + c->part_S);
     }
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
@@ -1962,7 +1983,6 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (p->nCol > kWideMaxCol) return fail(MCMC_E_ARG, "nCol > 65535 is not supported (uint16 colour replicas)");
         if (ref) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
         if (!gd.row_off) return fail(MCMC_E_ARG, "nCol > 256 needs a CSR graph (mcmc_graph_upload / _simulate)");
-        if (v_begin != 0 || v_end != gd.n) return fail(MCMC_E_ARG, "nCol > 256: whole-graph contexts only");
     }
     if (ref) {
         // a colour may equal nCol (initColoring at u = 1.0f): it must fit the uint8 replicas
@@ -2713,24 +2733,34 @@ void mcmc_destroy(mcmc_ctx* c) {
 }
 
 // ---- vertex-partitioned step (device-resident; exchange by the caller) -----------------------
-int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P) {
+int mcmc_part_layout2(uint32_t n, uint32_t world, uint32_t color_bytes, uint64_t* S, uint64_t* P) {
     if (!S || !P) return fail(MCMC_E_ARG, "NULL argument");
     if (world == 0 || world > 64) return fail(MCMC_E_ARG, "bad world (1..64 ranks)");
+    if (color_bytes != 1 && color_bytes != 2) return fail(MCMC_E_ARG, "colour bytes: 1 or 2");
     const uint64_t s = (((uint64_t)n + world - 1) / world + 15) / 16 * 16;
     *S = s;
-    *P = s + 4ull * kFooterWords;
+    *P = color_bytes * s + 4ull * kFooterWords;
     return MCMC_OK;
+}
+
+int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P) { return mcmc_part_layout2(n, world, 1, S, P); }
+
+// The replica element size mcmc_create picks for nCol (the wide sweep: uint16).
+uint32_t mcmc_color_bytes(uint32_t nCol) {
+    const char* gv = getenv("MCMC_GATHER");
+    return (nCol > 256 || (gv && std::string(gv) == "wide")) ? 2u : 1u;
 }
 
 int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
                      uint64_t colors_bytes, void* stream) {
     if (!c || !colors0 || !colors1) return fail(MCMC_E_ARG, "NULL argument");
     if (world == 0 || world > 64 || rank >= world) return fail(MCMC_E_ARG, "bad world/rank (1..64 ranks)");
-    if (c->variant != 3) return fail(MCMC_E_STATE, "partitioned contexts need the tiled sweep (MCMC_GATHER=tiled)");
+    if (c->variant != 3 && c->variant != 4)
+        return fail(MCMC_E_STATE, "partitioned contexts need the tiled (MCMC_GATHER=tiled) or the wide sweep");
     uint64_t S = 0, P = 0;
-    (void)mcmc_part_layout(c->n, world, &S, &P);
-    if (colors_bytes < P * world) return fail(MCMC_E_ARG, "colour buffers must hold world * P bytes (mcmc_part_layout)");
-    if (S * world + 4ull * kFooterWords * world > 0xFFFFFFF0ull)
+    (void)mcmc_part_layout2(c->n, world, c->cbytes, &S, &P);
+    if (colors_bytes < P * world) return fail(MCMC_E_ARG, "colour buffers must hold world * P bytes (mcmc_part_layout2)");
+    if (P * world > 0xFFFFFFF0ull)
         return fail(MCMC_E_ARG, "partitioned colour buffers beyond 4 GiB are not supported");
     if (c->v_begin != std::min<uint64_t>(S * rank, c->n) || c->v_end != std::min<uint64_t>(S * (rank + 1), c->n))
         return fail(MCMC_E_ARG, "context rows must be [rank*S, min(n,(rank+1)*S)) (mcmc_part_layout)");
@@ -2754,6 +2784,7 @@ int mcmc_part_sweep_async(mcmc_ctx* c) {
     c->ran = true;
     SweepArgs a = make_args(c, 1);
     c->sweep(a, c->grid, c->block, c->lds, c->stream);
+    if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }
@@ -2761,7 +2792,8 @@ int mcmc_part_sweep_async(mcmc_ctx* c) {
 int mcmc_part_commit_async(mcmc_ctx* c) {
     if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
     SweepArgs a = make_args(c, 1);
-    part_commit_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }

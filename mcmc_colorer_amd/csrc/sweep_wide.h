@@ -17,7 +17,8 @@
 //                      changes speed). Every local edge is stored ONCE (in the slab of one end,
 //                      picked by the parity of i + j) and a monochromatic edge flags both ends; an
 //                      arc to another rank's row is kept and flags its own row. Entries are 32-bit:
-//                      row delta from the 256-entry chunk's base row | slab-local column.
+//                      row delta from the 256-entry chunk's base row | slab-local column, stored
+//                      lane-transposed (lane l: entries l, l + 64, l + 128, l + 192).
 //   wide_scan_kernel   fallback (MCMC_WIDE_SCAN=csr, or no layout): arc-parallel pass over the CSR
 //                      in 256-arc chunks, the row of an arc found by binary search.
 //   wide_eval_kernel   lane per vertex, 8 vertices per lane with every load issued up front: viol ->
@@ -553,7 +554,10 @@ __global__ void xs_fill_kernel(const uint64_t* __restrict__ key, const uint32_t*
         const uint32_t g = chunk0[s] + rel / kWideChunk;
         const uint32_t d = l - base[g];
         if (d > dmax) atomicOr(err, 1u);
-        ent[(size_t)g * kWideChunk + rel % kWideChunk] = (d << cbits) | val[i];
+        // lane-transposed chunk: lane l's 16-byte word holds entries l, 64 + l, 128 + l, 192 + l, so
+        // each of a wave's four gathers covers 64 consecutive (row-ascending) entries
+        const uint32_t q = rel % kWideChunk;
+        ent[(size_t)g * kWideChunk + 4u * (q & 63u) + (q >> 6)] = (d << cbits) | val[i];
     }
 }
 

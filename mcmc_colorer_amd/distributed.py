@@ -3,8 +3,8 @@
 SURVEY.md §8e. The sweep of vertex v depends only on the colours of N(v), on u_v (a function of the
 global id and the sweep number) and on taboo[v], so rows shard exactly. Rank r of R owns rows
 [r*S, min(n,(r+1)*S)), S = ceil(n/R) rounded up to 16, keeps global ids and a full colour replica.
-A colour buffer is R regions of P = S + 4096 bytes: region r holds the colours of rank r's rows
-followed by rank r's footer (local Cviol + sorted overflow events). Per sweep:
+A colour buffer is R regions of P = b*S + 4096 bytes (b = 1 colour byte, 2 for the wide sweep's
+nCol > 256): region r holds the colours of rank r's rows followed by rank r's footer (local Cviol + sorted overflow events). Per sweep:
 
   1. local sweep (HIP kernel): next colours of the owned rows + the footer, into the rank's own
      region of the next-colour buffer,
@@ -40,9 +40,10 @@ def partition(n: int, world: int, rank: int) -> tuple[int, int, int]:
     return S, min(rank * S, n), min((rank + 1) * S, n)
 
 
-def region_bytes(n: int, world: int) -> int:
-    """P: bytes of one rank's region of a partitioned colour buffer (slab + footer)."""
-    return partition(n, world, 0)[0] + 4 * FOOTER_WORDS
+def region_bytes(n: int, world: int, color_bytes: int = 1) -> int:
+    """P: bytes of one rank's region of a partitioned colour buffer (slab of colours + footer);
+    color_bytes = mcmc_color_bytes(nCol): 2 for the wide sweep (nCol > 256)."""
+    return color_bytes * partition(n, world, 0)[0] + 4 * FOOTER_WORDS
 
 
 class HipRank:
@@ -58,7 +59,8 @@ class HipRank:
         self.graph = graph
         self.params = params
         S, P = ctypes.c_uint64(), ctypes.c_uint64()
-        check(lib().mcmc_part_layout(self.n, world, ctypes.byref(S), ctypes.byref(P)))
+        self.color_bytes = int(lib().mcmc_color_bytes(params.nCol))   # 2: the wide sweep's uint16 replicas
+        check(lib().mcmc_part_layout2(self.n, world, self.color_bytes, ctypes.byref(S), ctypes.byref(P)))
         assert S.value == self.S
         self.P = P.value
         size = world * self.P + 256

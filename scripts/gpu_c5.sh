@@ -13,6 +13,12 @@ if [ -z "$SKIP_SUITE" ]; then
 fi
 timeout -k 10 600 python -u bench.py --config c5 --steps 20 --warmup 3 "$@" > gpurun_out/bench_c5.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench_c5.log | cut -c1-3000; [ $rc -ne 0 ] && exit $rc
+if [ -n "$DIST" ]; then   # the partitioned driver: world 1 over RCCL, world 2 on one GPU over gloo
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --config c5 --steps 10 --warmup 2 --no-cpu-baseline --no-refstruct > gpurun_out/bench_c5_d1.log 2>&1
+  rc=$?; echo "dist1 rc=$rc"; tail -1 gpurun_out/bench_c5_d1.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 2 --config c5 --steps 5 --warmup 1 --backend gloo --same-device --no-cpu-baseline --no-refstruct > gpurun_out/bench_c5_d2.log 2>&1
+  rc=$?; echo "dist2 rc=$rc"; tail -1 gpurun_out/bench_c5_d2.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
+fi
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --config c5 --steps 20 --warmup 2 --no-cpu-baseline --no-refstruct "$@" > $OUT/bench_trace.log 2>&1

@@ -24,19 +24,26 @@ class NumpyRank:
         self.n = len(off) - 1
         self.nCol, self.eps, self.maxRip, self.tabooIter, self.z = nCol, np.float32(eps), maxRip, taboo, z
         self.world, self.rank = world, rank
-        # region layout of mcmc_part_layout: S = ceil(n/world) rounded up to 16, region r =
-        # [colours of rows r*S .. r*S+S-1 | footer of rank r], P = S + 4*FOOTER_WORDS bytes
+        # region layout of mcmc_part_layout2: S = ceil(n/world) rounded up to 16, region r =
+        # [colours of rows r*S .. r*S+S-1 | footer of rank r], P = cb*S + 4*FOOTER_WORDS bytes with
+        # cb = 2 colour bytes for nCol > 256 (the wide sweep), else 1
         self.S = ((self.n + world - 1) // world + 15) // 16 * 16
-        self.P = self.S + 4 * FOOTER_WORDS
+        self.cb = 2 if nCol > 256 else 1
+        self.P = self.cb * self.S + 4 * FOOTER_WORDS
         self.v_begin, self.v_end = min(rank * self.S, self.n), min((rank + 1) * self.S, self.n)
         self.colors = [torch.zeros(world * self.P + 256, dtype=torch.uint8) for _ in range(2)]
 
     def _view(self, buf):
         """Colours of all n vertices (a copy) from a partitioned buffer."""
-        return np.concatenate([buf[r * self.P: r * self.P + self.S].numpy() for r in range(self.world)])[: self.n]
+        dt = np.uint16 if self.cb == 2 else np.uint8
+        return np.concatenate([buf[r * self.P: r * self.P + self.cb * self.S].numpy().view(dt)
+                               for r in range(self.world)])[: self.n]
 
     def _put(self, buf, v, c):
-        buf[(v // self.S) * self.P + v % self.S] = c
+        o = (v // self.S) * self.P + self.cb * (v % self.S)
+        buf[o] = c & 0xFF
+        if self.cb == 2:
+            buf[o + 1] = c >> 8
 
     # -- interface used by PartitionedColoringMCMC ------------------------------------------------
     def init(self, seed, glibc):
@@ -102,14 +109,14 @@ class NumpyRank:
         f = np.zeros(FOOTER_WORDS, dtype=np.uint32)
         f[0], f[1], f[2] = viol_local & 0xFFFFFFFF, viol_local >> 32, len(events)
         f[4:4 + len(events)] = sorted(events)
-        off = self.rank * self.P + self.S
+        off = self.rank * self.P + self.cb * self.S
         nxt[off: off + 4 * FOOTER_WORDS] = torch.from_numpy(f.view(np.uint8))
 
     def commit(self):
         if self.done:
             return
         nb = self.colors[(self.t + 1) & 1].numpy()
-        F = np.stack([nb[r * self.P + self.S: (r + 1) * self.P].view(np.uint32) for r in range(self.world)])
+        F = np.stack([nb[r * self.P + self.cb * self.S: (r + 1) * self.P].view(np.uint32) for r in range(self.world)])
         viol = int(sum(int(r[0]) | (int(r[1]) << 32) for r in F))
         events = [int(e) for r in F for e in r[4:4 + int(r[2])]]
         t = self.t

@@ -14,6 +14,7 @@ CASES = [
     # n, p, nCol, seed, eps, taboo, maxRip
     (90, 0.2, 6, 4, 1e-8, 0, 30),
     (120, 0.3, 7, 9, 3.3e6, 1, 12),     # CDF-overflow events on every rank
+    (80, 0.3, 300, 5, 1e-3, 0, 6),      # nCol > 256: the wide sweep's 2-byte colour regions
 ]
 
 

@@ -218,3 +218,27 @@ def test_wide_asymmetric_csr(M):
     off = np.cumsum(off).astype(np.uint64)
     run_both(M, off, idx, 300, maxRip=30)
     run_both(M, off, idx, 20000, maxRip=10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("scan", ["lds", "csr"])
+def test_wide_partitioned_lockstep(M, monkeypatch, world, scan):
+    """configs[4]'s multi-GPU shape: the wide sweep vertex-partitioned (2-byte colour regions +
+    footers, one all-gather per sweep, rank-ordered glibc replay), ranks in lock-step on one GPU,
+    equal to the unpartitioned oracle run -- at nCol = maxDeg and with persistent violators."""
+    from test_gpu_parity import _lockstep
+
+    monkeypatch.setenv("MCMC_WIDE_SCAN", scan)
+    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    for ncol, maxrip in ((O.max_deg(off), 250), (300, 20)):
+        ranks = _lockstep(M, off, idx, ncol, 1, world, maxRip=maxrip, draws=0)
+        O.srand(1)
+        r = O.mcmc_run(off, idx, ncol, 1, maxRip=maxrip)
+        for b in ranks:
+            assert b.info()["variant"] == "wide"
+            assert b.state()[0]
+            assert b.coloring().tolist() == r.colors.tolist()
+            assert b.trajectory().tolist() == r.traj.tolist()
+        for b in ranks:
+            b.close()
