@@ -87,6 +87,8 @@ struct SweepArgs {
     uint32_t aN;                // 16807^n mod (2^31-1): minstd advance per sweep
     float eps, hi;              // epsilon and 1 - (nCol-1)*epsilon (fill_p, :406)
     float emax;                 // wide: E[nCol - 1], the largest eps prefix (walk_own_tab_e fast path)
+    const uint16_t* ftab;       // wide: F(u) = first k with E[k] > u, for u = i 2^-31 < emax, i < ftab_n
+    uint32_t ftab_n;
     int check_done;             // device-resident loop: exit immediately once done
     int fused;                  // last-arriving workgroup: 1 = runs the commit (single-context loop),
                                 //                          2 = packs this rank's footer (partitioned)
@@ -130,6 +132,9 @@ struct SweepArgs {
     uint32_t* wcount;           // their number
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
+    uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
+    uint32_t* evcnt;            // wide: their number per workgroup [nblk] (written every sweep)
+    uint32_t evnblk;            // wide: evaluation workgroups
     // wide: XCD-slab edge layout of the violation scan (sweep_wide.h, get_xslab); xs_ent == nullptr
     // -> the CSR arc scan
     const uint32_t* xs_ent;     // [xs_chunk0[8] * 256] entries (row delta << cbits | slab-local column)
@@ -158,6 +163,8 @@ __device__ __forceinline__ uint32_t caddr(const SweepArgs& a, uint32_t v) {
 
 __constant__ uint32_t kMinstdLanePow[64];   // 16807^j mod (2^31-1), j = 0..63
 __constant__ uint32_t kMinstdPow2[64];      // 16807^(2^i) mod (2^31-1), i = 0..63
+constexpr uint32_t kGlibcTabK = 4096;       // glibc draws per table block (commit_accept)
+__device__ uint32_t kGlibcTab[31 * kGlibcTabK];   // [i][k]: coefficient i of x^(k+31) mod (x^31 - x^28 - 1)
 
 // 16807^e mod (2^31-1) from the squares table: one mulmod per set bit of e.
 __device__ __forceinline__ uint32_t minstd_pow_tab(uint64_t e) {
@@ -221,6 +228,7 @@ __device__ __forceinline__ void wave_or(uint32_t (&m)[NW]) {
 constexpr int kCommitThreads = 256;
 constexpr uint32_t kLdsSortCap = 8192;
 constexpr uint32_t kRankSortMax = 1024;   // commit: rank-sort event lists up to this length
+constexpr uint32_t kEvSlot = 32;          // wide evaluation: events a workgroup keeps in order
 
 __device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
     for (uint32_t k = 2; k <= P; k <<= 1) {
@@ -241,28 +249,50 @@ __device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
 // Applies the accepted sweep: replays E sorted events, advances the RNG, flips buffers.
 // `ev` holds the events (global ids, any order) and is sorted in place (via LDS when small).
 // CT: the colour replica's element type (uint8_t; uint16_t for the wide sweep, nCol > 256).
+// Diagnostics (MCMC_PHASE_DUMP): commit phase stamps in the phase buffer's last 8 slots.
+#define MCMC_COMMIT_PHASE(a, k)                                                                       \
+    do {                                                                                              \
+        if ((a).phase_ts && threadIdx.x == 0) (a).phase_ts[8u * 4095u + (k)] = wall_clock64();       \
+    } while (0)
+
 template <typename CT = uint8_t>
 __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
-                              uint32_t lds_cap) {
+                              uint32_t lds_cap, bool sorted = false) {
     DevState* st = a.st;
+    MCMC_COMMIT_PHASE(a, 1);
     const CT* C = reinterpret_cast<const CT*>((t & 1) ? a.colors1 : a.colors0);
     CT* Cs = reinterpret_cast<CT*>((t & 1) ? a.colors0 : a.colors1);
     if (E > 0) {
         // Ascending vertex order. Events are distinct vertices, so a short list is ranked directly
-        // (each event counts the smaller ids: all threads, LDS broadcast reads); longer ones take
-        // the bitonic sort.
+        // (each event counts the smaller ids: all threads, LDS broadcast reads, 16 B at a time when
+        // aligned); longer ones take the bitonic sort. The top 64 words of `lds` hold the glibc window.
+        uint32_t* gw = lds + lds_cap - 64u;
+        lds_cap -= 64u;
         const uint32_t E4 = (E + 3u) & ~3u;
         uint32_t* s;
         uint32_t* draws = a.evdraw;
-        if (E <= kRankSortMax && 2u * E4 <= lds_cap) {
+        if (sorted) {   // already ascending (the wide evaluation's per-workgroup lists, in LDS)
+            s = ev;
+            if (ev == lds && 2u * E4 <= lds_cap) draws = lds + E4;
+        } else if (E <= kRankSortMax && 2u * E4 <= lds_cap) {
             for (uint32_t i = threadIdx.x; i < E4; i += blockDim.x) lds[i] = (i < E) ? ev[i] : 0xFFFFFFFFu;
             __syncthreads();
             s = lds + E4;
+            const bool al16 = (reinterpret_cast<uintptr_t>(lds) & 15u) == 0;
             for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
                 const uint32_t v = lds[i];
                 uint32_t r = 0;
+                if (al16) {
+                    const uint4* l4 = reinterpret_cast<const uint4*>(lds);
+#pragma unroll 8
+                    for (uint32_t j = 0; j < E4 / 4u; j++) {
+                        const uint4 q = l4[j];
+                        r += (q.x < v ? 1u : 0u) + (q.y < v ? 1u : 0u) + (q.z < v ? 1u : 0u) + (q.w < v ? 1u : 0u);
+                    }
+                } else {
 #pragma unroll 4
-                for (uint32_t j = 0; j < E4; j++) r += (lds[j] < v) ? 1u : 0u;
+                    for (uint32_t j = 0; j < E4; j++) r += (lds[j] < v) ? 1u : 0u;
+                }
                 s[r] = v;
             }
             __syncthreads();
@@ -279,29 +309,37 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             __syncthreads();
             bitonic_sort_block(s, P);
         }
-        // The events' rand() draws in ascending vertex order, by wave 0: lane j < 31 holds the TYPE_3
-        // window word r[n-31+j]; a round makes the next 31 draws x_j = r[n-31+j] + x_{j-3} (x_{-3..-1}
-        // = the window's last three words), three lanes per step, 11 steps.
-        if (threadIdx.x < 64) {
-            const uint32_t lane = threadIdx.x;
-            const uint32_t h0 = st->glibc_head;
-            uint32_t w = lane < 31u ? st->glibc_ring[(h0 + lane) % 31u] : 0u;
-            for (uint32_t b = 0; b < E; b += 31u) {
-                uint32_t x = w + (uint32_t)__shfl((int)w, (int)((lane + 28u) & 63u), 64);   // lanes 0..2
-                for (uint32_t k = 1; k < 11; k++) {
-                    const uint32_t y = (uint32_t)__shfl((int)x, (int)(lane >= 3u ? lane - 3u : lane), 64);
-                    if (lane >= 3u * k && lane < 3u * k + 3u) x = w + y;
-                }
-                if (lane < 31u && b + lane < E) {
-                    draws[b + lane] = x >> 1;
-                    w = x;   // a partial last round leaves lanes >= E - b as they were (ring head E % 31)
-                }
+        MCMC_COMMIT_PHASE(a, 2);
+        // The events' rand() draws in ascending vertex order. TYPE_3 is linear over Z/2^32: draw k
+        // after the window w (oldest first) is r = sum_i T[i][k] w[i], T = x^(k+31) mod
+        // (x^31 - x^28 - 1) (kGlibcTab, ensure_constants) -- every draw of a block of up to
+        // kGlibcTabK at once, then the window moves to the block's last 31 raw draws.
+        if (threadIdx.x < 31) gw[threadIdx.x] = st->glibc_ring[(st->glibc_head + threadIdx.x) % 31u];
+        __syncthreads();
+        for (uint32_t b = 0; b < E; b += kGlibcTabK) {
+            const uint32_t nb = min(kGlibcTabK, E - b);
+            for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int i = 0; i < 31; i++) acc += kGlibcTab[i * kGlibcTabK + k] * gw[i];
+                draws[b + k] = acc >> 1;
+                if (k + 31u >= nb) gw[32u + k + 31u - nb] = acc;   // gw[32 + j]: raw draw nb - 31 + j
             }
-            if (lane < 31u) st->glibc_ring[lane] = w;
-            if (lane == 0) st->glibc_head = E % 31u;
+            __syncthreads();
+            uint32_t nw = 0;
+            if (threadIdx.x < 31) {   // the window after the block: (w[nb..30], draws) or its last 31 draws
+                const uint32_t j = threadIdx.x;
+                nw = (nb < 31u && j < 31u - nb) ? gw[nb + j] : gw[32u + j];
+            }
+            __syncthreads();
+            if (threadIdx.x < 31) gw[threadIdx.x] = nw;
+            __syncthreads();
         }
+        if (threadIdx.x < 31) st->glibc_ring[threadIdx.x] = gw[threadIdx.x];
+        if (threadIdx.x == 0) st->glibc_head = 0;
         __threadfence_block();
         __syncthreads();
+        MCMC_COMMIT_PHASE(a, 3);
         for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
             const uint32_t v = s[i];
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
@@ -311,6 +349,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         }
         __syncthreads();
     }
+    MCMC_COMMIT_PHASE(a, 4);
     if (threadIdx.x == 0) {
         st->glibc_draws += E;
         st->x_t = minstd_mulmod(st->x_t, a.aN);
@@ -327,7 +366,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
 // state values; thread 0 writes the state.
 template <typename CT = uint8_t>
 __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
-                               uint32_t* lds, uint32_t lds_cap) {
+                               uint32_t* lds, uint32_t lds_cap, uint32_t* ev = nullptr, bool sorted = false) {
     DevState* st = a.st;
     if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
     const bool stop_cap = t == a.maxRip + 1;     // iter > maxiter after sweep maxRip
@@ -347,7 +386,48 @@ __device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long lon
         if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
         return;
     }
-    commit_accept<CT>(a, t, a.events, E, lds, lds_cap);
+    commit_accept<CT>(a, t, ev ? ev : a.events, E, lds, lds_cap, sorted);
+}
+
+// The wide evaluation's per-workgroup event lists (each ascending, workgroups in vertex order)
+// after the Eg events of the global list (walk events, list overflows). Eg == 0 and room in LDS:
+// concatenated in order into lds (*out = lds, sorted); else appended to a.events (*out =
+// a.events, unsorted). Returns the total. All threads call it.
+__device__ uint32_t wide_block_events(const SweepArgs& a, uint32_t Eg, uint32_t* lds, uint32_t cap,
+                                      uint32_t** out, bool* sorted) {
+    __shared__ uint32_t wtot[17];
+    const uint32_t nb = a.evnblk;
+    const uint32_t per = (nb + blockDim.x - 1u) / blockDim.x;
+    const uint32_t b0 = min(threadIdx.x * per, nb), b1 = min(b0 + per, nb);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; b++) sum += a.evcnt[b];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wtot[wave] = inc;
+    __syncthreads();
+    uint32_t off = inc - sum, tot = 0;
+    for (uint32_t w = 0; w < nw; w++) {
+        if (w < wave) off += wtot[w];
+        tot += wtot[w];
+    }
+    const bool inl = Eg == 0 && tot <= cap;
+    uint32_t* dst = inl ? lds : a.events + Eg;
+    const uint32_t lim = inl ? cap : (a.ev_cap > Eg ? a.ev_cap - Eg : 0u);
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint32_t c = a.evcnt[b];
+        for (uint32_t i = 0; i < c; i++)
+            if (off + i < lim) dst[off + i] = a.evblk[(size_t)b * kEvSlot + i];
+        off += c;
+    }
+    __threadfence_block();
+    __syncthreads();
+    *out = inl ? lds : a.events;
+    *sorted = inl;
+    return Eg + tot;
 }
 
 // Loop control of the reference's GPU run() (coloringMCMC_main.cu:160-269), fused into the last
@@ -385,10 +465,11 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
 // NT threads: the wide sweep's hundreds of events per sweep rank-sort faster on 1024.
 template <typename CT, int NT = kCommitThreads>
 __global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
-    __shared__ uint32_t lds[kLdsSortCap];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsSortCap];
     __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
     __shared__ unsigned long long sh_viol;
     DevState* st = a.st;
+    MCMC_COMMIT_PHASE(a, 0);
     if (threadIdx.x == 0) {
         sh_done = st->done;
         sh_t = st->t;
@@ -398,7 +479,13 @@ __global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
     }
     __syncthreads();
     if (sh_done) return;
-    commit_control<CT>(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+    uint32_t E = sh_E;
+    uint32_t* ev = nullptr;
+    bool sorted = false;
+    if (a.evcnt) E = wide_block_events(a, sh_E, lds, kLdsSortCap - 64u, &ev, &sorted);
+    commit_control<CT>(a, sh_t, sh_viol, E, sh_err, lds, kLdsSortCap, ev, sorted);
+    MCMC_COMMIT_PHASE(a, 5);
+    if (a.phase_ts && threadIdx.x == 0) a.phase_ts[8u * 4095u + 6] = sh_E;
 }
 
 // ---- vertex-partitioned sweep: footer exchange ------------------------------------------------
@@ -408,12 +495,12 @@ constexpr uint32_t kFooterEvents = kFooterWords - 4;
 // Last workgroup of a partitioned sweep: sort this rank's overflow events and publish
 // [Cviol_local, E, flags, events] for the all-gather; reset the local accumulators.
 __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
-                            uint32_t* lds, uint32_t lds_cap) {
+                            uint32_t* lds, uint32_t lds_cap, uint32_t* presorted = nullptr) {
     DevState* st = a.st;
     // this rank's footer slot: after its colour slab, in the next-colour buffer
     uint32_t* footer = reinterpret_cast<uint32_t*>(((t & 1) ? a.colors0 : a.colors1) + a.footer_off);
-    uint32_t* s = a.events;
-    if (E > 0 && E <= a.ev_cap) {
+    uint32_t* s = presorted ? presorted : a.events;
+    if (!presorted && E > 0 && E <= a.ev_cap) {
         uint32_t P = 1;
         while (P < E) P <<= 1;
         s = (P <= lds_cap) ? lds : a.events;
@@ -495,7 +582,10 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
     }
     __syncthreads();
     if (sh_done) return;
-    pack_footer(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+    uint32_t* ev = nullptr;
+    bool sorted = false;
+    const uint32_t E = wide_block_events(a, sh_E, lds, kLdsSortCap, &ev, &sorted);
+    pack_footer(a, sh_t, sh_viol, E, sh_err, lds, kLdsSortCap, sorted ? ev : nullptr);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1536,8 +1626,7 @@ void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
     }
     else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
-    const uint32_t nloc = a.v_end - a.v_begin;
-    wide_eval_kernel<<<std::max<uint32_t>(1u, (nloc + 256u * kWideEvalPer - 1u) / (256u * kWideEvalPer)), 256, 0, s>>>(a);
+    wide_eval_kernel<<<a.evnblk, 256, 0, s>>>(a);
     wide_walk_kernel<<<g.x * 8u, kWideWalkThreads, 0, s>>>(a);
 }
 template <int NW, bool LDSC>
@@ -1648,6 +1737,11 @@ struct mcmc_ctx {
     uint32_t* wcount = nullptr;
     float* etab = nullptr;
     float emax = 0.0f;
+    uint16_t* ftab = nullptr;       // F(u) table of the evaluation (ftab_n entries)
+    uint32_t ftab_n = 0;
+    uint32_t* evblk = nullptr;      // per evaluation workgroup event lists
+    uint32_t* evcnt = nullptr;
+    uint32_t evnblk = 0;
     const XSlabLayout* xs = nullptr;   // wide: XCD-slab edge layout (graph-owned; nullptr: CSR arc scan)
 };
 
@@ -1768,6 +1862,11 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.wcount = c->wcount;
         a.etab = c->etab;
         a.emax = c->emax;
+        a.ftab = c->ftab;
+        a.ftab_n = c->ftab_n;
+        a.evblk = c->evblk;
+        a.evcnt = c->evcnt;
+        a.evnblk = c->evnblk;
         a.fused = 0;
         if (c->xs) {
             a.xs_ent = c->xs->ent;
@@ -1797,6 +1896,18 @@ int ensure_constants() {
         for (int j = 1; j < 64; j++) p2[j] = minstd_mulmod(p2[j - 1], p2[j - 1]);
         g_const_err = hipMemcpyToSymbol(HIP_SYMBOL(kMinstdLanePow), pw, sizeof(pw));
         if (g_const_err == hipSuccess) g_const_err = hipMemcpyToSymbol(HIP_SYMBOL(kMinstdPow2), p2, sizeof(p2));
+        // the glibc draw table: x^31 = x^28 + 1, then one multiplication by x per draw
+        std::vector<uint32_t> tab((size_t)31 * kGlibcTabK);
+        GlibcPoly q;
+        for (int i = 0; i < 31; i++) q.c[i] = 0;
+        q.c[0] = 1;
+        q.c[28] = 1;
+        for (uint32_t k = 0; k < kGlibcTabK; k++) {
+            for (int i = 0; i < 31; i++) tab[(size_t)i * kGlibcTabK + k] = q.c[i];
+            q = glibc_poly_mulx(q);
+        }
+        if (g_const_err == hipSuccess)
+            g_const_err = hipMemcpyToSymbol(HIP_SYMBOL(kGlibcTab), tab.data(), sizeof(uint32_t) * tab.size());
     });
     if (g_const_err != hipSuccess) return fail(MCMC_E_HIP, std::string("constant upload: ") + hipGetErrorString(g_const_err));
     return MCMC_OK;
@@ -2195,8 +2306,29 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         std::vector<float> et((size_t)p->nCol + 1);
         eps_table(p->epsilon, p->nCol, et.data());
         c->emax = et[p->nCol - 1];
+        // F(u_i) for u_i = i 2^-31 < emax (both monotone: one merge), when emax < hi and the table
+        // stays below 2^22 entries (8 MiB)
+        std::vector<uint16_t> ft;
+        const float hi = 1.0f - (float)(p->nCol - 1) * p->epsilon;
+        if (p->epsilon > 0.0f && c->emax < hi && (double)c->emax * 2147483648.0 < 4194304.0) {
+            uint32_t k = 1;
+            for (uint32_t i = 0;; i++) {
+                const float u = (float)i * 0x1p-31f;
+                if (!(u < c->emax)) break;
+                while (!(et[k] > u)) k++;   // k <= nCol - 1 since E[nCol-1] > u
+                ft.push_back((uint16_t)k);
+            }
+        }
+        c->ftab_n = (uint32_t)ft.size();
+        if (ew == hipSuccess && !ft.empty()) ew = hipMalloc(&c->ftab, sizeof(uint16_t) * ft.size());
+        if (ew == hipSuccess && !ft.empty())
+            ew = hipMemcpy(c->ftab, ft.data(), sizeof(uint16_t) * ft.size(), hipMemcpyHostToDevice);
         if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
         if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
+        c->evnblk = std::max<uint32_t>(1u, (nloc + 256u * kWideEvalPer - 1u) / (256u * kWideEvalPer));
+        if (ew == hipSuccess) ew = hipMalloc(&c->evblk, sizeof(uint32_t) * kEvSlot * c->evnblk);
+        if (ew == hipSuccess) ew = hipMalloc(&c->evcnt, sizeof(uint32_t) * c->evnblk);
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->evcnt, 0, sizeof(uint32_t) * c->evnblk, c->stream);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, std::max<size_t>(nloc, 1), c->stream);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, sizeof(uint32_t), c->stream);
         if (ew == hipSuccess) {
@@ -2618,8 +2750,8 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
     if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
-    if (c->phase_ts) {   // diagnostics: the last sweep's per-workgroup phase timestamps
-        std::vector<unsigned long long> h_ts((size_t)8 * c->grid.x);
+    if (c->phase_ts) {   // diagnostics: the last sweep's per-workgroup phase timestamps (+ commit stamps)
+        std::vector<unsigned long long> h_ts((size_t)8 * 4096u);
         MCMC_HIP_TRY(hipMemcpy(h_ts.data(), c->phase_ts, h_ts.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("MCMC_PHASE_DUMP"), "wb")) {
             fwrite(h_ts.data(), sizeof(unsigned long long), h_ts.size(), f);
@@ -2634,7 +2766,9 @@ uint32_t mcmc_cdf_walk(const uint32_t* mask, uint32_t nCol, uint32_t cv, float e
     if (!mask) {
         std::vector<float> E((size_t)nCol + 1);
         eps_table(eps, nCol, E.data());
-        return walk_own_tab(E.data(), nCol, cv < nCol ? cv : nCol - 1u, eps, p, u);
+        const uint32_t c = cv < nCol ? cv : nCol - 1u;   // the table walk and the binade walk must agree
+        const uint32_t r = walk_own_tab(E.data(), nCol, c, eps, p, u);
+        return r == walk_own(nCol, c, eps, p, u) ? r : 0xFFFFFFFFu;
     }
     // the wave walk of wide_walk_kernel (host build: the 64 lanes as a loop); the per-word serial
     // walk must agree, else the hook reports 0xFFFFFFFF
@@ -2723,6 +2857,9 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->chunk_row);
     (void)hipFree(c->wflag);
     (void)hipFree(c->wfp);
+    (void)hipFree(c->evblk);
+    (void)hipFree(c->ftab);
+    (void)hipFree(c->evcnt);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
     (void)hipFree(c->etab);

@@ -22,8 +22,9 @@
 //   wide_scan_kernel   fallback (MCMC_WIDE_SCAN=csr, or no layout): arc-parallel pass over the CSR
 //                      in 256-arc chunks, the row of an arc found by binary search.
 //   wide_eval_kernel   lane per vertex, 8 vertices per lane with every load issued up front: viol ->
-//                      Cviol and, untaboo'd, the violator list; otherwise u_v, walk_own_tab_e
-//                      (cdf_walk.h), Cstar / taboo / overflow event.
+//                      Cviol and, untaboo'd, the violator list; otherwise u_v, the own-colour walk
+//                      (a range test, else walk_own; cdf_walk.h), Cstar / taboo / overflow event
+//                      into the workgroup's ordered event list.
 //   wide_walk_kernel   one 256-thread workgroup per violator: occupancy mask of nCol bits in LDS
 //                      (ds_or), word prefix counts, then one wave walks it (walk_mask_pre: the
 //                      first colour passing u found 64 words / 32 colours at a time).
@@ -101,6 +102,8 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 // no per-arc L2 request.
 constexpr uint32_t kTsLog = 17;                                  // 2^17 vertices per LDS tile
 constexpr int kTscanThreads = 1024;
+constexpr uint32_t kTsUnroll = 4;                               // chunks per wave step
+constexpr uint32_t kTsCand = 2048;                              // LDS candidate list (16 KiB)
 constexpr size_t kTscanLds = (size_t)1 << kTsLog;                // 128 KiB of fingerprints
 
 __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
@@ -126,8 +129,11 @@ __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
 
 __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lfp[];
+    __shared__ uint2 cand[kTsCand];   // fingerprint matches (local row, column) of the piece
+    __shared__ uint32_t ncand;
     DevState* st = a.st;
     if (a.check_done && st->done) return;
+    if (threadIdx.x == 0) ncand = 0;
     const uint32_t t = st->t;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
@@ -142,49 +148,103 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
         const uint32_t v0 = s << kTsLog;
         const uint32_t nv = min(1u << kTsLog, n - v0);
         __syncthreads();   // the previous piece's reads are done with the tile
-        for (uint32_t k = threadIdx.x; 16u * k < nv; k += blockDim.x)   // fp has 16 bytes of slack
-            *reinterpret_cast<uint4*>(lfp + 16u * k) = *reinterpret_cast<const uint4*>(fp + v0 + 16u * k);
-        __syncthreads();
-        uint32_t ch = c0 + wave;
-        if (ch >= c1) continue;
-        uint4 q = *reinterpret_cast<const uint4*>(ent + (size_t)ch * kWideChunk);
-        uint32_t base = a.xs_base[ch];
-        for (;;) {
-            const uint32_t nx = ch + nwave;
-            const bool more = nx < c1;
-            uint4 qn = make_uint4(kXsPad, kXsPad, kXsPad, kXsPad);
-            uint32_t bn = 0;
-            if (more) {
-                qn = *reinterpret_cast<const uint4*>(ent + (size_t)nx * kWideChunk);
-                bn = a.xs_base[nx];
-            }
-            const uint32_t e[4] = {q.x, q.y, q.z, q.w};
-            uint32_t r[4], fr[4], fc[4];
+        {   // stage the tile: all of a thread's 16-byte loads in flight, then the LDS stores
+            const uint32_t nk = (nv + 15u) / 16u;   // fp has 16 bytes of slack past n
+            for (uint32_t k0 = threadIdx.x; k0 < nk; k0 += 8u * blockDim.x) {
+                uint4 tmp[8];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                r[i] = base + (e[i] >> kTsLog);
-                fr[i] = 0;
-                fc[i] = 1;
-                if (e[i] != kXsPad) {
-                    fr[i] = fp[vb + r[i]];
-                    fc[i] = lfp[e[i] & cmask];
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t k = k0 + u * blockDim.x;
+                    if (k < nk) tmp[u] = *reinterpret_cast<const uint4*>(fp + v0 + 16u * k);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t k = k0 + u * blockDim.x;
+                    if (k < nk) *reinterpret_cast<uint4*>(lfp + 16u * k) = tmp[u];
                 }
             }
+        }
+        __syncthreads();
+        // a wave takes kTsUnroll chunks at a time (ch, ch + nwave, ...). Vector loads complete in
+        // order, so each step issues its fingerprint gathers BEFORE the next set's entries and
+        // waits only for the gathers; fingerprint matches go to an LDS candidate list settled once
+        // per piece (their colour loads would otherwise wait for the prefetch every step).
+        uint32_t ch = c0 + wave;
+        if (ch < c1) {
+            const uint4 pad4 = make_uint4(kXsPad, kXsPad, kXsPad, kXsPad);
+            uint4 q[kTsUnroll];
+            uint32_t bs[kTsUnroll];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (e[i] != kXsPad && fr[i] == fc[i]) {   // fingerprints match (1 in 256 at random): compare colours
-                    const uint32_t j = v0 + (e[i] & cmask);
-                    if (C[caddr(a, vb + r[i])] == C[caddr(a, j)]) {
-                        a.wflag[r[i]] = 1;
-                        if (a.xs_sym && j - vb < nloc) a.wflag[j - vb] = 1;
+            for (uint32_t u = 0; u < kTsUnroll; u++) {
+                const uint32_t c = ch + u * nwave;
+                q[u] = pad4;
+                bs[u] = 0;
+                if (c < c1) {
+                    q[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
+                    bs[u] = a.xs_base[c];
+                }
+            }
+            for (;;) {
+                uint32_t e[4 * kTsUnroll], r[4 * kTsUnroll], fr[4 * kTsUnroll], fc[4 * kTsUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kTsUnroll; u++) {
+                    e[4 * u] = q[u].x;
+                    e[4 * u + 1] = q[u].y;
+                    e[4 * u + 2] = q[u].z;
+                    e[4 * u + 3] = q[u].w;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < 4 * kTsUnroll; i++) {
+                    r[i] = bs[i / 4] + (e[i] >> kTsLog);
+                    fr[i] = 0;
+                    fc[i] = 1;
+                    if (e[i] != kXsPad) {
+                        fr[i] = fp[vb + r[i]];
+                        fc[i] = lfp[e[i] & cmask];
                     }
                 }
+                const uint32_t nx = ch + kTsUnroll * nwave;
+                const bool more = nx < c1;
+#pragma unroll
+                for (uint32_t u = 0; u < kTsUnroll; u++) {   // the next set, behind the gathers
+                    const uint32_t c = nx + u * nwave;
+                    q[u] = pad4;
+                    bs[u] = 0;
+                    if (more && c < c1) {
+                        q[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
+                        bs[u] = a.xs_base[c];
+                    }
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < 4 * kTsUnroll; i++) {
+                    if (e[i] != kXsPad && fr[i] == fc[i]) {   // fingerprints match (1 in 256 at random)
+                        const uint32_t k = atomicAdd(&ncand, 1u);
+                        if (k < kTsCand) {
+                            cand[k] = make_uint2(r[i], v0 + (e[i] & cmask));
+                        } else {   // list full: settle it here
+                            const uint32_t j = v0 + (e[i] & cmask);
+                            if (C[caddr(a, vb + r[i])] == C[caddr(a, j)]) {
+                                a.wflag[r[i]] = 1;
+                                if (a.xs_sym && j - vb < nloc) a.wflag[j - vb] = 1;
+                            }
+                        }
+                    }
+                }
+                if (!more) break;
+                ch = nx;
             }
-            if (!more) break;
-            ch = nx;
-            q = qn;
-            base = bn;
         }
+        __syncthreads();
+        const uint32_t nc = min(ncand, kTsCand);
+        for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {   // the candidates: compare colours
+            const uint2 rc = cand[k];
+            if (C[caddr(a, vb + rc.x)] == C[caddr(a, rc.y)]) {
+                a.wflag[rc.x] = 1;
+                if (a.xs_sym && rc.y - vb < nloc) a.wflag[rc.y - vb] = 1;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) ncand = 0;
     }
 }
 
@@ -235,10 +295,15 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
 // Grid: ceil(nloc / (256 * kWideEvalPer)) workgroups of 256; lane `tid` of workgroup b takes the
 // vertices b * 2048 + j * 256 + tid, j < 8 (coalesced per j).
 __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
-    __shared__ uint32_t sh_viol;
+    __shared__ uint32_t sh_viol, sh_nev;
+    __shared__ uint32_t sh_ev[kEvSlot];   // this workgroup's overflow events (ordered at the end)
     DevState* st = a.st;
     if (a.check_done && st->done) return;
-    if (threadIdx.x == 0) sh_viol = 0;
+    if (threadIdx.x == 0) {
+        sh_viol = 0;
+        sh_nev = 0;
+    }
+    __syncthreads();
     const uint32_t t = st->t, x_t = st->x_t;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
@@ -246,7 +311,6 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t l0 = blockIdx.x * (256u * kWideEvalPer) + threadIdx.x;
     uint32_t viol[kWideEvalPer], cv[kWideEvalPer], tab[kWideEvalPer];
-    float ecv[kWideEvalPer];
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
         const uint32_t l = l0 + 256u * j;
@@ -265,27 +329,24 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + blockIdx.x * (256u * kWideEvalPer) +
                                                                  (threadIdx.x & ~63u) + 1)),
                                kMinstdLanePow[lane]);
-    float u[kWideEvalPer];
+    uint32_t xs[kWideEvalPer];
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
-        u[j] = minstd_canonical(x);
+        xs[j] = x;
         x = minstd_mulmod(x, a256);
     }
-    // E[cv] decides the walk only when u < E[nCol-1] or u >= hi (probability about (nCol-1) eps);
-    // otherwise no prefix passes u and the own colour's step does: the result is cv, no lookup
-    const bool tabled = a.eps > 0.0f;   // walk_own_tab_e reads E only for eps > 0
-#pragma unroll
-    for (int j = 0; j < kWideEvalPer; j++) {
-        ecv[j] = 0.0f;
-        if (l0 + 256u * j < nloc && !viol[j] && tab[j] == 0 && tabled && !(a.emax <= u[j] && u[j] < a.hi))
-            ecv[j] = a.etab[cv[j]];
-    }
+    // The own-colour walk (cases (i)/(iii)): for E[nCol-1] <= u < hi (all but about 2 (nCol-1) eps
+    // of the draws) no eps prefix passes u and the own colour's step does -- the colour stays. For
+    // u < E[nCol-1] the answer depends on u alone up to cv: F(u) = first k with E[k] > u, one load
+    // of the host table ftab (indexed by x - 1, u = (x - 1) 2^-31 exactly); else the table walk.
+    const bool tabled = a.eps > 0.0f;
     uint32_t cviol = 0;
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
         const uint32_t l = l0 + 256u * j;
         const bool valid = l < nloc;
         const uint32_t v = a.v_begin + l;
+        const float u = minstd_canonical(xs[j]);
         cviol += viol[j];
         bool event = false, walk = false;
         if (valid) {
@@ -296,9 +357,15 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
             } else if (viol[j]) {
                 walk = true;   // case (i) or (ii): needs the occupancy set
             } else {           // case (iii)
-                const uint32_t nc = (tabled && a.emax <= u[j] && u[j] < a.hi)
-                                        ? cv[j]
-                                        : walk_own_tab_e(a.etab, ecv[j], a.nCol, cv[j], a.eps, a.hi, u[j]);
+                uint32_t nc;
+                if (tabled && a.emax <= u && u < a.hi) {
+                    nc = cv[j];
+                } else if (tabled && u < a.emax && xs[j] - 1u < a.ftab_n) {   // ftab_n > 0 only if emax < hi
+                    const uint32_t F = a.ftab[xs[j] - 1u];
+                    nc = F <= cv[j] ? F - 1u : cv[j];
+                } else {
+                    nc = walk_own_tab(a.etab, a.nCol, cv[j], a.eps, a.hi, u);
+                }
                 event = nc == a.nCol;
                 Cs[caddr(a, v)] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
@@ -311,19 +378,27 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
             b = __shfl(b, 0, 64);
             if (walk) a.wlist[b + (uint32_t)__popcll(wb & ((1ull << lane) - 1ull))] = v;
         }
-        const uint64_t eb = __ballot(event);
-        if (eb) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
-            b = __shfl(b, 0, 64);
-            if (event) {
-                const uint32_t idx = b + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
+        if (event) {   // into this workgroup's LDS list; past kEvSlot, the global list
+            const uint32_t k = atomicAdd(&sh_nev, 1u);
+            if (k < kEvSlot) {
+                sh_ev[k] = v;
+            } else {
+                const uint32_t idx = atomicAdd(&st->ev_count, 1u);
                 if (idx < a.ev_cap) a.events[idx] = v;
                 else atomicOr(&st->err, 1u);
             }
         }
     }
     __syncthreads();
+    // this workgroup's list, ascending (rank of each event among at most kEvSlot), and its count
+    const uint32_t ne = min(sh_nev, kEvSlot);
+    if (threadIdx.x < ne) {
+        const uint32_t v = sh_ev[threadIdx.x];
+        uint32_t rk = 0;
+        for (uint32_t k = 0; k < ne; k++) rk += sh_ev[k] < v ? 1u : 0u;
+        a.evblk[(size_t)blockIdx.x * kEvSlot + rk] = v;
+    }
+    if (threadIdx.x == 0) a.evcnt[blockIdx.x] = ne;
     for (int off = 32; off >= 1; off >>= 1) cviol += __shfl_xor(cviol, off, 64);
     if (lane == 0 && cviol) atomicAdd(&sh_viol, cviol);
     __syncthreads();
