@@ -1732,7 +1732,7 @@ struct mcmc_ctx {
     uint32_t nchunks = 0;
     uint64_t arc_begin = 0, arc_count = 0;
     uint8_t* wflag = nullptr;
-    uint8_t* wfp = nullptr;       // wide LDS scan: colour fingerprints, n (+16) bytes
+    uint8_t* wfp = nullptr;       // wide LDS scan: colour fingerprints, n (+2048) bytes
     uint32_t* wlist = nullptr;
     uint32_t* wcount = nullptr;
     float* etab = nullptr;
@@ -2351,8 +2351,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 return rx;
             }
             if (c->xs && c->xs->mode == 1) {
-                ew = hipMalloc(&c->wfp, (size_t)gd.n + 16);
-                if (ew == hipSuccess) ew = hipMemset(c->wfp, 0, (size_t)gd.n + 16);
+                ew = hipMalloc(&c->wfp, (size_t)gd.n + 2048);   // slack: tile staging and row windows
+                if (ew == hipSuccess) ew = hipMemset(c->wfp, 0, (size_t)gd.n + 2048);
             }
         }
         if (ew != hipSuccess) {

@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 constexpr uint32_t kTsLog = 17;                                  // 2^17 vertices per LDS tile
 constexpr int kTscanThreads = 1024;
 constexpr uint32_t kTsUnroll = 4;                               // chunks per wave step
-constexpr uint32_t kTsCand = 2048;                              // LDS candidate list (16 KiB)
+constexpr uint32_t kTsCand = 1024;                              // LDS candidate list (8 KiB)
+constexpr uint32_t kTsWin = 1024;                               // row-fingerprint window per wave (bytes)
 constexpr size_t kTscanLds = (size_t)1 << kTsLog;                // 128 KiB of fingerprints
 
 __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
@@ -131,6 +132,7 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
     extern __shared__ __attribute__((aligned(16))) uint8_t lfp[];
     __shared__ uint2 cand[kTsCand];   // fingerprint matches (local row, column) of the piece
     __shared__ uint32_t ncand;
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kTscanThreads / 64][kTsWin];   // row windows, one per wave
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     if (threadIdx.x == 0) ncand = 0;
@@ -141,6 +143,7 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
     const uint32_t vb = a.v_begin, nloc = a.v_end - a.v_begin, n = a.n;
     const uint32_t p1 = a.xs_wgp[blockIdx.x + 1];
+    uint8_t* win = wins[wave];
     const uint32_t* __restrict__ ent = a.xs_ent + 4u * lane;
     constexpr uint32_t cmask = (1u << kTsLog) - 1u;
     for (uint32_t p = a.xs_wgp[blockIdx.x]; p < p1; p++) {
@@ -193,15 +196,20 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
                     e[4 * u + 2] = q[u].z;
                     e[4 * u + 3] = q[u].w;
                 }
+                // row fingerprints: each chunk's rows ascend from its base, so one 16-byte load per
+                // lane fetches a 1 KiB window of them (from base rounded down to 16); entries past
+                // the window (rare) gather their byte
+                uint4 wv[kTsUnroll];
+                uint32_t w0[kTsUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kTsUnroll; u++) {
+                    w0[u] = (vb + bs[u]) & ~15u;
+                    wv[u] = *reinterpret_cast<const uint4*>(fp + w0[u] + 16u * lane);   // fp has 2 KiB of slack
+                }
 #pragma unroll
                 for (uint32_t i = 0; i < 4 * kTsUnroll; i++) {
                     r[i] = bs[i / 4] + (e[i] >> kTsLog);
-                    fr[i] = 0;
-                    fc[i] = 1;
-                    if (e[i] != kXsPad) {
-                        fr[i] = fp[vb + r[i]];
-                        fc[i] = lfp[e[i] & cmask];
-                    }
+                    fc[i] = e[i] != kXsPad ? (uint32_t)lfp[e[i] & cmask] : 1u;
                 }
                 const uint32_t nx = ch + kTsUnroll * nwave;
                 const bool more = nx < c1;
@@ -213,6 +221,16 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
                     if (more && c < c1) {
                         q[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
                         bs[u] = a.xs_base[c];
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kTsUnroll; u++) {   // the wave's window slot: its own LDS ops stay in order
+                    *reinterpret_cast<uint4*>(win + 16u * lane) = wv[u];
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++) {
+                        const uint32_t i = 4 * u + k;
+                        const uint32_t d = vb + r[i] - w0[u];
+                        fr[i] = e[i] == kXsPad ? 0u : d < kTsWin ? (uint32_t)win[d] : (uint32_t)fp[vb + r[i]];
                     }
                 }
 #pragma unroll
