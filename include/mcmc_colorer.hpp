@@ -391,3 +391,64 @@ private:
     std::vector<uint32_t> coloring;
     std::vector<uint64_t> trajectory, tail;
 };
+
+// ---- other colorers ------------------------------------------------------
+// ColoringGreedyFF (graph_coloring/coloringGreedyFF.h / .cu): run(), getColoring()->nCol / colClass
+// (1-based colours), saveStats / saveColor in the reference's report layout (:225-303).
+struct Coloring {
+    uint32_t nCol{0};
+    const uint32_t* colClass{nullptr};
+};
+
+template <typename nodeW, typename edgeW>
+class ColoringGreedyFF {
+public:
+    explicit ColoringGreedyFF(Graph<nodeW, edgeW>* graph_d) : graph(graph_d) {}
+    void run() {
+        colors.resize(graph->getNNodes());
+        MCMC_CHECK(mcmc_greedyff_run(graph->handle(), colors.data(), &numColors, &rounds));
+        coloring.nCol = numColors;
+        coloring.colClass = colors.data();
+    }
+    Coloring* getColoring() { return &coloring; }
+    uint32_t getRounds() const { return rounds; }
+    void saveStats(size_t iteration, float duration, std::ofstream& file) const {
+        file << "Greedy First Fit Colorer - GPU implementation - Report\n";
+        file << "-------------------------------------------\n";
+        file << "GRAPH INFO\n";
+        file << "Nodes: " << graph->getNNodes() << " - Edges: " << graph->getNEdges() << "\n";
+        file << "Max deg: " << graph->getMaxNodeDeg() << " - Min deg: " << graph->getMinNodeDeg()
+             << " - Avg deg: " << graph->getMeanNodeDeg() << "\n";
+        file << "Edge Probability (for randomly generated graphs): " << graph->prob << "\n";
+        file << "-------------------------------------------\n";
+        file << "EXECUTION INFO\n";
+        file << "Repetition: " << iteration << "\n";
+        file << "Execution time: " << duration << "\n";
+        file << "-------------------------------------------\n";
+        file << "Number of colors: " << numColors << "\n";
+        file << "Color histogram: \n";
+        // convert_to_standard_notation (:200-209): class sizes of colours 1..numColors
+        std::vector<uint32_t> histogram(numColors, 0);
+        for (uint32_t c : colors)
+            if (c >= 1 && c <= numColors) histogram[c - 1]++;
+        for (uint32_t i = 1; i < numColors + 1; ++i) file << i << "\t: " << histogram[i - 1] << "\n";
+        int sum = 0;   // std::accumulate(.., 0): an int sum
+        for (uint32_t h : histogram) sum += (int)h;
+        const float mean = sum / static_cast<float>(numColors);
+        float variance = 0;
+        for (uint32_t h : histogram) variance += (h - mean) * (h - mean);
+        variance /= static_cast<float>(numColors);
+        file << "Average number of nodes for each color: " << mean << "\n";
+        file << "Variance: " << variance << "\n";
+        file << "StD: " << sqrtf(variance) << "\n";
+    }
+    void saveColor(std::ofstream& file) const {
+        for (uint32_t i = 0; i < graph->getNNodes(); ++i) file << i << " " << colors[i] << "\n";
+    }
+
+private:
+    Graph<nodeW, edgeW>* graph;
+    std::vector<uint32_t> colors;
+    uint32_t numColors{0}, rounds{0};
+    Coloring coloring;
+};

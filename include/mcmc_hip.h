@@ -218,6 +218,15 @@ int mcmc_part_commit_async(mcmc_ctx* c);
 /* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final). */
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
 
+/* ---- other colorers -------------------------------------------------
+ * The reference's parallel greedy first-fit colorer (ColoringGreedyFF::run,
+ * graph_coloring/coloringGreedyFF.cu:50-84, `--grdffgpu`): Jacobi rounds of a tentative first fit
+ * (each uncoloured node's forbidden set gains its neighbours' colours and is never cleared; the
+ * first colour i >= 1, i <= maxDeg, not forbidden; node 0 always 1) and a conflict pass (the
+ * larger id of a same-coloured pair is uncoloured) until every node is coloured. Deterministic.
+ * colors: n host words, 1-based; num_colors = distinct colours; rounds = loop iterations. */
+int mcmc_greedyff_run(const mcmc_graph* g, uint32_t* colors, uint32_t* num_colors, uint32_t* rounds);
+
 /* ---- reference-GPU-semantics mode ------------------------------------
  * The per-vertex cuRAND XORWOW states of the reference's GPURand (GPUutils/GPURandomizer.cu:8-13,
  * 85-101: curand_init(seed, v, 0) for every vertex v), shared by all repetitions (main.cu:80,193).

@@ -427,3 +427,29 @@ def write_report(path: str, flavour: str, graph: Graph, p: ColoringMCMCParams, s
     ]
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
+
+
+class ColoringGreedyFF:
+    """ColoringGreedyFF (graph_coloring/coloringGreedyFF.h/.cu, ``--grdffgpu``):
+    the reference's deterministic parallel greedy first-fit colorer on the GPU (csrc/greedyff.hip).
+    Colours are 1-based; ``numColors`` counts the distinct colours (coloringGreedyFF.cu:79-80)."""
+
+    def __init__(self, graph: "Graph"):
+        self.graph = graph
+        self.colors = None
+        self.numColors = 0
+        self.rounds = 0
+
+    def run(self) -> None:
+        out = np.zeros(self.graph.nNodes, dtype=np.uint32)
+        nc, r = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().mcmc_greedyff_run(self.graph.handle, u32ptr(out), ctypes.byref(nc), ctypes.byref(r)))
+        self.colors, self.numColors, self.rounds = out, nc.value, r.value
+
+    def getColoring(self) -> tuple[int, np.ndarray]:
+        return self.numColors, self.colors
+
+    def saveColor(self, path: str) -> None:
+        """saveColor (coloringGreedyFF.cu:305-310): one "<node> <colour>" line per node."""
+        with open(path, "w") as f:
+            f.writelines(f"{i} {int(c)}\n" for i, c in enumerate(self.colors))

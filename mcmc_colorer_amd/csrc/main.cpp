@@ -108,6 +108,7 @@ void help(const char* argv0) {
               << "                       for n where the reference's O(n^2) generator is infeasible (1e7)\n"
               << "  --mcmcgpu            MCMC colorer on the MI355X (default)\n"
               << "  --mcmcgpu-ref        the reference's GPU colorer semantics (XORWOW, balance-dynamic)\n"
+              << "  --grdffgpu           parallel greedy first-fit colorer (ColoringGreedyFF)\n"
               << "  --nCol N             number of colours (default maxDeg / numColRatio)\n"
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
               << "  --tabooIteration N   taboo iterations (default 0)\n"
@@ -126,7 +127,7 @@ int main(int argc, char** argv) {
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
     bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false,
-         tailcutRepair = false, mcmcgpuref = false;
+         tailcutRepair = false, mcmcgpuref = false, greedyff = false;
     uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
@@ -154,7 +155,8 @@ int main(int argc, char** argv) {
                 case 'n': if (std::stoi(optarg) < 1) throw 1; n = std::stoi(optarg); break;
                 case '1': mcmccpu = true; break;
                 case '2': mcmcgpu = true; break;
-                case '3': case '4': case '5': other = true; break;
+                case '4': greedyff = true; break;
+                case '3': case '5': other = true; break;
                 case 'k': if (std::stoi(optarg) < 1) throw 1; nCol = std::stoi(optarg); break;
                 case 'r': numColRatio = std::stod(optarg); if (numColRatio < 1.0 || numColRatio > 16.0) throw 1; break;
                 case 't': if (std::stoi(optarg) < 1) throw 1; tabooIteration = std::stoi(optarg); break;
@@ -186,15 +188,17 @@ int main(int argc, char** argv) {
         return 255;
     }
     if (other) {
-        std::cout << "--lubygpu / --grdffgpu / --vffgpu are outside this build (see DESIGN.md)" << std::endl;
+        std::cout << "--lubygpu / --vffgpu are outside this build (see DESIGN.md)" << std::endl;
         return 255;
     }
     if (mcmcgpu && mcmcgpuref) {
         std::cout << "--mcmcgpu and --mcmcgpu-ref write the same files: choose one" << std::endl;
         return 255;
     }
-    if (!mcmcgpu && !mcmcgpuref)
+    if (!mcmcgpu && !mcmcgpuref && !greedyff) {
         std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
+        mcmcgpu = true;
+    }
     if (simulate && n == 0) { std::cout << "Simualtion enabled: specify the number of nodes (-n)." << std::endl; return 255; }
     if (numColRatio == 0.0) numColRatio = 1.0;
     if (seed == 0) {                                              // ArgHandle.cpp:272-276
@@ -243,6 +247,19 @@ int main(int argc, char** argv) {
     CurandStates* curand = mcmcgpuref ? new CurandStates(g->getNNodes(), (long)seed, device) : nullptr;   // main.cu:80
     for (uint32_t i = 0; i < repetitions; i++) {
         std::cout << "Repetition: " << i << std::endl;
+        if (greedyff) {   // main.cu:111-132
+            ColoringGreedyFF<float, float> greedy(g);
+            const auto s0 = std::chrono::steady_clock::now();
+            greedy.run();
+            const double duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+            std::cout << "Parallel Greedy First Fit - number of colors: " << greedy.getColoring()->nCol << std::endl;
+            std::cout << "Parallel Greedy First Fit - elapsed time: " << duration << std::endl;
+            std::ofstream gffFileLog(outDir + "/" + graphName + "-GFF-" + std::to_string(i) + ".log");
+            greedy.saveStats(i, (float)duration, gffFileLog);
+            std::ofstream gffFileColors(outDir + "/" + graphName + "-GFF-" + std::to_string(i) + "-colors.txt");
+            greedy.saveColor(gffFileColors);
+        }
+        if (!mcmcgpu && !mcmcgpuref) continue;
         ColoringMCMCParams params;                                   // main.cu:160-168
         params.numColorRatio = numColorRatio;
         params.nCol = (nCol != 0) ? nCol : (col_sz)(g->getMaxNodeDeg() * numColorRatio);

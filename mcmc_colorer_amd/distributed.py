@@ -19,6 +19,10 @@ tests/test_distributed.py).
 
 The exchange sequence lives in ``PartitionedColoringMCMC``; the per-rank work sits behind a small
 backend interface (``HipRank`` here), which is what lets tests drive the same code over gloo.
+
+torch and libmcmc_hip.so each bring a HIP runtime: initialise torch's device (``torch.cuda`` calls,
+as ``torch.distributed.run`` launches do) before the library is first loaded, or one of the two
+finds no GPU.
 """
 from __future__ import annotations
 

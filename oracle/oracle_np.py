@@ -301,3 +301,55 @@ def rmat(scale: int, edge_factor: int, a: float, b: float, c: float, seed: int):
     off = np.zeros(n + 1, dtype=np.uint64)
     np.add.at(off, rows + 1, 1)
     return np.cumsum(off).astype(np.uint64), (keys & _M32).astype(np.uint32)
+
+
+def greedy_ff(off, idx):
+    """ColoringGreedyFF::run (graph_coloring/coloringGreedyFF.cu:50-84; kernels tentative_coloring
+    :88-129, conflict_detection :134-163, update_coloring_GPU :166-174, check_uncolored_nodes :179-190),
+    restated with numpy, one Jacobi round per loop iteration. Returns (colours, 1-based; rounds).
+
+    Semantics kept from the reference:
+      * every round, each uncoloured node marks the colours of its neighbours (the colouring at the
+        round's start, 0 included) in its row of forbiddenColors by writing its own id; the rows are
+        never cleared, so marks from earlier rounds stay (a sticky forbidden set), and it takes the
+        first colour i >= 1 (i < maxDeg + 1) not marked;
+      * node 0 always takes colour 1 (:99-101; its all-zero row reads as fully marked);
+      * a coloured node with a same-coloured neighbour of smaller id is uncoloured (:154-160);
+      * the loop ends when no node is uncoloured.
+    The reference reads the rows of cudaMalloc'ed (uninitialised) memory; zero-initialised rows are
+    assumed, which is what a fresh allocation returns in practice. Colours stop at maxDeg (i <
+    maxDeg + 1, :17), so a node whose forbidden set fills up (K2: node 1 needs colour 2) never gets
+    one and the reference never returns; this restatement (and the HIP colorer) raise instead,
+    after 4 maxColors + 64 rounds."""
+    off = np.asarray(off, dtype=np.int64)
+    idx = np.asarray(idx, dtype=np.int64)
+    n = len(off) - 1
+    if n == 0:
+        return np.zeros(0, dtype=np.uint32), 0
+    deg = np.diff(off)
+    max_colors = int(deg.max()) + 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+    col = np.zeros(n, dtype=np.int64)
+    temp = np.zeros(n, dtype=np.int64)
+    forb = np.zeros((n, max_colors), dtype=bool)
+    rounds = 0
+    while True:
+        rounds += 1
+        unc = col == 0
+        temp[0] = 1
+        m = unc[rows]
+        forb[rows[m], col[idx[m]]] = True
+        free = ~forb[:, 1:]
+        has = free.any(axis=1)
+        first = np.argmax(free, axis=1) + 1 if max_colors > 1 else np.ones(n, dtype=np.int64)
+        upd = unc & has
+        upd[0] = False
+        temp[upd] = first[upd]
+        col = temp.copy()
+        bad = (col[rows] != 0) & (col[rows] == col[idx]) & (rows > idx)
+        temp[rows[bad]] = 0
+        col = temp.copy()
+        if not (col == 0).any():
+            return col.astype(np.uint32), rounds
+        if rounds > 4 * max_colors + 64:   # a full forbidden set: the reference loops forever here
+            raise RuntimeError("greedy first fit: no progress (a node's forbidden set is full)")

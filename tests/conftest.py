@@ -18,23 +18,29 @@ def pytest_configure(config):
 _TORCH_READY = []
 
 
-@pytest.fixture(autouse=True)
-def _torch_before_library(request):
-    """GPU tests: torch (its own HIP runtime) initialises the device before the product library's
-    runtime does -- in the other order torch finds no GPU, and the partitioned tests hand torch
-    tensors to the library."""
-    if request.node.get_closest_marker("gpu") and not _TORCH_READY:
+def _torch_first():
+    """torch (its own HIP runtime) initialises the device before the product library is even
+    loaded: with the library's HIP runtime loaded or initialised first, one of the two finds no
+    GPU, and the partitioned tests hand torch tensors to the library."""
+    if not _TORCH_READY:
         _TORCH_READY.append(1)
         import torch
 
         if torch.cuda.is_available():
             torch.cuda.init()
+
+
+@pytest.fixture(autouse=True)
+def _torch_before_library(request):
+    if request.node.get_closest_marker("gpu"):
+        _torch_first()
     yield
 
 
 @pytest.fixture(scope="session")
 def hip_lib():
     """The product library; GPU tests fail loudly (no fallback) when it is missing."""
+    _torch_first()   # session fixtures are set up before the autouse one above
     from mcmc_colorer_amd import _lib
 
     return _lib.lib()
