@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 // no per-arc L2 request.
 constexpr uint32_t kTsLog = 17;                                  // 2^17 vertices per LDS tile
 constexpr int kTscanThreads = 1024;
-constexpr uint32_t kTsUnroll = 4;                               // chunks per wave step
+constexpr uint32_t kTsUnroll = 3;                               // chunks per wave step
 constexpr uint32_t kTsCand = 1024;                              // LDS candidate list (8 KiB)
 constexpr uint32_t kTsWin = 1024;                               // row-fingerprint window per wave (bytes)
 constexpr size_t kTscanLds = (size_t)1 << kTsLog;                // 128 KiB of fingerprints
@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) {
+// one workgroup per CU (its LDS): 4 waves per SIMD, so up to 128 VGPRs without spilling
+__global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lfp[];
     __shared__ uint2 cand[kTsCand];   // fingerprint matches (local row, column) of the piece
     __shared__ uint32_t ncand;
@@ -153,18 +154,18 @@ __global__ __launch_bounds__(kTscanThreads) void wide_tscan_kernel(SweepArgs a) 
         __syncthreads();   // the previous piece's reads are done with the tile
         {   // stage the tile: all of a thread's 16-byte loads in flight, then the LDS stores
             const uint32_t nk = (nv + 15u) / 16u;   // fp has 16 bytes of slack past n
-            for (uint32_t k0 = threadIdx.x; k0 < nk; k0 += 8u * blockDim.x) {
-                uint4 tmp[8];
-#pragma unroll
-                for (uint32_t u = 0; u < 8; u++) {
-                    const uint32_t k = k0 + u * blockDim.x;
-                    if (k < nk) tmp[u] = *reinterpret_cast<const uint4*>(fp + v0 + 16u * k);
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < 8; u++) {
-                    const uint32_t k = k0 + u * blockDim.x;
-                    if (k < nk) *reinterpret_cast<uint4*>(lfp + 16u * k) = tmp[u];
-                }
+            const uint32_t bd = blockDim.x;
+            const uint4 z4 = make_uint4(0, 0, 0, 0);
+            for (uint32_t k0 = threadIdx.x; k0 < nk; k0 += 8u * bd) {
+                // eight named registers (an array here was placed in scratch)
+#define MCMC_TS_LD(u) const uint4 t##u = (k0 + (u) * bd < nk) ? *reinterpret_cast<const uint4*>(fp + v0 + 16u * (k0 + (u) * bd)) : z4;
+#define MCMC_TS_ST(u) if (k0 + (u) * bd < nk) *reinterpret_cast<uint4*>(lfp + 16u * (k0 + (u) * bd)) = t##u;
+                MCMC_TS_LD(0) MCMC_TS_LD(1) MCMC_TS_LD(2) MCMC_TS_LD(3)
+                MCMC_TS_LD(4) MCMC_TS_LD(5) MCMC_TS_LD(6) MCMC_TS_LD(7)
+                MCMC_TS_ST(0) MCMC_TS_ST(1) MCMC_TS_ST(2) MCMC_TS_ST(3)
+                MCMC_TS_ST(4) MCMC_TS_ST(5) MCMC_TS_ST(6) MCMC_TS_ST(7)
+#undef MCMC_TS_LD
+#undef MCMC_TS_ST
             }
         }
         __syncthreads();
