@@ -127,9 +127,14 @@ struct SweepArgs {
     const uint32_t* chunk_row;  // [nchunks + 1] first local row of every 256-arc chunk
     uint32_t nchunks;
     uint8_t* wflag;             // [nloc] viol flags of the running sweep (cleared by the evaluation)
-    uint8_t* wfp;               // wide LDS scan: [n] colour fingerprints (low byte) of C_t
-    uint32_t* wlist;            // [nloc] violating, untaboo'd vertices (global ids)
-    uint32_t* wcount;           // their number
+    uint8_t* wfp0;              // wide LDS scan: [n] colour fingerprints (low byte) of colors0 / colors1
+    uint8_t* wfp1;
+    int fp_live;                // 1: the sweep's writers keep the next colouring's fingerprints (no wide_fp_kernel)
+    uint32_t* wlist;            // [2][nloc] violating, untaboo'd vertices (global ids), split-walk slot
+    uint32_t* wcount;           // [4]: violators, -, extra split-walk tasks, slots taken (sweep_wide.h)
+    uint32_t* gmask;            // wide: [kSplitMax][kWideMaskWords] occupancy of split walks (zero between sweeps)
+    uint32_t* gdone;            // wide: [3][kSplitMax] tasks counted per split walk (zero between sweeps), list index, xbase
+    uint32_t split_arcs;        // wide: arcs per task of a split walk
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
     uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
@@ -344,6 +349,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             const uint32_t v = s[i];
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
             Cs[caddr(a, v)] = (CT)c;
+            if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                 a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
         }
@@ -470,6 +476,7 @@ __global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
     __shared__ unsigned long long sh_viol;
     DevState* st = a.st;
     MCMC_COMMIT_PHASE(a, 0);
+    if (a.wcount && threadIdx.x < 4) a.wcount[threadIdx.x] = 0;   // the walk list, for the next sweep
     if (threadIdx.x == 0) {
         sh_done = st->done;
         sh_t = st->t;
@@ -573,6 +580,7 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
     __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
     __shared__ unsigned long long sh_viol;
     DevState* st = a.st;
+    if (threadIdx.x < 4) a.wcount[threadIdx.x] = 0;   // the walk list, for the next sweep
     if (threadIdx.x == 0) {
         sh_done = st->done;
         sh_t = st->t;
@@ -1621,13 +1629,13 @@ using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
 // evaluation one workgroup per 2048 vertices, walk 8 per CU
 void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
     if (a.xs_ent && a.xs_mode == 1) {
-        wide_fp_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 2047u) / 2048u, 4096u)), 256, 0, s>>>(a);
+        if (!a.fp_live)
+            wide_fp_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 2047u) / 2048u, 4096u)), 256, 0, s>>>(a);
         wide_tscan_kernel<<<a.xs_nwg, kTscanThreads, kTscanLds, s>>>(a);
     }
     else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
-    wide_eval_kernel<<<a.evnblk, 256, 0, s>>>(a);
-    wide_walk_kernel<<<g.x * 8u, kWideWalkThreads, 0, s>>>(a);
+    wide_eval_kernel<<<a.evnblk + kWalkBlocks, 256, 0, s>>>(a);
 }
 template <int NW, bool LDSC>
 void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
@@ -1732,9 +1740,11 @@ struct mcmc_ctx {
     uint32_t nchunks = 0;
     uint64_t arc_begin = 0, arc_count = 0;
     uint8_t* wflag = nullptr;
-    uint8_t* wfp = nullptr;       // wide LDS scan: colour fingerprints, n (+2048) bytes
+    uint8_t* wfp[2] = {nullptr, nullptr};   // wide LDS scan: fingerprints of colors[0/1], n (+2048) bytes
     uint32_t* wlist = nullptr;
     uint32_t* wcount = nullptr;
+    uint32_t* gmask = nullptr;      // split walks: masks, then kSplitMax task counters
+    uint32_t split_arcs = kSplitArcs;   // MCMC_SPLIT_ARCS (tests)
     float* etab = nullptr;
     float emax = 0.0f;
     uint16_t* ftab = nullptr;       // F(u) table of the evaluation (ftab_n entries)
@@ -1857,9 +1867,14 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.chunk_row = c->chunk_row;
         a.nchunks = c->nchunks;
         a.wflag = c->wflag;
-        a.wfp = c->wfp;
+        a.wfp0 = c->wfp[0];
+        a.wfp1 = c->wfp[1];
+        a.fp_live = (c->wfp[0] && !c->part) ? 1 : 0;   // partitioned: remote colours arrive by the exchange
         a.wlist = c->wlist;
         a.wcount = c->wcount;
+        a.gmask = c->gmask;
+        a.gdone = c->gmask ? c->gmask + (size_t)kSplitMax * kWideMaskWords : nullptr;
+        a.split_arcs = c->split_arcs;
         a.etab = c->etab;
         a.emax = c->emax;
         a.ftab = c->ftab;
@@ -2300,9 +2315,13 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->arc_count = ends[1] - ends[0];
         c->nchunks = (uint32_t)((c->arc_count + kWideChunk - 1) / kWideChunk);
         if (ew == hipSuccess) ew = hipMalloc(&c->chunk_row, sizeof(uint32_t) * ((size_t)c->nchunks + 1));
-        if (ew == hipSuccess) ew = hipMalloc(&c->wflag, std::max<size_t>(nloc, 1));
-        if (ew == hipSuccess) ew = hipMalloc(&c->wlist, sizeof(uint32_t) * std::max<size_t>(nloc, 1));
-        if (ew == hipSuccess) ew = hipMalloc(&c->wcount, sizeof(uint32_t));
+        if (ew == hipSuccess) ew = hipMalloc(&c->wflag, (nloc + 4u) & ~(size_t)3);   // word atomics (flag_violator)
+        if (ew == hipSuccess) ew = hipMalloc(&c->wlist, 2 * sizeof(uint32_t) * std::max<size_t>(nloc, 1));
+        if (ew == hipSuccess) ew = hipMalloc(&c->wcount, 4 * sizeof(uint32_t));
+        const size_t gmb = sizeof(uint32_t) * ((size_t)kSplitMax * kWideMaskWords + 3 * kSplitMax);
+        if (ew == hipSuccess) ew = hipMalloc(&c->gmask, gmb);
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->gmask, 0, gmb, c->stream);
+        if (const char* e = getenv("MCMC_SPLIT_ARCS")) c->split_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(e, nullptr, 10));
         std::vector<float> et((size_t)p->nCol + 1);
         eps_table(p->epsilon, p->nCol, et.data());
         c->emax = et[p->nCol - 1];
@@ -2329,8 +2348,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMalloc(&c->evblk, sizeof(uint32_t) * kEvSlot * c->evnblk);
         if (ew == hipSuccess) ew = hipMalloc(&c->evcnt, sizeof(uint32_t) * c->evnblk);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->evcnt, 0, sizeof(uint32_t) * c->evnblk, c->stream);
-        if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, std::max<size_t>(nloc, 1), c->stream);
-        if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, sizeof(uint32_t), c->stream);
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, (nloc + 4u) & ~(size_t)3, c->stream);
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, 4 * sizeof(uint32_t), c->stream);
         if (ew == hipSuccess) {
             const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((c->nchunks + 256) / 256, 4096u));
             wide_chunk_row_kernel<<<blocks, 256, 0, c->stream>>>(gd.row_off + v_begin, nloc, c->arc_begin,
@@ -2351,8 +2370,10 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 return rx;
             }
             if (c->xs && c->xs->mode == 1) {
-                ew = hipMalloc(&c->wfp, (size_t)gd.n + 2048);   // slack: tile staging and row windows
-                if (ew == hipSuccess) ew = hipMemset(c->wfp, 0, (size_t)gd.n + 2048);
+                for (int q = 0; q < 2 && ew == hipSuccess; q++) {   // slack: tile staging and row windows
+                    ew = hipMalloc(&c->wfp[q], (size_t)gd.n + 2048);
+                    if (ew == hipSuccess) ew = hipMemset(c->wfp[q], 0, (size_t)gd.n + 2048);
+                }
             }
         }
         if (ew != hipSuccess) {
@@ -2492,6 +2513,12 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * (c->v_end - c->v_begin), c->stream));
     int rc = upload_state(c, 0);
     if (rc) return rc;
+    if (c->wfp[0]) {   // the fingerprints of C_0 (later sweeps' writers keep them when fp_live)
+        SweepArgs a = make_args(c, 0);
+        wide_fp_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((c->n + 2047u) / 2048u, 4096u)), 256, 0, c->stream>>>(a);
+        MCMC_HIP_TRY(hipGetLastError());
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     c->initialized = true;
     c->ran = false;
     return MCMC_OK;
@@ -2856,12 +2883,14 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->hist);
     (void)hipFree(c->chunk_row);
     (void)hipFree(c->wflag);
-    (void)hipFree(c->wfp);
+    (void)hipFree(c->wfp[0]);
+    (void)hipFree(c->wfp[1]);
     (void)hipFree(c->evblk);
     (void)hipFree(c->ftab);
     (void)hipFree(c->evcnt);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
+    (void)hipFree(c->gmask);
     (void)hipFree(c->etab);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);

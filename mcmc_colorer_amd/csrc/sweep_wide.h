@@ -8,9 +8,12 @@
 //   * most vertices are NOT violating, and then fill_p is the "own colour" distribution (cases
 //     (i)/(iii), :402-412, :471-479) whose walk needs only C[v] and u_v -- no occupancy set;
 //   * only violating vertices need the occupancy set and pf (case (ii), :414-420).
-// So a sweep is three launches plus the commit (commit_kernel<uint16_t>):
-//   wide_xscan_kernel  violation flags (violation_count, :329-351) from the XCD-slab edge layout
-//                      (get_xslab below). The column space is cut into 8 slabs of S vertices;
+// So a sweep is two launches plus the commit (commit_kernel<uint16_t>):
+//   wide_tscan_kernel  (default) violation flags (violation_count, :329-351) from the slab edge
+//                      layout with LDS colour-fingerprint tiles (see the kernel); every violator
+//                      found is flagged once (word atomic) and, untaboo'd, listed for a walk.
+//   wide_xscan_kernel  (MCMC_WIDE_SCAN=l2) the same from the XCD-slab edge layout (get_xslab
+//                      below). The column space is cut into 8 slabs of S vertices;
 //                      slab s's entries are read only by workgroups b with b % 8 == s, which share
 //                      one XCD under round-robin dispatch, so the slab's colours (2 S bytes: 1 MiB at
 //                      C5) stay in that XCD's 4 MiB L2 while the entries stream past (placement only
@@ -22,12 +25,13 @@
 //   wide_scan_kernel   fallback (MCMC_WIDE_SCAN=csr, or no layout): arc-parallel pass over the CSR
 //                      in 256-arc chunks, the row of an arc found by binary search.
 //   wide_eval_kernel   lane per vertex, 8 vertices per lane with every load issued up front: viol ->
-//                      Cviol and, untaboo'd, the violator list; otherwise u_v, the own-colour walk
-//                      (a range test, else walk_own; cdf_walk.h), Cstar / taboo / overflow event
-//                      into the workgroup's ordered event list.
-//   wide_walk_kernel   one 256-thread workgroup per violator: occupancy mask of nCol bits in LDS
-//                      (ds_or), word prefix counts, then one wave walks it (walk_mask_pre: the
-//                      first colour passing u found 64 words / 32 colours at a time).
+//                      Cviol; otherwise u_v, the own-colour walk (a range test, the F(u) table, else
+//                      walk_own_tab; cdf_walk.h), Cstar / taboo / overflow event into the
+//                      workgroup's ordered event list. Beside it, in the same launch, kWalkBlocks
+//                      walk workgroups take the violators (walk_tasks): occupancy mask of nCol bits
+//                      in LDS (ds_or), word prefix counts, then one wave walks it (walk_mask_pre:
+//                      the first colour passing u found 64 words / 32 colours at a time); a hub's
+//                      gathers are split over several workgroups through a global mask.
 // All are grid-stride or one-shot and exit at once when the loop is done.
 
 constexpr uint32_t kWideChunk = 256;      // entries (arcs) per wave chunk: 64 lanes x 4
@@ -35,13 +39,49 @@ constexpr uint32_t kWideMaskWords = 2048; // nCol <= 65536
 constexpr uint32_t kWideMaxCol = 65535;
 constexpr int kWideWalkThreads = 256;
 constexpr int kWideEvalPer = 8;           // vertices per evaluation lane
+constexpr uint32_t kSplitArcs = 2048;     // arcs per task of a split walk (SweepArgs::split_arcs)
+constexpr uint32_t kWalkBlocks = 256;     // walk workgroups beside the evaluation
+constexpr uint32_t kSplitMax = 64;        // violators with a global occupancy mask (split walks)
 constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
+
+// Violators. The scans flag vertex l (byte wflag[l]; one atomic per flag decides the first) and
+// list it for a walk unless it is taboo'd (the evaluation keeps those). The walks (fill_p cases
+// (i)/(ii)) run as extra workgroups of the evaluation launch, beside the evaluation proper: task k <
+// count walks violator k (from chunk 0 of its arcs); a violator above split_arcs arcs, while
+// kSplitMax global masks last, takes a slot and nt - 1 more tasks (count + xbase[slot] ...), its
+// arcs dealt out split_arcs per task. wcount: [0] violators, [2..3] one 64-bit word (extra tasks,
+// slots taken) -- zeroed by the commit (the sweep's last kernel) for the next sweep.
+__device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
+    const uint32_t idx = atomicAdd(&a.wcount[0], 1u);
+    uint32_t slot = 0xFFFFFFFFu;
+    if (deg > a.split_arcs) {
+        const uint32_t nx = (uint32_t)((deg + a.split_arcs - 1) / a.split_arcs) - 1u;
+        const unsigned long long r =
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.wcount + 2), (1ull << 32) | (unsigned long long)nx);
+        const uint32_t s = (uint32_t)(r >> 32);
+        if (s < kSplitMax) {   // past kSplitMax: its extra tasks lie beyond every live slot's and do nothing
+            slot = s;
+            a.gdone[kSplitMax + s] = idx;            // sidx
+            a.gdone[2 * kSplitMax + s] = (uint32_t)r; // xbase
+        }
+    }
+    a.wlist[idx] = a.v_begin + l;
+    a.wlist[nloc + idx] = slot;
+}
+__device__ __forceinline__ void flag_violator(const SweepArgs& a, uint32_t l) {
+    if (a.wflag[l]) return;
+    const uint32_t bit = 1u << (8u * (l & 3u));
+    if (atomicOr(reinterpret_cast<uint32_t*>(a.wflag) + (l >> 2), bit) & bit) return;
+    if (a.taboo != nullptr && a.taboo[l] > 0) return;
+    push_violator(a, l);
+}
 
 __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     const uint32_t t = st->t;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     const uint32_t s = blockIdx.x & (kXSlabs - 1u);   // blocks b, b + 8, ... share an XCD: one slab
     const uint32_t wpb = blockDim.x >> 6;
@@ -80,8 +120,8 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             if (e[i] != kXsPad && cr[i] == cc[i]) {   // rare: a monochromatic edge
-                a.wflag[r[i]] = 1;
-                if (a.xs_sym && j[i] - vb < nloc) a.wflag[j[i] - vb] = 1;
+                flag_violator(a, r[i]);
+                if (a.xs_sym && j[i] - vb < nloc) flag_violator(a, j[i] - vb);
             }
         }
         if (!more) break;
@@ -124,7 +164,7 @@ __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
         } else {
             for (uint32_t i = 0; v + i < n; i++) w[i >> 2] |= ((uint32_t)C[caddr(a, v + i)] & 0xFFu) << (8u * (i & 3u));
         }
-        *reinterpret_cast<uint2*>(a.wfp + v) = make_uint2(w[0], w[1]);
+        *reinterpret_cast<uint2*>(((t & 1) ? a.wfp1 : a.wfp0) + v) = make_uint2(w[0], w[1]);
     }
 }
 
@@ -138,9 +178,8 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
     if (a.check_done && st->done) return;
     if (threadIdx.x == 0) ncand = 0;
     const uint32_t t = st->t;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
-    const uint8_t* __restrict__ fp = a.wfp;
+    const uint8_t* __restrict__ fp = (t & 1) ? a.wfp1 : a.wfp0;   // fingerprints of C_t
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
     const uint32_t vb = a.v_begin, nloc = a.v_end - a.v_begin, n = a.n;
     const uint32_t p1 = a.xs_wgp[blockIdx.x + 1];
@@ -243,8 +282,8 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
                         } else {   // list full: settle it here
                             const uint32_t j = v0 + (e[i] & cmask);
                             if (C[caddr(a, vb + r[i])] == C[caddr(a, j)]) {
-                                a.wflag[r[i]] = 1;
-                                if (a.xs_sym && j - vb < nloc) a.wflag[j - vb] = 1;
+                                flag_violator(a, r[i]);
+                                if (a.xs_sym && j - vb < nloc) flag_violator(a, j - vb);
                             }
                         }
                     }
@@ -258,8 +297,8 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
         for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {   // the candidates: compare colours
             const uint2 rc = cand[k];
             if (C[caddr(a, vb + rc.x)] == C[caddr(a, rc.y)]) {
-                a.wflag[rc.x] = 1;
-                if (a.xs_sym && rc.y - vb < nloc) a.wflag[rc.y - vb] = 1;
+                flag_violator(a, rc.x);
+                if (a.xs_sym && rc.y - vb < nloc) flag_violator(a, rc.y - vb);
             }
         }
         __syncthreads();
@@ -271,7 +310,6 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     const uint32_t t = st->t;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.wcount = 0;   // the walk list of this sweep
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     const uint64_t* __restrict__ ro = a.row_off;
     const uint64_t a0 = a.arc_begin, m = a.arc_count;
@@ -306,18 +344,191 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
                 do { r++; rend = ro[r + 1] - a0; } while (rend <= k);
                 own = C[caddr(a, a.v_begin + r)];
             }
-            if (nc[i] == own) a.wflag[r] = 1;
+            if (nc[i] == own) flag_violator(a, r);
         }
     }
 }
 
-// Grid: ceil(nloc / (256 * kWideEvalPer)) workgroups of 256; lane `tid` of workgroup b takes the
-// vertices b * 2048 + j * 256 + tid, j < 8 (coalesced per j).
+// Occupancy of arcs [k0, k1) of N(v) (count_free_colors, coloringMCMC_CPU.cpp:362-383) OR-ed into
+// the LDS mask, 8 independent gathers per thread in flight.
+__device__ __forceinline__ void walk_gather(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t* mask,
+                                            uint64_t k0, uint64_t k1) {
+    for (uint64_t k = k0 + threadIdx.x; k < k1; k += 8u * blockDim.x) {
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t kk = k + (uint64_t)j * blockDim.x;
+            c[j] = kk < k1 ? (uint32_t)C[caddr(a, a.col_idx[kk])] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
+    }
+}
+
+// The resample of violator v (fill_p case (ii) / (i)) from its occupancy mask in LDS, by a whole
+// 256-thread workgroup: word prefix counts, then one wave walks them. `ev` (LDS list + count,
+// capacity cap): where an overflow event goes; past cap, or with ev == nullptr, the global list.
+// All threads call it; it ends with a barrier.
+__device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
+                            uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* wsum,
+                            uint32_t* ev, uint32_t* nev, uint32_t cap) {
+    DevState* st = a.st;
+    const uint32_t NWW = (a.nCol + 31u) >> 5;
+    const uint32_t per = (NWW + kWideWalkThreads - 1u) / kWideWalkThreads;   // words per thread (prefix)
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t l = v - a.v_begin;
+    // pre[w] = occupied colours in words < w: per-thread word runs, wave scan, workgroup offsets
+    const uint32_t w0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) s += __popc(mask[w]);
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - s;
+    for (uint32_t k = 0; k < wave; k++) run += wsum[k];
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
+        pre[w] = run;
+        run += __popc(mask[w]);
+    }
+    if (threadIdx.x == 0) {
+        uint32_t T = 0;
+        for (uint32_t k = 0; k < kWideWalkThreads / 64; k++) T += wsum[k];
+        pre[NWW] = T;
+    }
+    __syncthreads();
+    if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
+        const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
+        const uint32_t cv = C[caddr(a, v)];
+        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1));
+        const float u = minstd_canonical(x);
+        uint32_t nc;
+        if (Zvcomp > 0) {   // case (ii)
+            const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
+            nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
+        } else {            // case (i)
+            nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+        }
+        if (lane == 0) {
+            const bool event = nc == a.nCol;
+            Cs[caddr(a, v)] = (uint16_t)(event ? cv : nc);
+            if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)(event ? cv : nc);
+            if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+            if (event) {
+                const uint32_t k = ev ? atomicAdd(nev, 1u) : cap;
+                if (k < cap) {
+                    ev[k] = v;
+                } else {
+                    const uint32_t idx = atomicAdd(&st->ev_count, 1u);
+                    if (idx < a.ev_cap) a.events[idx] = v;
+                    else atomicOr(&st->err, 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// One violator's whole resample by one workgroup.
+__device__ void walk_violator(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
+                              uint16_t* __restrict__ Cs, uint32_t* mask, uint32_t* pre, uint32_t* wsum, uint32_t* ev,
+                              uint32_t* nev, uint32_t cap) {
+    const uint32_t NWW = (a.nCol + 31u) >> 5;
+    const uint32_t l = v - a.v_begin;
+    for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
+    __syncthreads();
+    walk_gather(a, C, mask, a.row_off[l], a.row_off[l + 1]);
+    __syncthreads();
+    walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, ev, nev, cap);
+}
+
+// The walk workgroups of the evaluation launch: tasks b, b + nb, ... (push_violator). A one-task
+// violator: its whole occupancy mask and walk here. A split violator (a hub, whose gathers would
+// otherwise be one workgroup's serial latency chain): each task ORs its part of the occupancy into
+// the slot's global mask, and the workgroup finishing the last task takes the mask back
+// (atomicExch: read and clear for the next sweep) and walks.
+__device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t t, uint32_t x_t) {
+    __shared__ uint32_t mask[kWideMaskWords];
+    __shared__ uint32_t pre[kWideMaskWords + 1];
+    __shared__ uint32_t wsum[kWideWalkThreads / 64];
+    __shared__ uint32_t sh_last;
+    const uint32_t cnt = a.wcount[0];
+    const uint32_t nx = a.wcount[2], ns = min(a.wcount[3], kSplitMax);
+    const uint32_t T = cnt + nx;
+    if (b >= T) return;
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
+    const uint32_t NWW = (a.nCol + 31u) >> 5;
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint32_t* sidx = a.gdone + kSplitMax;
+    const uint32_t* xbase = a.gdone + 2 * kSplitMax;
+    const uint32_t SA = a.split_arcs;
+    for (uint32_t task = b; task < T; task += nb) {
+        uint32_t idx, c = 0;
+        if (task < cnt) {
+            idx = task;
+        } else {   // extra task j: the slot with the last xbase <= j
+            const uint32_t j = task - cnt;
+            if (ns == 0) break;
+            uint32_t lo = 0, hi = ns;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (xbase[mid] <= j) lo = mid;
+                else hi = mid;
+            }
+            idx = sidx[lo];
+            c = j - xbase[lo] + 1u;
+        }
+        const uint32_t v = a.wlist[idx], slot = a.wlist[nloc + idx], l = v - a.v_begin;
+        if (slot == 0xFFFFFFFFu) {
+            walk_violator(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0);
+            continue;
+        }
+        const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
+        const uint32_t nt = (uint32_t)((re - rb + SA - 1) / SA);
+        if (c >= nt) continue;   // an extra task of a slotless split violator
+        uint32_t* gm = a.gmask + (size_t)slot * kWideMaskWords;
+        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
+        __syncthreads();
+        walk_gather(a, C, mask, rb + (uint64_t)c * SA, min<uint64_t>(re, rb + (uint64_t)(c + 1) * SA));
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x)
+            if (mask[w]) atomicOr(&gm[w], mask[w]);
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t done = atomicAdd(&a.gdone[slot], 1u) + 1u;
+            sh_last = done == nt;
+            if (done == nt) a.gdone[slot] = 0;   // every task of this sweep has counted
+        }
+        __syncthreads();
+        if (sh_last) {
+            __threadfence();
+            for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
+            __syncthreads();
+            walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0);
+        }
+        __syncthreads();   // sh_last and mask are reused by the next task
+    }
+}
+
+// Grid: kWalkBlocks walk workgroups (walk_tasks; first, so that they start at once), then evnblk =
+// ceil(nloc / (256 * kWideEvalPer)) evaluation workgroups of 256; lane `tid` of evaluation
+// workgroup eb takes the vertices eb * 2048 + j * 256 + tid, j < 8 (coalesced per j).
 __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol, sh_nev;
     __shared__ uint32_t sh_ev[kEvSlot];   // this workgroup's overflow events (ordered at the end)
     DevState* st = a.st;
     if (a.check_done && st->done) return;
+    if (blockIdx.x < kWalkBlocks) {   // the walks, beside the evaluation (dispatched first)
+        walk_tasks(a, blockIdx.x, kWalkBlocks, st->t, st->x_t);
+        return;
+    }
+    const uint32_t eb = blockIdx.x - kWalkBlocks;   // evaluation workgroup
     if (threadIdx.x == 0) {
         sh_viol = 0;
         sh_nev = 0;
@@ -328,7 +539,8 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t nloc = a.v_end - a.v_begin;
     const int lane = threadIdx.x & 63;
-    const uint32_t l0 = blockIdx.x * (256u * kWideEvalPer) + threadIdx.x;
+    const uint32_t l0 = eb * (256u * kWideEvalPer) + threadIdx.x;
+    uint8_t* __restrict__ fpn = a.fp_live ? ((t & 1) ? a.wfp0 : a.wfp1) : nullptr;   // fingerprints of C_{t+1}
     uint32_t viol[kWideEvalPer], cv[kWideEvalPer], tab[kWideEvalPer];
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
@@ -345,7 +557,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139); the
     // lane's draw moves by 16807^256 from one j to the next
     const uint32_t a256 = minstd_pow_tab(256);
-    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + blockIdx.x * (256u * kWideEvalPer) +
+    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + eb * (256u * kWideEvalPer) +
                                                                  (threadIdx.x & ~63u) + 1)),
                                kMinstdLanePow[lane]);
     uint32_t xs[kWideEvalPer];
@@ -367,14 +579,15 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         const uint32_t v = a.v_begin + l;
         const float u = minstd_canonical(xs[j]);
         cviol += viol[j];
-        bool event = false, walk = false;
+        bool event = false;
         if (valid) {
             if (viol[j]) a.wflag[l] = 0;
             if (tab[j] > 0) {   // :496-501
                 Cs[caddr(a, v)] = (uint16_t)cv[j];
+                if (fpn) fpn[v] = (uint8_t)cv[j];
                 a.taboo[l] = tab[j] - 1;
             } else if (viol[j]) {
-                walk = true;   // case (i) or (ii): needs the occupancy set
+                // case (i) or (ii): a walk workgroup's (walk_tasks)
             } else {           // case (iii)
                 uint32_t nc;
                 if (tabled && a.emax <= u && u < a.hi) {
@@ -387,15 +600,9 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
                 }
                 event = nc == a.nCol;
                 Cs[caddr(a, v)] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
+                if (fpn) fpn[v] = (uint8_t)(event ? cv[j] : nc);
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
             }
-        }
-        const uint64_t wb = __ballot(walk);
-        if (wb) {
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(a.wcount, (uint32_t)__popcll(wb));
-            b = __shfl(b, 0, 64);
-            if (walk) a.wlist[b + (uint32_t)__popcll(wb & ((1ull << lane) - 1ull))] = v;
         }
         if (event) {   // into this workgroup's LDS list; past kEvSlot, the global list
             const uint32_t k = atomicAdd(&sh_nev, 1u);
@@ -415,95 +622,13 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         const uint32_t v = sh_ev[threadIdx.x];
         uint32_t rk = 0;
         for (uint32_t k = 0; k < ne; k++) rk += sh_ev[k] < v ? 1u : 0u;
-        a.evblk[(size_t)blockIdx.x * kEvSlot + rk] = v;
+        a.evblk[(size_t)eb * kEvSlot + rk] = v;
     }
-    if (threadIdx.x == 0) a.evcnt[blockIdx.x] = ne;
+    if (threadIdx.x == 0) a.evcnt[eb] = ne;
     for (int off = 32; off >= 1; off >>= 1) cviol += __shfl_xor(cviol, off, 64);
     if (lane == 0 && cviol) atomicAdd(&sh_viol, cviol);
     __syncthreads();
     if (threadIdx.x == 0 && sh_viol) atomicAdd(&st->viol, (unsigned long long)sh_viol);
-}
-
-__global__ __launch_bounds__(kWideWalkThreads) void wide_walk_kernel(SweepArgs a) {
-    __shared__ uint32_t mask[kWideMaskWords];
-    __shared__ uint32_t pre[kWideMaskWords + 1];
-    __shared__ uint32_t wsum[kWideWalkThreads / 64];
-    DevState* st = a.st;
-    if (a.check_done && st->done) return;
-    const uint32_t t = st->t, x_t = st->x_t;
-    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
-    uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
-    const uint32_t cnt = *a.wcount;
-    const uint32_t NWW = (a.nCol + 31u) >> 5;
-    const uint32_t per = (NWW + kWideWalkThreads - 1u) / kWideWalkThreads;   // words per thread (prefix)
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const uint32_t v = a.wlist[i];
-        const uint32_t l = v - a.v_begin;
-        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
-        __syncthreads();
-        // count_free_colors (:362-383): occupancy of N(v), 4 independent gathers per thread in flight
-        const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
-        for (uint64_t k = rb + threadIdx.x; k < re; k += 4u * blockDim.x) {
-            uint32_t c[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint64_t kk = k + (uint64_t)j * blockDim.x;
-                c[j] = kk < re ? (uint32_t)C[caddr(a, a.col_idx[kk])] : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
-        }
-        __syncthreads();
-        // pre[w] = occupied colours in words < w: per-thread word runs, wave scan, workgroup offsets
-        const uint32_t w0 = threadIdx.x * per;
-        uint32_t s = 0;
-        for (uint32_t w = w0; w < w0 + per && w < NWW; w++) s += __popc(mask[w]);
-        uint32_t inc = s;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += y;
-        }
-        if (lane == 63u) wsum[wave] = inc;
-        __syncthreads();
-        uint32_t run = inc - s;
-        for (uint32_t k = 0; k < wave; k++) run += wsum[k];
-        for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
-            pre[w] = run;
-            run += __popc(mask[w]);
-        }
-        if (threadIdx.x == 0) {
-            uint32_t T = 0;
-            for (uint32_t k = 0; k < kWideWalkThreads / 64; k++) T += wsum[k];
-            pre[NWW] = T;
-        }
-        __syncthreads();
-        if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
-            const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
-            const uint32_t cv = C[caddr(a, v)];
-            const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1));
-            const float u = minstd_canonical(x);
-            uint32_t nc;
-            if (Zvcomp > 0) {   // case (ii)
-                const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
-                nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
-            } else {            // case (i)
-                nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
-            }
-            if (lane == 0) {
-                const bool event = nc == a.nCol;
-                Cs[caddr(a, v)] = (uint16_t)(event ? cv : nc);
-                if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
-                if (event) {
-                    const uint32_t idx = atomicAdd(&st->ev_count, 1u);
-                    if (idx < a.ev_cap) a.events[idx] = v;
-                    else atomicOr(&st->err, 1u);
-                }
-            }
-        }
-        __syncthreads();
-    }
 }
 
 // First local row of every 256-arc chunk (the row owning the chunk's first arc); entry nchunks =

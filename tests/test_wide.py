@@ -200,6 +200,18 @@ def test_wide_rmat_both_scans(M, monkeypatch, scan):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split_arcs", [7, 64, 1 << 20])
+def test_wide_split_walks(M, monkeypatch, split_arcs):
+    """The walk kernel's tasks: a violator above split_arcs arcs has its gathers dealt out over the
+    grid and merged in a global mask that the last task walks (while kSplitMax masks last; then one
+    workgroup each). Hubs cut into many tasks, more split violators than masks, no split at all."""
+    monkeypatch.setenv("MCMC_SPLIT_ARCS", str(split_arcs))
+    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    run_both(M, off, idx, O.max_deg(off))
+    run_both(M, off, idx, 300, maxRip=25)
+
+
+@pytest.mark.gpu
 def test_wide_asymmetric_csr(M):
     """Directed arcs without their reverse (mcmc_graph_upload accepts any CSR): the slab layout
     must keep every arc and flag only its row (violation_count reads N(v) only, :329-351)."""
