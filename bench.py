@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 KERNELS = {"lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
-           "tiled": "sweep_tiled_kernel", "wide": "wide_scan+wide_eval+wide_walk+commit (one sweep)"}
+           "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)"}
 
 
 def load_traffic(key: str):
@@ -293,7 +293,7 @@ def main() -> int:
     b_fmt, b_ref = info["sweep_bytes"], info["ref_bytes"]
     achieved = b_fmt / (kernel_ms * 1e-3) / 1e9
     variant = info["variant"]
-    key = f"{a.config}/{variant}" if (world == 1 and (a.config == "c3" or n_req == 100000)) else None
+    key = f"{a.config}/{variant}" if (world == 1 and (a.config in ("c3", "c5") or n_req == 100000)) else None
     if key and ref:
         key += "-ref"
     data = {"c2": "synthetic (reference --simulate generator replayed exactly on the GPU)",
