@@ -452,3 +452,59 @@ private:
     uint32_t numColors{0}, rounds{0};
     Coloring coloring;
 };
+
+// ColoringLuby (graph_coloring/coloringLuby.h:17-68): ColoringLuby(Graph*, randStates), run_fast()
+// (coloringLubyFast.cu:21-49), getColoringGPU()->nCol, saveStats / saveColor in the layout of
+// coloringLuby.cu:151-215. randStates: the per-vertex XORWOW states (CurandStates), advanced.
+template <typename nodeW, typename edgeW>
+class ColoringLuby {
+public:
+    ColoringLuby(Graph<nodeW, edgeW>* graph_d, CurandStates* randStates) : graph(graph_d), states(randStates) {}
+    void run_fast() {
+        colors.resize(graph->getNNodes());
+        MCMC_CHECK(mcmc_luby_run(graph->handle(), states->handle(), colors.data(), &numOfColors, &rounds));
+        coloring.nCol = numOfColors;
+        coloring.colClass = colors.data();
+    }
+    void run() { run_fast(); }
+    Coloring* getColoringGPU() { return &coloring; }
+    uint32_t getRounds() const { return rounds; }
+    void saveStats(size_t it, float duration, std::ofstream& outFile) const {
+        outFile << "Luby Colorer - GPU version - Report" << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "GRAPH INFO" << std::endl;
+        outFile << "Nodes: " << graph->getNNodes() << " - Edges: " << graph->getNEdges() << std::endl;
+        outFile << "Max deg: " << graph->getMaxNodeDeg() << " - Min deg: " << graph->getMinNodeDeg()
+                << " - Avg deg: " << graph->getMeanNodeDeg() << std::endl;
+        outFile << "Edge probability (for randomly generated graphs): " << graph->prob << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "EXECUTION INFO" << std::endl;
+        outFile << "Repetition: " << it << std::endl;
+        outFile << "Execution time: " << duration << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "Number of colors: " << numOfColors << std::endl;
+        outFile << "Color histogram:" << std::endl;
+        std::vector<size_t> histBins(numOfColors, 0);   // bins of colours 1..k, printed from index 0
+        for (uint32_t c : colors) histBins[c - 1]++;
+        for (size_t i = 0; i < histBins.size(); i++) outFile << i << ": " << histBins[i] << std::endl;
+        int sum = 0;   // std::accumulate(.., 0): an int sum
+        for (size_t h : histBins) sum += (int)h;
+        const float mean = sum / (float)numOfColors;
+        float variance = 0;
+        for (size_t h : histBins) variance += ((h - mean) * (h - mean));
+        variance /= (float)numOfColors;
+        outFile << "Average number of nodes for each color: " << mean << std::endl;
+        outFile << "Variance: " << variance << std::endl;
+        outFile << "StD: " << sqrtf(variance) << std::endl;
+    }
+    void saveColor(std::ofstream& outfile) const {
+        for (size_t i = 0; i < colors.size(); i++) outfile << i << " " << colors[i] << std::endl;
+    }
+
+private:
+    Graph<nodeW, edgeW>* graph;
+    CurandStates* states;
+    std::vector<uint32_t> colors;
+    uint32_t numOfColors{0}, rounds{0};
+    Coloring coloring;
+};

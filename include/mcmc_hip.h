@@ -226,6 +226,18 @@ int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
  * larger id of a same-coloured pair is uncoloured) until every node is coloured. Deterministic.
  * colors: n host words, 1-based; num_colors = distinct colours; rounds = loop iterations. */
 int mcmc_greedyff_run(const mcmc_graph* g, uint32_t* colors, uint32_t* num_colors, uint32_t* rounds);
+/* The reference's Luby colorer (ColoringLuby::run_fast, graph_coloring/coloringLubyFast.cu:21-174,
+ * `--lubygpu`): one colour per outer round, built as an independent set by inner rounds in which
+ * every node draws curand_uniform from its XORWOW state in `rand` (advanced in place, as the
+ * reference's GPURand states are: set_initial_distr_k, coloringLuby.cu:232-243), candidates with
+ * u < 0.5 are selected, a selected node with a selected neighbour of degree >= its own is dropped
+ * (check_conflicts_fast_k :121-148, on the round's snapshot: the reference's in-place version is
+ * timing-dependent, this is its every-read-before-any-write schedule), and the survivors and their
+ * neighbours leave the candidates (update_eligible_fast_k :150-168). colors: n host words, 1..k;
+ * num_colors = k; rounds = inner rounds. A node that can never survive (self loop) makes the
+ * reference spin; this returns MCMC_E_DEVICE ("no progress") instead. */
+int mcmc_luby_run(const mcmc_graph* g, mcmc_gpurand* rand, uint32_t* colors, uint32_t* num_colors,
+                  uint32_t* rounds);
 
 /* ---- reference-GPU-semantics mode ------------------------------------
  * The per-vertex cuRAND XORWOW states of the reference's GPURand (GPUutils/GPURandomizer.cu:8-13,

@@ -24,7 +24,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: bit-exact fp32 with the reference's (non-FMA) host arithmetic.
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-LIB_SOURCES = ["mcmc_sweep.hip", "graph.hip", "tiled_layout.hip", "refstruct.hip", "tailcut.hip", "refmode.hip", "rmat.hip", "greedyff.hip"]
+LIB_SOURCES = ["mcmc_sweep.hip", "graph.hip", "tiled_layout.hip", "refstruct.hip", "tailcut.hip", "refmode.hip", "rmat.hip", "greedyff.hip", "luby.hip"]
 
 
 def _run(cmd: list[str]) -> None:

@@ -453,3 +453,34 @@ class ColoringGreedyFF:
         """saveColor (coloringGreedyFF.cu:305-310): one "<node> <colour>" line per node."""
         with open(path, "w") as f:
             f.writelines(f"{i} {int(c)}\n" for i, c in enumerate(self.colors))
+
+
+class ColoringLuby:
+    """ColoringLuby (graph_coloring/coloringLuby.h:17-68, ``run_fast`` coloringLubyFast.cu:21-174,
+    ``--lubygpu``): Luby independent sets, one colour per outer round, on the
+    GPU (csrc/luby.hip). ``randStates``: the per-vertex XORWOW states (CurandStates), advanced in
+    place by every inner round's draw, as the reference's GPURand states are. Colours are 1..k."""
+
+    def __init__(self, graph: "Graph", randStates: "CurandStates"):
+        self.graph = graph
+        self.randStates = randStates
+        self.colors = None
+        self.numOfColors = 0
+        self.rounds = 0
+
+    def run_fast(self) -> None:
+        out = np.zeros(self.graph.nNodes, dtype=np.uint32)
+        nc, r = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().mcmc_luby_run(self.graph.handle, self.randStates.handle, u32ptr(out), ctypes.byref(nc),
+                                  ctypes.byref(r)))
+        self.colors, self.numOfColors, self.rounds = out, nc.value, r.value
+
+    run = run_fast
+
+    def getColoringGPU(self) -> tuple[int, np.ndarray]:
+        return self.numOfColors, self.colors
+
+    def saveColor(self, path: str) -> None:
+        """saveColor (coloringLuby.cu:209-215): one "<node> <colour>" line per node."""
+        with open(path, "w") as f:
+            f.writelines(f"{i} {int(c)}\n" for i, c in enumerate(self.colors))

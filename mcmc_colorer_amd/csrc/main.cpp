@@ -11,7 +11,8 @@
 //   with its inner loop fixed (k++; the reference's never returns), at most 1000 passes
 // Outputs <outDir>/<graphName>-MCMC_GPU-<i>.log and -colors.txt per repetition.
 // --mcmccpu is served by the test-infrastructure oracle (oracle/build/mcmc_cpu_ref, same flags);
-// --lubygpu/--grdffgpu/--vffgpu are other colorers, outside this build's scope.
+// --lubygpu (ColoringLuby) and --grdffgpu (ColoringGreedyFF) write <graphName>-LUBY-<i> / -GFF-<i>
+// .log and -colors.txt; --vffgpu is outside this build.
 #include <getopt.h>
 #include <sys/stat.h>
 
@@ -109,6 +110,7 @@ void help(const char* argv0) {
               << "  --mcmcgpu            MCMC colorer on the MI355X (default)\n"
               << "  --mcmcgpu-ref        the reference's GPU colorer semantics (XORWOW, balance-dynamic)\n"
               << "  --grdffgpu           parallel greedy first-fit colorer (ColoringGreedyFF)\n"
+              << "  --lubygpu            Luby independent-set colorer (ColoringLuby::run_fast)\n"
               << "  --nCol N             number of colours (default maxDeg / numColRatio)\n"
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
               << "  --tabooIteration N   taboo iterations (default 0)\n"
@@ -127,7 +129,7 @@ int main(int argc, char** argv) {
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
     bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false,
-         tailcutRepair = false, mcmcgpuref = false, greedyff = false;
+         tailcutRepair = false, mcmcgpuref = false, greedyff = false, lubygpu = false;
     uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
@@ -156,7 +158,8 @@ int main(int argc, char** argv) {
                 case '1': mcmccpu = true; break;
                 case '2': mcmcgpu = true; break;
                 case '4': greedyff = true; break;
-                case '3': case '5': other = true; break;
+                case '3': lubygpu = true; break;
+                case '5': other = true; break;
                 case 'k': if (std::stoi(optarg) < 1) throw 1; nCol = std::stoi(optarg); break;
                 case 'r': numColRatio = std::stod(optarg); if (numColRatio < 1.0 || numColRatio > 16.0) throw 1; break;
                 case 't': if (std::stoi(optarg) < 1) throw 1; tabooIteration = std::stoi(optarg); break;
@@ -188,14 +191,14 @@ int main(int argc, char** argv) {
         return 255;
     }
     if (other) {
-        std::cout << "--lubygpu / --vffgpu are outside this build (see DESIGN.md)" << std::endl;
+        std::cout << "--vffgpu is outside this build (see DESIGN.md)" << std::endl;
         return 255;
     }
     if (mcmcgpu && mcmcgpuref) {
         std::cout << "--mcmcgpu and --mcmcgpu-ref write the same files: choose one" << std::endl;
         return 255;
     }
-    if (!mcmcgpu && !mcmcgpuref && !greedyff) {
+    if (!mcmcgpu && !mcmcgpuref && !greedyff && !lubygpu) {
         std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
         mcmcgpu = true;
     }
@@ -244,9 +247,21 @@ int main(int argc, char** argv) {
               << " - Mean Degree: " << g->getMeanNodeDeg() << "  (graph ready in " << tgen << " s)" << std::endl;
 
     GPURand GPURandGen(g->getNNodes(), (long)seed);
-    CurandStates* curand = mcmcgpuref ? new CurandStates(g->getNNodes(), (long)seed, device) : nullptr;   // main.cu:80
+    CurandStates* curand = (mcmcgpuref || lubygpu) ? new CurandStates(g->getNNodes(), (long)seed, device) : nullptr;   // main.cu:80
     for (uint32_t i = 0; i < repetitions; i++) {
         std::cout << "Repetition: " << i << std::endl;
+        if (lubygpu) {   // main.cu:89-109 (first: it advances the shared states)
+            ColoringLuby<float, float> colLuby(g, curand);
+            const auto s0 = std::chrono::steady_clock::now();
+            colLuby.run_fast();
+            const double duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+            std::cout << "LubyGPU - number of colors: " << colLuby.getColoringGPU()->nCol << std::endl;
+            std::cout << "LubyGPU elapsed time: " << duration << std::endl;
+            std::ofstream lubyFileLog(outDir + "/" + graphName + "-LUBY-" + std::to_string(i) + ".log");
+            colLuby.saveStats(i, (float)duration, lubyFileLog);
+            std::ofstream lubyFileColors(outDir + "/" + graphName + "-LUBY-" + std::to_string(i) + "-colors.txt");
+            colLuby.saveColor(lubyFileColors);
+        }
         if (greedyff) {   // main.cu:111-132
             ColoringGreedyFF<float, float> greedy(g);
             const auto s0 = std::chrono::steady_clock::now();
@@ -270,7 +285,7 @@ int main(int argc, char** argv) {
         params.tabooIteration = tabooIteration;
         params.tailcut = tailcut;
         params.tailcutRepair = tailcutRepair ? 1000u : 0u;
-        if (curand) {
+        if (mcmcgpuref) {
             ColoringMCMCGpuRef<float, float> colRef(g, curand, params);
             colRef.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));
             colRef.run((int)i);

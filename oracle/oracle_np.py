@@ -353,3 +353,67 @@ def greedy_ff(off, idx):
             return col.astype(np.uint32), rounds
         if rounds > 4 * max_colors + 64:   # a full forbidden set: the reference loops forever here
             raise RuntimeError("greedy first fit: no progress (a node's forbidden set is full)")
+
+
+def xorwow_step(states):
+    """One curand() call on every state at once (xorwow: cuRAND's device header, restated in
+    mcmc_colorer_amd/csrc/xorwow.h and pinned by tests/test_xorwow.py). states: [n][6] uint32
+    {v0..v4, d}, advanced in place; returns the outputs."""
+    s = states
+    t = s[:, 0] ^ (s[:, 0] >> np.uint32(2))
+    s[:, 0:4] = s[:, 1:5].copy()
+    s[:, 4] = (s[:, 4] ^ (s[:, 4] << np.uint32(4))) ^ (t ^ (t << np.uint32(1)))
+    s[:, 5] = s[:, 5] + np.uint32(362437)
+    return s[:, 4] + s[:, 5]
+
+
+def curand_uniform(x):
+    """curand_uniform: x 2^-32 + 2^-33 in fp32, the product exact, one rounding of the sum."""
+    return x.astype(F32) * F32(2.0 ** -32) + F32(2.0 ** -33)
+
+
+def luby(off, idx, states, max_stale: int = 100000):
+    """ColoringLuby::run_fast (graph_coloring/coloringLubyFast.cu:21-110: fast_colorer_k's loops;
+    kernels prune_eligible_clear_is :112-118, set_initial_distr_k coloringLuby.cu:232-243,
+    check_conflicts_fast_k :121-148, update_eligible_fast_k :150-168, check_finished_k
+    coloringLuby.cu:316-324, add_color_and_check_uncolored_k :328-341), restated with numpy.
+    states: [n][6] uint32 per-node XORWOW states (GPURand), advanced in place -- every node draws
+    once per inner round. Returns (colours 1..k, k, inner rounds).
+
+    The conflict step reads the round's selection snapshot (the reference clears flags in place,
+    so its result depends on thread timing; this is its schedule with every read before every
+    write): a selected node survives iff no selected neighbour has degree >= its own. A candidate
+    that can never survive (a self loop) makes the reference spin; this raises after max_stale
+    rounds without a survivor."""
+    off = np.asarray(off, dtype=np.int64)
+    idx = np.asarray(idx, dtype=np.int64)
+    n = len(off) - 1
+    deg = np.diff(off)
+    rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+    coloring = np.zeros(n, dtype=np.uint32)
+    k = rounds = 0
+    if n == 0:
+        return coloring, 0, 0
+    while True:
+        cand = coloring == 0
+        is_ = np.zeros(n, dtype=bool)
+        stale = 0
+        while True:
+            rounds += 1
+            u = curand_uniform(xorwow_step(states))
+            sel = (u < F32(0.5)) & cand
+            clash = sel[rows] & sel[idx] & (deg[rows] <= deg[idx])
+            keep = sel.copy()
+            keep[rows[clash]] = False
+            is_ |= keep
+            cand &= ~keep
+            cand[idx[keep[rows]]] = False
+            if not cand.any():
+                break
+            stale = 0 if keep.any() else stale + 1
+            if stale > max_stale:
+                raise RuntimeError("Luby: no progress")
+        k += 1
+        coloring[is_] = k
+        if not (coloring == 0).any():
+            return coloring, k, rounds
