@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iostream>
 #include <string>
 #include <vector>
 
@@ -506,5 +507,66 @@ private:
     CurandStates* states;
     std::vector<uint32_t> colors;
     uint32_t numOfColors{0}, rounds{0};
+    Coloring coloring;
+};
+
+// ColoringVFF (graph_coloring/coloringVFF.h:8-48): ColoringVFF(Graph*), run() (greedy first fit,
+// then the rebalancing), getColoring()->nCol / colClass, saveStats / saveColor in the layout of
+// coloringVFF.cu:437-490 (saveStats prints "Valid result? (boolean)" = not_looping).
+template <typename nodeW, typename edgeW>
+class ColoringVFF {
+public:
+    explicit ColoringVFF(Graph<nodeW, edgeW>* graph_d) : graph(graph_d) {}
+    void run() {
+        colors.resize(graph->getNNodes());
+        int v = 1;
+        MCMC_CHECK(mcmc_vff_run(graph->handle(), colors.data(), &numColors, &iterations, &v));
+        notLooping = v != 0;
+        if (!notLooping) std::cout << "Rebalancing failed. Coloring resetted to Greedy First Fit.\n\n";
+        coloring.nCol = numColors;
+        coloring.colClass = colors.data();
+    }
+    Coloring* getColoring() { return &coloring; }
+    uint32_t getIterations() const { return iterations; }
+    bool isValid() const { return notLooping; }
+    void saveStats(size_t iteration, float duration, std::ofstream& file) const {
+        file << "Greedy FF Colorer followed by Vertex First Fit Rebalancing - GPU implementation - Report\n";
+        file << "-------------------------------------------\n";
+        file << "GRAPH INFO\n";
+        file << "Nodes: " << graph->getNNodes() << " - Edges: " << graph->getNEdges() << "\n";
+        file << "Max deg: " << graph->getMaxNodeDeg() << " - Min deg: " << graph->getMinNodeDeg()
+             << " - Avg deg: " << graph->getMeanNodeDeg() << "\n";
+        file << "Edge Probability (for randomly generated graphs): " << graph->prob << "\n";
+        file << "-------------------------------------------\n";
+        file << "EXECUTION INFO\n";
+        file << "Repetition: " << iteration << "\n";
+        file << "Execution time: " << duration << "\n";
+        file << "Valid result? (boolean) " << notLooping << "\n";
+        file << "-------------------------------------------\n";
+        file << "Number of colors: " << numColors << "\n";
+        file << "Color histogram: \n";
+        std::vector<uint32_t> histogram(numColors, 0);   // convert_to_standard_notation's class sizes
+        for (uint32_t c : colors)
+            if (c >= 1 && c <= numColors) histogram[c - 1]++;
+        for (uint32_t i = 1; i < numColors + 1; ++i) file << i << "\t: " << histogram[i - 1] << "\n";
+        int sum = 0;   // std::accumulate(.., 0): an int sum
+        for (uint32_t h : histogram) sum += (int)h;
+        const float mean = sum / static_cast<float>(numColors);
+        float variance = 0;
+        for (uint32_t h : histogram) variance += (h - mean) * (h - mean);
+        variance /= static_cast<float>(numColors);
+        file << "Average number of nodes for each color: " << mean << "\n";
+        file << "Variance: " << variance << "\n";
+        file << "StD: " << sqrtf(variance) << "\n";
+    }
+    void saveColor(std::ofstream& file) const {
+        for (uint32_t i = 0; i < graph->getNNodes(); ++i) file << i << " " << colors[i] << "\n";
+    }
+
+private:
+    Graph<nodeW, edgeW>* graph;
+    std::vector<uint32_t> colors;
+    uint32_t numColors{0}, iterations{0};
+    bool notLooping{true};
     Coloring coloring;
 };

@@ -226,6 +226,17 @@ int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
  * larger id of a same-coloured pair is uncoloured) until every node is coloured. Deterministic.
  * colors: n host words, 1-based; num_colors = distinct colours; rounds = loop iterations. */
 int mcmc_greedyff_run(const mcmc_graph* g, uint32_t* colors, uint32_t* num_colors, uint32_t* rounds);
+/* The reference's greedy colorer followed by its rebalancing (ColoringVFF::run,
+ * graph_coloring/coloringVFF.cu:50-228, `--vffgpu`): the GreedyFF rounds, then iterations in which
+ * every unbalanced node (its colour's bin holds more than gamma = n / numColors nodes) other than
+ * node 0 moves to the first colour not used by itself or a neighbour whose bin holds MORE than
+ * gamma nodes (the reference's test, as written), bins are recounted, and a node stays unbalanced
+ * only while a neighbour of smaller id shares its new colour; until none is unbalanced or the
+ * unbalanced set repeats for nine snapshots (ensure_not_looping; then the result is the greedy
+ * colouring and *valid = 0). colors: n host words, 1..numColors; iterations = rebalancing
+ * iterations. Greedy colours that are not 1..numColors (the reference reads past its bins) and a
+ * cycle the history misses (the reference spins) return MCMC_E_DEVICE. */
+int mcmc_vff_run(const mcmc_graph* g, uint32_t* colors, uint32_t* num_colors, uint32_t* iterations, int* valid);
 /* The reference's Luby colorer (ColoringLuby::run_fast, graph_coloring/coloringLubyFast.cu:21-174,
  * `--lubygpu`): one colour per outer round, built as an independent set by inner rounds in which
  * every node draws curand_uniform from its XORWOW state in `rand` (advanced in place, as the

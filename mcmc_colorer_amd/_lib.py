@@ -32,6 +32,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_color_bytes": (c_uint32, [c_uint32]),
     "mcmc_greedyff_run": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
     "mcmc_luby_run": (c_int, [c_void_p, c_void_p, _u32p, _u32p, _u32p]),
+    "mcmc_vff_run": (c_int, [c_void_p, _u32p, _u32p, _u32p, POINTER(c_int)]),
     "mcmc_graph_device_ptrs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "mcmc_graph_download": (c_int, [c_void_p, _u64p, _u32p]),
     "mcmc_graph_destroy": (None, [c_void_p]),

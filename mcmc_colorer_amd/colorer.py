@@ -455,6 +455,34 @@ class ColoringGreedyFF:
             f.writelines(f"{i} {int(c)}\n" for i, c in enumerate(self.colors))
 
 
+class ColoringVFF:
+    """ColoringVFF (graph_coloring/coloringVFF.h/.cu, ``--vffgpu``): the
+    greedy first-fit colouring, then the reference's vertex-first-fit rebalancing, on the GPU
+    (csrc/greedyff.hip). ``valid`` is the reference's not_looping: False when the rebalancing was
+    found looping, and the colouring is then the greedy one."""
+
+    def __init__(self, graph: "Graph"):
+        self.graph = graph
+        self.colors = None
+        self.numColors = 0
+        self.iterations = 0
+        self.valid = True
+
+    def run(self) -> None:
+        out = np.zeros(self.graph.nNodes, dtype=np.uint32)
+        nc, it, v = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        check(lib().mcmc_vff_run(self.graph.handle, u32ptr(out), ctypes.byref(nc), ctypes.byref(it), ctypes.byref(v)))
+        self.colors, self.numColors, self.iterations, self.valid = out, nc.value, it.value, bool(v.value)
+
+    def getColoring(self) -> tuple[int, np.ndarray]:
+        return self.numColors, self.colors
+
+    def saveColor(self, path: str) -> None:
+        """saveColor (coloringVFF.cu:484-490): one "<node> <colour>" line per node."""
+        with open(path, "w") as f:
+            f.writelines(f"{i} {int(c)}\n" for i, c in enumerate(self.colors))
+
+
 class ColoringLuby:
     """ColoringLuby (graph_coloring/coloringLuby.h:17-68, ``run_fast`` coloringLubyFast.cu:21-174,
     ``--lubygpu``): Luby independent sets, one colour per outer round, on the

@@ -11,8 +11,8 @@
 //   with its inner loop fixed (k++; the reference's never returns), at most 1000 passes
 // Outputs <outDir>/<graphName>-MCMC_GPU-<i>.log and -colors.txt per repetition.
 // --mcmccpu is served by the test-infrastructure oracle (oracle/build/mcmc_cpu_ref, same flags);
-// --lubygpu (ColoringLuby) and --grdffgpu (ColoringGreedyFF) write <graphName>-LUBY-<i> / -GFF-<i>
-// .log and -colors.txt; --vffgpu is outside this build.
+// --lubygpu (ColoringLuby), --grdffgpu (ColoringGreedyFF) and --vffgpu (ColoringVFF) write
+// <graphName>-LUBY-<i> / -GFF-<i> / -VFF-<i> .log and -colors.txt.
 #include <getopt.h>
 #include <sys/stat.h>
 
@@ -111,6 +111,7 @@ void help(const char* argv0) {
               << "  --mcmcgpu-ref        the reference's GPU colorer semantics (XORWOW, balance-dynamic)\n"
               << "  --grdffgpu           parallel greedy first-fit colorer (ColoringGreedyFF)\n"
               << "  --lubygpu            Luby independent-set colorer (ColoringLuby::run_fast)\n"
+              << "  --vffgpu             greedy first fit + vertex-first-fit rebalancing (ColoringVFF)\n"
               << "  --nCol N             number of colours (default maxDeg / numColRatio)\n"
               << "  --numColRatio R      1.0 <= R <= 16.0 (default 1.0)\n"
               << "  --tabooIteration N   taboo iterations (default 0)\n"
@@ -128,8 +129,8 @@ int main(int argc, char** argv) {
     std::string graphFilename, outDir;
     double prob = 0.0, numColRatio = 0.0;
     uint32_t n = 0, nCol = 0, seed = 0, repetitions = 1, tabooIteration = 0;
-    bool simulate = false, mcmccpu = false, mcmcgpu = false, other = false, tailcut = false, fast = false,
-         tailcutRepair = false, mcmcgpuref = false, greedyff = false, lubygpu = false;
+    bool simulate = false, mcmccpu = false, mcmcgpu = false, tailcut = false, fast = false,
+         tailcutRepair = false, mcmcgpuref = false, greedyff = false, lubygpu = false, vffgpu = false;
     uint64_t erSeed = 1;
     int device = 0;
     const struct option longopts[] = {
@@ -159,7 +160,7 @@ int main(int argc, char** argv) {
                 case '2': mcmcgpu = true; break;
                 case '4': greedyff = true; break;
                 case '3': lubygpu = true; break;
-                case '5': other = true; break;
+                case '5': vffgpu = true; break;
                 case 'k': if (std::stoi(optarg) < 1) throw 1; nCol = std::stoi(optarg); break;
                 case 'r': numColRatio = std::stod(optarg); if (numColRatio < 1.0 || numColRatio > 16.0) throw 1; break;
                 case 't': if (std::stoi(optarg) < 1) throw 1; tabooIteration = std::stoi(optarg); break;
@@ -190,15 +191,11 @@ int main(int argc, char** argv) {
                   << std::endl;
         return 255;
     }
-    if (other) {
-        std::cout << "--vffgpu is outside this build (see DESIGN.md)" << std::endl;
-        return 255;
-    }
     if (mcmcgpu && mcmcgpuref) {
         std::cout << "--mcmcgpu and --mcmcgpu-ref write the same files: choose one" << std::endl;
         return 255;
     }
-    if (!mcmcgpu && !mcmcgpuref && !greedyff && !lubygpu) {
+    if (!mcmcgpu && !mcmcgpuref && !greedyff && !lubygpu && !vffgpu) {
         std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
         mcmcgpu = true;
     }
@@ -273,6 +270,18 @@ int main(int argc, char** argv) {
             greedy.saveStats(i, (float)duration, gffFileLog);
             std::ofstream gffFileColors(outDir + "/" + graphName + "-GFF-" + std::to_string(i) + "-colors.txt");
             greedy.saveColor(gffFileColors);
+        }
+        if (vffgpu) {   // main.cu:134-158
+            ColoringVFF<float, float> balanced(g);
+            const auto s0 = std::chrono::steady_clock::now();
+            balanced.run();
+            const double duration = std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+            std::cout << "Vertex-centric First Fit rebalancing after Greedy FF coloring - number of colors: " << balanced.getColoring()->nCol << std::endl;
+            std::cout << "Vertex-centric First Fit rebalancing after Greedy FF coloring - elapsed time: " << duration << std::endl;
+            std::ofstream vffFileLog(outDir + "/" + graphName + "-VFF-" + std::to_string(i) + ".log");
+            balanced.saveStats(i, (float)duration, vffFileLog);
+            std::ofstream vffFileColors(outDir + "/" + graphName + "-VFF-" + std::to_string(i) + "-colors.txt");
+            balanced.saveColor(vffFileColors);
         }
         if (!mcmcgpu && !mcmcgpuref) continue;
         ColoringMCMCParams params;                                   // main.cu:160-168

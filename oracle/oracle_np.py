@@ -417,3 +417,74 @@ def luby(off, idx, states, max_stale: int = 100000):
         coloring[is_] = k
         if not (coloring == 0).any():
             return coloring, k, rounds
+
+
+def vff(off, idx, max_iter: int = 100000):
+    """ColoringVFF::run (graph_coloring/coloringVFF.cu: run :50-56, run_coloring :58-99 -- the
+    GreedyFF rounds, restated by greedy_ff above -- run_balancing :101-228, kernels
+    detect_unbalanced_nodes :300-311, is_unbalanced :314-323, tentative_rebalancing :326-365,
+    update_bins :368-383, solve_conflicts :386-409, ensure_not_looping :412-434), restated with
+    numpy. Returns (colours, numColors, balancing iterations, valid).
+
+    Kept from the reference: numColors = distinct greedy colours, gamma = n // numColors; a node is
+    unbalanced when its colour's bin holds more than gamma nodes; each iteration an unbalanced node
+    forbids its own and its neighbours' colours (of the iteration's input colouring) and moves to
+    the first colour 1..numColors not forbidden whose bin (sizes of the previous iteration) holds
+    MORE than gamma nodes -- the reference's test, kept as written; node 0's forbidden row is
+    flagged with 0, the memset value, so it never moves; then bins are recounted, and an unbalanced
+    node stops being unbalanced unless a neighbour of smaller id has its new colour (its colour is
+    not reverted). The loop stops when no node is unbalanced or when the unbalanced set has been
+    the same for nine snapshots, the ten-row history starting all-false (ensure_not_looping): then
+    the result is the greedy colouring and valid is False -- also when one iteration balances
+    everything, since the history is then all-false. Deviations: greedy colours that are not
+    1..numColors make the reference read past its bins and forbidden rows; this raises instead, as
+    it does after max_iter iterations (a cycle longer than the history never ends there)."""
+    off = np.asarray(off, dtype=np.int64)
+    idx = np.asarray(idx, dtype=np.int64)
+    n = len(off) - 1
+    gff, _ = greedy_ff(off, idx)
+    if n == 0:
+        return gff, 0, 0, True
+    gff = gff.astype(np.int64)
+    ncol = len(np.unique(gff))
+    if gff.max() != ncol or gff.min() < 1:
+        raise RuntimeError("VFF: greedy colours are not 1..numColors")
+    deg = np.diff(off)
+    rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+    gamma = n // ncol
+    bins = np.bincount(gff, minlength=ncol + 1)
+    bins[0] = 0
+    unb = gamma < bins[gff]
+    coloring = gff.copy()
+    hist = [np.zeros(n, dtype=bool) for _ in range(8)]   # the 8 previous snapshots, oldest first
+    it = 0
+    valid = True
+    while unb.any() and valid:
+        it += 1
+        if it > max_iter:
+            raise RuntimeError("VFF: no progress")
+        temp = coloring.copy()
+        over = gamma < bins                                  # bins[0] = 0: colour 0 never qualifies
+        movers = np.nonzero(unb)[0]
+        movers = movers[movers != 0]
+        if len(movers):
+            forb = np.zeros((n, ncol + 1), dtype=bool)
+            forb[movers, coloring[movers]] = True
+            m = unb[rows] & (rows != 0)
+            forb[rows[m], coloring[idx[m]]] = True
+            ok = ~forb[movers] & over[None, :]
+            ok[:, 0] = False
+            has = ok.any(axis=1)
+            temp[movers[has]] = np.argmax(ok[has], axis=1)
+        bins = np.bincount(temp, minlength=ncol + 1)
+        bins[0] = 0
+        clash = unb[rows] & (temp[rows] == temp[idx]) & (rows > idx)
+        stay = np.zeros(n, dtype=bool)
+        stay[rows[clash]] = True
+        unb = unb & stay
+        coloring = temp
+        if all(np.array_equal(unb, h) for h in hist):
+            valid = False
+        hist = hist[1:] + [unb.copy()]
+    out = coloring if valid else gff
+    return out.astype(np.uint32), ncol, it, valid
