@@ -11,6 +11,12 @@ Reference lines restated (paths relative to /root/reference/src):
   graph_coloring/coloringMCMC_CPU.cpp   ctor :53-61, run :115-270, violation_count :329-351,
                                         count_free_colors :362-383, fill_p :393-481,
                                         extract_new_color :493-528
+  graph_coloring/coloringGreedyFF.cu    run :50-84 and its kernels (greedy_ff)
+  graph_coloring/coloringLubyFast.cu    run_fast / fast_colorer_k and the Luby kernels (luby,
+  graph_coloring/coloringLuby.cu        with xorwow_step / curand_uniform for GPURand's states)
+  graph_coloring/coloringVFF.cu         run, run_balancing and its kernels (vff)
+Also the build's own generators (er_fast: csrc/er_gen.h; rmat: the C5 stand-in), which have no
+reference counterpart. The colorer restatements are vectorised numpy (n up to a few thousand).
 """
 from __future__ import annotations
 
