@@ -15,7 +15,8 @@
 // the flags are read from the draw's snapshot and the survivors written to a second array. It is
 // one of the reference's possible executions, deterministic, and always an independent set.
 // The reference's fast_colorer_k drives the rounds with device-side launches (dynamic
-// parallelism); here the host drives them, one flag read-back per inner round as in run().
+// parallelism); here every kernel of a round reads a device control block (LubyCtl) and returns
+// once the loop is over, so the host enqueues rounds in batches and reads the block once per batch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,13 +29,32 @@ namespace mcmc {
 namespace {
 
 constexpr int kLubyThreads = 256;
+constexpr uint32_t kLubyBatch = 32;   // rounds enqueued per host check
 
-// set_initial_distr_k: every node advances its state once; sel = u < 0.5 && cand. Flags `left`
-// when a candidate exists (the inner loop's check_finished_k of the previous round is folded here:
-// the host reads it after the round's update).
+// The round loop's state, on the device: every kernel of a round returns at once when `finished`,
+// so rounds are enqueued in batches and the host reads this block once per batch.
+struct LubyCtl {
+    uint32_t finished;   // no node left uncoloured (or an error)
+    uint32_t left;       // this round: a candidate is left (check_finished_k)
+    uint32_t grew;       // this round: the independent set gained a node
+    uint32_t k;          // colours given so far
+    uint32_t r;          // inner rounds run
+    uint32_t stale;      // consecutive inner rounds without a survivor
+    uint32_t unc;        // after a colour: a node is still uncoloured
+    uint32_t err;        // no progress
+};
+
+// set_initial_distr_k: every node advances its state once; sel = u < 0.5 && cand. Opens the
+// round in the control block (round count, cleared left / grew flags).
 __global__ __launch_bounds__(kLubyThreads) void luby_draw_kernel(uint32_t n, uint32_t* __restrict__ st,
                                                                  const uint8_t* __restrict__ cand,
-                                                                 uint8_t* __restrict__ sel) {
+                                                                 uint8_t* __restrict__ sel, LubyCtl* ctl) {
+    if (ctl->finished) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->r++;
+        ctl->left = 0;
+        ctl->grew = 0;
+    }
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         xw::State s;
 #pragma unroll
@@ -53,7 +73,8 @@ __global__ __launch_bounds__(kLubyThreads) void luby_draw_kernel(uint32_t n, uin
 __global__ __launch_bounds__(kLubyThreads) void luby_conflict_kernel(const uint64_t* __restrict__ ro,
                                                                      const uint32_t* __restrict__ col, uint32_t n,
                                                                      const uint8_t* __restrict__ sel,
-                                                                     uint8_t* __restrict__ keep) {
+                                                                     uint8_t* __restrict__ keep, const LubyCtl* ctl) {
+    if (ctl->finished) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < n; v += nw) {
@@ -77,7 +98,9 @@ __global__ __launch_bounds__(kLubyThreads) void luby_conflict_kernel(const uint6
 __global__ __launch_bounds__(kLubyThreads) void luby_update_kernel(const uint64_t* __restrict__ ro,
                                                                    const uint32_t* __restrict__ col, uint32_t n,
                                                                    const uint8_t* __restrict__ keep,
-                                                                   uint8_t* __restrict__ cand, uint8_t* __restrict__ is) {
+                                                                   uint8_t* __restrict__ cand, uint8_t* __restrict__ is,
+                                                                   const LubyCtl* ctl) {
+    if (ctl->finished) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < n; v += nw) {
@@ -92,21 +115,25 @@ __global__ __launch_bounds__(kLubyThreads) void luby_update_kernel(const uint64_
 
 // check_finished_k: *left = 1 if a candidate is left; *grew = 1 if the set gained a node this round.
 __global__ __launch_bounds__(kLubyThreads) void luby_check_kernel(uint32_t n, const uint8_t* __restrict__ cand,
-                                                                  const uint8_t* __restrict__ keep, uint32_t* flags) {
+                                                                  const uint8_t* __restrict__ keep, LubyCtl* ctl) {
+    if (ctl->finished) return;
     bool c = false, g = false;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         c |= cand[v] != 0;
         g |= keep[v] != 0;
     }
-    if (__ballot(c) && (threadIdx.x & 63u) == 0) flags[0] = 1;
-    if (__ballot(g) && (threadIdx.x & 63u) == 0) flags[1] = 1;
+    if (__ballot(c) && (threadIdx.x & 63u) == 0) ctl->left = 1;
+    if (__ballot(g) && (threadIdx.x & 63u) == 0) ctl->grew = 1;
 }
 
-// add_color_and_check_uncolored_k then prune_eligible_clear_is for the next colour: coloring[is] =
-// k; cand = uncoloured; is = 0; flags[2] = 1 if a node is uncoloured.
-__global__ __launch_bounds__(kLubyThreads) void luby_color_kernel(uint32_t n, uint32_t k, uint32_t* __restrict__ coloring,
+// When the round left no candidate: add_color_and_check_uncolored_k then prune_eligible_clear_is
+// for the next colour: coloring[is] = k + 1; cand = uncoloured; is = 0; unc = 1 if a node is
+// uncoloured.
+__global__ __launch_bounds__(kLubyThreads) void luby_color_kernel(uint32_t n, uint32_t* __restrict__ coloring,
                                                                   uint8_t* __restrict__ is, uint8_t* __restrict__ cand,
-                                                                  uint32_t* flags) {
+                                                                  LubyCtl* ctl) {
+    if (ctl->finished || ctl->left) return;
+    const uint32_t k = ctl->k + 1u;   // ctl->k moves in luby_tick_kernel, after every block has read it
     bool u = false;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         uint32_t c = coloring[v];
@@ -115,7 +142,24 @@ __global__ __launch_bounds__(kLubyThreads) void luby_color_kernel(uint32_t n, ui
         cand[v] = c == 0 ? 1 : 0;
         u |= c == 0;
     }
-    if (__ballot(u) && (threadIdx.x & 63u) == 0) flags[2] = 1;
+    if (__ballot(u) && (threadIdx.x & 63u) == 0) ctl->unc = 1;
+}
+
+// The loop control of the round (fast_colorer_k's while / do-while): one thread.
+__global__ void luby_tick_kernel(LubyCtl* ctl) {
+    if (ctl->finished) return;
+    if (ctl->left) {   // the inner loop goes on
+        ctl->stale = ctl->grew ? 0u : ctl->stale + 1u;
+        if (ctl->stale > 100000u) {   // a self-loop node can never survive its own check: the reference spins
+            ctl->err = 1;
+            ctl->finished = 1;
+        }
+        return;
+    }
+    ctl->k++;
+    ctl->stale = 0;
+    if (!ctl->unc) ctl->finished = 1;
+    ctl->unc = 0;
 }
 
 }  // namespace
@@ -137,8 +181,8 @@ extern "C" int mcmc_luby_run(const mcmc_graph* g, mcmc_gpurand* rand, uint32_t* 
     MCMC_HIP_TRY(hipSetDevice(gd.device));
     uint32_t* C = nullptr;
     uint8_t* b = nullptr;   // cand | sel | keep | is, n bytes each
-    uint32_t* flags = nullptr;
-    auto cleanup = [&]() { (void)hipFree(C); (void)hipFree(b); (void)hipFree(flags); };
+    LubyCtl* ctl = nullptr;
+    auto cleanup = [&]() { (void)hipFree(C); (void)hipFree(b); (void)hipFree(ctl); };
 #define LTRY(expr)                                                                                  \
     do {                                                                                            \
         hipError_t _e = (expr);                                                                     \
@@ -149,7 +193,8 @@ extern "C" int mcmc_luby_run(const mcmc_graph* g, mcmc_gpurand* rand, uint32_t* 
     } while (0)
     LTRY(hipMalloc(&C, sizeof(uint32_t) * n));
     LTRY(hipMalloc(&b, 4ull * n));
-    LTRY(hipMalloc(&flags, 4 * sizeof(uint32_t)));
+    LTRY(hipMalloc(&ctl, sizeof(LubyCtl)));
+    LTRY(hipMemset(ctl, 0, sizeof(LubyCtl)));
     uint8_t *cand = b, *sel = b + n, *keep = b + 2ull * n, *is = b + 3ull * n;
     LTRY(hipMemset(C, 0, sizeof(uint32_t) * n));   // run_fast :30-33
     LTRY(hipMemset(is, 0, n));
@@ -157,32 +202,25 @@ extern "C" int mcmc_luby_run(const mcmc_graph* g, mcmc_gpurand* rand, uint32_t* 
     uint32_t* st = rand->states[rand->cur];
     const uint32_t tblocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + kLubyThreads - 1) / kLubyThreads, 8192u));
     const uint32_t wblocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 3u) / 4u, 65535u));
-    uint32_t k = 0, r = 0, h[4];
-    for (;;) {   // one colour per outer round
-        uint32_t stale = 0;
-        for (;;) {   // inner rounds until no candidate is left
-            r++;
-            LTRY(hipMemsetAsync(flags, 0, 2 * sizeof(uint32_t), 0));
-            luby_draw_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, st, cand, sel);
-            luby_conflict_kernel<<<wblocks, kLubyThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, sel, keep);
-            luby_update_kernel<<<wblocks, kLubyThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, keep, cand, is);
-            luby_check_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, cand, keep, flags);
-            LTRY(hipGetLastError());
-            LTRY(hipMemcpy(h, flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-            if (!h[0]) break;
-            stale = h[1] ? 0 : stale + 1;
-            if (stale > 100000u) {   // a self-loop node can never survive its own check: the reference spins
-                cleanup();
-                return fail(MCMC_E_DEVICE, "Luby: no progress (a candidate can never be selected: self loop?)");
-            }
+    LubyCtl h{};
+    for (;;) {   // kLubyBatch rounds per host check; rounds past the end are no-ops
+        for (uint32_t q = 0; q < kLubyBatch; q++) {
+            luby_draw_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, st, cand, sel, ctl);
+            luby_conflict_kernel<<<wblocks, kLubyThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, sel, keep, ctl);
+            luby_update_kernel<<<wblocks, kLubyThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, keep, cand, is, ctl);
+            luby_check_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, cand, keep, ctl);
+            luby_color_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, C, is, cand, ctl);
+            luby_tick_kernel<<<1, 1, 0, 0>>>(ctl);
         }
-        k++;
-        LTRY(hipMemsetAsync(flags + 2, 0, sizeof(uint32_t), 0));
-        luby_color_kernel<<<tblocks, kLubyThreads, 0, 0>>>(n, k, C, is, cand, flags);
         LTRY(hipGetLastError());
-        LTRY(hipMemcpy(h + 2, flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));
-        if (!h[2]) break;
+        LTRY(hipMemcpy(&h, ctl, sizeof(LubyCtl), hipMemcpyDeviceToHost));
+        if (h.finished) break;
     }
+    if (h.err) {
+        cleanup();
+        return fail(MCMC_E_DEVICE, "Luby: no progress (a candidate can never be selected: self loop?)");
+    }
+    const uint32_t k = h.k, r = h.r;
     LTRY(hipMemcpy(colors, C, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
 #undef LTRY
     cleanup();
