@@ -40,7 +40,8 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
                                                                     uint32_t W, uint32_t maxColors,
                                                                     const uint32_t* __restrict__ cin,
                                                                     uint32_t* __restrict__ cout,
-                                                                    uint32_t* __restrict__ forb) {
+                                                                    uint32_t* __restrict__ forb,
+                                                                    uint8_t* __restrict__ fresh) {
     extern __shared__ uint32_t lm[];   // [4 waves][W] forbidden bitmask of the wave's node
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t* m = lm + (size_t)wv * W;
@@ -48,7 +49,10 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
     for (uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < n; v += nw) {
         const uint32_t c0 = cin[v];
         if (v == 0 || c0 != 0) {   // node 0 always takes colour 1; coloured nodes keep theirs
-            if (lane == 0) cout[v] = v == 0 ? 1u : c0;
+            if (lane == 0) {
+                cout[v] = v == 0 ? 1u : c0;
+                fresh[v] = (v == 0 && c0 != 1u) ? 1 : 0;
+            }
             continue;
         }
         uint32_t* fv = forb + (size_t)v * W;
@@ -76,21 +80,29 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
             }
         }
         for (uint32_t w = lane; w < W; w += 64) fv[w] = m[w];
-        if (lane == 0) cout[v] = pick;
+        if (lane == 0) {
+            cout[v] = pick;
+            fresh[v] = pick != 0 ? 1 : 0;
+        }
     }
 }
 
 // cout[v] = 0 if a same-coloured neighbour has a smaller id, else cin[v]; *left |= uncoloured.
+// Only a node coloured this round (fresh) can lose: its pick avoided the colours every neighbour
+// had at the round's start, so a conflict needs a neighbour coloured this round too, and a pair
+// of older nodes was settled in the round the later of them was coloured -- the other rows are
+// not scanned (same result as the reference's full conflict_detection pass).
 __global__ __launch_bounds__(kGffThreads) void gff_conflict_kernel(const uint64_t* __restrict__ ro,
                                                                    const uint32_t* __restrict__ col, uint32_t n,
                                                                    const uint32_t* __restrict__ cin,
-                                                                   uint32_t* __restrict__ cout, uint32_t* left) {
+                                                                   uint32_t* __restrict__ cout, uint32_t* left,
+                                                                   const uint8_t* __restrict__ fresh) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < n; v += nw) {
         const uint32_t cv = cin[v];
         bool lose = false;
-        if (cv != 0) {
+        if (cv != 0 && fresh[v]) {
             for (uint64_t k = ro[v] + lane; k < ro[v + 1]; k += 64) {
                 const uint32_t w = col[k];
                 if (w < v && cin[w] == cv) lose = true;
@@ -242,6 +254,8 @@ namespace {
 // device colouring A (n words, zeroed here); *rounds = loop iterations.
 int gff_color(const GraphDev& gd, uint32_t* A, uint32_t* B, uint32_t* forb, uint32_t* left, uint32_t* rounds) {
     const uint32_t n = gd.n;
+    DevBuf<uint8_t> fresh;
+    MCMC_HIP_TRY(fresh.alloc(n));
     const uint32_t maxColors = gd.maxDeg + 1;   // :17 (getMaxNodeDeg() + 1)
     const uint32_t W = (maxColors + 31u) / 32u;
     MCMC_HIP_TRY(hipMemset(A, 0, sizeof(uint32_t) * n));
@@ -254,8 +268,9 @@ int gff_color(const GraphDev& gd, uint32_t* A, uint32_t* B, uint32_t* forb, uint
     while (h) {
         r++;
         MCMC_HIP_TRY(hipMemsetAsync(left, 0, sizeof(uint32_t), 0));
-        gff_tentative_kernel<<<blocks, kGffThreads, lds, 0>>>(gd.row_off, gd.col_idx, n, W, maxColors, A, B, forb);
-        gff_conflict_kernel<<<blocks, kGffThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, B, A, left);
+        gff_tentative_kernel<<<blocks, kGffThreads, lds, 0>>>(gd.row_off, gd.col_idx, n, W, maxColors, A, B, forb,
+                                                              fresh.p);
+        gff_conflict_kernel<<<blocks, kGffThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, B, A, left, fresh.p);
         MCMC_HIP_TRY(hipGetLastError());
         MCMC_HIP_TRY(hipMemcpy(&h, left, sizeof(uint32_t), hipMemcpyDeviceToHost));
         if (r > 4u * maxColors + 64u)   // the reference loops forever when a forbidden set fills up
