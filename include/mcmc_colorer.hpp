@@ -5,8 +5,8 @@
 //   struct ColoringMCMCParams                      graph_coloring/coloring.h:65-74
 //   template<nodeW,edgeW> struct GraphStruct       graph/graph.h:37-79  (uint64 cumulDegs here)
 //   template<nodeW,edgeW> class Graph              graph/graph.h:84-133
-//       Graph(node nn, float prob, uint32_t seed)  -> setupRnd2 (graphCPU.cpp:424-537), on the GPU
-//       Graph(fileImporter*, bool)                 -> setupImporterNew (graphCPU.cpp:245-303)
+//       Graph(node nn, float prob, uint32_t seed)  -> setupRnd2 (graphCPU.cpp:291-404), on the GPU
+//       Graph(fileImporter*, bool)                 -> setupImporterNew (graphCPU.cpp:112-170)
 //       Graph(Graph* host)                         -> device copy (graphGPU.cu:210-226)
 //   class GPURand(n, seed), member randStates      GPUutils/GPURandomizer.h:42-55
 //   template<nodeW,edgeW> class ColoringMCMC       graph_coloring/coloringMCMC.h:44-140
@@ -90,7 +90,7 @@ struct GraphStruct {
 template <typename nodeW, typename edgeW>
 class Graph {
 public:
-    // Graph(n, prob, seed) -> setupRnd2; `seed` is unused by the reference too (graphCPU.cpp:424).
+    // Graph(n, prob, seed) -> setupRnd2; `seed` is unused by the reference too (graphCPU.cpp:291).
     Graph(node nn, float prob_, uint32_t /*seed*/, int device = 0) : prob(prob_), device_(device) {
         MCMC_CHECK(mcmc_graph_simulate(nn, prob_, mcmc::glibc_global().w, device, &h_));
         info();
@@ -196,7 +196,7 @@ public:
         if (!directory.empty()) save();
     }
 
-    // Report in the layout of saveStats (coloringMCMC_CPUutils.cpp:177-210), parseable by the
+    // Report in the layout of saveStats (coloringMCMC_CPUutils.cpp:70-102), parseable by the
     // reference's pyScripts/logParser.py, plus the per-sweep trajectory; colours as "<v> <c>".
     void save() const {
         std::ofstream out(directory + ".log");

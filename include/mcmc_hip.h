@@ -55,7 +55,7 @@ typedef struct {
     uint32_t seed;           /* engine seed (std::default_random_engine(seed), :53)                */
 } mcmc_params;
 
-/* Per-run summary; the fields the reference writes to its .log (coloringMCMC_CPUutils.cpp:177-210). */
+/* Per-run summary; the fields the reference writes to its .log (coloringMCMC_CPUutils.cpp:70-102). */
 typedef struct {
     uint32_t iter;             /* "Iteration performed"                                          */
     int32_t  maxIterReached;   /* "Max iteration reached"                                        */
@@ -72,7 +72,7 @@ const char* mcmc_last_error(void);
 int mcmc_version(void);
 
 /* ---- glibc rand() stream (the process-global stream the reference shares between setupRnd2
- *      (graphCPU.cpp:441) and the overflow fallback (coloringMCMC_CPU.cpp:518)) ---------------
+ *      (graphCPU.cpp:308) and the overflow fallback (coloringMCMC_CPU.cpp:518)) ---------------
  * A position is the 31-word window of glibc TYPE_3 state. srand(seed) followed by `draws` calls
  * of rand(); jumps in O(31^2 log draws). Replaces nothing in the reference (it used the libc
  * global); needed because the GPU replays the reference's exact rand() draws. */
@@ -84,7 +84,7 @@ int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out); /* adva
  * graph.h:19-20) to the device. */
 int mcmc_graph_upload(const uint64_t* row_off, const uint32_t* col_idx, uint32_t n, uint64_t m,
                       int device, mcmc_graph** out);
-/* Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537) generated ON the device, bit-exact:
+/* Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:291-404) generated ON the device, bit-exact:
  * the n(n+1)/2 glibc draws start at `window` (advanced on return, as the reference's global
  * stream is). Neighbour lists ascending, as the reference's. */
 int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device, mcmc_graph** out);

@@ -52,7 +52,7 @@ class GlibcRand:
     """Position in glibc's rand() stream (TYPE_3 window of 31 words).
 
     The reference uses the process-global stream: unseeded (== srand(1)) when --seed is given
-    (ArgHandle.cpp:272-276), advanced n(n+1)/2 draws by setupRnd2 (graphCPU.cpp:441) and one
+    (ArgHandle.cpp:272-276), advanced n(n+1)/2 draws by setupRnd2 (graphCPU.cpp:308) and one
     draw per CDF overflow (coloringMCMC_CPU.cpp:518)."""
 
     def __init__(self, seed: int = 1, draws: int = 0):
@@ -95,7 +95,7 @@ class Graph:
 
     @classmethod
     def simulate(cls, n: int, prob: float, rand: GlibcRand, device: int = 0) -> "Graph":
-        """Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537), generated on the GPU.
+        """Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:291-404), generated on the GPU.
         Advances ``rand`` by n(n+1)/2 draws, as the reference's global stream is."""
         h = ctypes.c_void_p()
         check(lib().mcmc_graph_simulate(n, ctypes.c_float(prob), u32ptr(rand.window), device, ctypes.byref(h)))
@@ -199,7 +199,7 @@ class ColoringMCMC:
     ``run(iteration)`` colours with engine seed ``rand.seed + iteration`` (main.cu:171's seed+i)
     from the glibc stream position held by ``rand.glibc`` (advanced in place), and, when a
     directory path is set, writes ``<dir>.log`` and ``<dir>-colors.txt`` like the reference's
-    colorers (coloringMCMC_prints.cu:37-38; report fields of coloringMCMC_CPUutils.cpp:177-217)."""
+    colorers (coloringMCMC_prints.cu:37-38; report fields of coloringMCMC_CPUutils.cpp:70-109)."""
 
     def __init__(self, graph_d: Graph, randStates: GPURand, params: ColoringMCMCParams,
                  v_begin: int = 0, v_end: Optional[int] = None):
@@ -392,7 +392,7 @@ class ColoringMCMCGpuRef:
 
 def write_report(path: str, flavour: str, graph: Graph, p: ColoringMCMCParams, seed: int, rep: int,
                  duration: float, st: MCMCRunStats, C: np.ndarray) -> None:
-    """The .log block of saveStats (coloringMCMC_CPUutils.cpp:177-210), parseable by the
+    """The .log block of saveStats (coloringMCMC_CPUutils.cpp:70-102), parseable by the
     reference's pyScripts/logParser.py lineParser."""
     nCol = p.nCol
     hist = np.bincount(C, minlength=nCol).astype(np.int64)

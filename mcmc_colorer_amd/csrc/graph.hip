@@ -1,9 +1,9 @@
 // mcmc_colorer_amd/csrc/graph.hip -- device-resident CSR graphs for the sweep.
 //
 //  mcmc_graph_upload    Graph(Graph* host) device copy (graph/graphGPU.cu:210-226), uint64 offsets.
-//  mcmc_graph_simulate  Graph(n, prob, seed) -> setupRnd2 (graph/graphCPU.cpp:424-537), bit-exact,
+//  mcmc_graph_simulate  Graph(n, prob, seed) -> setupRnd2 (graph/graphCPU.cpp:291-404), bit-exact,
 //                       generated on the GPU: the n(n+1)/2 glibc rand() draws of the upper
-//                       triangle (row-major, diagonal included, :440-446) are split into chunks;
+//                       triangle (row-major, diagonal included, :307-308) are split into chunks;
 //                       each thread jumps the glibc window to its chunk with a precomputed
 //                       31x31 jump matrix per power of two (the recurrence is linear over Z/2^32)
 //                       and replays its chunk. Pass 1 counts degrees, an exclusive scan gives the
@@ -117,7 +117,7 @@ __global__ void deg_to_u64(const uint32_t* __restrict__ deg, uint64_t* __restric
 }
 
 // Smallest r in [0, 2^31] with (double)r / RAND_MAX >= (double)prob: the edge test of setupRnd2
-// (graphCPU.cpp:441) is then exactly r < thr.
+// (graphCPU.cpp:308) is then exactly r < thr.
 uint32_t edge_threshold(float prob) {
     const double p = (double)prob;
     uint64_t lo = 0, hi = 2147483648ull;   // answer in [lo, hi]

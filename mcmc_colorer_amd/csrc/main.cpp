@@ -40,7 +40,7 @@ std::vector<std::string> split_str(const std::string& s, const std::string& deli
     return out;
 }
 
-// fileImporter (utils/fileImporter.cpp:5-66, 118-143) + Graph::setupImporterNew (graphCPU.cpp:245-303).
+// fileImporter (utils/fileImporter.cpp:5-66, 118-143) + Graph::setupImporterNew (graphCPU.cpp:112-170).
 // Vertex ids follow std::unordered_set<std::string> iteration order (same libstdc++ => same ids);
 // the first line is a header; self loops are dropped; both arc directions are added in file order.
 bool import_edge_list(const std::string& path, std::vector<uint64_t>& cumulDegs, std::vector<node>& neighs) {

@@ -10,7 +10,7 @@
 //    "fallback (2 divisions)"), used for the initial coloring (coloringMCMC_CPU.cpp:61).
 //  * glibc rand() TYPE_3 (stdlib/random_r.c): r[i] = r[i-3] + r[i-31] mod 2^32, output r >> 1.
 //    Linear over Z/2^32, so it jumps ahead with x^k mod (x^31 - x^28 - 1). The reference draws
-//    from it in setupRnd2 (graphCPU.cpp:441) and on CDF overflow (coloringMCMC_CPU.cpp:518).
+//    from it in setupRnd2 (graphCPU.cpp:308) and on CDF overflow (coloringMCMC_CPU.cpp:518).
 #pragma once
 #include <stdint.h>
 

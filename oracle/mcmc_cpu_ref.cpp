@@ -374,9 +374,9 @@ uint64_t oracle_uniform_int_seq(uint32_t seed, uint32_t nCol, uint64_t count, ui
     return count_init_draws(seed, nCol, count);
 }
 
-// Graph::setupRnd2 (graph/graphCPU.cpp:424-537). Upper triangle including the diagonal, row-major,
+// Graph::setupRnd2 (graph/graphCPU.cpp:291-404). Upper triangle including the diagonal, row-major,
 // bit k set iff (double)rand()/RAND_MAX < prob (float prob promoted to double, :441); diagonal
-// cleared in the degree pass (:467-468); neighbour lists come out ascending.
+// cleared in the degree pass (:333-335); neighbour lists come out ascending.
 int oracle_setup_rnd2(uint32_t n, float prob, uint64_t** row_off, uint32_t** col_idx, uint64_t* m) {
     const size_t nn = n;
     const size_t vecSize = nn * (nn + 1) / 2;
@@ -490,7 +490,7 @@ int oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, u
     return 0;
 }
 
-// Graph::doStats (graphCPU.cpp:566-583) -> maxDeg, the default nCol (main.cu:162).
+// Graph::doStats (graphCPU.cpp:433-450) -> maxDeg, the default nCol (main.cu:162).
 uint32_t oracle_max_deg(uint32_t n, const uint64_t* row_off) {
     uint32_t maxDeg = 0;
     for (uint32_t v = 0; v < n; v++) maxDeg = std::max<uint32_t>(maxDeg, (uint32_t)(row_off[v + 1] - row_off[v]));
@@ -522,7 +522,7 @@ int oracle_mcmc_run(uint32_t n, const uint64_t* row_off, const uint32_t* col_idx
     return 0;
 }
 
-// saveStats / saveColor (graph_coloring/coloringMCMC_CPUutils.cpp:177-217).
+// saveStats / saveColor (graph_coloring/coloringMCMC_CPUutils.cpp:70-109).
 int oracle_save_outputs(const char* log_path, const char* colors_path, uint32_t n, uint64_t nEdges, uint32_t maxDeg,
                         uint32_t minDeg, float meanDeg, float prob, uint32_t seed, uint32_t repetition, float duration,
                         const oracle_params* prm, const oracle_result* res, const uint32_t* colors) {

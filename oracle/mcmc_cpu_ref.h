@@ -2,8 +2,8 @@
 //
 // CPU restatement of the reference's `--mcmccpu` path, written from the source text of
 //   src/graph_coloring/coloringMCMC_CPU.{h,cpp}   (ColoringMCMC_CPU)
-//   src/graph/graphCPU.cpp:424-537                 (Graph::setupRnd2, the --simulate generator)
-//   src/graph/graphCPU.cpp:566-583                 (Graph::doStats -> maxDeg)
+//   src/graph/graphCPU.cpp:291-404                 (Graph::setupRnd2, the --simulate generator)
+//   src/graph/graphCPU.cpp:433-450                 (Graph::doStats -> maxDeg)
 //   src/main.cu:160-171                            (ColoringMCMCParams defaults, seed+i per repetition)
 // It calls the SAME third-party arithmetic the reference calls: libstdc++ <random>
 // (std::default_random_engine = minstd_rand0, uniform_int_distribution<uint32_t>,
@@ -62,7 +62,7 @@ void     oracle_minstd_seq(uint32_t seed, uint64_t count, uint32_t* out);
 void     oracle_canonical_seq(uint32_t seed, uint64_t skip, uint64_t count, float* out);
 uint64_t oracle_uniform_int_seq(uint32_t seed, uint32_t nCol, uint64_t count, uint32_t* out);
 
-// ---- graph: Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:424-537) ----
+// ---- graph: Graph(n, prob, seed) -> setupRnd2 (graphCPU.cpp:291-404) ----
 // Consumes n(n+1)/2 glibc rand() draws from the current process stream.
 // Allocates *row_off (n+1) and *col_idx (m) with malloc; free with oracle_free.
 int      oracle_setup_rnd2(uint32_t n, float prob, uint64_t** row_off, uint32_t** col_idx, uint64_t* m);
@@ -115,7 +115,7 @@ int      oracle_mcmc_gpu_run(uint32_t n, const uint64_t* row_off, const uint32_t
                              uint32_t* states, uint32_t* out_colors, uint64_t* traj, uint64_t traj_cap,
                              uint32_t tail_max_passes, uint64_t* tail_traj, oracle_gpu_result* res);
 
-// Writes the reference's saveStats / saveColor text outputs (coloringMCMC_CPUutils.cpp:177-217).
+// Writes the reference's saveStats / saveColor text outputs (coloringMCMC_CPUutils.cpp:70-109).
 int      oracle_save_outputs(const char* log_path, const char* colors_path, uint32_t n, uint64_t nEdges,
                              uint32_t maxDeg, uint32_t minDeg, float meanDeg, float prob, uint32_t seed,
                              uint32_t repetition, float duration, const oracle_params* prm,

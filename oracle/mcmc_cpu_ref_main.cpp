@@ -21,7 +21,7 @@
 
 #include "mcmc_cpu_ref.h"
 
-// fileImporter (utils/fileImporter.cpp:5-66, 118-143) + setupImporterNew (graph/graphCPU.cpp:245-303):
+// fileImporter (utils/fileImporter.cpp:5-66, 118-143) + setupImporterNew (graph/graphCPU.cpp:112-170):
 // ids in std::unordered_set<std::string> iteration order, header line skipped, self loops dropped,
 // both arc directions in file order.
 static bool import_graph(const std::string& path, std::vector<uint64_t>& cumulDegs, std::vector<uint32_t>& neighs) {

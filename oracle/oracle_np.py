@@ -7,7 +7,7 @@ real libraries, exactly like the reference) on small graphs, so that the C++ ora
 two restatements that share no code. Pure-Python loops: keep n small (<= a few hundred).
 
 Reference lines restated (paths relative to /root/reference/src):
-  graph/graphCPU.cpp:424-537            setupRnd2 (Erdos-Renyi via glibc rand())
+  graph/graphCPU.cpp:291-404            setupRnd2 (Erdos-Renyi via glibc rand())
   graph_coloring/coloringMCMC_CPU.cpp   ctor :53-61, run :115-270, violation_count :329-351,
                                         count_free_colors :362-383, fill_p :393-481,
                                         extract_new_color :493-528
