@@ -30,8 +30,11 @@ max over ranks. Prints ONE JSON line (rank 0). Besides the driver contract field
                  "the reference CUDA path's vertex-updates/sec", which cannot run on MI355X)
   cpu_baseline : the oracle (faithful single-thread restatement of --mcmccpu, kind "port") on this
                  host, a bounded number of sweeps
-For c3 the refstruct and CPU legs run on `--simulate 0.1 -n 100000` (C3's mean degree, 1e4): C3's
-CSR cannot exist on the host or one GPU.
+For c3 the CPU leg runs on `--simulate 0.1 -n 100000` (C3's mean degree, 1e4) and the refstruct leg on a
+2e6-row graph of the same degree (full occupancy at thread-per-vertex): C3's own uint32 CSR (400 GB)
+cannot exist on the host or one GPU. Every single-GPU line also carries `convergence`: the reference
+loop run from the initial colouring (sweeps-to-zero-conflict, or not converged at 251 + final Cviol +
+trajectory).
 """
 from __future__ import annotations
 
@@ -67,27 +70,63 @@ def load_traffic(key: str):
         return None
 
 
+def host_info() -> dict:
+    """The GPU box's host: logical CPUs, the CPUs this process may use, the CPU model."""
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window: np.ndarray, n: int,
                  max_seconds: float = 20.0):
-    """Oracle (tests/oracle_ref.py) on this host, single thread, bounded sample of sweeps."""
+    """Oracle (tests/oracle_ref.py) on this host, a bounded sample of sweeps: the faithful
+    single-thread restatement of ColoringMCMC_CPU::run (the reference's --mcmccpu is single-threaded:
+    the headline value, cores = 1), then its OpenMP variant (bit-identical colouring) on all the CPUs
+    this process may use (OMP_NUM_THREADS, else the affinity mask) as `all_cores`."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as O
 
-    O.set_glibc_window(window)
+    def sample(threads: int, budget: float):
+        O.set_glibc_window(window)
+        r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=1, nthreads=threads)
+        one = r.res.loopSeconds
+        k = max(1, min(30, int(budget / max(one, 1e-3))))
+        O.set_glibc_window(window)
+        r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=k, nthreads=threads)
+        return n * r.res.sweepsRun / r.res.loopSeconds, r.res.sweepsRun, r
+
     t0 = time.perf_counter()
-    r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=1, nthreads=1)
-    one = r.res.loopSeconds
-    k = max(1, min(30, int(max_seconds / max(one, 1e-3))))
-    O.set_glibc_window(window)
-    r = O.mcmc_run(off, idx, ncol, seed, sweep_limit=k, nthreads=1)
+    v1, k1, r1 = sample(1, max_seconds)
+    w1 = time.perf_counter() - t0
+    info = host_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or info["usable_cpus"] or 1)
+    t0 = time.perf_counter()
+    vN, kN, rN = sample(threads, max_seconds / 2)
+    wN = time.perf_counter() - t0
     return {
-        "value": n * r.res.sweepsRun / r.res.loopSeconds,
+        "value": v1,
         "unit": "vertex-updates/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"first {r.res.sweepsRun} sweeps of the same graph/seed (oracle single-thread restatement of "
-                  f"ColoringMCMC_CPU::run incl. its 4 arc passes/sweep, debugger hook excluded); "
-                  f"{time.perf_counter() - t0:.1f} s wall",
+        "sample": f"first {k1} sweeps of the same graph/seed (oracle single-thread restatement of "
+                  f"ColoringMCMC_CPU::run incl. its 4 arc passes/sweep, debugger hook excluded); {w1:.1f} s wall",
+        "host": info,
+        "all_cores": {"value": vN, "unit": "vertex-updates/s", "cores": threads, "kind": "port",
+                      "sample": f"first {kN} sweeps, OpenMP variant of the oracle on {threads} threads (same "
+                                f"colouring as the single-thread run; loop 2 / fill_qstar, output-dead, skipped); "
+                                f"{wN:.1f} s wall",
+                      "identical_trajectory_prefix": bool(np.array_equal(r1.traj[:min(k1, kN)], rN.traj[:min(k1, kN)]))},
     }
 
 
@@ -121,18 +160,46 @@ def cpu_baseline_ref(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, n: 
 
 def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: float) -> dict:
     """The reference CUDA path's per-sweep structure re-expressed in HIP (mcmc_refstruct_bench):
-    the stand-in for 'the reference CUDA path's vertex-updates/sec', which cannot run on MI355X."""
+    the stand-in for 'the reference CUDA path's vertex-updates/sec', which cannot run on MI355X. Its analytic
+    byte model (§8d): 3 uint32 arc passes (2 conflict counts + the selection) + 3 offset passes + the n*nCol
+    checker reset + the per-vertex colour/state traffic, and 8n B over PCIe (4n B D2H of the colouring for
+    the host histogram, plus the conflict partial sums)."""
     from mcmc_colorer_amd._lib import check, lib
 
     ms = ctypes.c_double()
     conf = ctypes.c_uint64()
     check(lib().mcmc_refstruct_bench(g.handle, ncol, sweeps, seed, ctypes.byref(ms), ctypes.byref(conf)))
     v = n / (ms.value * 1e-3)
+    m = g.nEdges
+    # uint32 ids of 3 arc passes; row offsets of 3 passes; checker reset + the selection's nCol scan of
+    # it; own colour / count / taboo / Cs / qs words; 48 B XORWOW state read + written per vertex
+    hbm = 3 * 4 * m + 3 * 8 * (n + 1) + 2 * n * ncol + 4 * n * 6 + 48 * 2 * n
     return {"value": v, "unit": "vertex-updates/s", "ms_per_sweep": ms.value, "sweeps": sweeps,
             "speedup": value / v,
+            "model_bytes_hbm": hbm, "model_bytes_pcie": 8 * n,
+            "achieved_GBs": hbm / (ms.value * 1e-3) / 1e9, "frac_of_hbm_peak": hbm / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "what": "HIP re-expression of ColoringMCMC::run's per-sweep structure (thread-per-vertex serial "
                     "row walks, 64-thread blocks, n*nCol checker memset, 2 conflict passes + host sums, 4n B "
-                    "D2H + host histogram + H2D), same graph, host wall per sweep"}
+                    "D2H + host histogram + H2D), host wall per sweep"}
+
+
+def refstruct_full_occupancy(dev: int, ncol: int, seed: int, value: float, sweeps: int) -> dict:
+    """refstruct on a graph with C3's mean degree (1e4) that fills the chip at thread-per-vertex: 2e6
+    rows (31250 64-thread blocks, ~30 waves per SIMD), 2e10 arcs, the reference's uint32 CSR (80 GB)
+    materialised on the device from the build's G(n, p). Per-vertex work is per-degree, so its rate
+    compares directly with C3's (same degree, 1e7 rows)."""
+    import mcmc_colorer_amd.colorer as M
+    from mcmc_colorer_amd._lib import check, lib
+
+    t0 = time.perf_counter()
+    g = M.Graph.er_fast(2_000_000, 0.005, 1, device=dev)
+    check(lib().mcmc_graph_materialize_csr(g.handle))
+    gen = time.perf_counter() - t0
+    r = refstruct_baseline(g, ncol, sweeps, seed, g.nNodes, value)
+    r["graph"] = (f"the build's G(n, p) with n = 2e6, p = 0.005 (mean degree {g.nEdges / g.nNodes:.0f} = C3's), "
+                  f"{g.nEdges} arcs as a uint32 CSR on the device ({gen:.1f} s to build)")
+    g.close()
+    return r
 
 
 def main() -> int:
@@ -150,6 +217,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-refstruct", action="store_true", help="skip the refstruct (reference-structure) leg")
+    ap.add_argument("--no-convergence", action="store_true", help="skip the reference-loop run (sweeps-to-zero-conflict)")
     ap.add_argument("--refstruct-sweeps", type=int, default=10)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
@@ -222,16 +290,25 @@ def main() -> int:
 
     ref = a.semantics == "ref"
     conv = None
-    if a.config == "c5" and dist is None:
-        # the reference loop itself (run(), coloringMCMC_CPU.cpp:115-270): until Cviol == 0 or the cap
-        cr = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=a.ncol))
+    if dist is None and not ref and not a.no_convergence:
+        # the reference loop itself (run(), coloringMCMC_CPU.cpp:115-270) from the initial colouring:
+        # until Cviol <= z or the cap (maxRip 250: at most 251 sweeps, :264-269); the metric's second
+        # half -- sweeps-to-zero-conflict, or "not converged at 251" with the final Cviol and the
+        # per-sweep trajectory
+        window = (M.GlibcRand(1, n_req * (n_req + 1) // 2) if a.config == "c2" else M.GlibcRand(1))
+        cr = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, window), M.ColoringMCMCParams(nCol=a.ncol))
         t0 = time.perf_counter()
         st = cr.run(0)
         cw = time.perf_counter() - t0
+        tr = [int(x) for x in cr.trajectory()]
         conv = {"sweeps_to_zero_conflict": int(st.iter) if st.finalViol == 0 else None,
-                "converged": bool(st.finalViol == 0), "final_Cviol": int(st.finalViol),
+                "converged": bool(st.finalViol == 0),
+                "status": (f"converged after {int(st.iter)} sweeps" if st.finalViol == 0 else
+                           f"not converged at {int(st.iter)} (maxRip 250 cap: {int(st.sweepsRun)} sweeps run)"),
+                "iterations": int(st.iter), "max_iter_reached": bool(st.maxIterReached),
+                "final_Cviol": int(st.finalViol), "sweeps_run": int(st.sweepsRun),
                 "loop_ms": st.loopMs, "wall_s": round(cw, 4), "glibc_draws": int(st.glibcDraws),
-                "trajectory": [int(x) for x in cr.trajectory()[:64]]}
+                "trajectory": tr}
         cr.close()
     if ref and dist is not None:
         raise SystemExit("--semantics ref runs on one GPU")
@@ -347,6 +424,10 @@ def main() -> int:
         out["cpu_baseline"]["sample"] += (f"; graph R-MAT scale 18 (same generator and seed, n = {cs.nNodes}, "
                                           f"nCol = maxDeg = {cpu_ncol}; the oracle is O(nCol) per vertex)")
         cs.close()
+    if rank == 0 and world == 1 and a.config == "c3" and not a.no_refstruct:
+        # refstruct at full occupancy (the C3 CSR itself would be 400 GB): a 2e6-row graph of C3's degree
+        g.close()
+        out["refstruct"] = refstruct_full_occupancy(dev, a.ncol, a.seed, value, max(2, min(a.refstruct_sweeps, 4)))
     if rank == 0 and world == 1 and not (a.no_refstruct and a.no_cpu_baseline):
         if a.config == "c3":
             g.close()
@@ -356,7 +437,7 @@ def main() -> int:
             sample_note = "--simulate 0.1 -n 100000 (mean degree 1e4 = C3's; C3's CSR cannot exist: 400 GB)"
         else:
             sample_window = M.GlibcRand(1, n_req * (n_req + 1) // 2).window
-    if rank == 0 and world == 1 and not a.no_refstruct:
+    if rank == 0 and world == 1 and not a.no_refstruct and a.config != "c3":
         out["refstruct"] = refstruct_baseline(sample, a.ncol, a.refstruct_sweeps, a.seed, sample_n, value)
         if sample_note:
             out["refstruct"]["graph"] = sample_note

@@ -99,6 +99,10 @@ int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device,
 int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out);
 int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t world, uint32_t rank, int device,
                             mcmc_graph** out);
+/* The CSR (uint64 offsets, uint32 ids; rows in layout order, not sorted) of a graph generated with
+ * mcmc_graph_er_fast, built on the device from its tiled layout and kept on the handle (then
+ * mcmc_graph_device_ptrs works). For the refstruct baseline at full occupancy (bench.py). */
+int mcmc_graph_materialize_csr(mcmc_graph* g);
 /* R-MAT power-law graph (configs[4] stand-in: SNAP LiveJournal / Reddit are not available; SURVEY.md
  * §8d C5), generated on the device as a CSR with ascending neighbour lists: 2^scale vertices,
  * edge_factor * 2^scale Philox-driven quadrant draws with probabilities (a, b, c, 1-a-b-c), ids
@@ -107,6 +111,12 @@ int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t wor
 int mcmc_graph_rmat(uint32_t scale, uint32_t edge_factor, double a, double b, double c, uint64_t seed, int device,
                     mcmc_graph** out);
 int mcmc_graph_info(const mcmc_graph* g, uint32_t* n, uint64_t* m, uint32_t* maxDeg, uint32_t* minDeg);
+/* Test hook (no reference counterpart): rows of a graph as stored on the device -- the full-range
+ * tiled layout of a generated graph, or the CSR. off: [k+1]; ids: NULL for the degrees only, else
+ * cap >= off[k] entries (each row's ids in layout order); pos: optional [k], the layout index
+ * (uint64) of each row's first stored id. Lets tests check rows of graphs too large to download. */
+int mcmc_graph_rows(const mcmc_graph* g, const uint32_t* rows, uint32_t k, uint64_t* off, uint32_t* ids,
+                    uint64_t cap, uint64_t* pos);
 /* Device pointers (row_off: uint64[n+1], col_idx: uint32[m]) for zero-copy callers. */
 int mcmc_graph_device_ptrs(const mcmc_graph* g, const uint64_t** row_off, const uint32_t** col_idx);
 int mcmc_graph_download(const mcmc_graph* g, uint64_t* row_off, uint32_t* col_idx);
@@ -136,6 +146,10 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats);
  * Cviol in finalViol and the passes in tailcutPasses (the trajectory is the loop's). 0 disables.
  * Whole-graph contexts only; costs n bytes of flag writes per sweep while enabled. */
 int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes);
+/* Test hook: conflicting vertices of the current colouring (violation_count, coloringMCMC_CPU.cpp:
+ * 329-351) recounted by the tail cut's kernel, independently of the sweep's own count; flags
+ * (optional, n bytes) receives the per-vertex flags. */
+int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags /* nullable, n bytes */);
 int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out /* n */);
 int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 /* Timed throughput mode for benchmarks: exactly `sweeps` sweeps of the loop body (no

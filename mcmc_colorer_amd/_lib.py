@@ -35,6 +35,8 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_vff_run": (c_int, [c_void_p, _u32p, _u32p, _u32p, POINTER(c_int)]),
     "mcmc_graph_device_ptrs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p)]),
     "mcmc_graph_download": (c_int, [c_void_p, _u64p, _u32p]),
+    "mcmc_graph_materialize_csr": (c_int, [c_void_p]),
+    "mcmc_graph_rows": (c_int, [c_void_p, _u32p, c_uint32, _u64p, _u32p, c_uint64, _u64p]),
     "mcmc_graph_destroy": (None, [c_void_p]),
     "mcmc_create": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, POINTER(c_void_p)]),
     "mcmc_set_glibc_window": (c_int, [c_void_p, _u32p]),
@@ -42,6 +44,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_init_coloring": (c_int, [c_void_p, _u32p]),
     "mcmc_run": (c_int, [c_void_p, c_uint32, c_void_p]),
     "mcmc_get_coloring": (c_int, [c_void_p, _u32p]),
+    "mcmc_count_violations": (c_int, [c_void_p, _u64p, c_void_p]),
     "mcmc_set_tailcut_repair": (c_int, [c_void_p, c_uint32]),
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),

@@ -149,6 +149,17 @@ class Graph:
             self._struct = GraphStruct(self.nNodes, self.nEdges, off, idx[: self.nEdges])
         return self._struct
 
+    def rows(self, rows) -> tuple[list[np.ndarray], np.ndarray]:
+        """Rows as stored on the device (mcmc_graph_rows: the tiled layout of a generated graph, else
+        the CSR), each in layout order, and the layout index of each row's first stored id."""
+        r = np.ascontiguousarray(rows, dtype=np.uint32)
+        off = np.zeros(len(r) + 1, dtype=np.uint64)
+        pos = np.zeros(max(len(r), 1), dtype=np.uint64)
+        check(lib().mcmc_graph_rows(self._h, u32ptr(r), len(r), u64ptr(off), None, 0, u64ptr(pos)))
+        ids = np.zeros(max(int(off[-1]), 1), dtype=np.uint32)
+        check(lib().mcmc_graph_rows(self._h, u32ptr(r), len(r), u64ptr(off), u32ptr(ids), len(ids), None))
+        return [ids[off[i]:off[i + 1]] for i in range(len(r))], pos[: len(r)]
+
     def getMaxNodeDeg(self) -> int:
         return self.maxDeg
 
@@ -243,6 +254,20 @@ class ColoringMCMC:
         if self.directory:
             self.save(iteration)
         return st
+
+    def step(self, sweeps: int) -> MCMCRunStats:
+        """Continues the loop of an initialised context by at most `sweeps` sweeps (no re-init)."""
+        st = MCMCRunStats()
+        check(lib().mcmc_run(self._ctx, sweeps, ctypes.byref(st)))
+        return st
+
+    def count_violations(self, flags: bool = False):
+        """Cviol of the current colouring, recounted by the tail cut's kernel (mcmc_count_violations);
+        flags=True also returns the per-vertex flags."""
+        c = ctypes.c_uint64()
+        f = np.zeros(self.graph.nNodes, dtype=np.uint8) if flags else None
+        check(lib().mcmc_count_violations(self._ctx, ctypes.byref(c), f.ctypes.data_as(ctypes.c_void_p) if flags else None))
+        return (c.value, f) if flags else c.value
 
     # -- results ------------------------------------------------------------------------------
     def coloring(self) -> np.ndarray:

@@ -166,6 +166,56 @@ int sort_rows_inplace(GraphDev& g) {
     return MCMC_OK;
 }
 
+// bad |= 1 unless every arc (i, j) of rows [vb, vb + nloc) with j in the range has its reverse
+// (rows ascending). One wave per row: hub rows are tens of thousands of arcs.
+__global__ __launch_bounds__(256) void csr_symcheck_kernel(const uint64_t* __restrict__ row_off,
+                                                           const uint32_t* __restrict__ col, uint32_t vb,
+                                                           uint32_t nloc, uint32_t* bad) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
+        const uint32_t i = vb + l;
+        const uint64_t e = row_off[i + 1];
+        bool ok = true;
+        for (uint64_t k = row_off[i] + lane; k < e; k += 64) {
+            const uint32_t j = col[k];
+            if (j - vb >= nloc) continue;
+            uint64_t lo = row_off[j], hi = row_off[j + 1];
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (col[mid] < i) lo = mid + 1; else hi = mid;
+            }
+            if (lo == row_off[j + 1] || col[lo] != i) ok = false;
+        }
+        if (__ballot(!ok) && lane == 0) atomicOr(bad, 1u);
+    }
+}
+
+int csr_symmetric(GraphDev& g, uint32_t vb, uint32_t nloc, hipStream_t s, bool* sym) {
+    const bool whole = vb == 0 && nloc == g.n;
+    if (whole && g.sym >= 0) { *sym = g.sym == 1; return MCMC_OK; }
+    if (!g.row_off) return fail(MCMC_E_STATE, "symmetry check needs a CSR");
+    if (!g.sorted) {
+        if (int rc = sort_rows_inplace(g)) return rc;
+    }
+    uint32_t* bad = nullptr;
+    MCMC_HIP_TRY(hipMalloc(&bad, sizeof(uint32_t)));
+    uint32_t h = 0;
+    hipError_t e = hipMemsetAsync(bad, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && nloc) {
+        csr_symcheck_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 3u) / 4u, 65535u)), 256, 0, s>>>(
+            g.row_off, g.col_idx, vb, nloc, bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, bad, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(bad);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("symmetry check: ") + hipGetErrorString(e));
+    *sym = h == 0;
+    if (whole) g.sym = *sym ? 1 : 0;
+    return MCMC_OK;
+}
+
 }  // namespace mcmc
 
 using namespace mcmc;

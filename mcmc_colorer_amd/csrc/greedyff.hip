@@ -28,6 +28,14 @@ namespace {
 
 constexpr int kGffThreads = 256;   // 4 waves, one node each at a time
 
+// Orders one wave's LDS accesses between phases (plain stores, then ds_or atomics from other
+// lanes, then reads): the HIP memory model does not promise wave lock-step ordering by itself.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <typename T>
 struct DevBuf {   // device allocation freed on every return path
     T* p = nullptr;
@@ -57,10 +65,12 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
         }
         uint32_t* fv = forb + (size_t)v * W;
         for (uint32_t w = lane; w < W; w += 64) m[w] = fv[w];
+        wave_lds_sync();
         for (uint64_t k = ro[v] + lane; k < ro[v + 1]; k += 64) {
             const uint32_t c = cin[col[k]];   // < maxColors: first-fit never picks past it
             atomicOr(&m[c >> 5], 1u << (c & 31u));
         }
+        wave_lds_sync();
         uint32_t pick = 0;   // 0: no free colour (the node stays uncoloured this round)
         for (uint32_t wb = 0; wb < W; wb += 64) {
             const uint32_t w = wb + lane;
@@ -80,6 +90,7 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
             }
         }
         for (uint32_t w = lane; w < W; w += 64) fv[w] = m[w];
+        wave_lds_sync();   // the next node's stores must not pass these reads
         if (lane == 0) {
             cout[v] = pick;
             fresh[v] = pick != 0 ? 1 : 0;
@@ -88,21 +99,24 @@ __global__ __launch_bounds__(kGffThreads) void gff_tentative_kernel(const uint64
 }
 
 // cout[v] = 0 if a same-coloured neighbour has a smaller id, else cin[v]; *left |= uncoloured.
-// Only a node coloured this round (fresh) can lose: its pick avoided the colours every neighbour
-// had at the round's start, so a conflict needs a neighbour coloured this round too, and a pair
-// of older nodes was settled in the round the later of them was coloured -- the other rows are
-// not scanned (same result as the reference's full conflict_detection pass).
+// On a symmetric CSR only a node coloured this round (fresh) can lose: its pick avoided the colours
+// every neighbour had at the round's start, so a conflict needs a neighbour coloured this round
+// too, and a pair of older nodes was settled in the round the later of them was coloured -- the
+// other rows are not scanned (same result as the reference's full conflict_detection pass). On an
+// asymmetric CSR a fresh w < v whose row lacks v may take v's colour, so every coloured row is
+// scanned (fresh_only = 0), as the reference does.
 __global__ __launch_bounds__(kGffThreads) void gff_conflict_kernel(const uint64_t* __restrict__ ro,
                                                                    const uint32_t* __restrict__ col, uint32_t n,
                                                                    const uint32_t* __restrict__ cin,
                                                                    uint32_t* __restrict__ cout, uint32_t* left,
-                                                                   const uint8_t* __restrict__ fresh) {
+                                                                   const uint8_t* __restrict__ fresh,
+                                                                   uint32_t fresh_only) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t v = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < n; v += nw) {
         const uint32_t cv = cin[v];
         bool lose = false;
-        if (cv != 0 && fresh[v]) {
+        if (cv != 0 && (fresh[v] || !fresh_only)) {
             for (uint64_t k = ro[v] + lane; k < ro[v + 1]; k += 64) {
                 const uint32_t w = col[k];
                 if (w < v && cin[w] == cv) lose = true;
@@ -184,11 +198,13 @@ __global__ __launch_bounds__(kGffThreads) void vff_tentative_kernel(const uint64
             continue;
         }
         for (uint32_t w = lane; w < W; w += 64) m[w] = 0;
+        wave_lds_sync();
         if (lane == 0) atomicOr(&m[c0 >> 5], 1u << (c0 & 31u));
         for (uint64_t k = ro[v] + lane; k < ro[v + 1]; k += 64) {
             const uint32_t c = cin[col[k]];
             atomicOr(&m[c >> 5], 1u << (c & 31u));
         }
+        wave_lds_sync();
         uint32_t pick = c0;
         for (uint32_t wb = 0; wb < W; wb += 64) {
             const uint32_t w = wb + lane;
@@ -201,6 +217,7 @@ __global__ __launch_bounds__(kGffThreads) void vff_tentative_kernel(const uint64
                 break;
             }
         }
+        wave_lds_sync();   // the next node's clearing stores must not pass the search's reads
         if (lane == 0) cout[v] = pick;
     }
 }
@@ -256,6 +273,8 @@ int gff_color(const GraphDev& gd, uint32_t* A, uint32_t* B, uint32_t* forb, uint
     const uint32_t n = gd.n;
     DevBuf<uint8_t> fresh;
     MCMC_HIP_TRY(fresh.alloc(n));
+    bool sym = false;
+    if (int rc = csr_symmetric(const_cast<GraphDev&>(gd), 0, n, 0, &sym)) return rc;
     const uint32_t maxColors = gd.maxDeg + 1;   // :17 (getMaxNodeDeg() + 1)
     const uint32_t W = (maxColors + 31u) / 32u;
     MCMC_HIP_TRY(hipMemset(A, 0, sizeof(uint32_t) * n));
@@ -270,7 +289,8 @@ int gff_color(const GraphDev& gd, uint32_t* A, uint32_t* B, uint32_t* forb, uint
         MCMC_HIP_TRY(hipMemsetAsync(left, 0, sizeof(uint32_t), 0));
         gff_tentative_kernel<<<blocks, kGffThreads, lds, 0>>>(gd.row_off, gd.col_idx, n, W, maxColors, A, B, forb,
                                                               fresh.p);
-        gff_conflict_kernel<<<blocks, kGffThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, B, A, left, fresh.p);
+        gff_conflict_kernel<<<blocks, kGffThreads, 0, 0>>>(gd.row_off, gd.col_idx, n, B, A, left, fresh.p,
+                                                            sym ? 1u : 0u);
         MCMC_HIP_TRY(hipGetLastError());
         MCMC_HIP_TRY(hipMemcpy(&h, left, sizeof(uint32_t), hipMemcpyDeviceToHost));
         if (r > 4u * maxColors + 64u)   // the reference loops forever when a forbidden set fills up

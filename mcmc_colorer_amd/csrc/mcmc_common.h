@@ -30,12 +30,16 @@ struct GraphDev {
     uint64_t m = 0;
     uint32_t maxDeg = 0, minDeg = 0;
     bool sorted = false;           // every neighbour list ascending
+    int sym = -1;                  // whole CSR symmetric: 1 yes, 0 no, -1 not checked (csr_symmetric)
     uint64_t* row_off = nullptr;   // [n+1]
     uint32_t* col_idx = nullptr;   // [m]
 };
 
 // Sorts every neighbour list ascending on the device, in place (graph.hip).
 int sort_rows_inplace(GraphDev& g);
+// *sym = every arc (i, j) of rows [vb, vb + nloc) with j in that range has its reverse (one wave per
+// row, binary search of row j; sorts the rows first). The whole-graph answer is cached in g.sym.
+int csr_symmetric(GraphDev& g, uint32_t vb, uint32_t nloc, hipStream_t s, bool* sym);
 
 }  // namespace mcmc
 

@@ -2587,6 +2587,34 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     return MCMC_OK;
 }
 
+// Conflicting vertices of the context's current colouring (violation_count, coloringMCMC_CPU.cpp:
+// 329-351), counted by the tail cut's recount kernel -- a code path independent of the sweep's
+// fused count (test hook for the full-size checks). Whole-graph uint8 contexts. flags: optional
+// [n] host bytes, the per-vertex flags.
+int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
+    if (!c || !count) return fail(MCMC_E_ARG, "NULL argument");
+    if (c->part || c->wide || c->v_begin != 0 || c->v_end != c->n)
+        return fail(MCMC_E_STATE, "violation recount: whole-graph contexts with uint8 colours");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    int rc = ensure_tail_buffers(c);
+    if (rc) return rc;
+    uint32_t which = 0;
+    if (c->ran) {
+        DevState h{};
+        rc = download_state(c, &h);
+        if (rc) return rc;
+        which = h.t & 1u;
+    }
+    rc = tail_count(tail_view(c), c->colors[which], c->vflags, c->tc_count, c->stream, false);
+    if (rc) return rc;
+    unsigned long long hv = 0;
+    MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
+    if (flags) MCMC_HIP_TRY(hipMemcpyAsync(flags, c->vflags, c->n, hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    *count = hv;
+    return MCMC_OK;
+}
+
 int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (c->part || c->v_begin != 0 || c->v_end != c->n)

@@ -666,32 +666,6 @@ __device__ __forceinline__ bool xs_keep(uint32_t i, uint32_t j, uint32_t vb, uin
     return !sym || j - vb >= nloc || ((i + j) & 1u) == (i < j ? 1u : 0u);
 }
 
-// bad |= 1 unless every local arc (i, j) with j local has its reverse (rows ascending): the
-// one-entry-per-edge layout needs a symmetric CSR (--simulate, R-MAT and --graph imports are).
-// One wave per row: hub rows are tens of thousands of arcs.
-__global__ __launch_bounds__(256) void xs_symcheck_kernel(const uint64_t* __restrict__ row_off,
-                                                          const uint32_t* __restrict__ col, uint32_t vb, uint32_t nloc,
-                                                          uint32_t* bad) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
-        const uint32_t i = vb + l;
-        const uint64_t e = row_off[i + 1];
-        bool ok = true;
-        for (uint64_t k = row_off[i] + lane; k < e; k += 64) {
-            const uint32_t j = col[k];
-            if (j - vb >= nloc) continue;
-            uint64_t lo = row_off[j], hi = row_off[j + 1];
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (col[mid] < i) lo = mid + 1; else hi = mid;
-            }
-            if (lo == row_off[j + 1] || col[lo] != i) ok = false;
-        }
-        if (!ok) atomicOr(bad, 1u);
-    }
-}
-
 // cnt[l] = kept arcs of local row l. One wave per row.
 __global__ __launch_bounds__(256) void xs_rowcount_kernel(const uint64_t* __restrict__ ro,
                                                           const uint32_t* __restrict__ col, uint32_t nloc, uint32_t vb,
@@ -895,11 +869,9 @@ int get_xslab(mcmc_graph* gh, uint32_t vb, uint32_t ve, uint32_t mode, uint32_t 
     uint32_t h[2] = {0, 0};
     XTRY(hipMalloc(&flag, 2 * sizeof(uint32_t)));
     XTRY(hipMemsetAsync(flag, 0, 2 * sizeof(uint32_t), st));
-    xs_symcheck_kernel<<<wblocks, 256, 0, st>>>(gd.row_off, gd.col_idx, vb, nloc, flag);
-    XTRY(hipGetLastError());
-    XTRY(hipMemcpyAsync(h, flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    XTRY(hipStreamSynchronize(st));
-    L->sym = h[0] ? 0u : 1u;
+    bool symmetric = false;   // the one-entry-per-edge layout needs every local arc's reverse
+    if (int rs = csr_symmetric(gd, vb, nloc, st, &symmetric)) { cleanup(); return rs; }
+    L->sym = symmetric ? 1u : 0u;
     // kept arcs per row -> positions -> (slab, row) keys in CSR order -> stable sort by key
     XTRY(hipMalloc(&cnt, sizeof(uint32_t) * ((size_t)nloc + 1)));
     XTRY(hipMalloc(&pos, sizeof(uint32_t) * ((size_t)nloc + 1)));

@@ -351,6 +351,28 @@ uint32_t tiled_default_rows(uint32_t nloc, uint32_t cus, uint32_t rmax) {
     return std::max<uint32_t>(std::min<uint32_t>(32u, rmax), std::min<uint32_t>(rmax, R));
 }
 
+// Selected rows of a full-range tiled layout (test hook mcmc_graph_rows; all rows for
+// mcmc_graph_materialize_csr): thread per row walks its nb segments; pass 1 (ids == nullptr) the
+// degrees, pass 2 the ids at off[i].
+__global__ void tile_rows_kernel(const uint16_t* __restrict__ tcol, const uint64_t* __restrict__ gbase,
+                                 const uint32_t* __restrict__ tseg, uint32_t R, uint32_t nb, uint32_t block_log2,
+                                 const uint32_t* __restrict__ rows, uint32_t k, const uint64_t* __restrict__ off,
+                                 uint64_t* __restrict__ deg, uint32_t* __restrict__ ids, uint64_t* __restrict__ pos) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const uint32_t v = rows ? rows[i] : i, g = v / R, r = v - g * R;   // rows == nullptr: all rows
+    uint64_t d = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t* t = tseg + ((size_t)g * nb + b) * tseg_stride(R);
+        const uint64_t q0 = gbase[g] + (t[r] & kTsegPos), q1 = gbase[g] + (t[r + 1] & kTsegPos) - (t[r] & 7u);
+        if (b == 0 && pos) pos[i] = q0;
+        if (ids)
+            for (uint64_t q = q0; q < q1; q++) ids[off[i] + d + (q - q0)] = (b << block_log2) | tcol[q];
+        d += q1 - q0;
+    }
+    if (deg) deg[i] = d;
+}
+
 // CSR of a generated graph whose layout covers all rows (tests and small exports): every row's
 // padded segments concatenated, padding duplicates dropped, ascending.
 int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx) {
@@ -457,6 +479,125 @@ static int er_fast_range(uint32_t n, double prob, uint64_t seed, uint32_t vb, ui
     g->g.minDeg = nloc ? (uint32_t)h[2] : 0;
     g->tiles.push_back(std::move(L));
     *out = g.release();
+    return MCMC_OK;
+}
+
+// Test hook: rows of a graph as stored on the device -- the full-range tiled layout of a generated
+// graph (CSR-less), or the CSR. off: [k + 1] (off[0] = 0); ids: NULL for the degrees only, else
+// cap >= off[k] entries, each row's ids in layout order; pos: optional [k], the tcol index of each
+// row's first stored id (layout graphs; 0 for a CSR).
+extern "C" int mcmc_graph_rows(const mcmc_graph* g, const uint32_t* rows, uint32_t k, uint64_t* off, uint32_t* ids,
+                               uint64_t cap, uint64_t* pos) {
+    if (!g || (k && (!rows || !off))) return fail(MCMC_E_ARG, "NULL argument");
+    for (uint32_t i = 0; i < k; i++)
+        if (rows[i] >= g->g.n) return fail(MCMC_E_ARG, "row out of range");
+    MCMC_HIP_TRY(hipSetDevice(g->g.device));
+    off[0] = 0;
+    if (k == 0) return MCMC_OK;
+    if (g->g.row_off) {
+        std::vector<uint64_t> ro(2);
+        for (uint32_t i = 0; i < k; i++) {
+            MCMC_HIP_TRY(hipMemcpy(ro.data(), g->g.row_off + rows[i], 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            off[i + 1] = off[i] + (ro[1] - ro[0]);
+            if (pos) pos[i] = 0;
+            if (ids) {
+                if (off[i + 1] > cap) return fail(MCMC_E_ARG, "ids capacity too small");
+                MCMC_HIP_TRY(hipMemcpy(ids + off[i], g->g.col_idx + ro[0], sizeof(uint32_t) * (ro[1] - ro[0]),
+                                       hipMemcpyDeviceToHost));
+            }
+        }
+        return MCMC_OK;
+    }
+    const TiledLayout* L = nullptr;
+    for (auto& t : g->tiles)
+        if (t->v_begin == 0 && t->v_end == g->g.n) L = t.get();
+    if (!L) return fail(MCMC_E_STATE, "graph has neither a CSR nor a full-range tiled layout");
+    uint32_t* d_rows = nullptr;
+    uint64_t *d_off = nullptr, *d_deg = nullptr, *d_pos = nullptr;
+    uint32_t* d_ids = nullptr;
+    hipError_t e = hipMalloc(&d_rows, sizeof(uint32_t) * k);
+    if (e == hipSuccess) e = hipMalloc(&d_off, sizeof(uint64_t) * (k + 1));
+    if (e == hipSuccess) e = hipMalloc(&d_deg, sizeof(uint64_t) * k);
+    if (e == hipSuccess) e = hipMalloc(&d_pos, sizeof(uint64_t) * k);
+    if (e == hipSuccess) e = hipMemcpy(d_rows, rows, sizeof(uint32_t) * k, hipMemcpyHostToDevice);
+    const uint32_t blocks = (k + 255) / 256;
+    if (e == hipSuccess) {
+        tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2, d_rows,
+                                          k, nullptr, d_deg, nullptr, d_pos);
+        e = hipDeviceSynchronize();
+    }
+    std::vector<uint64_t> deg(k);
+    if (e == hipSuccess) e = hipMemcpy(deg.data(), d_deg, sizeof(uint64_t) * k, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && pos) e = hipMemcpy(pos, d_pos, sizeof(uint64_t) * k, hipMemcpyDeviceToHost);
+    for (uint32_t i = 0; i < k; i++) off[i + 1] = off[i] + deg[i];
+    if (e == hipSuccess && ids) {
+        if (off[k] > cap) e = hipErrorInvalidValue;
+        if (e == hipSuccess) e = hipMalloc(&d_ids, sizeof(uint32_t) * std::max<uint64_t>(off[k], 1));
+        if (e == hipSuccess) e = hipMemcpy(d_off, off, sizeof(uint64_t) * (k + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2,
+                                              d_rows, k, d_off, nullptr, d_ids, nullptr);
+            e = hipDeviceSynchronize();
+        }
+        if (e == hipSuccess) e = hipMemcpy(ids, d_ids, sizeof(uint32_t) * off[k], hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d_rows);
+    (void)hipFree(d_off);
+    (void)hipFree(d_deg);
+    (void)hipFree(d_pos);
+    (void)hipFree(d_ids);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("graph rows: ") + hipGetErrorString(e));
+    return MCMC_OK;
+}
+
+// The CSR of a generated graph (uint64 offsets, uint32 ids), built on the device from its
+// full-range tiled layout: for callers that need the reference's layout itself (the refstruct
+// baseline at full occupancy). Rows keep layout order (not sorted: above 2^31 arcs the segmented
+// sort does not apply); the sweep and the layout are unaffected.
+extern "C" int mcmc_graph_materialize_csr(mcmc_graph* g) {
+    if (!g) return fail(MCMC_E_ARG, "NULL graph");
+    if (g->g.row_off) return MCMC_OK;
+    const TiledLayout* L = nullptr;
+    for (auto& t : g->tiles)
+        if (t->v_begin == 0 && t->v_end == g->g.n) L = t.get();
+    if (!L) return fail(MCMC_E_STATE, "graph has no full-range tiled layout");
+    MCMC_HIP_TRY(hipSetDevice(g->g.device));
+    const uint32_t n = g->g.n;
+    uint64_t *deg = nullptr, *off = nullptr;
+    uint32_t* idx = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hipError_t e = hipMalloc(&deg, sizeof(uint64_t) * ((size_t)n + 1));
+    if (e == hipSuccess) e = hipMalloc(&off, sizeof(uint64_t) * ((size_t)n + 1));
+    const uint32_t blocks = (n + 255) / 256;
+    if (e == hipSuccess) {
+        tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2,
+                                          nullptr, n, nullptr, deg, nullptr, nullptr);
+        e = hipMemset(deg + n, 0, sizeof(uint64_t));
+    }
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, deg, off, n + 1);
+    if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16));
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, deg, off, n + 1);
+    uint64_t m = 0;
+    if (e == hipSuccess) e = hipMemcpy(&m, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && m != g->g.m) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipMalloc(&idx, sizeof(uint32_t) * (m + 4));
+    if (e == hipSuccess) e = hipMemset(idx, 0, sizeof(uint32_t) * (m + 4));
+    if (e == hipSuccess) {
+        tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2,
+                                          nullptr, n, off, nullptr, idx, nullptr);
+        e = hipDeviceSynchronize();
+    }
+    (void)hipFree(deg);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) {
+        (void)hipFree(off);
+        (void)hipFree(idx);
+        return fail(MCMC_E_HIP, std::string("materialize CSR: ") + hipGetErrorString(e));
+    }
+    g->g.row_off = off;
+    g->g.col_idx = idx;
+    g->g.sorted = false;
     return MCMC_OK;
 }
 

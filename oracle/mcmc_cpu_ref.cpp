@@ -445,36 +445,52 @@ double series_log(double u) {
 
 }  // namespace
 
-int oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, uint32_t** col_idx, uint64_t* m) {
-    const double p = (double)(float)prob;
-    const int mode = p >= 1.0 ? 1 : (p <= 0.0 ? 2 : 0);
-    const double inv = mode == 0 ? 1.0 / std::log1p(-p) : 0.0;
-    const uint32_t T = 65536, nb = (uint32_t)(((uint64_t)n + T - 1) / T);
-    std::vector<std::pair<uint32_t, uint32_t>> edges;
-    for (uint32_t i = 0; i < n && mode != 2; i++) {
-        for (uint32_t Y = i / T; Y < nb; Y++) {
-            const uint64_t end = std::min<uint64_t>(n, (uint64_t)(Y + 1) * T);
-            uint64_t j = std::max<uint64_t>((uint64_t)Y * T, (uint64_t)i + 1);
-            if (j >= end) continue;
-            if (mode == 1) {
-                for (; j < end; j++) edges.emplace_back(i, (uint32_t)j);
-                continue;
-            }
-            j -= 1;
-            bool done = false;
-            for (uint32_t k = 0; !done; k++) {
-                uint32_t c[4] = {k, i, Y, 0x45524721u};
-                philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-                for (int q = 0; q < 4 && !done; q++) {
-                    const double t = series_log(((double)c[q] + 1.0) * 2.3283064365386963e-10) * inv;
-                    const uint64_t skip = (t < 2147483647.0) ? 1u + (uint32_t)t : 0x7FFFFFFFu;
-                    j += skip;
-                    if (j >= end) done = true;
-                    else edges.emplace_back(i, (uint32_t)j);
-                }
-            }
+// Stream (i, Y) of the definition: calls emit(j) for every present column j of block Y, j > i.
+}  // extern "C"
+namespace {
+template <class Emit>
+void er_walk_stream(uint32_t n, int mode, double inv, uint64_t seed, uint32_t i, uint32_t Y, Emit&& emit) {
+    const uint32_t T = 65536;
+    const uint64_t end = std::min<uint64_t>(n, (uint64_t)(Y + 1) * T);
+    uint64_t j = std::max<uint64_t>((uint64_t)Y * T, (uint64_t)i + 1);
+    if (j >= end || mode == 2) return;
+    if (mode == 1) {
+        for (; j < end; j++) emit((uint32_t)j);
+        return;
+    }
+    j -= 1;
+    for (uint32_t k = 0;; k++) {
+        uint32_t c[4] = {k, i, Y, 0x45524721u};
+        philox10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        for (int q = 0; q < 4; q++) {
+            const double t = series_log(((double)c[q] + 1.0) * 2.3283064365386963e-10) * inv;
+            const uint64_t skip = (t < 2147483647.0) ? 1u + (uint32_t)t : 0x7FFFFFFFu;
+            j += skip;
+            if (j >= end) return;
+            emit((uint32_t)j);
         }
     }
+}
+
+struct ErConst {
+    int mode;
+    double inv;
+};
+ErConst er_const(double prob) {
+    const double p = (double)(float)prob;
+    const int mode = p >= 1.0 ? 1 : (p <= 0.0 ? 2 : 0);
+    return ErConst{mode, mode == 0 ? 1.0 / std::log1p(-p) : 0.0};
+}
+}  // namespace
+extern "C" {
+
+int oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, uint32_t** col_idx, uint64_t* m) {
+    const ErConst ec = er_const(prob);
+    const uint32_t T = 65536, nb = (uint32_t)(((uint64_t)n + T - 1) / T);
+    std::vector<std::pair<uint32_t, uint32_t>> edges;
+    for (uint32_t i = 0; i < n && ec.mode != 2; i++)
+        for (uint32_t Y = i / T; Y < nb; Y++)
+            er_walk_stream(n, ec.mode, ec.inv, seed, i, Y, [&](uint32_t j) { edges.emplace_back(i, j); });
     uint64_t* off = (uint64_t*)calloc((size_t)n + 1, sizeof(uint64_t));
     if (!off) return -1;
     for (auto& e : edges) { off[e.first + 1]++; off[e.second + 1]++; }
@@ -488,6 +504,104 @@ int oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, u
     *col_idx = idx;
     *m = off[n];
     return 0;
+}
+
+// Neighbour lists of selected rows of the same G(n, p), without enumerating the whole graph (the
+// C3 graph has 1e11 arcs): row v's arcs are its own streams (v, Y), Y >= v's block (j > v), plus
+// every i < v whose stream (i, block(v)) emits v -- all streams (i, X) into the sampled rows' blocks
+// X are walked once (OpenMP over i). *row_off[k + 1], *col_idx: rows in the given order, each
+// ascending. Allocates like oracle_er_fast.
+int oracle_er_rows(uint32_t n, double prob, uint64_t seed, const uint32_t* rows, uint32_t k, int nthreads,
+                   uint64_t** row_off, uint32_t** col_idx) {
+    const ErConst ec = er_const(prob);
+    const uint32_t T = 65536, nb = (uint32_t)(((uint64_t)n + T - 1) / T);
+    std::vector<std::vector<uint32_t>> adj(k);
+    for (uint32_t s = 0; s < k; s++) {
+        if (rows[s] >= n) return -1;
+        for (uint32_t Y = rows[s] / T; Y < nb; Y++)
+            er_walk_stream(n, ec.mode, ec.inv, seed, rows[s], Y, [&](uint32_t j) { adj[s].push_back(j); });
+    }
+    std::vector<uint32_t> blocks;
+    for (uint32_t s = 0; s < k; s++) blocks.push_back(rows[s] / T);
+    std::sort(blocks.begin(), blocks.end());
+    blocks.erase(std::unique(blocks.begin(), blocks.end()), blocks.end());
+    for (uint32_t X : blocks) {
+        std::vector<int32_t> slot(T, -1);   // block-local column -> sampled row
+        for (uint32_t s = 0; s < k; s++)
+            if (rows[s] / T == X) slot[rows[s] - X * T] = (int32_t)s;
+        const uint32_t iend = (uint32_t)std::min<uint64_t>(n, (uint64_t)(X + 1) * T);
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> found(std::max(nthreads, 1));
+#ifdef _OPENMP
+        #pragma omp parallel for num_threads(std::max(nthreads, 1)) schedule(dynamic, 4096)
+#endif
+        for (int64_t ii = 0; ii < (int64_t)iend; ii++) {
+            int tid = 0;
+#ifdef _OPENMP
+            tid = omp_get_thread_num();
+#endif
+            const uint32_t i = (uint32_t)ii;
+            er_walk_stream(n, ec.mode, ec.inv, seed, i, X, [&](uint32_t j) {
+                const int32_t s = slot[j - X * T];
+                if (s >= 0) found[tid].emplace_back((uint32_t)s, i);
+            });
+        }
+        for (auto& f : found)
+            for (auto& e : f) adj[e.first].push_back(e.second);
+    }
+    uint64_t* off = (uint64_t*)calloc((size_t)k + 1, sizeof(uint64_t));
+    if (!off) return -1;
+    for (uint32_t s = 0; s < k; s++) off[s + 1] = off[s] + adj[s].size();
+    uint32_t* idx = (uint32_t*)malloc(std::max<uint64_t>(off[k], 1) * sizeof(uint32_t));
+    if (!idx) { free(off); return -1; }
+    for (uint32_t s = 0; s < k; s++) {
+        std::sort(adj[s].begin(), adj[s].end());
+        std::copy(adj[s].begin(), adj[s].end(), idx + off[s]);
+    }
+    *row_off = off;
+    *col_idx = idx;
+    return 0;
+}
+
+// u of engine draw number pos[i] (1-based) of std::default_random_engine(seed): the bulk draw of
+// coloringMCMC_CPU.cpp:139 gives vertex v of sweep t draw K0 + t n + v + 1. minstd skip-ahead
+// x_pos = x_0 16807^pos mod (2^31 - 1), then generate_canonical (canonical_from_state); pinned
+// against g.discard() by tests/test_oracle.py.
+void oracle_canonical_at(uint32_t seed, const uint64_t* pos, uint64_t k, float* out) {
+    uint64_t x0 = (uint64_t)seed % kM;
+    if (x0 == 0) x0 = 1;
+    for (uint64_t i = 0; i < k; i++) out[i] = canonical_from_state(mulmod(x0, powmod(kA, pos[i])));
+}
+
+// One vertex of loop 1 (coloringMCMC_CPU.cpp:183-204) from its neighbours' colours: violation flag
+// (violation_count :329-351: own colour used by a neighbour), count_free_colors (:361-383), fill_p
+// (:392-481, colorIdx the identity) and extract_new_color (:492-528, taboo 0). Returns 1 for a CDF
+// overflow (the colour then comes from rand(), :516-520; *color untouched), else 0.
+int oracle_vertex_update(uint32_t nCol, float epsilon, uint32_t cv, const uint32_t* nbr_colors, uint64_t deg,
+                         float u, uint32_t* color, int* viol) {
+    std::vector<bool> fc(nCol, true);
+    bool v = false;
+    for (uint64_t i = 0; i < deg; i++) {
+        fc[nbr_colors[i]] = false;
+        v = v || nbr_colors[i] == cv;
+    }
+    *viol = v ? 1 : 0;
+    const size_t Zvcomp = std::count(fc.begin(), fc.end(), true);
+    const size_t Zv = nCol - Zvcomp;
+    std::vector<float> p(nCol);
+    for (uint32_t c = 0; c < nCol; c++) {
+        if (v) {
+            if (Zvcomp == 0) p[c] = (c == cv) ? 1.0f - (nCol - 1) * epsilon : epsilon;
+            else p[c] = fc[c] ? (1.0f - epsilon * Zv) / (float)Zvcomp : epsilon;
+        } else {
+            p[c] = (c == cv) ? 1.0f - (nCol - 1) * epsilon : epsilon;
+        }
+    }
+    float cdf = 0;
+    for (uint32_t c = 0; c < nCol; c++) {
+        cdf += p[c];
+        if (cdf > u) { *color = c; return 0; }
+    }
+    return 1;
 }
 
 // Graph::doStats (graphCPU.cpp:433-450) -> maxDeg, the default nCol (main.cu:162).

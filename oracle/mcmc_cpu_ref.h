@@ -75,7 +75,19 @@ uint32_t oracle_max_deg(uint32_t n, const uint64_t* row_off);
 // 1 + floor(ln(u) / log1p(-p)), u = (x + 1) / 2^32, ln by the same +-*/ series.
 // Rows ascending. Allocates like oracle_setup_rnd2.
 int      oracle_er_fast(uint32_t n, double prob, uint64_t seed, uint64_t** row_off, uint32_t** col_idx, uint64_t* m);
+// Neighbour lists (ascending) of selected rows of that graph, without enumerating the whole of it:
+// the C3 graph (1e11 arcs) checked row by row. *row_off: [k + 1], rows in the given order.
+int      oracle_er_rows(uint32_t n, double prob, uint64_t seed, const uint32_t* rows, uint32_t k, int nthreads,
+                        uint64_t** row_off, uint32_t** col_idx);
 void     oracle_free(void* p);
+
+// ---- per-vertex pieces for sampled checks at sizes where the whole run cannot be restated ----
+// u of engine draw pos[i] (1-based) of default_random_engine(seed) (coloringMCMC_CPU.cpp:139).
+void     oracle_canonical_at(uint32_t seed, const uint64_t* pos, uint64_t k, float* out);
+// One vertex of the sweep from its neighbours' colours (violation_count, count_free_colors, fill_p,
+// extract_new_color with taboo 0). Returns 1 on a CDF overflow (colour from rand()), else 0.
+int      oracle_vertex_update(uint32_t nCol, float epsilon, uint32_t cv, const uint32_t* nbr_colors, uint64_t deg,
+                              float u, uint32_t* color, int* viol);
 
 // ---- MCMC: ColoringMCMC_CPU(g, params, seed) + run() ----
 // out_init   : optional [n]  initial coloring (after the ctor)

@@ -58,6 +58,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_er_fast.argtypes = [c_uint32, ctypes.c_double, c_uint64, POINTER(POINTER(c_uint64)),
                                      POINTER(POINTER(c_uint32)), POINTER(c_uint64)]
         L.oracle_max_deg.restype = c_uint32
+        L.oracle_er_rows.argtypes = [c_uint32, ctypes.c_double, c_uint64, c_void_p, c_uint32, c_int,
+                                     POINTER(POINTER(c_uint64)), POINTER(POINTER(c_uint32))]
+        L.oracle_canonical_at.argtypes = [c_uint32, c_void_p, c_uint64, c_void_p]
+        L.oracle_vertex_update.argtypes = [c_uint32, c_float, c_uint32, c_void_p, c_uint64, c_float,
+                                           POINTER(c_uint32), POINTER(c_int)]
         L.oracle_free.argtypes = [c_void_p]
         L.oracle_mcmc_run.argtypes = [c_uint32, c_void_p, c_void_p, POINTER(OracleParams), c_uint32, c_void_p,
                                       c_void_p, c_void_p, c_uint64, c_uint32, c_int, POINTER(OracleResult)]
@@ -113,6 +118,41 @@ def er_fast(n: int, prob: float, seed: int) -> tuple[np.ndarray, np.ndarray]:
     lib().oracle_free(ctypes.cast(off, c_void_p))
     lib().oracle_free(ctypes.cast(idx, c_void_p))
     return a, b
+
+
+def er_rows(n: int, prob: float, seed: int, rows, nthreads: int = 0) -> list[np.ndarray]:
+    """Neighbour lists (ascending) of the given rows of er_fast(n, prob, seed), found without
+    enumerating the graph (streams into the rows' column blocks only)."""
+    import os
+
+    r = np.ascontiguousarray(rows, dtype=np.uint32)
+    off = POINTER(c_uint64)()
+    idx = POINTER(c_uint32)()
+    th = nthreads or int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    rc = lib().oracle_er_rows(n, prob, seed, _p(r), len(r), th, byref(off), byref(idx))
+    assert rc == 0
+    o = np.ctypeslib.as_array(off, (len(r) + 1,)).copy()
+    m = int(o[-1])
+    b = np.ctypeslib.as_array(idx, (max(m, 1),))[:m].copy()
+    lib().oracle_free(ctypes.cast(off, c_void_p))
+    lib().oracle_free(ctypes.cast(idx, c_void_p))
+    return [b[o[i]:o[i + 1]] for i in range(len(r))]
+
+
+def canonical_at(seed: int, positions) -> np.ndarray:
+    """u of engine draws `positions` (1-based) of default_random_engine(seed)."""
+    pos = np.ascontiguousarray(positions, dtype=np.uint64)
+    out = np.zeros(len(pos), dtype=np.float32)
+    lib().oracle_canonical_at(seed & 0xFFFFFFFF, _p(pos), len(pos), _p(out))
+    return out
+
+
+def vertex_update(nCol: int, eps: float, cv: int, nbr_colors: np.ndarray, u: float):
+    """(new colour or None on a CDF overflow, viol) of one vertex (coloringMCMC_CPU.cpp:183-204)."""
+    nc = np.ascontiguousarray(nbr_colors, dtype=np.uint32)
+    col, viol = c_uint32(), c_int()
+    ov = lib().oracle_vertex_update(nCol, eps, cv, _p(nc) if len(nc) else None, len(nc), u, byref(col), byref(viol))
+    return (None if ov else col.value), bool(viol.value)
 
 
 def max_deg(row_off: np.ndarray) -> int:

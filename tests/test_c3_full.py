@@ -1,0 +1,84 @@
+"""configs[2] (C3) at full size: `--mcmcgpu --simulate 0.001 -n 10000000`, 32 colours, one MI355X.
+
+The only other GPU runs of this path are reduced (tests/test_gpu_parity.py::test_er_fast_*, n <= 2e5).
+Here the real graph is built (the build's G(n, p), csrc/er_gen.h, seed 1: 1e7 rows, ~1e11 arcs, 153
+column blocks, layout indices far past 2^32) and checked against the oracle without enumerating it:
+
+  * rows: ~1000 sampled rows of three column blocks (first, middle, last) read back from the tiled
+    layout (mcmc_graph_rows) equal the oracle's per-row restatement of the generator
+    (oracle_er_rows: the rows' own streams plus every stream into their blocks);
+  * C_0 equals ColoringMCMC_CPU's initial colouring (uniform_int from default_random_engine(seed),
+    coloringMCMC_CPU.cpp:53-61) on all 1e7 vertices;
+  * sweeps 0..2: for every sampled vertex, C_{t+1}[v] equals the oracle's one-vertex update
+    (count_free_colors / fill_p / extract_new_color, coloringMCMC_CPU.cpp:361-528) from C_t on its
+    regenerated row and u_v = engine draw K0 + t n + v + 1 (:139); the per-vertex violation flags
+    of the tail cut's recount kernel (a second code path over the layout) equal the oracle's for
+    the sampled rows; the recount's total equals the sweep's fused Cviol_t (the trajectory).
+"""
+import time
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+
+N, P, SEED, NCOL, EPS = 10_000_000, 0.001, 1, 32, 1e-8
+T = 65536
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c3_full_size_rows_and_sweeps(hip_lib):
+    import mcmc_colorer_amd.colorer as M
+
+    t0 = time.perf_counter()
+    g = M.Graph.er_fast(N, P, SEED)
+    print(f"\nC3 graph: n={g.nNodes} m={g.nEdges} maxDeg={g.maxDeg} ({time.perf_counter() - t0:.1f} s)", flush=True)
+    assert g.nNodes == N and g.nEdges > 9.9e10
+    rng = np.random.default_rng(2026)
+    rows = []
+    for X in (0, 76, (N - 1) // T):
+        lo, hi = X * T, min(N, (X + 1) * T)
+        rows += [lo, lo + 1, hi - 1] + rng.integers(lo, hi, 330).tolist()
+    rows = np.unique(np.array(rows, dtype=np.uint32))
+    got, pos = g.rows(rows)
+    t1 = time.perf_counter()
+    ref = O.er_rows(N, P, SEED, rows)
+    print(f"oracle rows: {len(rows)} rows in {time.perf_counter() - t1:.1f} s; layout index of the first id "
+          f"(sample): " + ", ".join(f"row {int(v)} @ {int(q)}" for v, q in list(zip(rows, pos))[::150]), flush=True)
+    for v, a, b in zip(rows, got, ref):
+        assert np.array_equal(np.sort(a), b), f"row {v}"
+    assert int((pos >= 2**32).sum()) >= 600, "sampled rows must reach layout indices past 2^32"
+
+    col = M.ColoringMCMC(g, M.GPURand(N, SEED, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=NCOL))
+    col.init(0)
+    C = [col.coloring()]
+    exp0 = np.zeros(N, dtype=np.uint32)
+    k0 = int(O.lib().oracle_uniform_int_seq(SEED, NCOL, N, O._p(exp0)))
+    assert np.array_equal(C[0], exp0), "initial colouring"
+    counts, flags = [], []
+    for t in range(3):
+        c, f = col.count_violations(flags=True)
+        counts.append(c)
+        flags.append(f[rows])
+        st = col.step(1)
+        C.append(col.coloring())
+    assert st.initDraws == k0
+    traj = col.trajectory()
+    print(f"Cviol trajectory {traj.tolist()}, recount {counts}", flush=True)
+    assert traj.tolist() == counts, "fused Cviol_t != recount of C_t"
+    checked = events = 0
+    for t in range(3):
+        u = O.canonical_at(SEED, k0 + t * N + rows.astype(np.uint64) + 1)
+        for i, v in enumerate(rows.tolist()):
+            c, viol = O.vertex_update(NCOL, EPS, int(C[t][v]), C[t][ref[i]], float(u[i]))
+            assert bool(flags[t][i]) == viol, f"violation flag of {v} at sweep {t}"
+            if c is None:
+                events += 1
+            else:
+                assert int(C[t + 1][v]) == c, f"C_{t + 1}[{v}]"
+                checked += 1
+    print(f"checked {checked} vertex updates ({events} CDF overflows skipped)", flush=True)
+    assert checked >= 2900
+    col.close()
+    g.close()

@@ -88,6 +88,28 @@ def test_full_forbidden_set_is_reported():
         literal_greedy_ff(off, idx)
 
 
+def asymmetric_graph(n=400, arcs=2400, seed=5):
+    """Directed arcs without their reverse (mcmc_graph_upload accepts any CSR), rows ascending."""
+    rng = np.random.default_rng(seed)
+    E = set()
+    while len(E) < arcs:
+        a, b = (int(x) for x in rng.integers(0, n, 2))
+        if a != b:
+            E.add((a, b))
+    E = sorted(E)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.add.at(off, np.array([a for a, _ in E]) + 1, 1)
+    return np.cumsum(off).astype(np.uint64), np.array([b for _, b in E], dtype=np.uint32)
+
+
+def test_restatement_matches_literal_kernels_asymmetric():
+    """On an asymmetric CSR an older node can lose to a fresh smaller neighbour whose row lacks it."""
+    off, idx = asymmetric_graph()
+    a, ra = NP.greedy_ff(off, idx)
+    b, rb = literal_greedy_ff(off, idx)
+    assert a.tolist() == b.tolist() and ra == rb
+
+
 def test_restatement_is_a_proper_colouring():
     O.srand(1)
     off, idx = O.setup_rnd2(1500, 0.05)
@@ -119,6 +141,28 @@ def test_gpu_greedyff_simulate(hip_lib, n, p):
     c, r = NP.greedy_ff(off, idx)
     assert col.colors.tolist() == c.tolist()
     assert col.rounds == r and col.numColors == len(set(c.tolist()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [5, 6, 7])
+def test_gpu_greedyff_asymmetric_csr(hip_lib, seed):
+    """the fresh-only conflict scan is valid on symmetric CSRs only; an asymmetric one
+    scans every coloured row, as conflict_detection (coloringGreedyFF.cu:134-163) does."""
+    off, idx = asymmetric_graph(seed=seed)
+    col = _gpu(off, idx)
+    c, r = NP.greedy_ff(off, idx)
+    assert col.colors.tolist() == c.tolist() and col.rounds == r
+
+
+@pytest.mark.gpu
+def test_gpu_vff_asymmetric_csr(hip_lib):
+    import mcmc_colorer_amd.colorer as M
+
+    off, idx = asymmetric_graph(seed=8)
+    col = M.ColoringVFF(M.Graph.from_csr(off, idx))
+    col.run()
+    c, K, it, valid = NP.vff(off, idx)
+    assert col.colors.tolist() == c.tolist() and (col.numColors, col.iterations, col.valid) == (K, it, valid)
 
 
 @pytest.mark.gpu

@@ -173,3 +173,41 @@ def test_oracle_tail_cut_equals_python_restatement(n, p, ncol, seed, maxrip, tai
     assert rep.colors.tolist() == C.tolist()
     assert (rep.res.finalViol, rep.res.tailcutPasses) == (cviol, passes)
     assert passes > 0 or base.res.finalViol == 0
+
+
+# ---- per-row / per-vertex pieces used by the full-size C3 check (tests/test_c3_full.py) ----------
+def test_er_rows_equal_full_generator_rows():
+    """oracle_er_rows (streams into the sampled rows' blocks only) == the rows of oracle_er_fast."""
+    n, p, seed = 140000, 0.0002, 7   # 3 column blocks
+    off, idx = O.er_fast(n, p, seed)
+    rng = np.random.default_rng(3)
+    rows = np.concatenate([[0, 1, 65535, 65536, 131071, 131072, n - 1], rng.integers(0, n, 60)]).astype(np.uint32)
+    got = O.er_rows(n, p, seed, rows, nthreads=4)
+    for v, g in zip(rows, got):
+        assert g.tolist() == idx[off[v]:off[v + 1]].tolist(), v
+
+
+def test_canonical_at_equals_sequential_draws():
+    seq = np.zeros(3000, dtype=np.float32)
+    O.lib().oracle_canonical_seq(5, 0, 3000, O._p(seq))
+    pos = np.array([1, 2, 3, 999, 2000, 3000], dtype=np.uint64)
+    assert O.canonical_at(5, pos).tolist() == seq[(pos - 1).astype(np.int64)].tolist()
+
+
+@pytest.mark.parametrize("ncol,eps", [(16, 1e-8), (7, 1e-8), (12, 3e7)])
+def test_vertex_update_equals_one_oracle_sweep(ncol, eps):
+    """Every vertex of one full oracle sweep, recomputed from C_0, its neighbours and u_v = draw
+    K0 + v + 1; CDF-overflow vertices (colour from rand()) are the only ones left out."""
+    O.srand(1)
+    off, idx = O.setup_rnd2(600, 0.05)
+    n = len(off) - 1
+    r1 = O.mcmc_run(off, idx, ncol, 3, epsilon=eps, sweep_limit=1)
+    u = O.canonical_at(3, r1.res.initDraws + np.arange(n, dtype=np.uint64) + 1)
+    events = 0
+    for v in range(n):
+        c, viol = O.vertex_update(ncol, eps, int(r1.init[v]), r1.init[idx[off[v]:off[v + 1]]], float(u[v]))
+        if c is None:
+            events += 1
+        else:
+            assert c == r1.colors[v], v
+    assert events == r1.res.glibcDraws
