@@ -178,6 +178,10 @@ def refstruct_baseline(g, ncol: int, sweeps: int, seed: int, n: int, value: floa
             "speedup": value / v,
             "model_bytes_hbm": hbm, "model_bytes_pcie": 8 * n,
             "achieved_GBs": hbm / (ms.value * 1e-3) / 1e9, "frac_of_hbm_peak": hbm / (ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            # the same structure if it streamed its model bytes at the HBM peak: an upper bound for any
+            # implementation of the reference's per-sweep structure on this chip
+            "bound_value_at_hbm_peak": n / (hbm / (HBM_PEAK_GBS * 1e9)),
+            "speedup_vs_bound": value / (n / (hbm / (HBM_PEAK_GBS * 1e9))),
             "what": "HIP re-expression of ColoringMCMC::run's per-sweep structure (thread-per-vertex serial "
                     "row walks, 64-thread blocks, n*nCol checker memset, 2 conflict passes + host sums, 4n B "
                     "D2H + host histogram + H2D), host wall per sweep"}
