@@ -6,7 +6,9 @@ infeasible there (5e13 sequential glibc draws), so the graph is the build's docu
 G(n, p) (mcmc_colorer_amd/csrc/er_gen.h, seed 1), generated on the GPU straight into
 the sweep's tiled layout (1e11 arcs, 217 GB; no CSR could exist: 400 GB). Under torchrun (N > 1) it
 is configs[3]: the same graph vertex-partitioned over N GPUs (strong scaling), every rank generating
-only its own rows, one RCCL all-gather per sweep (mcmc_colorer_amd/distributed.py).
+only its own rows; the loop runs natively with the RCCL communicator inside libmcmc_hip.so
+(mcmc_part_run, csrc/multi.hip: per sweep the row ranges travel by P2P sends over xGMI -- or one
+all-gather for equal ranges -- plus one all-gather of the 4 KiB footers).
 `--config c2`: configs[1], `--simulate 0.01 -n 100000 --nCol 16` with the reference's exact setupRnd2
 graph (weak scaling at N > 1: N*1e5 rows, p 0.01/N).
 `--config c5`: configs[4] (power-law, nCol = maxDeg). SNAP LiveJournal / Reddit are not available, so
@@ -224,10 +226,8 @@ def main() -> int:
     ap.add_argument("--no-convergence", action="store_true", help="skip the reference-loop run (sweeps-to-zero-conflict)")
     ap.add_argument("--refstruct-sweeps", type=int, default=10)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
-    ap.add_argument("--force-dist", action="store_true", help="partitioned driver even at world size 1 (testing)")
-    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
-                    help="torch.distributed backend (nccl = RCCL; gloo only to rehearse ranks sharing one GPU)")
-    ap.add_argument("--same-device", action="store_true", help="every rank on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="the native partitioned driver (RCCL inside the library) even at world size 1")
     ap.add_argument("--semantics", choices=["cpu", "ref"], default="cpu",
                     help="cpu: --mcmccpu semantics (the north-star path); ref: the reference GPU colorer's own "
                          "semantics (--mcmcgpu-ref), one GPU")
@@ -244,18 +244,16 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.same_device:
-        local = 0
     dist = None
     if world > 1 or a.force_dist:
         import torch
         import torch.distributed as dist
 
+        # The data path's RCCL communicator lives inside libmcmc_hip.so (mcmc_comm_init_rank,
+        # mcmc_part_run); torch.distributed only carries rank 0's unique id, the barriers and the
+        # max over ranks, on the CPU (gloo)
         torch.cuda.set_device(local)
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")
 
     import mcmc_colorer_amd.colorer as M
     from mcmc_colorer_amd._lib import check, lib
@@ -270,16 +268,27 @@ def main() -> int:
         n_req, p_req = a.vertices * world, a.prob / world
     t_gen = time.perf_counter()
     rng = M.GlibcRand(1)
+    bounds = None
     if a.config == "c3":
         # setupRnd2 is infeasible at n = 1e7 (5e13 draws): the build's documented generator, fixed seed 1,
-        # written straight into the tiled layout; under torchrun each rank generates only its rows
-        g = M.Graph.er_fast(n_req, p_req, 1, device=dev, world=world if dist is not None else 1,
-                            rank=rank if dist is not None else 0)
+        # written straight into the tiled layout; under torchrun each rank generates only its rows of
+        # the equal-rows plan (G(n, p) is uniform: equal rows are arc-balanced)
+        if dist is not None:
+            from mcmc_colorer_amd.distributed import plan_rows
+
+            bounds = plan_rows(n_req, world)
+            g = M.Graph.er_fast(n_req, p_req, 1, device=dev, rows=(int(bounds[rank]), int(bounds[rank + 1])))
+        else:
+            g = M.Graph.er_fast(n_req, p_req, 1, device=dev)
     elif a.config == "c5":
         g = M.Graph.rmat(22, 10, 0.5, 0.2, 0.2, 1, device=dev)
         a.ncol = g.getMaxNodeDeg()   # main.cu:162 default: maxDeg * numColRatio (1)
     else:
         g = M.Graph.simulate(n_req, p_req, rng, device=dev)
+    if dist is not None and bounds is None:   # power-law C5: arc-balanced plan from the degree prefix
+        from mcmc_colorer_amd.distributed import plan
+
+        bounds = plan(g, world, balance=True)
     t_gen = time.perf_counter() - t_gen
     params = M.ColoringMCMCParams(nCol=a.ncol, maxRip=0x7FFFFFF0)   # throughput mode: no cap
     tot = ctypes.c_double()
@@ -335,28 +344,25 @@ def main() -> int:
     else:
         import torch
 
-        from mcmc_colorer_amd.distributed import PartitionedColoringMCMC
+        from mcmc_colorer_amd._lib import MCMCRunStats
+        from mcmc_colorer_amd.distributed import NativePartitionedColoringMCMC
 
-        drv = PartitionedColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params)
-        drv.b.init(a.seed, rng)
-        for t in range(a.warmup):
-            drv._step(t)
+        drv = NativePartitionedColoringMCMC(g, M.GPURand(g.nNodes, a.seed, rng), params, bounds, device=local)
+        drv.init(0)
+        check(lib().mcmc_set_bench_mode(drv._ctx, 1))   # throughput mode: no convergence stop
+        arr = (ctypes.c_void_p * 1)(drv._ctx.value)
+        st = MCMCRunStats()
+        if a.warmup:
+            check(lib().mcmc_part_run(arr, 1, a.warmup, ctypes.byref(st)))
         barrier()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        ev0.record()
-        for t in range(a.warmup, a.warmup + a.steps):
-            drv._step(t)
-        ev1.record()
+        check(lib().mcmc_part_run(arr, 1, a.steps, ctypes.byref(st)))   # sweeps + RCCL exchanges + commits
         barrier()
         wall = time.perf_counter() - t0
-        done, _, err = drv.b.state()
-        if err:
-            raise RuntimeError("device error flag during the partitioned bench")
-        kernel_ms = ev0.elapsed_time(ev1) / a.steps   # whole step per rank: sweep + exchange + commit
-        info = drv.b.info()
-        rdev = f"cuda:{local}" if a.backend == "nccl" else "cpu"
-        w = torch.tensor([wall], dtype=torch.float64, device=rdev)
+        kernel_ms = st.loopMs / a.steps   # device time of one whole step on this rank's stream
+        info = drv.info()
+        info["bounds"] = [int(x) for x in bounds]
+        w = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
 
@@ -364,7 +370,7 @@ def main() -> int:
     if dist is not None and a.config == "c3":   # per-rank graphs hold their rows' arcs only
         import torch
 
-        mt = torch.tensor([m], dtype=torch.float64, device=f"cuda:{local}" if a.backend == "nccl" else "cpu")
+        mt = torch.tensor([m], dtype=torch.float64)
         dist.all_reduce(mt)
         m = int(mt.item())
     value = n * a.steps / wall          # all ranks together update n vertices per sweep
@@ -401,7 +407,8 @@ def main() -> int:
                    "config": a.config,
                    "semantics": "reference GPU colorer (--mcmcgpu-ref)" if ref else "--mcmccpu (north star)",
                    "n": n, "arcs": m, "nCol": a.ncol,
-                   "parallelism": f"vertex-partitioned x{world} (RCCL all-gather per sweep)" if world > 1 else "single",
+                   "parallelism": (f"vertex-partitioned x{world} (native RCCL exchange per sweep, "
+                                   f"{'arc-balanced' if a.config == 'c5' else 'equal-row'} plan)") if world > 1 else "single",
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,

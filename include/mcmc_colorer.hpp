@@ -102,6 +102,12 @@ public:
         MCMC_CHECK(mcmc_graph_er_fast(nn, prob_, seed, device, &h_));
         info();
     }
+    // Only rows [v_begin, v_end) of that graph (one rank of a partitioned run).
+    Graph(ErFast, node nn, float prob_, uint64_t seed, int device, node v_begin, node v_end)
+        : prob(prob_), device_(device) {
+        MCMC_CHECK(mcmc_graph_er_fast_rows(nn, prob_, seed, v_begin, v_end, device, &h_));
+        info();
+    }
     // Host CSR (e.g. from the edge-list importer) -> device copy.
     Graph(const std::vector<uint64_t>& cumulDegs, const std::vector<node>& neighs, float prob_, int device = 0)
         : prob(prob_), device_(device) {
@@ -131,6 +137,7 @@ public:
     node getMinNodeDeg() const { return minDeg_; }
     float getMeanNodeDeg() const { return n_ ? (float)m_ / (float)n_ : 0.0f; }
     const mcmc_graph* handle() const { return h_; }
+    int device() const { return device_; }
     float prob{0.0f};
 
 private:
@@ -163,13 +170,34 @@ class ColoringMCMC {
 public:
     ColoringMCMC(Graph<nodeW, edgeW>* inGraph_d, GPURandHandle* randStates, ColoringMCMCParams params)
         : graph(inGraph_d), seed(randStates->seed), param(params) {}
-    ~ColoringMCMC() { if (ctx) mcmc_destroy(ctx); }
+    // Extension: the same colorer vertex-partitioned over several GPUs of this node,
+    // one graph per device (each holding at least the rows [bounds[i], bounds[i+1]) of its rank, in
+    // rank order), driven from this thread with RCCL inside the library (mcmc_comm_init_all,
+    // mcmc_part_create, mcmc_part_run). run() / save() / the results are those of the one-GPU run.
+    ColoringMCMC(std::vector<Graph<nodeW, edgeW>*> perDevice, std::vector<uint32_t> bounds_, GPURandHandle* randStates,
+                 ColoringMCMCParams params)
+        : graph(perDevice.at(0)), parts(perDevice), bounds(bounds_), seed(randStates->seed), param(params) {
+        if (bounds.size() != parts.size() + 1) {
+            std::fprintf(stderr, "ColoringMCMC: %zu graphs need %zu bounds\n", parts.size(), parts.size() + 1);
+            std::abort();
+        }
+        std::vector<int> devs;
+        for (auto* g : parts) devs.push_back(g->device());
+        comms.resize(parts.size());
+        MCMC_CHECK(mcmc_comm_init_all(devs.data(), (uint32_t)devs.size(), comms.data()));
+    }
+    ~ColoringMCMC() {
+        if (ctx) mcmc_destroy(ctx);
+        for (auto* c : pctx) mcmc_destroy(c);
+        for (auto* c : comms) mcmc_comm_destroy(c);
+    }
 
     void setDirectoryPath(std::string directory) { this->directory = directory; }
 
     // One repetition: engine seed = seed + iteration (main.cu:171), glibc stream = process global.
     void run(int iteration) {
         if (ctx) mcmc_destroy(ctx);
+        ctx = nullptr;
         mcmc_params p{};
         p.nCol = param.nCol;
         p.epsilon = param.epsilon;
@@ -180,17 +208,38 @@ public:
         p.tabooIteration = param.tabooIteration;
         p.tailcut = param.tailcut;
         p.seed = seed + (uint32_t)iteration;
-        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
-        MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));
-        if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(ctx, param.tailcutRepair));
-        MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
-        MCMC_CHECK(mcmc_run(ctx, 0, &stats));
-        MCMC_CHECK(mcmc_get_glibc_window(ctx, mcmc::glibc_global().w));
+        mcmc_ctx* res = nullptr;
+        if (parts.empty()) {
+            MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
+            MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));
+            if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(ctx, param.tailcutRepair));
+            MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
+            MCMC_CHECK(mcmc_run(ctx, 0, &stats));
+            res = ctx;
+        } else {
+            if (param.tailcutRepair) {
+                std::fprintf(stderr, "ColoringMCMC: the tail-cut repair runs on one GPU\n");
+                std::abort();
+            }
+            for (auto* c : pctx) mcmc_destroy(c);
+            pctx.assign(parts.size(), nullptr);
+            const uint32_t world = (uint32_t)parts.size();
+            for (uint32_t r = 0; r < world; r++) {
+                MCMC_CHECK(mcmc_part_create(parts[r]->handle(), &p, world, r, bounds.data(), comms[r], &pctx[r]));
+                MCMC_CHECK(mcmc_set_glibc_window(pctx[r], mcmc::glibc_global().w));
+                MCMC_CHECK(mcmc_init_coloring(pctx[r], nullptr));
+            }
+            std::vector<mcmc_run_stats> st(world);
+            MCMC_CHECK(mcmc_part_run(pctx.data(), world, 0, st.data()));
+            stats = st[0];
+            res = pctx[0];
+        }
+        MCMC_CHECK(mcmc_get_glibc_window(res, mcmc::glibc_global().w));
         coloring.resize(graph->getNNodes());
-        MCMC_CHECK(mcmc_get_coloring(ctx, coloring.data()));
+        MCMC_CHECK(mcmc_get_coloring(res, coloring.data()));
         trajectory.resize(stats.trajLen);
         uint64_t len = 0;
-        MCMC_CHECK(mcmc_get_trajectory(ctx, trajectory.data(), trajectory.size(), &len));
+        MCMC_CHECK(mcmc_get_trajectory(res, trajectory.data(), trajectory.size(), &len));
         lastSeed = p.seed;
         lastRepetition = iteration;
         if (!directory.empty()) save();
@@ -245,6 +294,10 @@ public:
 
 private:
     Graph<nodeW, edgeW>* graph;
+    std::vector<Graph<nodeW, edgeW>*> parts;   // partitioned: one graph per device, rank order
+    std::vector<uint32_t> bounds;
+    std::vector<mcmc_comm*> comms;
+    std::vector<mcmc_ctx*> pctx;
     uint32_t seed;
     ColoringMCMCParams param;
     std::string directory;

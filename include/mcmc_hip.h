@@ -94,10 +94,13 @@ int mcmc_graph_simulate(uint32_t n, float prob, uint32_t window[31], int device,
  * The graph is written straight into the sweep's tiled layout -- no CSR is materialised (C3's
  * would be 400 GB) -- so the handle serves mcmc_create and mcmc_graph_info; mcmc_graph_download
  * reconstructs a CSR (small graphs), mcmc_graph_device_ptrs fails. _part generates only the rows
- * rank `rank` of `world` owns (mcmc_part_layout), for a partitioned run; its m counts those rows'
- * arcs. */
+ * rank `rank` of `world` owns under mcmc_part_plan_rows, for a partitioned run; its m counts those
+ * rows' arcs. */
 int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int device, mcmc_graph** out);
 int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t world, uint32_t rank, int device,
+                            mcmc_graph** out);
+/* Rows [v_begin, v_end) only (any partition plan's range). */
+int mcmc_graph_er_fast_rows(uint32_t n, double prob, uint64_t seed, uint32_t v_begin, uint32_t v_end, int device,
                             mcmc_graph** out);
 /* The CSR (uint64 offsets, uint32 ids; rows in layout order, not sorted) of a graph generated with
  * mcmc_graph_er_fast, built on the device from its tiled layout and kept on the handle (then
@@ -160,6 +163,10 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
 /* Captures and uploads the `sweeps`-launch graph ahead of mcmc_bench_sweeps (keeps graph
  * instantiation out of a host-timed region). */
 int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps);
+/* Throughput mode for any context (partitioned ones included): sweeps never stop on convergence
+ * (Cviol <= z), so a timed run of a convergent configuration still resamples every vertex each
+ * sweep; lift the cap with a large maxRip. The trajectory keeps at most 2^20 entries. */
+int mcmc_set_bench_mode(mcmc_ctx* c, int on);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.
@@ -202,35 +209,74 @@ void mcmc_destroy(mcmc_ctx* c);
 int mcmc_refstruct_bench(const mcmc_graph* g, uint32_t nCol, uint32_t sweeps, uint32_t seed,
                          double* ms_per_sweep, uint64_t* conflicts);
 
-/* ---- vertex-partitioned multi-GPU step (one process per GPU; exchange by the caller) --------
- * SURVEY.md §8e. Rank r of `world` sweeps rows [r*S, min(n,(r+1)*S)) with global
- * ids and full-length colour replicas. A partitioned colour buffer is a sequence of per-rank
- * regions: region r = [r*P, (r+1)*P) holds the colours of vertices [r*S, r*S + S) followed by
- * rank r's footer (MCMC_FOOTER_WORDS uint32: local Cviol, event count, flags, sorted overflow
- * events); S = ceil(n/world) rounded up to 16, P = S + 4*MCMC_FOOTER_WORDS. Vertex v lives at
- * byte v + (v/S) * 4*MCMC_FOOTER_WORDS. Per sweep, all on the caller's stream, no host sync:
- *   mcmc_part_sweep_async  sweep of the local rows into the local region of the next-colour
- *                          buffer colors[(t+1)&1]: colours and footer
- *   caller                 ONE in-place all-gather of the regions (P bytes per rank) of that
- *                          buffer -- colours and footers travel together
- *   mcmc_part_commit_async global Cviol, stop test, rank-ordered glibc replay -- identical on
- *                          every replica -- RNG advance, buffer flip
- * The colour buffers (>= world*P bytes each) are caller-owned device memory (e.g. torch tensors);
- * `stream` is the caller's hipStream_t, used as given (0 = the legacy null stream, torch's default
- * current stream). Partitioned contexts need the tiled sweep (nCol <= 256, the default variant) or
- * the wide sweep (nCol > 256: uint16 colours, so a region is 2 S colour bytes + the footer).
- * mcmc_part_layout is the uint8 layout; mcmc_part_layout2 takes the colour size in bytes
- * (mcmc_color_bytes(nCol): 1, or 2 for the wide sweep) and gives P = bytes * S + 4*MCMC_FOOTER_WORDS. */
+/* ---- vertex-partitioned multi-GPU run -----------------------------------------
+ * Rank r of `world` sweeps rows [bounds[r], bounds[r+1]) with global ids, full-length colour
+ * replicas in vertex order (C_t in colors[t & 1], 1 byte per colour, 2 for the wide sweep: nCol >
+ * 256, mcmc_color_bytes) and a replicated glibc window. Per sweep t, on the rank's stream, no host
+ * sync:
+ *   mcmc_part_sweep_async   sweep of the local rows into colors[(t+1)&1] and this rank's footer slot
+ *                           (MCMC_FOOTER_WORDS uint32 at foot[(t+1)&1] + rank * MCMC_FOOTER_WORDS:
+ *                           local Cviol, event count, flags, sorted overflow events)
+ *   exchange                every rank's rows [bounds[r], bounds[r+1]) of colors[(t+1)&1] and its
+ *                           footer slot of foot[(t+1)&1] to every rank (mcmc_part_run does it over
+ *                           RCCL; a caller may do it itself)
+ *   mcmc_part_commit_async  global Cviol, stop test, the rank-ordered glibc replay -- identical on
+ *                           every replica -- RNG advance, buffer flip
+ * A rank whose overflow events of a sweep outgrow its footer (> MCMC_FOOTER_WORDS - 4) pauses the
+ * loop at that sweep on every rank (mcmc_part_state: err bit 1, done 0): the driver all-gathers
+ * the full sorted lists (mcmc_part_spill_local / _counts) with a common stride and resumes with
+ * mcmc_part_spill_commit_async. Plans: inner bounds are multiples of 64 rows. */
 #define MCMC_FOOTER_WORDS 1024
-int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P);
-int mcmc_part_layout2(uint32_t n, uint32_t world, uint32_t color_bytes, uint64_t* S, uint64_t* P);
+#define MCMC_COMM_ID_BYTES 128
+typedef struct mcmc_comm mcmc_comm;
+/* Equal row ranges (ceil(n/world) rounded up to 64). */
+int mcmc_part_plan_rows(uint32_t n, uint32_t world, uint32_t* bounds /* world + 1 */);
+/* balance 0: equal rows; 1: arc-balanced -- each rank gets ~1/world of sum(deg(v) + 16) from the
+ * CSR's degree prefix (power-law graphs whose hubs cluster in id ranges, configs[4]). Graphs without
+ * a CSR (the generator's per-rank layouts; G(n,p) is uniform) get equal rows. */
+int mcmc_part_plan(const mcmc_graph* g, uint32_t world, int balance, uint32_t* bounds /* world + 1 */);
+/* The arc-balanced plan from a host CSR's offsets (row_off[n + 1]). */
+int mcmc_part_plan_csr(const uint64_t* row_off, uint32_t n, uint32_t world, uint32_t* bounds /* world + 1 */);
 uint32_t mcmc_color_bytes(uint32_t nCol);
-int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
-                     uint64_t colors_bytes, void* stream);
+/* Caller-exchanged contexts: a context on rows [bounds[rank], bounds[rank+1]) (mcmc_create) is
+ * attached to caller-owned device buffers: colour replicas of >= (n + 256) * mcmc_color_bytes(nCol)
+ * bytes and footer buffers of world * MCMC_FOOTER_WORDS uint32; `stream` is the caller's
+ * hipStream_t, used as given (0 = the legacy null stream). */
+int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t* bounds, void* colors0,
+                     void* colors1, uint64_t colors_bytes, void* foot0, void* foot1, void* stream);
 int mcmc_part_sweep_async(mcmc_ctx* c);
 int mcmc_part_commit_async(mcmc_ctx* c);
-/* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final). */
+/* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final);
+ * *err: bit 0 a fatal device error, bit 1 a spill exchange is pending (then *t is the paused sweep). */
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
+/* Spill exchange of a paused sweep: every rank's list length (from the exchanged footers), this
+ * rank's sorted list copied to device memory dst (NULL: the count only), and the resumption from
+ * the gathered lists (rank r's list at gathered[r * stride], device memory, stride >= every count). */
+int mcmc_part_spill_counts(mcmc_ctx* c, uint32_t* counts /* world */);
+int mcmc_part_spill_local(mcmc_ctx* c, void* dst, uint32_t* count);
+int mcmc_part_spill_commit_async(mcmc_ctx* c, const uint32_t* gathered, uint32_t stride);
+
+/* Native runs (csrc/multi.hip): RCCL communicators behind the ABI. One process per GPU:
+ * rank 0 calls mcmc_comm_unique_id and hands the bytes to the others (any channel), every rank
+ * mcmc_comm_init_rank; one process driving N GPUs: mcmc_comm_init_all. */
+int mcmc_comm_unique_id(uint8_t id[MCMC_COMM_ID_BYTES]);
+int mcmc_comm_init_rank(const uint8_t id[MCMC_COMM_ID_BYTES], uint32_t world, uint32_t rank, int device,
+                        mcmc_comm** out);
+int mcmc_comm_init_all(const int* devices, uint32_t ndev, mcmc_comm** out /* ndev */);
+void mcmc_comm_destroy(mcmc_comm* c);
+/* A partitioned context that owns its buffers and stream (rows [bounds[rank], bounds[rank+1]) of
+ * `g`, which must hold them: the whole CSR, or mcmc_graph_er_fast_rows of that range). comm NULL:
+ * the loopback transport -- every rank of the world in this process, exchanged by device copies
+ * (tests; several ranks may share a GPU). Initialise with mcmc_set_glibc_window +
+ * mcmc_init_coloring as a single context; destroy with mcmc_destroy. */
+int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, uint32_t rank, const uint32_t* bounds,
+                     mcmc_comm* comm, mcmc_ctx** out);
+/* run() (coloringMCMC_CPU.cpp:115-270) of this process's k ranks (k = 1: one process per GPU;
+ * k = world: one process driving them all, or the loopback transport) inside one call: sweeps,
+ * exchanges, commits, spill exchanges, until the loop stops (max_sweeps > 0: at most that many).
+ * stats: k entries (identical loop fields on every rank; loopMs = device time on ctxs[0]'s stream).
+ * Colourings and trajectories then come from mcmc_get_coloring / mcmc_get_trajectory of any rank. */
+int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_stats* stats /* k */);
 
 /* ---- other colorers -------------------------------------------------
  * The reference's parallel greedy first-fit colorer (ColoringGreedyFF::run,

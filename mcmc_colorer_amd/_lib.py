@@ -26,9 +26,9 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_graph_simulate": (c_int, [c_uint32, c_float, _u32p, c_int, POINTER(c_void_p)]),
     "mcmc_graph_er_fast": (c_int, [c_uint32, c_double, c_uint64, c_int, POINTER(c_void_p)]),
     "mcmc_graph_er_fast_part": (c_int, [c_uint32, c_double, c_uint64, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
+    "mcmc_graph_er_fast_rows": (c_int, [c_uint32, c_double, c_uint64, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "mcmc_graph_rmat": (c_int, [c_uint32, c_uint32, c_double, c_double, c_double, c_uint64, c_int, POINTER(c_void_p)]),
     "mcmc_graph_info": (c_int, [c_void_p, _u32p, _u64p, _u32p, _u32p]),
-    "mcmc_part_layout2": (c_int, [c_uint32, c_uint32, c_uint32, _u64p, _u64p]),
     "mcmc_color_bytes": (c_uint32, [c_uint32]),
     "mcmc_greedyff_run": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
     "mcmc_luby_run": (c_int, [c_void_p, c_void_p, _u32p, _u32p, _u32p]),
@@ -49,15 +49,28 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_bench_sweeps": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
     "mcmc_bench_prepare": (c_int, [c_void_p, c_uint32]),
+    "mcmc_set_bench_mode": (c_int, [c_void_p, c_int]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
     "mcmc_cdf_walk": (c_uint32, [_u32p, c_uint32, c_uint32, c_float, c_float, c_float]),
     "mcmc_refstruct_bench": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_double), _u64p]),
     "mcmc_destroy": (None, [c_void_p]),
-    "mcmc_part_layout": (c_int, [c_uint32, c_uint32, _u64p, _u64p]),
-    "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "mcmc_part_plan_rows": (c_int, [c_uint32, c_uint32, _u32p]),
+    "mcmc_part_plan": (c_int, [c_void_p, c_uint32, c_int, _u32p]),
+    "mcmc_part_plan_csr": (c_int, [_u64p, c_uint32, c_uint32, _u32p]),
+    "mcmc_part_attach": (c_int, [c_void_p, c_uint32, c_uint32, _u32p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p,
+                                 c_void_p]),
     "mcmc_part_sweep_async": (c_int, [c_void_p]),
     "mcmc_part_commit_async": (c_int, [c_void_p]),
     "mcmc_part_state": (c_int, [c_void_p, POINTER(c_int32), _u32p, _u32p]),
+    "mcmc_part_spill_counts": (c_int, [c_void_p, _u32p]),
+    "mcmc_part_spill_local": (c_int, [c_void_p, c_void_p, _u32p]),
+    "mcmc_part_spill_commit_async": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "mcmc_comm_unique_id": (c_int, [c_void_p]),
+    "mcmc_comm_init_rank": (c_int, [c_void_p, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
+    "mcmc_comm_init_all": (c_int, [POINTER(c_int), c_uint32, POINTER(c_void_p)]),
+    "mcmc_comm_destroy": (None, [c_void_p]),
+    "mcmc_part_create": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, _u32p, c_void_p, POINTER(c_void_p)]),
+    "mcmc_part_run": (c_int, [POINTER(c_void_p), c_uint32, c_uint32, c_void_p]),
     "mcmc_xorwow_state": (c_int, [c_uint64, c_uint64, c_int, _u32p]),
     "mcmc_gpurand_create": (c_int, [c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "mcmc_gpurand_states": (c_int, [c_void_p, _u32p]),

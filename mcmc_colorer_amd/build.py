@@ -24,7 +24,11 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 # -ffp-contract=off: bit-exact fp32 with the reference's (non-FMA) host arithmetic.
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-LIB_SOURCES = ["mcmc_sweep.hip", "graph.hip", "tiled_layout.hip", "refstruct.hip", "tailcut.hip", "refmode.hip", "rmat.hip", "greedyff.hip", "luby.hip"]
+LIB_SOURCES = ["mcmc_sweep.hip", "graph.hip", "tiled_layout.hip", "refstruct.hip", "tailcut.hip", "refmode.hip", "rmat.hip",
+               "greedyff.hip", "luby.hip", "multi.hip"]
+# RCCL (multi.hip: the native multi-GPU path); torch's bundled librccl.so.1 satisfies the same soname
+# when torch is loaded first
+LINK = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _run(cmd: list[str]) -> None:
@@ -54,7 +58,7 @@ def build_lib(force: bool = False) -> Path:
         with ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
             list(ex.map(_run, jobs))
     if force or _stale(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, *LINK, "-o", LIB])
     return LIB
 
 

@@ -102,12 +102,16 @@ class Graph:
         return cls(h, prob=float(np.float32(prob)), device=device)
 
     @classmethod
-    def er_fast(cls, n: int, prob: float, seed: int, device: int = 0, world: int = 1, rank: int = 0) -> "Graph":
+    def er_fast(cls, n: int, prob: float, seed: int, device: int = 0, world: int = 1, rank: int = 0,
+                rows: Optional[tuple[int, int]] = None) -> "Graph":
         """The build's counter-based G(n, p) (csrc/er_gen.h) for sizes where setupRnd2 is infeasible
         (SURVEY.md §8d C3/C4), generated on the GPU straight into the sweep's tiled layout.
-        world > 1: only the rows rank ``rank`` owns (a partitioned run); nEdges then counts those."""
+        world > 1: only the rows rank ``rank`` owns under the equal-rows plan (a partitioned run);
+        rows=(v_begin, v_end): only those rows. nEdges then counts those rows' arcs."""
         h = ctypes.c_void_p()
-        if world == 1:
+        if rows is not None:
+            check(lib().mcmc_graph_er_fast_rows(n, float(prob), seed, rows[0], rows[1], device, ctypes.byref(h)))
+        elif world == 1:
             check(lib().mcmc_graph_er_fast(n, float(prob), seed, device, ctypes.byref(h)))
         else:
             check(lib().mcmc_graph_er_fast_part(n, float(prob), seed, world, rank, device, ctypes.byref(h)))

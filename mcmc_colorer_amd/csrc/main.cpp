@@ -20,6 +20,7 @@
 #include <ctime>
 #include <iostream>
 #include <map>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <unordered_set>
@@ -120,7 +121,9 @@ void help(const char* argv0) {
               << "  --repet N            repetitions, seeds seed+i (default 1)\n"
               << "  --seed N             seed (default: time, which also srand()s glibc)\n"
               << "  --outDir D           output directory\n"
-              << "  --device D           HIP device (default 0)\n";
+              << "  --device D           HIP device (default 0)\n"
+              << "  --gpus N             --mcmcgpu vertex-partitioned over devices D .. D+N-1 of this node\n"
+              << "                       (RCCL inside the library; arc-balanced plan for CSR graphs)\n";
 }
 
 }  // namespace
@@ -132,7 +135,7 @@ int main(int argc, char** argv) {
     bool simulate = false, mcmccpu = false, mcmcgpu = false, tailcut = false, fast = false,
          tailcutRepair = false, mcmcgpuref = false, greedyff = false, lubygpu = false, vffgpu = false;
     uint64_t erSeed = 1;
-    int device = 0;
+    int device = 0, gpus = 1;
     const struct option longopts[] = {
         {"graph", required_argument, 0, 'g'},    {"outDir", required_argument, 0, 'o'},
         {"simulate", required_argument, 0, 's'}, {"nodes", required_argument, 0, 'n'},
@@ -144,7 +147,7 @@ int main(int argc, char** argv) {
         {"seed", required_argument, 0, 'S'},     {"help", no_argument, 0, 'h'},
         {"device", required_argument, 0, 'D'},   {"simulate-fast", required_argument, 0, 'F'},
         {"er-seed", required_argument, 0, 'E'},  {"tailcutRepair", no_argument, 0, 'X'},
-        {"mcmcgpu-ref", no_argument, 0, 'G'},
+        {"mcmcgpu-ref", no_argument, 0, 'G'},    {"gpus", required_argument, 0, 'P'},
         {0, 0, 0, 0}};
     int c;
     while ((c = getopt_long(argc, argv, "g:o:s:n:12345k:r:t:lR:S:hD:", longopts, nullptr)) != -1) {
@@ -174,6 +177,7 @@ int main(int argc, char** argv) {
                 case 'E': erSeed = std::stoull(optarg); break;
                 case 'X': tailcutRepair = true; break;
                 case 'G': mcmcgpuref = true; break;
+                case 'P': if (std::stoi(optarg) < 1) throw 1; gpus = std::stoi(optarg); break;
                 case 'h': help(argv[0]); return 0;
                 default: break;
             }
@@ -224,20 +228,46 @@ int main(int argc, char** argv) {
     mkdir(outDir.c_str(), 0775);
 
     const float numColorRatio = 1.0f / (float)numColRatio;        // main.cu:53
+    if (gpus > 1 && (mcmcgpuref || greedyff || lubygpu || vffgpu || tailcutRepair)) {
+        std::cout << "--gpus > 1 partitions --mcmcgpu only (no --mcmcgpu-ref, other colorers or --tailcutRepair)" << std::endl;
+        return 255;
+    }
     Graph<float, float>* g;
+    std::vector<Graph<float, float>*> parts;   // --gpus N: one graph per device, rank order
+    std::vector<uint32_t> bounds;
     auto t0 = std::chrono::steady_clock::now();
     if (fast) {
-        g = new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device);
+        if (gpus > 1) {   // every rank generates only its rows (G(n,p) is uniform: equal rows)
+            bounds.resize((size_t)gpus + 1);
+            MCMC_CHECK(mcmc_part_plan_rows(n, (uint32_t)gpus, bounds.data()));
+            for (int r = 0; r < gpus; r++)
+                parts.push_back(new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device + r,
+                                                        bounds[r], bounds[r + 1]));
+            g = parts[0];
+        } else {
+            g = new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device);
+        }
     } else if (simulate) {
-        g = new Graph<float, float>(n, (float)prob, seed, device);
+        const mcmc::GlibcWindow w0 = mcmc::glibc_global();
+        for (int r = 0; r < gpus; r++) {   // the exact graph on every device, from the same stream position
+            mcmc::glibc_global() = w0;
+            parts.push_back(new Graph<float, float>(n, (float)prob, seed, device + r));
+        }
+        g = parts[0];
     } else {
         std::vector<uint64_t> off;
         std::vector<node> idx;
         if (!import_edge_list(graphFilename, off, idx)) return 255;
         const uint32_t nn = (uint32_t)(off.size() - 1);
         const float p = (float)idx.size() / (float)(nn * nn);      // main.cu:68 (uint32 product, as the reference)
-        g = new Graph<float, float>(off, idx, p, device);
+        for (int r = 0; r < gpus; r++) parts.push_back(new Graph<float, float>(off, idx, p, device + r));
+        g = parts[0];
     }
+    if (gpus > 1 && bounds.empty()) {   // CSR graphs: arc-balanced plan from the degree prefix
+        bounds.resize((size_t)gpus + 1);
+        MCMC_CHECK(mcmc_part_plan(g->handle(), (uint32_t)gpus, 1, bounds.data()));
+    }
+    if (gpus == 1) parts.clear();
     const double tgen = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::cout << "Nodes: " << g->getNNodes() << " - Edges: " << g->getNEdges() << std::endl;
     std::cout << "Min Degree: " << g->getMinNodeDeg() << " - Max Degree: " << g->getMaxNodeDeg()
@@ -304,7 +334,10 @@ int main(int argc, char** argv) {
                       << (st.maxIterReached ? ", max iteration reached" : "") << ")" << std::endl << std::endl;
             continue;
         }
-        ColoringMCMC<float, float> colMCMC(g, GPURandGen.randStates, params);
+        std::unique_ptr<ColoringMCMC<float, float>> colPtr(
+            gpus > 1 ? new ColoringMCMC<float, float>(parts, bounds, GPURandGen.randStates, params)
+                     : new ColoringMCMC<float, float>(g, GPURandGen.randStates, params));
+        ColoringMCMC<float, float>& colMCMC = *colPtr;
         colMCMC.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));
         colMCMC.run((int)i);
         const auto& st = colMCMC.getStats();
@@ -315,6 +348,7 @@ int main(int argc, char** argv) {
                   << std::endl;
     }
     delete curand;
-    delete g;
+    if (parts.empty()) delete g;
+    for (auto* pg : parts) delete pg;
     return EXIT_SUCCESS;
 }

@@ -127,6 +127,32 @@ struct XSlabLayout {
 };
 }  // namespace mcmc
 
+struct mcmc_ctx;
+struct mcmc_comm;
+
+namespace mcmc {
+// A partitioned context's exchange buffers (mcmc_sweep.hip; used by the native driver, multi.hip).
+struct PartDesc {
+    uint8_t* colors[2];          // colour replicas (vertex order), C_t in colors[t & 1]
+    uint32_t* foot[2];           // footer buffers, world x MCMC_FOOTER_WORDS; sweep t writes foot[(t+1) & 1]
+    const uint32_t* bounds;      // [world + 1]
+    uint32_t world, rank, cbytes, n;
+    hipStream_t stream;
+    int device;
+    mcmc_comm* comm;             // nullptr: exchanged by the caller / the loopback transport
+    uint32_t* events;            // the rank's sorted list of a paused (spill) sweep
+    uint32_t maxRip;
+};
+int part_desc(mcmc_ctx* c, PartDesc* d);
+// Hands a native partitioned context its buffers (one allocation, freed by mcmc_destroy), its own
+// stream (destroyed there too) and its communicator (borrowed).
+int part_adopt(mcmc_ctx* c, void* mem, hipStream_t own_stream, mcmc_comm* comm);
+// Device buffer of world x stride words for a spill exchange (grown on demand, owned by the context).
+int part_spill_buffer(mcmc_ctx* c, uint32_t stride, uint32_t** buf);
+// Refreshes and returns the context's run summary (mcmc_part_state + the stats of mcmc_run).
+int part_stats(mcmc_ctx* c, mcmc_run_stats* s);
+}  // namespace mcmc
+
 struct mcmc_graph {
     mcmc::GraphDev g;
     std::vector<std::unique_ptr<mcmc::TiledLayout>> tiles;   // freed with the graph

@@ -108,11 +108,12 @@ struct SweepArgs {
     uint32_t slice_bytes;       // tiled: colour bytes a pair's slice can hold (resident: the replica)
     uint32_t seg_buf_bytes;     // tiled: LDS bytes of one segment-table buffer (1 KiB multiple)
     unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
-    // partitioned colour buffers: vertex v at element v + (v / part_S) * part_FB (part_FB = 0: plain;
-    // elements of the replica's colour type: a region is part_S colours + a 4 KiB footer)
-    uint32_t part_S, part_FB;
-    uint32_t own_off;           // rank * part_FB: byte offset of this rank's own vertices
-    uint64_t footer_off;        // bytes: colour size * (rank * (part_S + part_FB) + part_S): this rank's footer
+    // partitioned runs: colour replicas stay in vertex order; every rank's footer (kFooterWords:
+    // local Cviol, event count, flags, sorted events) sits in slot `rank` of the footer buffer of
+    // the next-colour parity (sweep t: foot[(t + 1) & 1], like colors[(t + 1) & 1])
+    uint32_t* foot0;
+    uint32_t* foot1;
+    uint32_t rank;
     // tail cutting enabled (mcmc_set_tailcut_repair): sweep t stores the violation flags of C_t at
     // vflags[(t & 1) * nloc + l] -- the tail cut's first pass needs those of the previous sweep
     uint8_t* vflags;
@@ -153,11 +154,6 @@ struct SweepArgs {
     uint32_t xs_sym;            // 1: one entry per local edge, flags both ends; 0: every arc, flags its row
 };
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
-
-// Byte address of vertex v in a colour buffer (partitioned buffers interleave per-rank footers).
-__device__ __forceinline__ uint32_t caddr(const SweepArgs& a, uint32_t v) {
-    return a.part_FB ? v + (v / a.part_S) * a.part_FB : v;
-}
 
 // Phase timestamps of the last sweep, 8 slots per workgroup (wall_clock64, 100 MHz): 0 start,
 // 1 first scan begins, 2 scans done, 3 evaluation done, 4 tail done (last workgroup: commit done).
@@ -348,10 +344,10 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
             const uint32_t v = s[i];
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
-            Cs[caddr(a, v)] = (CT)c;
+            Cs[v] = (CT)c;
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
-                a.taboo[v - a.v_begin] = (c == (uint32_t)C[caddr(a, v)]) ? a.tabooIteration : 0u;
+                a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
         }
         __syncthreads();
     }
@@ -498,14 +494,30 @@ __global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
 // ---- vertex-partitioned sweep: footer exchange ------------------------------------------------
 constexpr uint32_t kFooterWords = 1024;                 // MCMC_FOOTER_WORDS
 constexpr uint32_t kFooterEvents = kFooterWords - 4;
+constexpr uint32_t kMaxWorld = 64;                       // ranks of a partitioned run
+constexpr uint64_t kTrajCapMax = 1u << 20;               // trajectory entries kept (throughput runs lift maxRip)
+constexpr uint32_t kPartAlign = 64;                      // inner partition bounds: multiples of 64 rows
+constexpr double kPartRowWeight = 16.0;                  // arc-balanced plans: a row costs deg + 16
+
+// Footer flags (word 3): bit 0 fatal (the local list overflowed ev_cap, or a device error), bit 1
+// the sorted list did not fit the footer -- the commit then pauses for the spill exchange
+// (mcmc_part_spill_*), which takes every rank's full list from its `events` buffer.
+constexpr uint32_t kFootFatal = 1u, kFootSpill = 2u;
+// DevState::err bits: 1 fatal, 2 paused for a spill exchange (st->done is set meanwhile, so every
+// kernel of the steps a driver enqueued before it noticed returns at once).
+constexpr uint32_t kErrFatal = 1u, kErrSpill = 2u;
+
+__device__ __forceinline__ uint32_t* rank_footer(const SweepArgs& a, uint32_t t, uint32_t r) {
+    return ((t & 1) ? a.foot0 : a.foot1) + (size_t)r * kFooterWords;   // next-colour parity
+}
 
 // Last workgroup of a partitioned sweep: sort this rank's overflow events and publish
-// [Cviol_local, E, flags, events] for the all-gather; reset the local accumulators.
+// [Cviol_local, E, flags, events] for the exchange; reset the local accumulators. A list longer
+// than the footer stays sorted in a.events for the spill exchange.
 __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
                             uint32_t* lds, uint32_t lds_cap, uint32_t* presorted = nullptr) {
     DevState* st = a.st;
-    // this rank's footer slot: after its colour slab, in the next-colour buffer
-    uint32_t* footer = reinterpret_cast<uint32_t*>(((t & 1) ? a.colors0 : a.colors1) + a.footer_off);
+    uint32_t* footer = rank_footer(a, t, a.rank);
     uint32_t* s = presorted ? presorted : a.events;
     if (!presorted && E > 0 && E <= a.ev_cap) {
         uint32_t P = 1;
@@ -519,13 +531,18 @@ __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long v
         __syncthreads();
         bitonic_sort_block(s, P);
     }
+    const bool fatal = E > a.ev_cap || err;
+    if (E > kFooterEvents && !fatal && s != a.events) {   // keep the whole sorted list for the spill
+        for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) a.events[i] = s[i];
+        __syncthreads();
+    }
     const uint32_t En = min(E, kFooterEvents);
     for (uint32_t i = threadIdx.x; i < En; i += blockDim.x) footer[4 + i] = s[i];
     if (threadIdx.x == 0) {
         footer[0] = (uint32_t)viol;
         footer[1] = (uint32_t)(viol >> 32);
         footer[2] = E;
-        footer[3] = (E > kFooterEvents || E > a.ev_cap || err) ? 1u : 0u;
+        footer[3] = (fatal ? kFootFatal : 0u) | (E > kFooterEvents ? kFootSpill : 0u);
         st->viol = 0;
         st->ev_count = 0;
         st->arrive = 0;
@@ -533,44 +550,65 @@ __device__ void pack_footer(const SweepArgs& a, uint32_t t, unsigned long long v
     }
 }
 
-// Every rank, after the all-gathers: global Cviol = sum of the footers, events = rank-ordered
+// Every rank, after the exchange: global Cviol = sum of the footers, events = rank-ordered
 // concatenation (ranks own ascending vertex ranges, so it is ascending), then the same commit as
-// the single-context loop -- identical glibc replay on every replica.
+// the single-context loop -- identical glibc replay on every replica. A list that did not fit a
+// footer pauses the loop here (spill) unless the sweep stops anyway; spill = the full lists,
+// gathered by the driver (rank r's at spill[r * stride], E_r from its footer).
 template <typename CT>
-__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a) {
+__global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, const uint32_t* spill,
+                                                                     uint32_t stride) {
     __shared__ uint32_t lds[kLdsSortCap];
-    __shared__ uint32_t sh_done, sh_t, sh_E, sh_err;
+    __shared__ uint32_t sh_go, sh_t, sh_E, sh_err, sh_spill;
     __shared__ unsigned long long sh_viol;
-    __shared__ uint32_t sh_off[65];
+    __shared__ uint32_t sh_off[kMaxWorld + 1];
     DevState* st = a.st;
-    const uint32_t t0 = st->t;
-    const uint8_t* nxt = (t0 & 1) ? a.colors0 : a.colors1;
-    const size_t P = sizeof(CT) * ((size_t)a.part_S + a.part_FB);   // region bytes
     if (threadIdx.x == 0) {
-        sh_done = st->done;
+        const uint32_t t0 = st->t;
+        // spill == nullptr: the step's own commit (skipped once done); else the resumption of a
+        // loop paused for this sweep's spill exchange
+        sh_go = spill ? ((st->err & kErrSpill) != 0u) : (st->done == 0u);
         sh_t = t0;
         unsigned long long v = 0;
-        uint32_t E = 0, err = st->err;
+        uint32_t E = 0, err = st->err & kErrFatal, sp = 0;
         for (uint32_t r = 0; r < a.world; r++) {
-            const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + sizeof(CT) * a.part_S);
+            const uint32_t* f = rank_footer(a, t0, r);
             v += (unsigned long long)f[0] | ((unsigned long long)f[1] << 32);
             sh_off[r] = E;
-            E += min(f[2], kFooterEvents);
-            err |= f[3];
+            E += spill ? f[2] : min(f[2], kFooterEvents);
+            err |= f[3] & kFootFatal;
+            sp |= f[3] & kFootSpill;
         }
+        sh_off[a.world] = E;
         sh_viol = v;
         sh_E = E;
         sh_err = err;
+        sh_spill = sp;
+        if (sh_go && spill) {
+            st->done = 0;
+            st->err &= ~kErrSpill;
+        }
     }
     __syncthreads();
-    if (sh_done) return;
-    for (uint32_t r = 0; r < a.world; r++) {
-        const uint32_t* f = reinterpret_cast<const uint32_t*>(nxt + r * P + sizeof(CT) * a.part_S);
-        const uint32_t Er = min(f[2], kFooterEvents);
-        for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = f[4 + i];
+    if (!sh_go) return;
+    const uint32_t t = sh_t;
+    const bool stop = t == a.maxRip + 1 || (!a.bench && sh_viol <= a.z);
+    if (!spill && sh_spill && !stop && !sh_err) {   // pause: the driver gathers the full lists
+        if (threadIdx.x == 0) {
+            st->err |= kErrSpill;
+            st->done = 1;
+        }
+        return;
+    }
+    if (!stop && !sh_err && sh_E <= a.ev_cap) {
+        for (uint32_t r = 0; r < a.world; r++) {
+            const uint32_t* src = spill ? spill + (size_t)r * stride : rank_footer(a, t, r) + 4;
+            const uint32_t Er = sh_off[r + 1] - sh_off[r];
+            for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = src[i];
+        }
     }
     __syncthreads();
-    commit_control<CT>(a, sh_t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+    commit_control<CT>(a, t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
 }
 
 // The wide sweep's partitioned footer (its kernels have no fused last-workgroup step): this
@@ -1222,14 +1260,14 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
         for (uint32_t k = 0; k < kSliceBytes / 16u / 64u / 16u; k++) {   // 4 wave-instructions per wave
             const uint32_t piece = (k * nwaves + wid) * 64u;
             const uint32_t q = min(piece + (uint32_t)lane, nq16 - 1u);
-            glds16(C + caddr(a, lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
+            glds16(C + (lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
         }
     }
 }
 
 // REF, streaming: DMA of group g's own colours (the rows' bytes, from the 16-byte boundary at or
 // below the group's first vertex) into an own-colour buffer (a multiple of 1 KiB: every wave
-// instruction lands 64 x 16 B). Single context: colour buffers are plain (caddr = identity).
+// instruction lands 64 x 16 B).
 __device__ __forceinline__ void tile_dma_own(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
                                              uint32_t own_lds, uint32_t wid, uint32_t nwaves, int lane) {
     const uint32_t R = a.grp_rows, nloc = a.v_end - a.v_begin;
@@ -1379,7 +1417,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
 #pragma unroll
         for (int k = 0; k < kResPer; k++) {
             const uint32_t i = threadIdx.x + k * blockDim.x;
-            rr[k] = *reinterpret_cast<const u32x4*>(C + caddr(a, 16u * (i < nq16 ? i : 0u)));
+            rr[k] = *reinterpret_cast<const u32x4*>(C + (16u * (i < nq16 ? i : 0u)));
         }
 #pragma unroll
         for (int k = 0; k < kResPer; k++) {
@@ -1531,7 +1569,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 if (REF)
                     evaluate_ref_tile<NW>(a, C, Cs, t, r0 + e0, cnt, acc, lane, p_lds, hist_lds);
                 else
-                    wave_viol += evaluate_tile<NW>(a, st, C + a.own_off, Cs + a.own_off, x_t, r0 + e0, cnt, acc,
+                    wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, r0 + e0, cnt, acc,
                                                    lane, wave_ev, vf);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
@@ -1611,13 +1649,12 @@ __global__ void ref_init_kernel(uint8_t* __restrict__ C, uint32_t* __restrict__ 
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st,
-                                     uint32_t part_S, uint32_t part_FB) {
+__global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         const uint32_t x = minstd_mulmod(x0, minstd_pow_tab((uint64_t)v + 1));
         const uint32_t r = x - 1u;
         if (r >= k.past) atomicAdd(&st->init_rejections, 1u);
-        C[part_FB ? v + (v / part_S) * part_FB : v] = (uint8_t)min(r / k.scaling, 255u);
+        C[v] = (uint8_t)min(r / k.scaling, 255u);
     }
 }
 
@@ -1713,8 +1750,14 @@ struct mcmc_ctx {
     unsigned long long* phase_ts = nullptr;   // MCMC_PHASE_DUMP diagnostics
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
+    int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
     uint32_t world = 1, rank = 0;
-    uint32_t part_S = 0;                     // partitioned: slab stride (vertices), multiple of 16
+    std::vector<uint32_t> bounds;            // partitioned: rank r sweeps rows [bounds[r], bounds[r+1])
+    uint32_t* foot[2] = {nullptr, nullptr};  // partitioned: footer buffers, world x kFooterWords each
+    void* own_part = nullptr;                // native partitioned contexts: their own colour + footer buffers
+    mcmc_comm* comm = nullptr;               // native partitioned contexts: the RCCL communicator (borrowed)
+    uint32_t* spill = nullptr;               // native spill exchange: gathered lists, world x spill_stride
+    uint32_t spill_stride = 0;
     uint8_t* own_colors[2] = {nullptr, nullptr};   // the context's own replicas (freed at destroy)
     std::vector<uint32_t> host_events;
     // tail cutting (mcmc_set_tailcut_repair, tailcut.hip)
@@ -1757,30 +1800,15 @@ struct mcmc_ctx {
 
 namespace {
 
-// Host <-> device colour transfers (n bytes in vertex order); partitioned buffers are per-rank
-// regions of S colours followed by a footer.
+// Host <-> device colour transfers (n colours in vertex order; partitioned replicas too).
 int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
-    if (!c->part) {
-        MCMC_HIP_TRY(hipMemcpyAsync(dst, h, (size_t)c->n * c->cbytes, hipMemcpyHostToDevice, c->stream));
-    } else {
-        const uint64_t P = (uint64_t)c->cbytes * c->part_S + 4u * kFooterWords;
-        for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
-            MCMC_HIP_TRY(hipMemcpyAsync(dst + r * P, h + v * c->cbytes, c->cbytes * std::min<uint64_t>(c->part_S, c->n - v),
-                                        hipMemcpyHostToDevice, c->stream));
-    }
+    MCMC_HIP_TRY(hipMemcpyAsync(dst, h, (size_t)c->n * c->cbytes, hipMemcpyHostToDevice, c->stream));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     return MCMC_OK;
 }
 
 int download_colors(mcmc_ctx* c, const uint8_t* src, uint8_t* h) {
-    if (!c->part) {
-        MCMC_HIP_TRY(hipMemcpyAsync(h, src, (size_t)c->n * c->cbytes, hipMemcpyDeviceToHost, c->stream));
-    } else {
-        const uint64_t P = (uint64_t)c->cbytes * c->part_S + 4u * kFooterWords;
-        for (uint64_t r = 0, v = 0; v < c->n; r++, v += c->part_S)
-            MCMC_HIP_TRY(hipMemcpyAsync(h + v * c->cbytes, src + r * P, c->cbytes * std::min<uint64_t>(c->part_S, c->n - v),
-                                        hipMemcpyDeviceToHost, c->stream));
-    }
+    MCMC_HIP_TRY(hipMemcpyAsync(h, src, (size_t)c->n * c->cbytes, hipMemcpyDeviceToHost, c->stream));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     return MCMC_OK;
 }
@@ -1826,16 +1854,16 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
+    a.bench = c->bench_mode;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
     a.seg = c->seg;
     a.nblocks = c->nblocks;
     a.block_log2 = c->block_log2;
     a.chunk_rows = c->chunk_rows;
     if (c->part) {
-        a.part_S = c->part_S;
-        a.part_FB = 4u * kFooterWords / c->cbytes;   // the footer in colour elements
-        a.own_off = c->rank * a.part_FB;
-        a.footer_off = (uint64_t)c->cbytes * ((uint64_t)c->rank * (c->part_S + a.part_FB) + c->part_S);
+        a.foot0 = c->foot[0];
+        a.foot1 = c->foot[1];
+        a.rank = c->rank;
     }
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
@@ -2185,7 +2213,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     c->glibc = glibc_srand(1);
     const uint32_t nloc = v_end - v_begin;
     c->ev_cap = std::max<uint32_t>(nloc, 64u * 1024u);   // local events; also >= 64 ranks x footer events
-    c->traj_cap = p->maxRip + 2;
+    c->traj_cap = (uint32_t)std::min<uint64_t>((uint64_t)p->maxRip + 2, kTrajCapMax);
     hipError_t e = hipSuccess;
     auto chk = [&](hipError_t x) { if (x != hipSuccess && e == hipSuccess) e = x; };
     chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -2482,12 +2510,9 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
         if (c->wide)
             init_coloring_wide_kernel<<<blocks, 256, 0, c->stream>>>(reinterpret_cast<uint16_t*>(c->colors[0]), n, s0,
-                                                                     k, c->st, c->part ? c->part_S : 0u,
-                                                                     c->part ? 4u * kFooterWords / 2u : 0u);
+                                                                     k, c->st);
         else
-            init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st,
-                                                                 c->part ? c->part_S : 0u,
-                                                                 c->part ? 4u * kFooterWords : 0u);
+            init_coloring_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], n, s0, k, c->st);
         MCMC_HIP_TRY(hipGetLastError());
         DevState h;
         int rc = download_state(c, &h);
@@ -2612,6 +2637,13 @@ int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
     if (flags) MCMC_HIP_TRY(hipMemcpyAsync(flags, c->vflags, c->n, hipMemcpyDeviceToHost, c->stream));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     *count = hv;
+    return MCMC_OK;
+}
+
+int mcmc_set_bench_mode(mcmc_ctx* c, int on) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    c->bench_mode = on ? 1 : 0;
+    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
     return MCMC_OK;
 }
 
@@ -2923,44 +2955,169 @@ void mcmc_destroy(mcmc_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_part) {   // native partitioned contexts: their buffers and their own stream
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->own_part);
+        (void)hipFree(c->spill);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    }
     delete c;
 }
 
-// ---- vertex-partitioned step (device-resident; exchange by the caller) -----------------------
-int mcmc_part_layout2(uint32_t n, uint32_t world, uint32_t color_bytes, uint64_t* S, uint64_t* P) {
-    if (!S || !P) return fail(MCMC_E_ARG, "NULL argument");
-    if (world == 0 || world > 64) return fail(MCMC_E_ARG, "bad world (1..64 ranks)");
-    if (color_bytes != 1 && color_bytes != 2) return fail(MCMC_E_ARG, "colour bytes: 1 or 2");
-    const uint64_t s = (((uint64_t)n + world - 1) / world + 15) / 16 * 16;
-    *S = s;
-    *P = color_bytes * s + 4ull * kFooterWords;
+}  // extern "C"
+
+namespace mcmc {
+int part_desc(mcmc_ctx* c, PartDesc* d) {
+    if (!c || !d) return fail(MCMC_E_ARG, "NULL argument");
+    if (!c->part) return fail(MCMC_E_STATE, "not a partitioned context");
+    d->colors[0] = c->colors[0];
+    d->colors[1] = c->colors[1];
+    d->foot[0] = c->foot[0];
+    d->foot[1] = c->foot[1];
+    d->bounds = c->bounds.data();
+    d->world = c->world;
+    d->rank = c->rank;
+    d->cbytes = c->cbytes;
+    d->n = c->n;
+    d->stream = c->stream;
+    d->device = c->g->device;
+    d->comm = c->comm;
+    d->events = c->events;
+    d->maxRip = c->p.maxRip;
     return MCMC_OK;
 }
 
-int mcmc_part_layout(uint32_t n, uint32_t world, uint64_t* S, uint64_t* P) { return mcmc_part_layout2(n, world, 1, S, P); }
+int part_adopt(mcmc_ctx* c, void* mem, hipStream_t own_stream, mcmc_comm* comm) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "not a partitioned context");
+    c->own_part = mem;
+    c->borrowed_stream = true;   // mcmc_destroy frees own_stream through the own_part path
+    c->stream = own_stream;
+    c->comm = comm;
+    return MCMC_OK;
+}
 
+int part_stats(mcmc_ctx* c, mcmc_run_stats* s) {
+    int32_t done = 0;
+    uint32_t t = 0, err = 0;
+    int rc = mcmc_part_state(c, &done, &t, &err);
+    if (rc) return rc;
+    *s = c->last;
+    return MCMC_OK;
+}
+
+int part_spill_buffer(mcmc_ctx* c, uint32_t stride, uint32_t** buf) {
+    const size_t need = (size_t)c->world * stride;
+    if ((size_t)c->world * c->spill_stride < need || !c->spill) {
+        (void)hipFree(c->spill);
+        c->spill = nullptr;
+        MCMC_HIP_TRY(hipMalloc(&c->spill, sizeof(uint32_t) * std::max<size_t>(need, 1)));
+    }
+    c->spill_stride = stride;
+    *buf = c->spill;
+    return MCMC_OK;
+}
+}  // namespace mcmc
+
+extern "C" {
+
+// ---- vertex-partitioned step (device-resident; exchange by the caller or by mcmc_part_run) -----
 // The replica element size mcmc_create picks for nCol (the wide sweep: uint16).
 uint32_t mcmc_color_bytes(uint32_t nCol) {
     const char* gv = getenv("MCMC_GATHER");
     return (nCol > 256 || (gv && std::string(gv) == "wide")) ? 2u : 1u;
 }
 
-int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, void* colors1,
-                     uint64_t colors_bytes, void* stream) {
-    if (!c || !colors0 || !colors1) return fail(MCMC_E_ARG, "NULL argument");
-    if (world == 0 || world > 64 || rank >= world) return fail(MCMC_E_ARG, "bad world/rank (1..64 ranks)");
+int mcmc_part_plan_rows(uint32_t n, uint32_t world, uint32_t* bounds) {
+    if (!bounds) return fail(MCMC_E_ARG, "NULL argument");
+    if (world == 0 || world > kMaxWorld) return fail(MCMC_E_ARG, "bad world (1..64 ranks)");
+    const uint64_t S = (((uint64_t)n + world - 1) / world + kPartAlign - 1) / kPartAlign * kPartAlign;
+    for (uint32_t r = 0; r <= world; r++) bounds[r] = (uint32_t)std::min<uint64_t>(S * r, n);
+    bounds[world] = n;
+    return MCMC_OK;
+}
+
+int mcmc_part_plan_csr(const uint64_t* row_off, uint32_t n, uint32_t world, uint32_t* bounds) {
+    if (!row_off || !bounds) return fail(MCMC_E_ARG, "NULL argument");
+    if (world == 0 || world > kMaxWorld) return fail(MCMC_E_ARG, "bad world (1..64 ranks)");
+    // cost of rows [0, v): their arcs plus a per-row term for the evaluation, the own colour
+    // read/write and the (row, block) table entries
+    auto cost = [&](uint64_t v) { return (double)row_off[v] + kPartRowWeight * (double)v; };
+    const double total = cost(n);
+    bounds[0] = 0;
+    for (uint32_t r = 1; r < world; r++) {
+        const double target = total * r / world;
+        uint64_t lo = bounds[r - 1], hi = n;   // first v with cost(v) >= target
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (cost(mid) < target) lo = mid + 1; else hi = mid;
+        }
+        uint64_t b = (lo + kPartAlign / 2) / kPartAlign * kPartAlign;   // nearest aligned row
+        b = std::max<uint64_t>(b, bounds[r - 1]);
+        bounds[r] = (uint32_t)std::min<uint64_t>(b, n);
+    }
+    bounds[world] = n;
+    return MCMC_OK;
+}
+
+int mcmc_part_plan(const mcmc_graph* g, uint32_t world, int balance, uint32_t* bounds) {
+    if (!g || !bounds) return fail(MCMC_E_ARG, "NULL argument");
+    const uint32_t n = g->g.n;
+    if (!balance || !g->g.row_off || world == 1) return mcmc_part_plan_rows(n, world, bounds);
+    MCMC_HIP_TRY(hipSetDevice(g->g.device));
+    std::vector<uint64_t> ro((size_t)n + 1);
+    MCMC_HIP_TRY(hipMemcpy(ro.data(), g->g.row_off, sizeof(uint64_t) * ro.size(), hipMemcpyDeviceToHost));
+    return mcmc_part_plan_csr(ro.data(), n, world, bounds);
+}
+
+namespace {
+
+int check_bounds(uint32_t n, uint32_t world, const uint32_t* bounds) {
+    if (!bounds) return fail(MCMC_E_ARG, "NULL bounds");
+    if (bounds[0] != 0 || bounds[world] != n) return fail(MCMC_E_ARG, "bounds must run from 0 to n");
+    for (uint32_t r = 0; r < world; r++) {
+        if (bounds[r] > bounds[r + 1]) return fail(MCMC_E_ARG, "bounds must be ascending");
+        if (r > 0 && bounds[r] % kPartAlign && bounds[r] != n)
+            return fail(MCMC_E_ARG, "inner bounds must be multiples of 64 rows (mcmc_part_plan)");
+    }
+    return MCMC_OK;
+}
+
+// Partitioned contexts commit events of every rank: room for n of them.
+int grow_events(mcmc_ctx* c, uint32_t need) {
+    if (c->ev_cap >= need) return MCMC_OK;
+    uint32_t pcap = 1;
+    while (pcap < need) pcap <<= 1;
+    uint32_t *ev = nullptr, *dr = nullptr;
+    MCMC_HIP_TRY(hipMalloc(&ev, sizeof(uint32_t) * pcap));
+    MCMC_HIP_TRY(hipMalloc(&dr, sizeof(uint32_t) * pcap));
+    (void)hipFree(c->events);
+    (void)hipFree(c->evdraw);
+    c->events = ev;
+    c->evdraw = dr;
+    c->ev_cap = need;
+    return MCMC_OK;
+}
+
+}  // namespace
+
+int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t* bounds, void* colors0,
+                     void* colors1, uint64_t colors_bytes, void* foot0, void* foot1, void* stream) {
+    if (!c || !colors0 || !colors1 || !foot0 || !foot1) return fail(MCMC_E_ARG, "NULL argument");
+    if (world == 0 || world > kMaxWorld || rank >= world) return fail(MCMC_E_ARG, "bad world/rank (1..64 ranks)");
     if (c->variant != 3 && c->variant != 4)
         return fail(MCMC_E_STATE, "partitioned contexts need the tiled (MCMC_GATHER=tiled) or the wide sweep");
-    uint64_t S = 0, P = 0;
-    (void)mcmc_part_layout2(c->n, world, c->cbytes, &S, &P);
-    if (colors_bytes < P * world) return fail(MCMC_E_ARG, "colour buffers must hold world * P bytes (mcmc_part_layout2)");
-    if (P * world > 0xFFFFFFF0ull)
-        return fail(MCMC_E_ARG, "partitioned colour buffers beyond 4 GiB are not supported");
-    if (c->v_begin != std::min<uint64_t>(S * rank, c->n) || c->v_end != std::min<uint64_t>(S * (rank + 1), c->n))
-        return fail(MCMC_E_ARG, "context rows must be [rank*S, min(n,(rank+1)*S)) (mcmc_part_layout)");
+    if (int rc = check_bounds(c->n, world, bounds)) return rc;
+    if (colors_bytes < ((uint64_t)c->n + 256) * c->cbytes)
+        return fail(MCMC_E_ARG, "colour buffers must hold (n + 256) colours");
+    if (c->v_begin != bounds[rank] || c->v_end != bounds[rank + 1])
+        return fail(MCMC_E_ARG, "context rows must be [bounds[rank], bounds[rank+1])");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (int rc = grow_events(c, std::max<uint32_t>(c->n, 64u * 1024u))) return rc;
     c->colors[0] = static_cast<uint8_t*>(colors0);
     c->colors[1] = static_cast<uint8_t*>(colors1);
-    c->part_S = (uint32_t)S;
+    c->foot[0] = static_cast<uint32_t*>(foot0);
+    c->foot[1] = static_cast<uint32_t*>(foot1);
+    c->bounds.assign(bounds, bounds + world + 1);
     c->world = world;
     c->rank = rank;
     c->part = true;
@@ -2969,11 +3126,13 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, void* colors0, 
     c->stream = static_cast<hipStream_t>(stream);
     c->borrowed_stream = true;
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
+    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
     return MCMC_OK;
 }
 
 int mcmc_part_sweep_async(mcmc_ctx* c) {
     if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
     c->ran = true;
     SweepArgs a = make_args(c, 1);
@@ -2985,22 +3144,61 @@ int mcmc_part_sweep_async(mcmc_ctx* c) {
 
 int mcmc_part_commit_async(mcmc_ctx* c) {
     if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
     SweepArgs a = make_args(c, 1);
-    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a);
-    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a, nullptr, 0u);
+    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a, nullptr, 0u);
+    MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
+}
+
+int mcmc_part_spill_counts(mcmc_ctx* c, uint32_t* counts) {
+    if (!c || !c->part || !counts) return fail(MCMC_E_STATE, "partitioned context and counts required");
+    DevState h{};
+    int rc = download_state(c, &h);
+    if (rc) return rc;
+    if (!(h.err & kErrSpill)) return fail(MCMC_E_STATE, "no spill exchange pending");
+    const uint32_t* f = c->foot[(h.t + 1) & 1];
+    for (uint32_t r = 0; r < c->world; r++)
+        MCMC_HIP_TRY(hipMemcpyAsync(&counts[r], f + (size_t)r * kFooterWords + 2, sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
+
+int mcmc_part_spill_local(mcmc_ctx* c, void* dst, uint32_t* count) {
+    if (!c || !c->part || !count) return fail(MCMC_E_ARG, "NULL argument");
+    uint32_t cnt[kMaxWorld];
+    int rc = mcmc_part_spill_counts(c, cnt);
+    if (rc) return rc;
+    *count = cnt[c->rank];
+    if (dst && *count)
+        MCMC_HIP_TRY(hipMemcpyAsync(dst, c->events, sizeof(uint32_t) * *count, hipMemcpyDeviceToDevice, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    return MCMC_OK;
+}
+
+int mcmc_part_spill_commit_async(mcmc_ctx* c, const uint32_t* gathered, uint32_t stride) {
+    if (!c || !c->part || !gathered) return fail(MCMC_E_ARG, "NULL argument");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    SweepArgs a = make_args(c, 1);
+    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a, gathered, stride);
+    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a, gathered, stride);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }
 
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
     DevState h{};
     int rc = download_state(c, &h);
     if (rc) return rc;
-    if (done) *done = (int32_t)h.done;
+    const bool fin = h.done && !(h.err & kErrSpill);   // paused for a spill exchange: not done
+    if (done) *done = fin ? 1 : 0;
     if (t) *t = h.t;
     if (err) *err = h.err;
-    if (h.done) {
+    if (fin) {
         c->last.iter = h.iter;
         c->last.maxIterReached = (int32_t)h.maxIterReached;
         c->last.finalViol = h.finalViol;

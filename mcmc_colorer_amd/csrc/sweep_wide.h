@@ -113,8 +113,8 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
             cr[i] = 0;
             cc[i] = 1;
             if (e[i] != kXsPad) {
-                cr[i] = C[caddr(a, vb + r[i])];
-                cc[i] = C[caddr(a, j[i])];
+                cr[i] = C[(vb + r[i])];
+                cc[i] = C[j[i]];
             }
         }
 #pragma unroll
@@ -154,15 +154,15 @@ __global__ __launch_bounds__(256) void wide_fp_kernel(SweepArgs a) {
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     const uint32_t n = a.n;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; 8u * k < n; k += gridDim.x * blockDim.x) {
-        const uint32_t v = 8u * k;   // caddr keeps 8-aligned groups contiguous (part_S % 16 == 0)
+        const uint32_t v = 8u * k;
         uint32_t w[2] = {0, 0};
         if (v + 8u <= n) {
-            const uint4 q = *reinterpret_cast<const uint4*>(C + caddr(a, v));
+            const uint4 q = *reinterpret_cast<const uint4*>(C + v);
             const uint32_t c[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int i = 0; i < 4; i++) w[i >> 1] |= ((c[i] & 0xFFu) | ((c[i] >> 8) & 0xFF00u)) << (16u * (i & 1));
         } else {
-            for (uint32_t i = 0; v + i < n; i++) w[i >> 2] |= ((uint32_t)C[caddr(a, v + i)] & 0xFFu) << (8u * (i & 3u));
+            for (uint32_t i = 0; v + i < n; i++) w[i >> 2] |= ((uint32_t)C[(v + i)] & 0xFFu) << (8u * (i & 3u));
         }
         *reinterpret_cast<uint2*>(((t & 1) ? a.wfp1 : a.wfp0) + v) = make_uint2(w[0], w[1]);
     }
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
                             cand[k] = make_uint2(r[i], v0 + (e[i] & cmask));
                         } else {   // list full: settle it here
                             const uint32_t j = v0 + (e[i] & cmask);
-                            if (C[caddr(a, vb + r[i])] == C[caddr(a, j)]) {
+                            if (C[(vb + r[i])] == C[j]) {
                                 flag_violator(a, r[i]);
                                 if (a.xs_sym && j - vb < nloc) flag_violator(a, j - vb);
                             }
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
         const uint32_t nc = min(ncand, kTsCand);
         for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {   // the candidates: compare colours
             const uint2 rc = cand[k];
-            if (C[caddr(a, vb + rc.x)] == C[caddr(a, rc.y)]) {
+            if (C[(vb + rc.x)] == C[rc.y]) {
                 flag_violator(a, rc.x);
                 if (a.xs_sym && rc.y - vb < nloc) flag_violator(a, rc.y - vb);
             }
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
             if (k0 + i >= m) id[i] = 0u;   // slack past m: gather a valid address, ignore below
         uint32_t nc[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) nc[i] = C[caddr(a, id[i])];
+        for (int i = 0; i < 4; i++) nc[i] = C[id[i]];
         // row of arc k0: the largest r in [lo, hi] with ro[r] - a0 <= k0
         uint32_t lo = a.chunk_row[ch], hi = a.chunk_row[ch + 1];
         while (lo < hi) {
@@ -335,14 +335,14 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
         }
         uint32_t r = lo;
         uint64_t rend = ro[r + 1] - a0;
-        uint32_t own = C[caddr(a, a.v_begin + r)];
+        uint32_t own = C[(a.v_begin + r)];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint64_t k = k0 + i;
             if (k >= m) break;
             if (rend <= k) {
                 do { r++; rend = ro[r + 1] - a0; } while (rend <= k);
-                own = C[caddr(a, a.v_begin + r)];
+                own = C[(a.v_begin + r)];
             }
             if (nc[i] == own) flag_violator(a, r);
         }
@@ -358,7 +358,7 @@ __device__ __forceinline__ void walk_gather(const SweepArgs& a, const uint16_t* 
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint64_t kk = k + (uint64_t)j * blockDim.x;
-            c[j] = kk < k1 ? (uint32_t)C[caddr(a, a.col_idx[kk])] : 0xFFFFFFFFu;
+            c[j] = kk < k1 ? (uint32_t)C[a.col_idx[kk]] : 0xFFFFFFFFu;
         }
 #pragma unroll
         for (int j = 0; j < 8; j++)
@@ -403,7 +403,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
     __syncthreads();
     if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
         const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
-        const uint32_t cv = C[caddr(a, v)];
+        const uint32_t cv = C[v];
         const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1));
         const float u = minstd_canonical(x);
         uint32_t nc;
@@ -415,7 +415,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         }
         if (lane == 0) {
             const bool event = nc == a.nCol;
-            Cs[caddr(a, v)] = (uint16_t)(event ? cv : nc);
+            Cs[v] = (uint16_t)(event ? cv : nc);
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)(event ? cv : nc);
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
             if (event) {
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         tab[j] = 0;
         if (l < nloc) {
             viol[j] = a.wflag[l];
-            cv[j] = C[caddr(a, a.v_begin + l)];
+            cv[j] = C[(a.v_begin + l)];
             if (a.taboo != nullptr) tab[j] = a.taboo[l];
         }
     }
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         if (valid) {
             if (viol[j]) a.wflag[l] = 0;
             if (tab[j] > 0) {   // :496-501
-                Cs[caddr(a, v)] = (uint16_t)cv[j];
+                Cs[v] = (uint16_t)cv[j];
                 if (fpn) fpn[v] = (uint8_t)cv[j];
                 a.taboo[l] = tab[j] - 1;
             } else if (viol[j]) {
@@ -599,7 +599,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
                     nc = walk_own_tab(a.etab, a.nCol, cv[j], a.eps, a.hi, u);
                 }
                 event = nc == a.nCol;
-                Cs[caddr(a, v)] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
+                Cs[v] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
                 if (fpn) fpn[v] = (uint8_t)(event ? cv[j] : nc);
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
             }
@@ -648,13 +648,12 @@ __global__ void wide_chunk_row_kernel(const uint64_t* __restrict__ row_off, uint
 }
 
 // ColoringMCMC_CPU ctor colouring (coloringMCMC_CPU.cpp:61) into a uint16 replica.
-__global__ void init_coloring_wide_kernel(uint16_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st,
-                                          uint32_t part_S, uint32_t part_FB) {
+__global__ void init_coloring_wide_kernel(uint16_t* C, uint32_t n, uint32_t x0, UniformIntConst k, DevState* st) {
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
         const uint32_t x = minstd_mulmod(x0, minstd_pow_tab((uint64_t)v + 1));
         const uint32_t r = x - 1u;
         if (r >= k.past) atomicAdd(&st->init_rejections, 1u);
-        C[part_FB ? v + (v / part_S) * part_FB : v] = (uint16_t)min(r / k.scaling, 65535u);
+        C[v] = (uint16_t)min(r / k.scaling, 65535u);
     }
 }
 

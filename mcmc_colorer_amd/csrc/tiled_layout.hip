@@ -607,10 +607,14 @@ extern "C" int mcmc_graph_er_fast(uint32_t n, double prob, uint64_t seed, int de
 
 extern "C" int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t world, uint32_t rank,
                                        int device, mcmc_graph** out) {
-    uint64_t S = 0, P = 0;
-    int rc = mcmc_part_layout(n, world, &S, &P);
-    if (rc) return rc;
     if (rank >= world) return fail(MCMC_E_ARG, "rank >= world");
-    const uint32_t vb = (uint32_t)std::min<uint64_t>(S * rank, n), ve = (uint32_t)std::min<uint64_t>(S * (rank + 1), n);
-    return er_fast_range(n, prob, seed, vb, ve, device, out);
+    std::vector<uint32_t> b((size_t)world + 1);
+    int rc = mcmc_part_plan_rows(n, world, b.data());
+    if (rc) return rc;
+    return er_fast_range(n, prob, seed, b[rank], b[rank + 1], device, out);
+}
+
+extern "C" int mcmc_graph_er_fast_rows(uint32_t n, double prob, uint64_t seed, uint32_t v_begin, uint32_t v_end,
+                                       int device, mcmc_graph** out) {
+    return er_fast_range(n, prob, seed, v_begin, v_end, device, out);
 }

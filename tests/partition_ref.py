@@ -1,11 +1,13 @@
 """TEST INFRASTRUCTURE: a CPU rank backend for mcmc_colorer_amd.distributed.PartitionedColoringMCMC.
 
 It restates, in numpy/float32, the partitioned protocol the HIP kernels implement (sweep of the
-owned rows -> footer [Cviol_local, E, flags, sorted events] -> all-gather -> commit with the
-rank-ordered glibc replay), with the same partitioned buffer layout (per-rank regions of colours
-followed by the footer, one all-gather per sweep), using the oracle_np RNG restatements. Driving the product's driver
-over gloo with this backend checks the exchange sequence and the protocol on CPU; the HIP side of
-the same protocol is checked on the GPU (tests/test_gpu_parity.py::test_partitioned_lockstep).
+owned rows -> footer [Cviol_local, E, flags, sorted events] -> exchange -> commit with the
+rank-ordered glibc replay; a list longer than the footer pauses the loop for the spill exchange),
+with the same buffers (colour replicas in vertex order, rank r owning rows [bounds[r], bounds[r+1]);
+footer buffers of world x FOOTER_WORDS words), using the oracle_np RNG restatements. Driving the
+product's driver over gloo with this backend checks the exchange sequence and the protocol on CPU;
+the HIP side of the same protocol is checked on the GPU (tests/test_gpu_parity.py,
+tests/test_multi.py).
 """
 from __future__ import annotations
 
@@ -15,51 +17,45 @@ import torch
 import oracle_np as NP
 
 FOOTER_WORDS = 1024
+FOOTER_EVENTS = FOOTER_WORDS - 4
 M31 = 2147483647
 
 
 class NumpyRank:
-    def __init__(self, off, idx, nCol, world, rank, eps=1e-8, maxRip=250, taboo=0, z=0):
+    def __init__(self, off, idx, nCol, world, rank, eps=1e-8, maxRip=250, taboo=0, z=0, bounds=None):
         self.off, self.idx = off.astype(np.int64), idx.astype(np.int64)
         self.n = len(off) - 1
         self.nCol, self.eps, self.maxRip, self.tabooIter, self.z = nCol, np.float32(eps), maxRip, taboo, z
         self.world, self.rank = world, rank
-        # region layout of mcmc_part_layout2: S = ceil(n/world) rounded up to 16, region r =
-        # [colours of rows r*S .. r*S+S-1 | footer of rank r], P = cb*S + 4*FOOTER_WORDS bytes with
-        # cb = 2 colour bytes for nCol > 256 (the wide sweep), else 1
-        self.S = ((self.n + world - 1) // world + 15) // 16 * 16
+        if bounds is None:   # mcmc_part_plan_rows: ceil(n / world) rounded up to 64
+            S = ((self.n + world - 1) // world + 63) // 64 * 64
+            bounds = [min(r * S, self.n) for r in range(world)] + [self.n]
+        self.bounds = [int(x) for x in bounds]
         self.cb = 2 if nCol > 256 else 1
-        self.P = self.cb * self.S + 4 * FOOTER_WORDS
-        self.v_begin, self.v_end = min(rank * self.S, self.n), min((rank + 1) * self.S, self.n)
-        self.colors = [torch.zeros(world * self.P + 256, dtype=torch.uint8) for _ in range(2)]
+        self.dt = np.uint16 if self.cb == 2 else np.uint8
+        self.v_begin, self.v_end = self.bounds[rank], self.bounds[rank + 1]
+        self.colors = [torch.zeros((self.n + 256) * self.cb, dtype=torch.uint8) for _ in range(2)]
+        self.foot = [torch.zeros(world * FOOTER_WORDS, dtype=torch.int32) for _ in range(2)]
 
     def _view(self, buf):
-        """Colours of all n vertices (a copy) from a partitioned buffer."""
-        dt = np.uint16 if self.cb == 2 else np.uint8
-        return np.concatenate([buf[r * self.P: r * self.P + self.cb * self.S].numpy().view(dt)
-                               for r in range(self.world)])[: self.n]
+        return buf.numpy()[: self.n * self.cb].view(self.dt)
 
     def _put(self, buf, v, c):
-        o = (v // self.S) * self.P + self.cb * (v % self.S)
-        buf[o] = c & 0xFF
-        if self.cb == 2:
-            buf[o + 1] = c >> 8
+        self._view(buf)[v] = c
 
     # -- interface used by PartitionedColoringMCMC ------------------------------------------------
     def init(self, seed, glibc):
         gen = NP.Minstd(seed)
-        draws = 0
         C = np.zeros(self.n, dtype=np.int64)
         for v in range(self.n):
-            C[v], d = NP.uniform_int(gen, self.nCol)
-            draws += d
-        for v in range(self.n):
-            self._put(self.colors[0], v, int(C[v]))
+            C[v], _ = NP.uniform_int(gen, self.nCol)
+        self._view(self.colors[0])[:] = C.astype(self.dt)
         self.x0 = gen.x                      # engine state after K0 draws
-        self.t, self.done, self.err = 0, False, 0
+        self.t, self.done, self.err, self.paused = 0, False, 0, False
         self.ring = [int(w) for w in glibc.window]   # oldest first
         self.taboo = np.zeros(self.v_end - self.v_begin, dtype=np.int64)
         self.traj = []
+        self.events = []
         self.hi = np.float32(np.float32(1.0) - np.float32(self.nCol - 1) * self.eps)
 
     def _glibc(self):
@@ -68,7 +64,7 @@ class NumpyRank:
         return v >> 1
 
     def sweep(self):
-        if self.done:
+        if self.done or self.paused:
             return
         t, n = self.t, self.n
         C = self._view(self.colors[t & 1]).astype(np.int64)
@@ -106,25 +102,38 @@ class NumpyRank:
             else:
                 self._put(nxt, v, new)
                 self.taboo[l] = self.tabooIter if new == C[v] else 0
+        self.events = sorted(events)
         f = np.zeros(FOOTER_WORDS, dtype=np.uint32)
+        En = min(len(events), FOOTER_EVENTS)
         f[0], f[1], f[2] = viol_local & 0xFFFFFFFF, viol_local >> 32, len(events)
-        f[4:4 + len(events)] = sorted(events)
-        off = self.rank * self.P + self.cb * self.S
-        nxt[off: off + 4 * FOOTER_WORDS] = torch.from_numpy(f.view(np.uint8))
+        f[3] = 2 if len(events) > FOOTER_EVENTS else 0      # spill: the list does not fit the footer
+        f[4:4 + En] = self.events[:En]
+        self.foot[(t + 1) & 1][self.rank * FOOTER_WORDS:(self.rank + 1) * FOOTER_WORDS] = torch.from_numpy(f.view(np.int32))
 
-    def commit(self):
-        if self.done:
+    def _footers(self):
+        return self.foot[(self.t + 1) & 1].numpy().view(np.uint32).reshape(self.world, FOOTER_WORDS)
+
+    def commit(self, spill=None, stride=0):
+        if self.done or (self.paused and spill is None):
             return
-        nb = self.colors[(self.t + 1) & 1].numpy()
-        F = np.stack([nb[r * self.P + self.cb * self.S: (r + 1) * self.P].view(np.uint32) for r in range(self.world)])
+        F = self._footers()
         viol = int(sum(int(r[0]) | (int(r[1]) << 32) for r in F))
-        events = [int(e) for r in F for e in r[4:4 + int(r[2])]]
         t = self.t
+        stop = t == self.maxRip + 1 or viol <= self.z
+        if spill is None and not stop and any(int(r[3]) & 2 for r in F):
+            self.paused = True                # every rank sees the same footers: all pause here
+            return
+        self.paused = False
         self.traj.append(viol)
-        if t == self.maxRip + 1 or viol <= self.z:
+        if stop:
             self.done, self.iter, self.final = True, t, viol
             return
-        C = self._view(self.colors[t & 1])
+        if spill is None:
+            events = [int(e) for r in F for e in r[4:4 + int(r[2])]]
+        else:
+            sp = spill.numpy().view(np.uint32)
+            events = [int(e) for r in range(self.world) for e in sp[r * stride: r * stride + int(F[r][2])]]
+        C = self._view(self.colors[t & 1]).copy()
         nxt = self.colors[(t + 1) & 1]
         for v in events:                     # ascending: ranks own ascending ranges
             c = self._glibc() % (self.nCol - 1)
@@ -134,11 +143,23 @@ class NumpyRank:
         self.t = t + 1
 
     def state(self):
-        return self.done, self.t, self.err
+        return self.done, self.t, (2 if self.paused else 0)
 
-    def region(self, t):
-        nxt = self.colors[(t + 1) & 1]
-        return nxt[: self.world * self.P], nxt[self.rank * self.P:(self.rank + 1) * self.P]
+    def exchange_buffers(self, t):
+        nb = (t + 1) & 1
+        return (self.colors[nb], [(self.bounds[r] * self.cb, self.bounds[r + 1] * self.cb) for r in range(self.world)],
+                self.foot[nb])
+
+    def spill_counts(self):
+        return self._footers()[:, 2].astype(np.uint32)
+
+    def spill_local(self, stride):
+        out = np.zeros(max(stride, 1), dtype=np.uint32)
+        out[: len(self.events)] = self.events
+        return torch.from_numpy(out.view(np.int32))
+
+    def spill_commit(self, gathered, stride):
+        self.commit(spill=gathered, stride=stride)
 
     def glibc_window(self, glibc):
         glibc.window[:] = np.array(self.ring, dtype=np.uint32)

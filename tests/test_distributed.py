@@ -1,5 +1,7 @@
 """Multi-rank path on CPU (gloo): the product's PartitionedColoringMCMC driver with the numpy rank
-backend (tests/partition_ref.py), world sizes 2 and 3, against the unpartitioned oracle."""
+backend (tests/partition_ref.py), world sizes 2 and 3, against the unpartitioned oracle: equal-row
+and arc-balanced plans (mcmc_part_plan_csr), events on every rank, and more events per rank than a
+footer holds (the spill exchange)."""
 import os
 import socket
 
@@ -11,11 +13,38 @@ import torch.multiprocessing as mp
 import oracle_ref as O
 
 CASES = [
-    # n, p, nCol, seed, eps, taboo, maxRip
-    (90, 0.2, 6, 4, 1e-8, 0, 30),
-    (120, 0.3, 7, 9, 3.3e6, 1, 12),     # CDF-overflow events on every rank
-    (80, 0.3, 300, 5, 1e-3, 0, 6),      # nCol > 256: the wide sweep's 2-byte colour regions
+    # graph, n, p, nCol, seed, eps, taboo, maxRip, plan
+    ("simulate", 90, 0.2, 6, 4, 1e-8, 0, 30, "rows"),
+    ("simulate", 120, 0.3, 7, 9, 3.3e6, 1, 12, "rows"),     # CDF-overflow events on every rank
+    ("simulate", 80, 0.3, 300, 5, 1e-3, 0, 6, "rows"),      # nCol > 256: the wide sweep's 2-byte colours
+    ("skewed", 2000, 0.0, 12, 6, 1e-8, 0, 12, "arcs"),      # arc-balanced plan of a skewed graph
+    ("circulant", 10500, 0.0, 3, 21, 3e7, 0, 3, "rows"),    # > 1020 events per rank in sweep 0: spill
 ]
+
+
+def make_graph(kind, n, p):
+    if kind == "simulate":
+        O.srand(1)
+        return O.setup_rnd2(n, p)
+    if kind == "circulant":
+        from test_gpu_parity import circulant
+
+        return circulant(n, 4)
+    # skewed: low ids are hubs (degree falls with the id), the shape equal-row plans balance badly
+    rng = np.random.default_rng(n)
+    E = set()
+    for v in range(n):
+        for _ in range(max(1, 40 * (n - v) // n)):
+            w = int(rng.integers(0, n))
+            if w != v:
+                E.add((min(v, w), max(v, w)))
+    rows = [[] for _ in range(n)]
+    for a, b in E:
+        rows[a].append(b)
+        rows[b].append(a)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    return off, np.concatenate([np.sort(np.array(r, dtype=np.uint32)) for r in rows])
 
 
 def _free_port():
@@ -32,13 +61,14 @@ def _worker(rank, world, port, case, q):
     try:
         import partition_ref as PR
         from mcmc_colorer_amd import colorer as M
-        from mcmc_colorer_amd.distributed import PartitionedColoringMCMC
+        from mcmc_colorer_amd.distributed import PartitionedColoringMCMC, plan_csr, plan_rows
 
-        n, p, ncol, seed, eps, taboo, maxrip = case
-        O.srand(1)
-        off, idx = O.setup_rnd2(n, p)
-        backend = PR.NumpyRank(off, idx, ncol, world, rank, eps=eps, maxRip=maxrip, taboo=taboo)
-        rs = M.GPURand(n, seed, M.GlibcRand(1, n * (n + 1) // 2))
+        kind, n, p, ncol, seed, eps, taboo, maxrip, pl = case
+        off, idx = make_graph(kind, n, p)
+        bounds = plan_csr(off, world) if pl == "arcs" else plan_rows(n, world)
+        backend = PR.NumpyRank(off, idx, ncol, world, rank, eps=eps, maxRip=maxrip, taboo=taboo, bounds=bounds)
+        draws = n * (n + 1) // 2 if kind == "simulate" else 0
+        rs = M.GPURand(n, seed, M.GlibcRand(1, draws))
 
         class _G:   # only nNodes/maxDeg are read by the driver when nCol is given
             nNodes = n
@@ -49,35 +79,50 @@ def _worker(rank, world, port, case, q):
         for it in range(2):                    # two repetitions: seed + i, shared glibc stream
             drv.run(it)
             out.append((drv.coloring().tolist(), drv.trajectory().tolist(), backend.iter,
-                        rs.glibc.window.tolist()))
+                        rs.glibc.window.tolist(), drv.spills, bounds.tolist()))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1]}-{c[8]}")
 def test_partitioned_driver_gloo_matches_oracle(world, case):
-    n, p, ncol, seed, eps, taboo, maxrip = case
+    kind, n, p, ncol, seed, eps, taboo, maxrip, pl = case
+    off, idx = make_graph(kind, n, p)
     O.srand(1)
-    off, idx = O.setup_rnd2(n, p)
-    refs = [O.mcmc_run(off, idx, ncol, seed + i, epsilon=eps, tabooIteration=taboo, maxRip=maxrip) for i in range(2)]
+    if kind == "simulate":
+        O.setup_rnd2(n, p)   # the glibc stream position after the generator
+    refs = [O.mcmc_run(off, idx, ncol, seed + i, epsilon=eps, tabooIteration=taboo, maxRip=maxrip, nthreads=4)
+            for i in range(2)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
     for pr in procs:
         pr.start()
-    results = dict(q.get(timeout=300) for _ in range(world))
+    results = dict(q.get(timeout=600) for _ in range(world))
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
     for rank in range(world):
         for i, ref in enumerate(refs):
-            colors, traj, it, _ = results[rank][i]
+            colors, traj, it, _, spills, bounds = results[rank][i]
             assert colors == ref.colors.tolist(), (rank, i)
             assert traj == ref.traj.tolist(), (rank, i)
             assert it == ref.res.iter
     assert refs[0].res.glibcDraws + refs[1].res.glibcDraws > 0 or eps < 1
     # replicas leave the glibc stream at the same position
     assert len({tuple(results[r][1][3]) for r in range(world)}) == 1
+    if kind == "circulant":
+        assert results[0][0][4] >= 1, "the case must exercise the spill exchange"
+    if pl == "arcs":
+        b = results[0][0][5]
+        deg = np.diff(off.astype(np.int64))
+        loads = [int(deg[b[r]:b[r + 1]].sum()) for r in range(world)]
+        assert b != plan_rows_py(n, world) and max(loads) < 1.25 * sum(loads) / world, (b, loads)
+
+
+def plan_rows_py(n, world):
+    S = ((n + world - 1) // world + 63) // 64 * 64
+    return [min(r * S, n) for r in range(world)] + [n]

@@ -222,10 +222,51 @@ def test_c2_full_run_matches_golden(M):
         d["iter"], d["maxIterReached"], d["finalViol"], d["glibcDraws"])
 
 
-def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, draws=None):
+def _lockstep_exchange(ranks, t):
+    """The exchange of sweep t between HipRank backends on one GPU: every rank's row range and
+    footer slot copied into every other rank's buffers."""
+    from mcmc_colorer_amd.distributed import FOOTER_WORDS
+
+    bufs = [b.exchange_buffers(t) for b in ranks]
+    for q, (Cq, _, Fq) in enumerate(bufs):
+        for r, (Cr, rngs, Fr) in enumerate(bufs):
+            if r != q:
+                lo, hi = rngs[r]
+                Cq[lo:hi].copy_(Cr[lo:hi])
+                Fq[r * FOOTER_WORDS:(r + 1) * FOOTER_WORDS].copy_(Fr[r * FOOTER_WORDS:(r + 1) * FOOTER_WORDS])
+
+
+def _lockstep_drive(ranks, limit):
+    """Sweep / exchange / commit in lock-step until done, with the spill exchange (the full sorted
+    lists, all-gathered with a common stride) when a sweep pauses."""
+    import torch
+
+    t, spills = 0, 0
+    while t < limit:
+        for b in ranks:
+            b.sweep()
+        _lockstep_exchange(ranks, t)
+        for b in ranks:
+            b.commit()
+        t += 1
+        done, tdev, err = ranks[0].state()
+        assert not (err & 1)
+        if err & 2:
+            stride = int(max(1, ranks[0].spill_counts().max()))
+            gathered = torch.cat([b.spill_local(stride) for b in ranks])
+            for b in ranks:
+                b.spill_commit(gathered, stride)
+            spills += 1
+            done, t, err = ranks[0].state()
+        if done:
+            break
+    return spills
+
+
+def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, draws=None, bounds=None):
     """`world` HipRank backends on one GPU, exchanged by tensor copies in lock-step: the device
-    side of the partitioned protocol (region layout: colours + footer per rank, one all-gather,
-    rank-ordered replay)."""
+    side of the partitioned protocol (replicas in vertex order, per-rank row ranges and footer
+    slots exchanged, rank-ordered replay, spill exchange)."""
     import torch
 
     from mcmc_colorer_amd.distributed import HipRank
@@ -233,21 +274,12 @@ def _lockstep(M, off, idx, ncol, seed, world, eps=1e-8, taboo=0, maxRip=250, dra
     n = len(off) - 1
     g = M.Graph.from_csr(off, idx)
     params = M.ColoringMCMCParams(nCol=ncol, epsilon=eps, maxRip=maxRip, tabooIteration=taboo)
-    ranks = [HipRank(g, params, seed, world, r, torch.device("cuda", 0)) for r in range(world)]
+    ranks = [HipRank(g, params, seed, world, r, torch.device("cuda", 0), bounds=bounds) for r in range(world)]
     for b in ranks:
         b.init(seed, M.GlibcRand(1, n * (n + 1) // 2 if draws is None else draws))
-    t = 0
-    while t < maxRip + 2:
-        for b in ranks:
-            b.sweep()
-        gathered = torch.cat([b.region(t)[1] for b in ranks])   # the all-gather of the regions
-        for b in ranks:
-            b.region(t)[0].copy_(gathered)
-        for b in ranks:
-            b.commit()
-        t += 1
-        if ranks[0].state()[0]:
-            break
+    ranks_spills = _lockstep_drive(ranks, maxRip + 2)
+    for b in ranks:
+        b.spills = ranks_spills
     return ranks
 
 
@@ -390,18 +422,7 @@ def test_er_fast_part_lockstep(M, world):
     ranks = [HipRank(graphs[k], params, seed, world, k, torch.device("cuda", 0)) for k in range(world)]
     for b in ranks:
         b.init(seed, M.GlibcRand(1))
-    t = 0
-    while t < maxrip + 2:
-        for b in ranks:
-            b.sweep()
-        gathered = torch.cat([b.region(t)[1] for b in ranks])
-        for b in ranks:
-            b.region(t)[0].copy_(gathered)
-        for b in ranks:
-            b.commit()
-        t += 1
-        if ranks[0].state()[0]:
-            break
+    _lockstep_drive(ranks, maxrip + 2)
     for b in ranks:
         assert b.coloring().tolist() == r.colors.tolist()
         assert b.trajectory().tolist() == r.traj.tolist()
