@@ -253,6 +253,8 @@ def main() -> int:
         # mcmc_part_run); torch.distributed only carries rank 0's unique id, the barriers and the
         # max over ranks, on the CPU (gloo)
         torch.cuda.set_device(local)
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)   # --force-dist without a launcher: world 1
         dist.init_process_group("gloo")
 
     import mcmc_colorer_amd.colorer as M
