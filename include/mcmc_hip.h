@@ -167,6 +167,13 @@ int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps);
  * (Cviol <= z), so a timed run of a convergent configuration still resamples every vertex each
  * sweep; lift the cap with a large maxRip. The trajectory keeps at most 2^20 entries. */
 int mcmc_set_bench_mode(mcmc_ctx* c, int on);
+/* Diagnostics of the tiled sweep's scan (no reference counterpart): with stats on, every sweep adds
+ * the 16-byte id quads it loaded and the (group, column block) pairs it staged (table + colour
+ * slice); mcmc_set_scan_stats(c, 1) also zeroes them. The sweep stops scanning a row once its
+ * occupancy mask holds every colour (count_free_colors cannot change: results are unchanged);
+ * MCMC_FULL_SCAN=1 in the environment at mcmc_create scans every arc instead. */
+int mcmc_set_scan_stats(mcmc_ctx* c, int on);
+int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

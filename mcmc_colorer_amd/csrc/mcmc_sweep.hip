@@ -137,6 +137,10 @@ struct SweepArgs {
     uint32_t* gdone;            // wide: [3][kSplitMax] tasks counted per split walk (zero between sweeps), list index, xbase
     uint32_t split_arcs;        // wide: arcs per task of a split walk
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
+    // tiled sweep: stop scanning a row once its occupancy mask holds every colour (count_free_colors
+    // cannot change any more: the sweep's results are unchanged); 0 = scan every arc (A/B runs)
+    int early;
+    unsigned long long* scan_stats;   // diagnostics (MCMC_SCAN_STATS): [0] quads loaded, [1] pairs staged
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
     uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
     uint32_t* evcnt;            // wide: their number per workgroup [nblk] (written every sweep)
@@ -840,6 +844,7 @@ __device__ __forceinline__ void scan_tile(const uint32_t* __restrict__ tcol, con
 struct TailShared {
     uint32_t wg_viol, wg_ev, wg_last, t, E, err;
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
+    uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
     unsigned long long viol;
 };
 
@@ -1392,7 +1397,27 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint32_t g = blockIdx.x, b = 0, buf = 0;
     const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
     for (uint32_t i = threadIdx.x; i < R * NW; i += blockDim.x) smask[i] = 0;
-    if (threadIdx.x == 0) sh.cursor[0] = nwaves * nsub;
+    if (threadIdx.x == 0) {
+        sh.cursor[0] = nwaves * nsub;
+        sh.nfull[0] = sh.nfull[1] = sh.nfull[2] = 0;
+    }
+    // Early exit (not REF: its scan counts arcs): a row whose mask holds all nCol colours is done --
+    // its later segments are skipped, and once every row of a group is done its remaining pairs are.
+    const bool EXIT = !REF && a.early;
+    uint32_t fullw[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        const uint32_t lo = 32u * i;
+        fullw[i] = a.nCol >= lo + 32u ? ~0u : (a.nCol > lo ? (1u << (a.nCol - lo)) - 1u : 0u);
+    }
+    auto is_full = [&](const uint32_t (&x)[NW]) -> bool {
+        bool f = true;
+#pragma unroll
+        for (int i = 0; i < NW; i++) f = f && ((x[i] & fullw[i]) == fullw[i]);
+        return f;
+    };
+    uint32_t nfull_run = 0, kpair = 0;   // rows of the current group known full; pair counter
+    unsigned long long st_quads = 0, st_pairs = 0;
     if (g < a.ngroups) {
         tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
         if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
@@ -1433,10 +1458,22 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         const uint32_t r0 = g * R;
         const uint32_t rows = min(R, nloc - r0);
         const uint32_t q = (rows + nwaves - 1) / nwaves;   // evaluation share per wave
+        // early exit: rows that filled up in the previous pair (slot (k-1) % 3 is final: its pair
+        // ended at the barrier); slot (k+1) % 3 was last read at the top of pair k-1 and is next
+        // counted into in pair k+1, after this pair's barrier
+        bool allfull = false;
+        if (EXIT) {
+            nfull_run = (b == 0) ? 0u : nfull_run + sh.nfull[(kpair + 2u) % 3u];
+            allfull = b > 0 && nfull_run >= rows;
+            if (threadIdx.x == 0) sh.nfull[(kpair + 1u) % 3u] = 0;
+        }
+        const uint32_t kslot = kpair % 3u;
+        // the group's last pair: its last block, or every row already full
+        const bool last = (b + 1 == nb) || allfull;
         // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
         if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
-        const uint32_t ng = (b + 1 < nb) ? g : g + gridDim.x, nbn = (b + 1 < nb) ? b + 1 : 0u;
+        const uint32_t ng = last ? g + gridDim.x : g, nbn = last ? 0u : b + 1;
         const bool nvalid = ng < a.ngroups;
         if (nvalid) {
             tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane);
@@ -1465,10 +1502,21 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         auto own_of = [&](uint32_t r) -> uint32_t { return r < rows ? (uint32_t)ownp[r] : 0u; };
         uint32_t oc = REF ? own_of(row) : 0u;
         uint32_t claim = 0;
-        if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);
+        if (li == 0 && !allfull) claim = atomicAdd(&sh.cursor[buf], 1u);
         uint32_t m[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) m[i] = 0;
+        // the row's mask from earlier blocks; a full one makes its segment empty
+        uint32_t base[NW];
+        bool rowfull = false;
+#pragma unroll
+        for (int i = 0; i < NW; i++) base[i] = 0;
+        if (EXIT && b > 0 && row < rows) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
+            if (is_full(base)) end = pos;
+        }
+        if (a.scan_stats) st_pairs += (threadIdx.x == 0) ? 1u : 0u;
         // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
         // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
         // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
@@ -1478,7 +1526,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     {                                                                                                   \
         const bool act = row < rows;                                                                    \
         uint32_t npos2 = pos + step, nrow = row, nend2 = end, noc = oc, ntend = tend;                   \
-        const bool fin = act && (npos2 - 8u * li >= end);                                               \
+        uint32_t nbase[NW];                                                                             \
+        _Pragma("unroll") for (int i = 0; i < NW; i++) nbase[i] = base[i];                              \
+        /* the row's last step: its segment ends, or its mask filled up in the previous step */        \
+        const bool fin = act && (npos2 - 8u * li >= end || rowfull);                                    \
         if (__ballot(fin)) {                                                                            \
             const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
             if (fin) {                                                                                  \
@@ -1488,6 +1539,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     npos2 = (sraw & kTsegPos) + 8u * li;                                                \
                     nend2 = sseg[nrow + 1] & kTsegPos;                                                  \
                     ntend = nend2 - (sraw & 7u);                                                        \
+                    if (EXIT && b > 0) {                                                                \
+                        _Pragma("unroll") for (int i = 0; i < NW; i++) nbase[i] = smask[nrow * NW + i]; \
+                        if (is_full(nbase)) nend2 = npos2;   /* done in earlier blocks: empty segment */ \
+                    }                                                                                   \
                 }                                                                                       \
                 if (REF) noc = own_of(nrow);                                                            \
                 if (li == 0) claim = atomicAdd(&sh.cursor[buf], 1u);                                    \
@@ -1497,15 +1552,20 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         if (CONT) {                                                                                     \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                        \
                 const uint32_t pu = npos2 + 8u * L * u;                                                 \
-                NXT[u] = tile_load(gr, gcol, (nrow < rows && pu < nend2) ? 2u * pu : kTileOOB);         \
+                const bool ld = nrow < rows && pu < nend2;                                              \
+                if (a.scan_stats) st_quads += ld ? 1u : 0u;                                             \
+                NXT[u] = tile_load(gr, gcol, ld ? 2u * pu : kTileOOB);                                  \
             }                                                                                           \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
-                MCMC_TILE_GATHER(CUR[u], act && pos + 8u * L * u < end, pos + 8u * L * u);              \
+                MCMC_TILE_GATHER(CUR[u], act && !rowfull && pos + 8u * L * u < end, pos + 8u * L * u);  \
         } else {                                                                                        \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
-                MCMC_TILE_GATHER(CUR[u], act && pos + 8u * L * u < end, pos + 8u * L * u);              \
+                MCMC_TILE_GATHER(CUR[u], act && !rowfull && pos + 8u * L * u < end, pos + 8u * L * u);  \
         }                                                                                               \
-        if (__ballot(fin)) {                                                                            \
+        /* reduce over the sub-group: at a row's end (flush), and each step of a longer row when */  \
+        /* early exit can stop it */                                                                   \
+        const bool chk = EXIT && act && !fin;                                                           \
+        if (__ballot(fin || chk)) {                                                                     \
             uint32_t red[NW];                                                                           \
             _Pragma("unroll") for (int i = 0; i < NW; i++) {                                            \
                 uint32_t x = m[i];                                                                      \
@@ -1514,11 +1574,23 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             }                                                                                           \
             if (fin) {                                                                                  \
                 if (li == 0) {                                                                          \
-                    _Pragma("unroll") for (int i = 0; i < NW; i++) atomicOr(&smask[row * NW + i], red[i]); \
+                    _Pragma("unroll") for (int i = 0; i < NW; i++)                                      \
+                        if (red[i]) atomicOr(&smask[row * NW + i], red[i]);                             \
+                    if (EXIT) {                                                                         \
+                        uint32_t nm[NW];                                                                \
+                        _Pragma("unroll") for (int i = 0; i < NW; i++) nm[i] = red[i] | base[i];        \
+                        if (is_full(nm) && !is_full(base)) atomicAdd(&sh.nfull[kslot], 1u);             \
+                    }                                                                                   \
                 }                                                                                       \
                 _Pragma("unroll") for (int i = 0; i < NW; i++) m[i] = 0;                                \
+            } else if (chk) {                                                                           \
+                uint32_t nm[NW];                                                                        \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) nm[i] = red[i] | base[i];                \
+                rowfull = is_full(nm);                                                                  \
             }                                                                                           \
         }                                                                                               \
+        if (fin) rowfull = false;                                                                       \
+        _Pragma("unroll") for (int i = 0; i < NW; i++) base[i] = nbase[i];                              \
         row = nrow;                                                                                     \
         pos = npos2;                                                                                    \
         end = nend2;                                                                                    \
@@ -1531,7 +1603,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         else tile_gather<NW>(scb, Q, OK, m);                                                            \
     } while (0)
         uint4 v1[kTileU];
-        if (__ballot(row < rows)) {
+        if (!allfull && __ballot(row < rows)) {
             for (;;) {
                 bool c0, c1;
                 MCMC_TILE_STEP(v, v1, c0)
@@ -1554,7 +1626,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
         }
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_scan += t1 - tmark; tmark = t1; }
-        if (b + 1 == nb) {
+        if (last) {
             MCMC_LDS_BARRIER();   // every wave's mask ORs of the group are in
             // every wave evaluates a share of the group's rows and clears their masks for the next group
             for (uint32_t e0 = wid * min(q, 64u); e0 < rows; e0 += nwaves * min(q, 64u)) {
@@ -1580,6 +1652,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         g = ng;
         b = nbn;
         buf ^= 1u;
+        kpair++;
+    }
+    if (a.scan_stats) {   // diagnostics: quads loaded and pairs staged by this workgroup
+        unsigned long long x = st_quads;
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if (lane == 0 && x) atomicAdd(&a.scan_stats[0], x);
+        if (threadIdx.x == 0) atomicAdd(&a.scan_stats[1], st_pairs);
     }
     MCMC_PHASE(a, 3);
     if (timing && threadIdx.x == 0) {   // shader-clock cycles per phase kind, wave 0
@@ -1751,6 +1830,9 @@ struct mcmc_ctx {
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
+    int early = 1;              // tiled: early-exit scan (MCMC_FULL_SCAN=1: every arc)
+    unsigned long long* scan_stats = nullptr;   // mcmc_set_scan_stats: [quads loaded, pairs staged]
+    bool scan_stats_on = false;
     uint32_t world = 1, rank = 0;
     std::vector<uint32_t> bounds;            // partitioned: rank r sweeps rows [bounds[r], bounds[r+1])
     uint32_t* foot[2] = {nullptr, nullptr};  // partitioned: footer buffers, world x kFooterWords each
@@ -1855,6 +1937,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
     a.bench = c->bench_mode;
+    a.early = c->early;
+    a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
     a.seg = c->seg;
     a.nblocks = c->nblocks;
@@ -2159,6 +2243,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     c->nw = p->nCol <= 32 ? 1 : p->nCol <= 64 ? 2 : p->nCol <= 128 ? 4 : 8;
     c->ref = ref != nullptr;
     c->rand = ref;
+    if (const char* fs = getenv("MCMC_FULL_SCAN")) c->early = atoi(fs) ? 0 : 1;
     if (ref) c->fused = 1;
     // Variant: the tiled layout (16-bit block-local ids, replica LDS-resident when it fits, else
     // streamed 64 KiB slices) -- fastest on every measured shape. The CSR variants stay selectable
@@ -2640,6 +2725,29 @@ int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
     return MCMC_OK;
 }
 
+int mcmc_set_scan_stats(mcmc_ctx* c, int on) {
+    if (!c) return fail(MCMC_E_ARG, "NULL context");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 2 * sizeof(unsigned long long)));
+    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 2 * sizeof(unsigned long long)));
+    c->scan_stats_on = on != 0;
+    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
+    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
+    return MCMC_OK;
+}
+
+int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs) {
+    if (!c || !quads || !pairs) return fail(MCMC_E_ARG, "NULL argument");
+    unsigned long long h[2] = {0, 0};
+    if (c->scan_stats) {
+        MCMC_HIP_TRY(hipSetDevice(c->g->device));
+        MCMC_HIP_TRY(hipMemcpy(h, c->scan_stats, sizeof(h), hipMemcpyDeviceToHost));
+    }
+    *quads = h[0];
+    *pairs = h[1];
+    return MCMC_OK;
+}
+
 int mcmc_set_bench_mode(mcmc_ctx* c, int on) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     c->bench_mode = on ? 1 : 0;
@@ -2952,6 +3060,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wcount);
     (void)hipFree(c->gmask);
     (void)hipFree(c->etab);
+    (void)hipFree(c->scan_stats);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
