@@ -224,6 +224,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-refstruct", action="store_true", help="skip the refstruct (reference-structure) leg")
     ap.add_argument("--no-convergence", action="store_true", help="skip the reference-loop run (sweeps-to-zero-conflict)")
+    ap.add_argument("--no-full-scan", action="store_true", help="skip the full-scan (MCMC_FULL_SCAN=1) comparison")
     ap.add_argument("--refstruct-sweeps", type=int, default=10)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--force-dist", action="store_true",
@@ -380,8 +381,45 @@ def main() -> int:
     # §8d: with a compressed format the fraction is taken against the format's bytes), and the
     # same rows' B_alg in the reference's uint32 layout for comparison
     b_fmt, b_ref = info["sweep_bytes"], info["ref_bytes"]
-    achieved = b_fmt / (kernel_ms * 1e-3) / 1e9
     variant = info["variant"]
+    scan = None
+    b_alg = b_fmt
+    if dist is None and not ref and variant == "tiled":
+        # The tiled sweep stops scanning a row once its occupancy mask holds every colour (the
+        # result cannot change; MCMC_FULL_SCAN=1 scans every arc): the bytes one launch moves are
+        # counted on the device (mcmc_set_scan_stats, 3 sweeps outside the timed region) -- id quads,
+        # the staged (group, block) pairs' table rows and colour slices, own colour read + write
+        q, pr, tot2, ker2 = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        check(lib().mcmc_set_scan_stats(col._ctx, 1))
+        check(lib().mcmc_bench_sweeps(col._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
+        check(lib().mcmc_get_scan_stats(col._ctx, ctypes.byref(q), ctypes.byref(pr)))
+        check(lib().mcmc_set_scan_stats(col._ctx, 0))
+        quads, pairs = q.value / 3.0, pr.value / 3.0
+        R = info["grp_rows"]
+        table = 4 * ((R + 4) & ~3)
+        slice_b = 0 if info["resident"] else min(65536, ((g.nNodes + 15) // 16) * 16)
+        b_alg = 16 * quads + pairs * (table + slice_b) + 2 * g.nNodes
+        scan = {"early_exit": info.get("early", True), "quads_per_sweep": quads, "pairs_per_sweep": pairs,
+                "id_bytes": 16 * quads, "table_bytes": pairs * table, "slice_bytes": pairs * slice_b,
+                "layout_bytes_full_scan": b_fmt,
+                "note": "exact early exit: a row's scan stops once its mask holds all nCol colours "
+                        "(count_free_colors cannot change); a group skips its remaining column blocks once "
+                        "every row is full. Bit-identical results (tests/test_gpu_parity.py)."}
+        if not a.no_full_scan:
+            # the same sweep scanning every arc (MCMC_FULL_SCAN=1): the layout-bound reference point
+            os.environ["MCMC_FULL_SCAN"] = "1"
+            cf = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), params)
+            cf.init(0)
+            check(lib().mcmc_bench_sweeps(cf._ctx, 2, ctypes.byref(tot2), ctypes.byref(ker2)))
+            k = max(3, min(a.steps, 10))
+            check(lib().mcmc_bench_sweeps(cf._ctx, k, ctypes.byref(tot2), ctypes.byref(ker2)))
+            os.environ.pop("MCMC_FULL_SCAN")
+            scan["full_scan"] = {"ms_per_sweep": ker2.value, "value": g.nNodes / (ker2.value * 1e-3),
+                                 "sweeps": k, "bytes": b_fmt,
+                                 "achieved_GBs": b_fmt / (ker2.value * 1e-3) / 1e9,
+                                 "frac": b_fmt / (ker2.value * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            cf.close()
+    achieved = b_alg / (kernel_ms * 1e-3) / 1e9
     key = f"{a.config}/{variant}" if (world == 1 and (a.config in ("c3", "c5") or n_req == 100000)) else None
     if key and ref:
         key += "-ref"
@@ -416,13 +454,15 @@ def main() -> int:
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,
                      "kernel": KERNELS.get(variant, variant) + ("<REF>" if ref else "")
                                + ("" if world == 1 else " + exchange (per-rank step)"),
-                     "kernel_ms": kernel_ms, "algorithmic_bytes": b_fmt,
+                     "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg,
                      "ref_layout_bytes": b_ref, "ref_layout_equiv_GBs": b_ref / (kernel_ms * 1e-3) / 1e9,
                      "layout": info},
         "cpu_baseline": None,
     }
     if conv is not None:
         out["convergence"] = conv
+    if scan is not None:
+        out["scan"] = scan
     # CPU and refstruct legs: on the benchmarked graph for c2; for c3 (no CSR can exist: 400 GB) on
     # --simulate 0.1 -n 100000, which has C3's mean degree 1e4 (per-vertex work is per-degree)
     sample, sample_n, sample_window, sample_note = g, n, None, None

@@ -24,7 +24,7 @@ def main():
     else:
         g = M.Graph.simulate(100000, 0.01, M.GlibcRand(1))
         ncol, steps = 16, 200
-    for full in ("0", "1"):
+    for full in os.environ.get("MCMC_PROBE_MODES", "0,1").split(","):
         os.environ["MCMC_FULL_SCAN"] = full
         col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=0x7FFFFFF0))
         col.init(0)
