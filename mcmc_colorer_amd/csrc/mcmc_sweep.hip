@@ -140,6 +140,8 @@ struct SweepArgs {
     // tiled sweep: stop scanning a row once its occupancy mask holds every colour (count_free_colors
     // cannot change any more: the sweep's results are unchanged); 0 = scan every arc (A/B runs)
     int early;
+    uint32_t dbg_max_pairs;     // diagnostics only (MCMC_DEBUG_MAX_PAIRS): cut every group after k pairs (wrong results)
+    uint32_t drain_rows;        // tiled early exit: a group with at most this many rows left drains them (<= 256)
     unsigned long long* scan_stats;   // diagnostics (MCMC_SCAN_STATS): [0] quads loaded, [1] pairs staged
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
     uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
@@ -845,6 +847,8 @@ struct TailShared {
     uint32_t wg_viol, wg_ev, wg_last, t, E, err;
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
+    uint32_t dn;          // tiled drain: rows listed
+    uint16_t dlist[256];  // tiled drain: the group's rows whose masks are not full yet
     unsigned long long viol;
 };
 
@@ -1301,6 +1305,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_group_rsrc(const SweepArg
 #ifndef MCMC_TILE_BUFLOAD
 #define MCMC_TILE_BUFLOAD 0
 #endif
+#ifndef MCMC_TILE_NT
+#define MCMC_TILE_NT 0
+#endif
 // One quad of ids at byte offset `byte_off` of the group. MCMC_TILE_BUFLOAD=1: buffer load, slots
 // past the end return 0 without a request; 0 (default, measured faster on C3): a plain load
 // clamped to the group base.
@@ -1311,8 +1318,16 @@ __device__ __forceinline__ uint4 tile_load(__amdgpu_buffer_rsrc_t r, const uint1
     return make_uint4(x.x, x.y, x.z, x.w);
 #else
     (void)r;
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(gbase_ptr) +
-                                           (byte_off == kTileOOB ? 0u : byte_off));
+    const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(gbase_ptr) +
+                                                    (byte_off == kTileOOB ? 0u : byte_off));
+#if MCMC_TILE_NT
+    // ids are read once per sweep: non-temporal, so they do not push the pairs' colour slices
+    // (re-staged by every group) and segment tables out of L2
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    return *p;
+#endif
 #endif
 }
 
@@ -1338,6 +1353,66 @@ __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, u
 // __syncthreads() would drain them).
 #define MCMC_PAIR_BARRIER() asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define MCMC_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// Drain (early exit): the group's rows whose masks are still not full (at most drain_rows, few once
+// most rows filled up) finish every remaining column block in this pair, reading their segments'
+// bounds and ids from the global layout and the neighbours' colours straight from the replica
+// (L2/MALL) -- no more (table, slice) pairs are staged for them. Rounds of 4 blocks: a team of 4
+// lanes per (row, block) segment gathers its quads; masks are OR-ed into smask; a round is
+// followed by another only while a listed row is not full. All threads call it (uniform).
+template <int NW>
+__device__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g, uint32_t b, uint32_t rows,
+                           uint32_t* smask, TailShared& sh, const uint32_t (&fullw)[NW], int lane) {
+    auto row_full = [&](uint32_t r) -> bool {
+        bool f = true;
+#pragma unroll
+        for (int i = 0; i < NW; i++) f = f && ((smask[r * NW + i] & fullw[i]) == fullw[i]);
+        return f;
+    };
+    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x)
+        if (!row_full(r)) {
+            const uint32_t k = atomicAdd(&sh.dn, 1u);
+            if (k < 256u) sh.dlist[k] = (uint16_t)r;
+        }
+    __syncthreads();
+    const uint32_t na = min(sh.dn, 256u);
+    const uint32_t R = a.grp_rows, TS = tseg_stride(R);
+    const uint32_t team = threadIdx.x >> 2, tl = threadIdx.x & 3u, nteams = blockDim.x >> 2;
+    const uint16_t* __restrict__ gids = a.tcol + a.gbase[g];
+    for (uint32_t bb = b; bb < a.nblocks; bb += 4) {
+        for (uint32_t it = team; it < na * 4u; it += nteams) {
+            const uint32_t r = sh.dlist[it >> 2], blk = bb + (it & 3u);
+            uint32_t m[NW];
+#pragma unroll
+            for (int i = 0; i < NW; i++) m[i] = 0;
+            if (blk < a.nblocks) {
+                const uint32_t* ts = a.tseg + ((size_t)g * a.nblocks + blk) * TS;
+                const uint32_t s0 = ts[r] & kTsegPos, s1 = ts[r + 1] & kTsegPos;
+                const uint8_t* __restrict__ cb = C + ((size_t)blk << a.block_log2);
+                for (uint32_t q = s0 + 8u * tl; q < s1; q += 32u) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(gids + q);
+                    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        set_color_bit<NW>(m, cb[w8[e] & 0xFFFFu]);
+                        set_color_bit<NW>(m, cb[w8[e] >> 16]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NW; i++) {
+                uint32_t x = m[i];
+                x |= __shfl_xor(x, 1, 64);
+                x |= __shfl_xor(x, 2, 64);
+                if (tl == 0 && x) atomicOr(&smask[r * NW + i], x);
+            }
+        }
+        __syncthreads();
+        bool open = false;   // every wave reads the same masks: a uniform decision
+        for (uint32_t k = (uint32_t)lane; k < na; k += 64u) open = open || !row_full(sh.dlist[k]);
+        if (__ballot(open) == 0ull) break;
+    }
+}
 
 // RES: the whole replica is LDS-resident; otherwise the colour slice of each pair. One 1024-thread
 // workgroup per CU (two smaller ones per CU were measured to split the CU's issue unevenly: the
@@ -1461,15 +1536,20 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // early exit: rows that filled up in the previous pair (slot (k-1) % 3 is final: its pair
         // ended at the barrier); slot (k+1) % 3 was last read at the top of pair k-1 and is next
         // counted into in pair k+1, after this pair's barrier
-        bool allfull = false;
+        bool allfull = false, drain = false;
         if (EXIT) {
             nfull_run = (b == 0) ? 0u : nfull_run + sh.nfull[(kpair + 2u) % 3u];
             allfull = b > 0 && nfull_run >= rows;
-            if (threadIdx.x == 0) sh.nfull[(kpair + 1u) % 3u] = 0;
+            // few rows left: they finish every remaining block here (tile_drain), no more pairs
+            drain = !allfull && b > 0 && rows - nfull_run <= a.drain_rows && b + 1 < nb;
+            if (threadIdx.x == 0) {
+                sh.nfull[(kpair + 1u) % 3u] = 0;
+                if (b == 0) sh.dn = 0;   // the drain list of this group (its last use: an earlier group's pair)
+            }
         }
         const uint32_t kslot = kpair % 3u;
-        // the group's last pair: its last block, or every row already full
-        const bool last = (b + 1 == nb) || allfull;
+        // the group's last pair: its last block, every row already full, or the drain
+        const bool last = (b + 1 == nb) || allfull || drain || (a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
         // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
         if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
@@ -1603,7 +1683,9 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         else tile_gather<NW>(scb, Q, OK, m);                                                            \
     } while (0)
         uint4 v1[kTileU];
-        if (!allfull && __ballot(row < rows)) {
+        if (drain) {
+            tile_drain<NW>(a, C, g, b, rows, smask, sh, fullw, lane);
+        } else if (!allfull && __ballot(row < rows)) {
             for (;;) {
                 bool c0, c1;
                 MCMC_TILE_STEP(v, v1, c0)
@@ -1831,6 +1913,7 @@ struct mcmc_ctx {
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
     int early = 1;              // tiled: early-exit scan (MCMC_FULL_SCAN=1: every arc)
+    uint32_t drain_rows = 192;  // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256)
     unsigned long long* scan_stats = nullptr;   // mcmc_set_scan_stats: [quads loaded, pairs staged]
     bool scan_stats_on = false;
     uint32_t world = 1, rank = 0;
@@ -1938,6 +2021,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.check_done = check_done;
     a.bench = c->bench_mode;
     a.early = c->early;
+    a.drain_rows = c->drain_rows;
+    if (const char* dm = getenv("MCMC_DEBUG_MAX_PAIRS")) a.dbg_max_pairs = (uint32_t)atoi(dm);
     a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
     a.seg = c->seg;
@@ -2244,6 +2329,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     c->ref = ref != nullptr;
     c->rand = ref;
     if (const char* fs = getenv("MCMC_FULL_SCAN")) c->early = atoi(fs) ? 0 : 1;
+    if (const char* dr = getenv("MCMC_DRAIN_ROWS")) c->drain_rows = std::min<uint32_t>(256u, (uint32_t)atoi(dr));
     if (ref) c->fused = 1;
     // Variant: the tiled layout (16-bit block-local ids, replica LDS-resident when it fits, else
     // streamed 64 KiB slices) -- fastest on every measured shape. The CSR variants stay selectable

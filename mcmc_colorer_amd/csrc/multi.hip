@@ -6,9 +6,9 @@
 //   mcmc_part_sweep_async   the rank's rows -> its rows of colors[(t+1)&1] + its footer slot
 //   exchange                colours: P2P send/recv of every rank's row range to every peer (xGMI is a
 //                           full mesh of point-to-point links: each range travels once per link, in
-//                           parallel; arc-balanced ranges have unequal sizes) -- or one in-place
-//                           ncclAllGather when the plan's ranges are equal-stride; footers: one
-//                           in-place ncclAllGather of world x 4 KiB
+//                           parallel; arc-balanced ranges have unequal sizes) -- or, MCMC_EXCHANGE=
+//                           allgather, one in-place ncclAllGather for equal-stride plans; footers:
+//                           one in-place ncclAllGather of world x 4 KiB
 //   mcmc_part_commit_async  global Cviol, stop test, the rank-ordered glibc replay on every replica
 // Every check_every sweeps the host reads the device state: done, a fatal error, or a spill pause
 // (some rank's overflow-event list outgrew its footer): then the full sorted lists are all-gathered
@@ -56,12 +56,12 @@ uint32_t equal_stride(const PartDesc& d) {
     return S;
 }
 
-int exchange_mode() {   // MCMC_EXCHANGE = p2p | allgather | auto (default)
+// MCMC_EXCHANGE = p2p (default) | allgather. xGMI is a full mesh of point-to-point links: every
+// rank's range goes to each peer over its own link, all links at once (7 x n/8 bytes per rank at
+// 8 GPUs); the ring all-gather (equal-stride plans only) moves the same bytes through 7 hops.
+int exchange_mode() {
     const char* e = getenv("MCMC_EXCHANGE");
-    if (!e) return 0;
-    if (!strcmp(e, "p2p")) return 1;
-    if (!strcmp(e, "allgather")) return 2;
-    return 0;
+    return (e && !strcmp(e, "allgather")) ? 2 : 1;
 }
 
 struct Driver {
@@ -108,7 +108,7 @@ struct Driver {
         const uint32_t nb = (t + 1) & 1u;
         if (rccl) {
             const uint32_t S = equal_stride(d[0]);
-            const bool ag = S != 0 && mode != 1;   // equal-stride ranges: one all-gather (p2p forces sends)
+            const bool ag = S != 0 && mode == 2;   // equal-stride ranges may take one in-place all-gather
             if (world > 1) {
                 MCMC_NCCL_TRY(ncclGroupStart());
                 for (auto& x : d) {

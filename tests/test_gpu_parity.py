@@ -500,3 +500,24 @@ def test_tailcut_repair_generated_graph(M):
     st = col.run(0)
     assert_same(col, st, r)
     assert st.tailcutPasses == r.res.tailcutPasses
+
+
+@pytest.mark.parametrize("drain,rows,stream", [("0", "200", "1"), ("256", "200", "1"), ("256", "64", "0"),
+                                               ("48", "300", "1")])
+def test_early_exit_drain_matches_oracle(M, monkeypatch, drain, rows, stream):
+    """The early-exit scan (a row stops once its mask holds every colour; a group skips its
+    remaining blocks once all rows are full) and its drain (a group's last few open rows finish
+    every remaining block from the global layout and replica): 5 column blocks, small groups so
+    every group drains after its first block; the full scan and the oracle agree bit for bit."""
+    n, p, ncol, seed = 300000, 0.0006, 16, 12
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=5, nthreads=8)
+    monkeypatch.setenv("MCMC_DRAIN_ROWS", drain)
+    monkeypatch.setenv("MCMC_GROUP_ROWS", rows)
+    monkeypatch.setenv("MCMC_TILE_STREAM", stream)
+    col, st, _ = gpu_run(M, off, idx, ncol, seed, 0, maxRip=5)
+    assert_same(col, st, r)
+    monkeypatch.setenv("MCMC_FULL_SCAN", "1")
+    col2, st2, _ = gpu_run(M, off, idx, ncol, seed, 0, maxRip=5)
+    assert_same(col2, st2, r)
