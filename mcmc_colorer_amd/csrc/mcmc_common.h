@@ -90,14 +90,15 @@ struct TailView {
 };
 // flags[v] = colour of v used by a neighbour (violation_count, coloringMCMC_CPU.cpp:329-350); *count = sum.
 // edges: the reference GPU colorer's conflictCounter (same-colour neighbours with a larger id, counted).
-int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s,
-               bool edges);
+// C: the replica, cbytes = 1 (uint8) or 2 (uint16, the wide sweep).
+int tail_count(const TailView& g, const void* C, uint32_t cbytes, uint8_t* flags, unsigned long long* count,
+               hipStream_t s, bool edges);
 // Ascending list of the flagged vertices; *list_len on the device. tmp: scratch, grown on demand.
 int tail_select(const uint8_t* flags, uint32_t n, uint32_t* list, uint32_t* list_len, void** tmp, size_t* tmp_bytes,
                 hipStream_t s);
 // One corrected tail-cut pass (coloringMCMC_CPU.cpp:281-305, k++) over the listed vertices, in order.
 // ref: the GPU colorer's tailCutting rule over at most `limit` listed vertices.
-int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint32_t* list_len,
+int tail_repair(const TailView& g, void* C, uint32_t cbytes, const uint32_t* list, const uint32_t* list_len,
                 const uint32_t* colorIdx, uint32_t nCol, hipStream_t s, bool ref, unsigned long long limit);
 }  // namespace mcmc
 

@@ -848,6 +848,7 @@ struct TailShared {
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
     uint32_t dn;          // tiled drain: rows listed
+    uint32_t st_quads, st_pairs;   // diagnostics (scan_stats): quads loaded, pairs staged by the workgroup
     uint16_t dlist[256];  // tiled drain: the group's rows whose masks are not full yet
     unsigned long long viol;
 };
@@ -1361,8 +1362,23 @@ __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, u
 // lanes per (row, block) segment gathers its quads; masks are OR-ed into smask; a round is
 // followed by another only while a listed row is not full. All threads call it (uniform).
 template <int NW>
-__device__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g, uint32_t b, uint32_t rows,
-                           uint32_t* smask, TailShared& sh, const uint32_t (&fullw)[NW], int lane) {
+__device__ __forceinline__ void drain_quad(const uint8_t* __restrict__ cb, const uint4& v, bool ok, uint32_t (&m)[NW]) {
+    if (!ok) return;
+    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
+    uint32_t c[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        c[2 * e] = cb[w8[e] & 0xFFFFu];
+        c[2 * e + 1] = cb[w8[e] >> 16];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) set_color_bit<NW>(m, c[e]);
+}
+
+template <int NW>
+__device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g, uint32_t b,
+                                        uint32_t rows, uint32_t* smask, TailShared& sh, const uint32_t* fullw,
+                                        int lane) {
     auto row_full = [&](uint32_t r) -> bool {
         bool f = true;
 #pragma unroll
@@ -1389,14 +1405,14 @@ __device__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, ui
                 const uint32_t* ts = a.tseg + ((size_t)g * a.nblocks + blk) * TS;
                 const uint32_t s0 = ts[r] & kTsegPos, s1 = ts[r + 1] & kTsegPos;
                 const uint8_t* __restrict__ cb = C + ((size_t)blk << a.block_log2);
-                for (uint32_t q = s0 + 8u * tl; q < s1; q += 32u) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(gids + q);
-                    const uint32_t w8[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        set_color_bit<NW>(m, cb[w8[e] & 0xFFFFu]);
-                        set_color_bit<NW>(m, cb[w8[e] >> 16]);
-                    }
+                // the segment's quads two per lane at once, then their gathers: one memory round
+                // trip per two quads instead of per quad
+                for (uint32_t q = s0 + 8u * tl; q < s1; q += 64u) {
+                    const uint32_t q2 = q + 32u;
+                    const uint4 v0 = *reinterpret_cast<const uint4*>(gids + q);
+                    const uint4 v1 = *reinterpret_cast<const uint4*>(gids + (q2 < s1 ? q2 : q));
+                    drain_quad<NW>(cb, v0, true, m);
+                    drain_quad<NW>(cb, v1, q2 < s1, m);
                 }
             }
 #pragma unroll
@@ -1425,7 +1441,7 @@ __device__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, ui
 // REF: the reference-GPU-semantics sweep on the same pipeline -- the scan also counts the rows'
 // same-colour arcs (own colours from the replica, or streamed per group into LDS), the evaluation
 // is evaluate_ref_tile, the arrival carries the count (sweep_tail_ref).
-template <int NW, bool RES, bool REF>
+template <int NW, bool RES, bool REF, bool EX>
 __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
     __shared__ TailShared sh;
@@ -1478,7 +1494,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     }
     // Early exit (not REF: its scan counts arcs): a row whose mask holds all nCol colours is done --
     // its later segments are skipped, and once every row of a group is done its remaining pairs are.
-    const bool EXIT = !REF && a.early;
+    const bool EXIT = EX && !REF && a.early;   // EX = false: the full-scan instantiation (no early-exit code)
     uint32_t fullw[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) {
@@ -1492,7 +1508,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         return f;
     };
     uint32_t nfull_run = 0, kpair = 0;   // rows of the current group known full; pair counter
-    unsigned long long st_quads = 0, st_pairs = 0;
+    if (threadIdx.x == 0) sh.st_quads = sh.st_pairs = 0;
     if (g < a.ngroups) {
         tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
         if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
@@ -1596,7 +1612,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
             if (is_full(base)) end = pos;
         }
-        if (a.scan_stats) st_pairs += (threadIdx.x == 0) ? 1u : 0u;
+        if (a.scan_stats && threadIdx.x == 0) sh.st_pairs++;
         // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
         // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
         // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
@@ -1633,7 +1649,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                        \
                 const uint32_t pu = npos2 + 8u * L * u;                                                 \
                 const bool ld = nrow < rows && pu < nend2;                                              \
-                if (a.scan_stats) st_quads += ld ? 1u : 0u;                                             \
+                if (a.scan_stats && ld) atomicAdd(&sh.st_quads, 1u);                                    \
                 NXT[u] = tile_load(gr, gcol, ld ? 2u * pu : kTileOOB);                                  \
             }                                                                                           \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
@@ -1737,10 +1753,11 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         kpair++;
     }
     if (a.scan_stats) {   // diagnostics: quads loaded and pairs staged by this workgroup
-        unsigned long long x = st_quads;
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-        if (lane == 0 && x) atomicAdd(&a.scan_stats[0], x);
-        if (threadIdx.x == 0) atomicAdd(&a.scan_stats[1], st_pairs);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicAdd(&a.scan_stats[0], (unsigned long long)sh.st_quads);
+            atomicAdd(&a.scan_stats[1], (unsigned long long)sh.st_pairs);
+        }
     }
     MCMC_PHASE(a, 3);
     if (timing && threadIdx.x == 0) {   // shader-clock cycles per phase kind, wave 0
@@ -1848,13 +1865,13 @@ hipError_t allow_lds_blocked(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_blocked_kernel<NW>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-template <int NW, bool RES, bool REF = false>
+template <int NW, bool RES, bool REF = false, bool EX = false>
 void launch_tiled(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
-    sweep_tiled_kernel<NW, RES, REF><<<g, b, lds, s>>>(a);
+    sweep_tiled_kernel<NW, RES, REF, EX><<<g, b, lds, s>>>(a);
 }
-template <int NW, bool RES, bool REF = false>
+template <int NW, bool RES, bool REF = false, bool EX = false>
 hipError_t allow_lds_tiled(size_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES, REF>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES, REF, EX>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 template <int NW, bool LDSC>
@@ -2154,7 +2171,7 @@ int ensure_tail_buffers(mcmc_ctx* c) {
     MCMC_HIP_TRY(hipMalloc(&c->vflags, 2 * n));
     MCMC_HIP_TRY(hipMalloc(&c->tc_list, sizeof(uint32_t) * n));
     MCMC_HIP_TRY(hipMalloc(&c->tc_len, sizeof(uint32_t)));
-    MCMC_HIP_TRY(hipMalloc(&c->tc_colorIdx, sizeof(uint32_t) * 256));
+    MCMC_HIP_TRY(hipMalloc(&c->tc_colorIdx, sizeof(uint32_t) * std::max<uint32_t>(c->p.nCol, 256u)));
     MCMC_HIP_TRY(hipMalloc(&c->tc_count, sizeof(unsigned long long)));
     MCMC_HIP_TRY(hipMemsetAsync(c->vflags, 0, 2 * n, c->stream));
     return MCMC_OK;
@@ -2199,14 +2216,14 @@ int run_tailcut_ref(mcmc_ctx* c, const DevState& h, uint64_t cc, uint64_t* final
     MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ordered.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice,
                                 c->stream));
     const TailView tv = tail_view(c);
-    rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, true);
+    rc = tail_count(tv, C, 1u, c->vflags, c->tc_count, c->stream, true);
     if (rc) return rc;
     while (cc > 0 && *passes < c->tailcut_max) {
         rc = tail_select(c->vflags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
         if (rc) return rc;
-        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, true, cc);
+        rc = tail_repair(tv, C, 1u, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, true, cc);
         if (rc) return rc;
-        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, true);
+        rc = tail_count(tv, C, 1u, c->vflags, c->tc_count, c->stream, true);
         if (rc) return rc;
         unsigned long long hv = 0;
         MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
@@ -2231,11 +2248,12 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
     std::vector<size_t> colorIdx(nCol);
     for (uint32_t i = 0; i < nCol; i++) colorIdx[i] = i;
     if (c->z > 0) {
-        std::vector<uint8_t> hc(n);
+        std::vector<uint8_t> hc((size_t)n * c->cbytes);
         int rc = download_colors(c, C, hc.data());
         if (rc) return rc;
         std::vector<size_t> histBins(nCol, 0);
-        for (uint8_t v : hc) histBins[v]++;
+        for (uint32_t v = 0; v < n; v++)
+            histBins[c->cbytes == 2 ? reinterpret_cast<const uint16_t*>(hc.data())[v] : hc[v]]++;
         std::sort(colorIdx.begin(), colorIdx.end(), [&](int i, int j) { return histBins[i] < histBins[j]; });
     }
     if (*finalViol == 0) return MCMC_OK;
@@ -2249,9 +2267,9 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
     while (cviol > 0 && *passes < c->tailcut_max) {
         int rc = tail_select(flags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
         if (rc) return rc;
-        rc = tail_repair(tv, C, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, false, ~0ull);
+        rc = tail_repair(tv, C, c->cbytes, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, false, ~0ull);
         if (rc) return rc;
-        rc = tail_count(tv, C, c->vflags, c->tc_count, c->stream, false);   // :308
+        rc = tail_count(tv, C, c->cbytes, c->vflags, c->tc_count, c->stream, false);   // :308
         if (rc) return rc;
         unsigned long long hv = 0;
         MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
@@ -2496,6 +2514,20 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 c->sweep = tab[wi];
                 ea = wi == 0 ? allow_lds_tiled<1, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, false, true>(c->lds)
                    : wi == 2 ? allow_lds_tiled<4, false, true>(c->lds) : allow_lds_tiled<8, false, true>(c->lds);
+            }
+        } else if (c->early) {   // the early-exit instantiations
+            if (resident) {
+                static const SweepLaunch tab[4] = {launch_tiled<1, true, false, true>, launch_tiled<2, true, false, true>,
+                                                   launch_tiled<4, true, false, true>, launch_tiled<8, true, false, true>};
+                c->sweep = tab[wi];
+                ea = wi == 0 ? allow_lds_tiled<1, true, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, true, false, true>(c->lds)
+                   : wi == 2 ? allow_lds_tiled<4, true, false, true>(c->lds) : allow_lds_tiled<8, true, false, true>(c->lds);
+            } else {
+                static const SweepLaunch tab[4] = {launch_tiled<1, false, false, true>, launch_tiled<2, false, false, true>,
+                                                   launch_tiled<4, false, false, true>, launch_tiled<8, false, false, true>};
+                c->sweep = tab[wi];
+                ea = wi == 0 ? allow_lds_tiled<1, false, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, false, false, true>(c->lds)
+                   : wi == 2 ? allow_lds_tiled<4, false, false, true>(c->lds) : allow_lds_tiled<8, false, false, true>(c->lds);
             }
         } else if (resident) {
             static const SweepLaunch tab[4] = {launch_tiled<1, true>, launch_tiled<2, true>, launch_tiled<4, true>,
@@ -2799,8 +2831,8 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
 // [n] host bytes, the per-vertex flags.
 int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
     if (!c || !count) return fail(MCMC_E_ARG, "NULL argument");
-    if (c->part || c->wide || c->v_begin != 0 || c->v_end != c->n)
-        return fail(MCMC_E_STATE, "violation recount: whole-graph contexts with uint8 colours");
+    if (c->part || c->v_begin != 0 || c->v_end != c->n)
+        return fail(MCMC_E_STATE, "violation recount: whole-graph contexts");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     int rc = ensure_tail_buffers(c);
     if (rc) return rc;
@@ -2811,7 +2843,7 @@ int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
         if (rc) return rc;
         which = h.t & 1u;
     }
-    rc = tail_count(tail_view(c), c->colors[which], c->vflags, c->tc_count, c->stream, false);
+    rc = tail_count(tail_view(c), c->colors[which], c->cbytes, c->vflags, c->tc_count, c->stream, false);
     if (rc) return rc;
     unsigned long long hv = 0;
     MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
@@ -2855,7 +2887,6 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (c->part || c->v_begin != 0 || c->v_end != c->n)
         return fail(MCMC_E_STATE, "tail cutting runs on whole-graph contexts (mcmc_run)");
-    if (c->wide) return fail(MCMC_E_ARG, "tail cutting: nCol <= 256 (uint8 replicas) only");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (max_passes) {
         int rc = ensure_tail_buffers(c);

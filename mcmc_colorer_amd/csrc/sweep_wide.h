@@ -552,6 +552,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
             viol[j] = a.wflag[l];
             cv[j] = C[(a.v_begin + l)];
             if (a.taboo != nullptr) tab[j] = a.taboo[l];
+            if (a.vflags) a.vflags[(size_t)(t & 1u) * nloc + l] = (uint8_t)viol[j];   // Cviols of C_t (tail cut)
         }
     }
     // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139); the

@@ -63,8 +63,9 @@ __device__ __forceinline__ void for_neighbours(const TailView& g, uint32_t l, ui
 // EDGES = false: flag = any same-colour neighbour (violation_count), count = flagged vertices.
 // EDGES = true: per-vertex same-colour neighbours with a larger id (conflictCounter kernel),
 // flag = nonzero, count = their sum (calcConflicts).
-template <bool EDGES>
-__global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const uint8_t* __restrict__ C,
+// CT: the replica's colour type (uint8_t; uint16_t for the wide sweep's nCol > 256).
+template <bool EDGES, typename CT>
+__global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const CT* __restrict__ C,
                                                          uint8_t* __restrict__ flags,
                                                          unsigned long long* __restrict__ count) {
     const uint32_t lane = threadIdx.x & 63;
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const uint8
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     unsigned long long wave_total = 0;
     for (uint32_t l = gw; l < g.n; l += nw) {
-        const uint8_t cv = C[l];
+        const CT cv = C[l];
         uint32_t hits = 0;
         if (EDGES) {
             for_neighbours<true>(g, l, lane, 64u, [&](uint32_t w) { hits += (C[w] == cv && w > l) ? 1u : 0u; });
@@ -89,39 +90,51 @@ __global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const uint8
 }
 
 constexpr uint32_t kRepairThreads = 1024;
-constexpr int kMaskWords = 8;   // nCol <= 256 (uint8 colours)
+constexpr int kMaskWords = 8;            // nCol <= 256 (uint8 colours): masks in registers
+constexpr uint32_t kWideMaskWords = 2048;   // nCol <= 65535 (uint16 colours): the mask in LDS
 
 // REF = false: the corrected CPU rule (first free colour of colorIdx, unchanged when none is free).
 // REF = true: tailCutting (coloringMCMC_utils.cu:73-101): an own colour that is free (or >= nCol)
 // stays; otherwise the first free colour of orderedIndex, the last one when none is free. At most
-// `limit` listed vertices (resolved < conflictCounter).
-template <bool REF>
-__global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g, uint8_t* C,
+// `limit` listed vertices (resolved < conflictCounter). CT = uint16_t: the wide sweep's replicas;
+// the occupancy mask (nCol bits) is built in LDS.
+template <bool REF, typename CT>
+__global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g, CT* C,
                                                                      const uint32_t* __restrict__ list,
                                                                      const uint32_t* __restrict__ list_len,
                                                                      const uint32_t* __restrict__ colorIdx,
                                                                      uint32_t nCol, unsigned long long limit) {
-    __shared__ uint32_t mask[kMaskWords];
+    constexpr bool WIDE = sizeof(CT) == 2;
+    constexpr uint32_t MW = WIDE ? kWideMaskWords : (uint32_t)kMaskWords;
+    __shared__ uint32_t mask[MW];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t L = (uint32_t)min((unsigned long long)*list_len, limit);
+    const uint32_t words = WIDE ? (nCol + 31u) >> 5 : (uint32_t)kMaskWords;
     // colours of this pass are read with volatile (L1-bypassing) loads: vertex k must see the
     // colour thread 0 stored for an earlier vertex of the list
-    const volatile uint8_t* Cv = C;
+    const volatile CT* Cv = C;
     for (uint32_t k = 0; k < L; k++) {
         const uint32_t i = list[k];
-        if (tid < kMaskWords) mask[tid] = 0;
+        for (uint32_t w = tid; w < words; w += blockDim.x) mask[w] = 0;
         __syncthreads();
-        uint32_t m[kMaskWords] = {};
-        for_neighbours(g, i, tid, kRepairThreads, [&](uint32_t w) {
-            const uint32_t c = Cv[w];
+        if (WIDE) {
+            for_neighbours(g, i, tid, kRepairThreads, [&](uint32_t w) {
+                const uint32_t c = Cv[w];
+                if (c < nCol) atomicOr(&mask[c >> 5], 1u << (c & 31));
+            });
+        } else {
+            uint32_t m[kMaskWords] = {};
+            for_neighbours(g, i, tid, kRepairThreads, [&](uint32_t w) {
+                const uint32_t c = Cv[w];
 #pragma unroll
-            for (int q = 0; q < kMaskWords; q++) m[q] |= (c >> 5) == (uint32_t)q ? 1u << (c & 31) : 0u;
-        });
+                for (int q = 0; q < kMaskWords; q++) m[q] |= (c >> 5) == (uint32_t)q ? 1u << (c & 31) : 0u;
+            });
 #pragma unroll
-        for (int q = 0; q < kMaskWords; q++) {
-            uint32_t x = m[q];
-            for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
-            if (lane == 0 && x) atomicOr(&mask[q], x);
+            for (int q = 0; q < kMaskWords; q++) {
+                uint32_t x = m[q];
+                for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
+                if (lane == 0 && x) atomicOr(&mask[q], x);
+            }
         }
         __syncthreads();
         if (tid == 0) {
@@ -129,11 +142,11 @@ __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g,
             if (REF) {
                 uint32_t c = Cv[i];
                 for (uint32_t j = 0; used(c) && j < nCol; j++) c = colorIdx[j];
-                C[i] = (uint8_t)c;
+                C[i] = (CT)c;
             } else {
                 for (uint32_t j = 0; j < nCol; j++) {      // first free colour in colorIdx order
                     const uint32_t c = colorIdx[j];
-                    if (!used(c)) { C[i] = (uint8_t)c; break; }
+                    if (!used(c)) { C[i] = (CT)c; break; }
                 }
             }
             __threadfence();
@@ -144,13 +157,20 @@ __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g,
 
 }  // namespace
 
-int tail_count(const TailView& g, const uint8_t* C, uint8_t* flags, unsigned long long* count, hipStream_t s,
-               bool edges) {
+int tail_count(const TailView& g, const void* C, uint32_t cbytes, uint8_t* flags, unsigned long long* count,
+               hipStream_t s, bool edges) {
     MCMC_HIP_TRY(hipMemsetAsync(count, 0, sizeof(unsigned long long), s));
     if (g.n == 0) return MCMC_OK;
     const uint32_t blocks = std::min<uint32_t>((g.n + 3) / 4, 8192u);   // 4 rows (waves) per block
-    if (edges) tail_count_kernel<true><<<blocks, 256, 0, s>>>(g, C, flags, count);
-    else tail_count_kernel<false><<<blocks, 256, 0, s>>>(g, C, flags, count);
+    if (cbytes == 2) {
+        const uint16_t* c = static_cast<const uint16_t*>(C);
+        if (edges) tail_count_kernel<true, uint16_t><<<blocks, 256, 0, s>>>(g, c, flags, count);
+        else tail_count_kernel<false, uint16_t><<<blocks, 256, 0, s>>>(g, c, flags, count);
+    } else {
+        const uint8_t* c = static_cast<const uint8_t*>(C);
+        if (edges) tail_count_kernel<true, uint8_t><<<blocks, 256, 0, s>>>(g, c, flags, count);
+        else tail_count_kernel<false, uint8_t><<<blocks, 256, 0, s>>>(g, c, flags, count);
+    }
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }
@@ -170,11 +190,19 @@ int tail_select(const uint8_t* flags, uint32_t n, uint32_t* list, uint32_t* list
     return MCMC_OK;
 }
 
-int tail_repair(const TailView& g, uint8_t* C, const uint32_t* list, const uint32_t* list_len,
+int tail_repair(const TailView& g, void* C, uint32_t cbytes, const uint32_t* list, const uint32_t* list_len,
                 const uint32_t* colorIdx, uint32_t nCol, hipStream_t s, bool ref, unsigned long long limit) {
-    if (nCol > 32u * kMaskWords) return MCMC_E_ARG;
-    if (ref) tail_repair_kernel<true><<<1, kRepairThreads, 0, s>>>(g, C, list, list_len, colorIdx, nCol, limit);
-    else tail_repair_kernel<false><<<1, kRepairThreads, 0, s>>>(g, C, list, list_len, colorIdx, nCol, limit);
+    if (cbytes == 2) {
+        if (nCol > 32u * kWideMaskWords) return MCMC_E_ARG;
+        uint16_t* c = static_cast<uint16_t*>(C);
+        if (ref) tail_repair_kernel<true, uint16_t><<<1, kRepairThreads, 0, s>>>(g, c, list, list_len, colorIdx, nCol, limit);
+        else tail_repair_kernel<false, uint16_t><<<1, kRepairThreads, 0, s>>>(g, c, list, list_len, colorIdx, nCol, limit);
+    } else {
+        if (nCol > 32u * kMaskWords) return MCMC_E_ARG;
+        uint8_t* c = static_cast<uint8_t*>(C);
+        if (ref) tail_repair_kernel<true, uint8_t><<<1, kRepairThreads, 0, s>>>(g, c, list, list_len, colorIdx, nCol, limit);
+        else tail_repair_kernel<false, uint8_t><<<1, kRepairThreads, 0, s>>>(g, c, list, list_len, colorIdx, nCol, limit);
+    }
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }

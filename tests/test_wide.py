@@ -254,3 +254,36 @@ def test_wide_partitioned_lockstep(M, monkeypatch, world, scan):
             assert b.trajectory().tolist() == r.traj.tolist()
         for b in ranks:
             b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph,ncol,forced", [("simulate", 260, False), ("simulate", 300, False),
+                                               ("rmat", 60, True), ("rmat", 100, True), ("simulate", 40, True)])
+def test_wide_tailcut_repair(M, monkeypatch, graph, ncol, forced):
+    """The corrected tail cut (coloringMCMC_CPU.cpp:272-311, k++) on the wide sweep's uint16
+    replicas (--tailcut --tailcutRepair with nCol > 256, configs[4]'s shape on R-MAT graphs):
+    colouring, repaired Cviol, passes and trajectory equal the oracle's."""
+    if forced:
+        monkeypatch.setenv("MCMC_GATHER", "wide")
+    if graph == "rmat":
+        off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 3)
+        draws = 0
+    else:
+        O.srand(1)
+        off, idx = O.setup_rnd2(1500, 0.2)
+        draws = 1500 * 1501 // 2
+    n = len(off) - 1
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, maxRip=60, tailcut=True, tailcutRepair=1000)
+    col = M.ColoringMCMC(g, M.GPURand(n, 1, M.GlibcRand(1, draws)), params)
+    st = col.run(0)
+    O.srand(1)
+    if draws:
+        O.setup_rnd2(1500, 0.2)
+    r = O.mcmc_run(off, idx, ncol, 1, maxRip=60, tailcut=True, tailcutRepair=True)
+    assert col.info()["variant"] == "wide"
+    assert r.res.tailcutPasses >= 1 or ncol == 40
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, st.finalViol, st.tailcutPasses, st.glibcDraws) == (
+        r.res.iter, r.res.finalViol, r.res.tailcutPasses, r.res.glibcDraws)
