@@ -847,9 +847,9 @@ struct TailShared {
     uint32_t wg_viol, wg_ev, wg_last, t, E, err;
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
-    uint32_t dn;          // tiled drain: rows listed
+    uint32_t dn[2];       // tiled sparse pairs / drain: rows listed (by pair-buffer parity)
     uint32_t st_quads, st_pairs;   // diagnostics (scan_stats): quads loaded, pairs staged by the workgroup
-    uint16_t dlist[256];  // tiled drain: the group's rows whose masks are not full yet
+    uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
 };
 
@@ -1375,23 +1375,33 @@ __device__ __forceinline__ void drain_quad(const uint8_t* __restrict__ cb, const
     for (int e = 0; e < 8; e++) set_color_bit<NW>(m, c[e]);
 }
 
+// The group's rows whose masks are not full yet, into sh.dlist (any order); *count = sh.dn[par]
+// (zeroed at the top of the previous pair). All threads; a barrier follows.
+template <int NW>
+__device__ __forceinline__ void tile_open_rows(uint32_t rows, const uint32_t* smask, TailShared& sh,
+                                               const uint32_t* fullw, uint32_t par) {
+    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
+        bool f = true;
+#pragma unroll
+        for (int i = 0; i < NW; i++) f = f && ((smask[r * NW + i] & fullw[i]) == fullw[i]);
+        if (!f) {
+            const uint32_t k = atomicAdd(&sh.dn[par], 1u);
+            if (k < 256u) sh.dlist[k] = (uint16_t)r;
+        }
+    }
+    __syncthreads();
+}
+
 template <int NW>
 __device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g, uint32_t b,
-                                        uint32_t rows, uint32_t* smask, TailShared& sh, const uint32_t* fullw,
-                                        int lane) {
+                                           uint32_t na, uint32_t* smask, TailShared& sh, const uint32_t* fullw,
+                                           int lane) {
     auto row_full = [&](uint32_t r) -> bool {
         bool f = true;
 #pragma unroll
         for (int i = 0; i < NW; i++) f = f && ((smask[r * NW + i] & fullw[i]) == fullw[i]);
         return f;
     };
-    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x)
-        if (!row_full(r)) {
-            const uint32_t k = atomicAdd(&sh.dn, 1u);
-            if (k < 256u) sh.dlist[k] = (uint16_t)r;
-        }
-    __syncthreads();
-    const uint32_t na = min(sh.dn, 256u);
     const uint32_t R = a.grp_rows, TS = tseg_stride(R);
     const uint32_t team = threadIdx.x >> 2, tl = threadIdx.x & 3u, nteams = blockDim.x >> 2;
     const uint16_t* __restrict__ gids = a.tcol + a.gbase[g];
@@ -1491,6 +1501,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     if (threadIdx.x == 0) {
         sh.cursor[0] = nwaves * nsub;
         sh.nfull[0] = sh.nfull[1] = sh.nfull[2] = 0;
+        sh.dn[0] = sh.dn[1] = 0;
     }
     // Early exit (not REF: its scan counts arcs): a row whose mask holds all nCol colours is done --
     // its later segments are skipped, and once every row of a group is done its remaining pairs are.
@@ -1552,16 +1563,24 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // early exit: rows that filled up in the previous pair (slot (k-1) % 3 is final: its pair
         // ended at the barrier); slot (k+1) % 3 was last read at the top of pair k-1 and is next
         // counted into in pair k+1, after this pair's barrier
-        bool allfull = false, drain = false;
+        bool allfull = false, drain = false, sparse = false;
         if (EXIT) {
             nfull_run = (b == 0) ? 0u : nfull_run + sh.nfull[(kpair + 2u) % 3u];
             allfull = b > 0 && nfull_run >= rows;
+            const uint32_t nopen = rows - min(nfull_run, rows);
             // few rows left: they finish every remaining block here (tile_drain), no more pairs
-            drain = !allfull && b > 0 && rows - nfull_run <= a.drain_rows && b + 1 < nb;
+            drain = !allfull && b > 0 && nopen <= a.drain_rows && b + 1 < nb;
+            // a sparse pair: only the listed open rows are claimed (not every row of the group)
+            sparse = !allfull && !drain && b > 0 && nopen <= 256u;
             if (threadIdx.x == 0) {
                 sh.nfull[(kpair + 1u) % 3u] = 0;
-                if (b == 0) sh.dn = 0;   // the drain list of this group (its last use: an earlier group's pair)
+                sh.dn[buf ^ 1u] = 0;   // the next pair's list counter (its last use: the previous pair)
             }
+        }
+        uint32_t nlist = 0;
+        if (drain || sparse) {
+            tile_open_rows<NW>(rows, smask, sh, fullw, buf);
+            nlist = min(sh.dn[buf], 256u);
         }
         const uint32_t kslot = kpair % 3u;
         // the group's last pair: its last block, every row already full, or the drain
@@ -1607,7 +1626,25 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         bool rowfull = false;
 #pragma unroll
         for (int i = 0; i < NW; i++) base[i] = 0;
-        if (EXIT && b > 0 && row < rows) {
+        if (sparse) {
+            // sparse pair: the open rows of the list, the first nwaves * nsub of them assigned to the
+            // sub-groups (their first quads reloaded: the prefetched ones are the static rows'),
+            // the rest claimed (the cursor starts past them)
+            const uint32_t s = wid * nsub + sub;
+            row = s < nlist ? (uint32_t)sh.dlist[s] : rows;
+            if (row < rows) {
+                const uint32_t sraw = sseg[row];
+                pos = (sraw & kTsegPos) + 8u * li;
+                end = sseg[row + 1] & kTsegPos;
+#pragma unroll
+                for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
+            }
+#pragma unroll
+            for (int u = 0; u < kTileU; u++) {
+                const uint32_t pu = pos + 8u * L * u;
+                v[u] = tile_load(gr, gcol, (row < rows && pu < end) ? 2u * pu : kTileOOB);
+            }
+        } else if (EXIT && b > 0 && row < rows) {
 #pragma unroll
             for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
             if (is_full(base)) end = pos;
@@ -1630,6 +1667,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
             if (fin) {                                                                                  \
                 nrow = got;                                                                             \
+                if (sparse) nrow = (got < nlist) ? (uint32_t)sh.dlist[got] : rows;                      \
                 if (nrow < rows) {                                                                      \
                     const uint32_t sraw = sseg[nrow];                                                   \
                     npos2 = (sraw & kTsegPos) + 8u * li;                                                \
@@ -1700,7 +1738,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     } while (0)
         uint4 v1[kTileU];
         if (drain) {
-            tile_drain<NW>(a, C, g, b, rows, smask, sh, fullw, lane);
+            tile_drain<NW>(a, C, g, b, nlist, smask, sh, fullw, lane);
         } else if (!allfull && __ballot(row < rows)) {
             for (;;) {
                 bool c0, c1;
@@ -1930,7 +1968,7 @@ struct mcmc_ctx {
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
     int early = 1;              // tiled: early-exit scan (MCMC_FULL_SCAN=1: every arc)
-    uint32_t drain_rows = 192;  // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256)
+    uint32_t drain_rows = 32;   // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256; C3: 32 best)
     unsigned long long* scan_stats = nullptr;   // mcmc_set_scan_stats: [quads loaded, pairs staged]
     bool scan_stats_on = false;
     uint32_t world = 1, rank = 0;
