@@ -461,6 +461,17 @@ def main() -> int:
     }
     if conv is not None:
         out["convergence"] = conv
+    if dist is None and a.config == "c5" and not a.no_convergence:
+        # the wide sweep WITH violators in every timed sweep (nCol = maxDeg / 4 does not converge):
+        # the reference loop capped at 20 sweeps, device time per sweep and the per-sweep Cviol
+        nc4 = max(257, a.ncol // 4)
+        cv = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=nc4, maxRip=20))
+        sv = cv.run(0)
+        out["violators"] = {"nCol": nc4, "sweeps_run": int(sv.sweepsRun), "loop_ms": sv.loopMs,
+                            "ms_per_sweep": sv.loopMs / max(1, sv.sweepsRun),
+                            "value": g.nNodes * sv.sweepsRun / (sv.loopMs * 1e-3),
+                            "trajectory": [int(x) for x in cv.trajectory()]}
+        cv.close()
     if scan is not None:
         out["scan"] = scan
     # CPU and refstruct legs: on the benchmarked graph for c2; for c3 (no CSR can exist: 400 GB) on
