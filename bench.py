@@ -384,28 +384,33 @@ def main() -> int:
     variant = info["variant"]
     scan = None
     b_alg = b_fmt
-    if dist is None and not ref and variant == "tiled":
+    if not ref and variant == "tiled":
         # The tiled sweep stops scanning a row once its occupancy mask holds every colour (the
         # result cannot change; MCMC_FULL_SCAN=1 scans every arc): the bytes one launch moves are
         # counted on the device (mcmc_set_scan_stats, 3 sweeps outside the timed region) -- id quads,
         # the staged (group, block) pairs' table rows and colour slices, own colour read + write
         q, pr, tot2, ker2 = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
-        check(lib().mcmc_set_scan_stats(col._ctx, 1))
-        check(lib().mcmc_bench_sweeps(col._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
-        check(lib().mcmc_get_scan_stats(col._ctx, ctypes.byref(q), ctypes.byref(pr)))
-        check(lib().mcmc_set_scan_stats(col._ctx, 0))
+        sctx = col._ctx if dist is None else drv._ctx
+        check(lib().mcmc_set_scan_stats(sctx, 1))
+        if dist is None:
+            check(lib().mcmc_bench_sweeps(col._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
+        else:
+            check(lib().mcmc_part_run(arr, 1, 3, ctypes.byref(st)))
+        check(lib().mcmc_get_scan_stats(sctx, ctypes.byref(q), ctypes.byref(pr)))
+        check(lib().mcmc_set_scan_stats(sctx, 0))
         quads, pairs = q.value / 3.0, pr.value / 3.0
         R = info["grp_rows"]
         table = 4 * ((R + 4) & ~3)
         slice_b = 0 if info["resident"] else min(65536, ((g.nNodes + 15) // 16) * 16)
-        b_alg = 16 * quads + pairs * (table + slice_b) + 2 * g.nNodes
+        nloc = g.nNodes if dist is None else int(bounds[rank + 1] - bounds[rank])
+        b_alg = 16 * quads + pairs * (table + slice_b) + 2 * nloc
         scan = {"early_exit": info.get("early", True), "quads_per_sweep": quads, "pairs_per_sweep": pairs,
                 "id_bytes": 16 * quads, "table_bytes": pairs * table, "slice_bytes": pairs * slice_b,
                 "layout_bytes_full_scan": b_fmt,
                 "note": "exact early exit: a row's scan stops once its mask holds all nCol colours "
                         "(count_free_colors cannot change); a group skips its remaining column blocks once "
                         "every row is full. Bit-identical results (tests/test_gpu_parity.py)."}
-        if not a.no_full_scan:
+        if dist is None and not a.no_full_scan:
             # the same sweep scanning every arc (MCMC_FULL_SCAN=1): the layout-bound reference point
             os.environ["MCMC_FULL_SCAN"] = "1"
             cf = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), params)
