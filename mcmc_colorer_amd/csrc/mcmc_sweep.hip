@@ -641,31 +641,22 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
 }
 
 // ----------------------------------------------------------------------------------------------
-// Per-vertex evaluation of one tile, after the occupancy masks are built: lane j < cnt holds the
-// mask of vertex v = v_begin + l0 + j in `acc`. viol, fill_p, u_v, the CDF walk, the writes, the
-// Cviol ballot and the overflow-event append.
+// evaluate_core: the caller has loaded lane j's own colour cv and taboo counter tab and computed
+// x = the minstd state after draw v + 1 of this sweep (x_t 16807^(v+1) mod 2^31-1).
 template <int NW>
-__device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* __restrict__ st,
-                                              const uint8_t* __restrict__ Cown, uint8_t* __restrict__ Cs,
-                                              uint32_t x_t, uint32_t l0, uint32_t cnt, const uint32_t (&acc)[NW],
-                                              int lane, uint32_t& ev_flag, uint8_t* __restrict__ vf) {
+__device__ __forceinline__ uint32_t evaluate_core(const SweepArgs& a, DevState* __restrict__ st,
+                                                  uint8_t* __restrict__ Cs, uint32_t l0, uint32_t cnt,
+                                                  const uint32_t (&acc)[NW], int lane, uint32_t& ev_flag,
+                                                  uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x) {
     const bool valid = (uint32_t)lane < cnt;
     const uint32_t l = l0 + lane;
     const uint32_t v = a.v_begin + l;
-    const uint32_t cv = valid ? (uint32_t)Cown[v] : 0u;
     uint32_t pop = 0;
 #pragma unroll
     for (int i = 0; i < NW; i++) pop += __popc(acc[i]);
     const bool viol = valid && get_color_bit<NW>(acc, cv);
     const uint32_t Zvcomp = a.nCol - pop;
     if (vf != nullptr && valid) vf[l] = viol;   // Cviols of C_t (coloringMCMC_CPU.cpp:152)
-
-    uint32_t tab = 0;
-    if (a.taboo != nullptr && valid) tab = a.taboo[l];
-
-    // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
-    const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
-    const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
     const float u = minstd_canonical(x);
 
     // fill_p cases: (ii) viol with free colours -> occupied eps, free pf;
@@ -725,6 +716,24 @@ __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* 
         }
     }
     return nviol;
+}
+
+// Per-vertex evaluation of one tile, after the occupancy masks are built: lane j < cnt holds the
+// mask of vertex v = v_begin + l0 + j in `acc`. viol, fill_p, u_v, the CDF walk, the writes, the
+// Cviol ballot and the overflow-event append.
+template <int NW>
+__device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* __restrict__ st,
+                                              const uint8_t* __restrict__ Cown, uint8_t* __restrict__ Cs,
+                                              uint32_t x_t, uint32_t l0, uint32_t cnt, const uint32_t (&acc)[NW],
+                                              int lane, uint32_t& ev_flag, uint8_t* __restrict__ vf) {
+    const bool valid = (uint32_t)lane < cnt;
+    const uint32_t l = l0 + lane;
+    const uint32_t cv = valid ? (uint32_t)Cown[a.v_begin + l] : 0u;
+    const uint32_t tab = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;
+    // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
+    const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
+    const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
+    return evaluate_core<NW>(a, st, Cs, l0, cnt, acc, lane, ev_flag, vf, cv, tab, x);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1451,7 +1460,9 @@ __device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __
 // REF: the reference-GPU-semantics sweep on the same pipeline -- the scan also counts the rows'
 // same-colour arcs (own colours from the replica, or streamed per group into LDS), the evaluation
 // is evaluate_ref_tile, the arrival carries the count (sweep_tail_ref).
-template <int NW, bool RES, bool REF, bool EX>
+// DG: the diagnostics instantiation (scan_stats counters, MCMC_PHASE_DUMP cycle accounting,
+// MCMC_DEBUG_MAX_PAIRS), kept out of the timed kernels' registers.
+template <int NW, bool RES, bool REF, bool EX, bool DG = false>
 __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
     __shared__ TailShared sh;
@@ -1492,10 +1503,18 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t nbytes16 = (a.n + 15u) & ~15u;
     const uint32_t lds0 = lds_addr(lbase), seg_lds0 = lds_addr(seg_base);
     uint32_t wave_viol = 0, wave_ev = 0;
-    const bool timing = a.phase_ts != nullptr;
+    const bool timing = DG && a.phase_ts != nullptr;
     uint64_t cyc_wait = 0, cyc_scan = 0, cyc_eval = 0, tmark = 0;
 
     uint32_t g = blockIdx.x, b = 0, buf = 0;
+    // u_v (evaluation): xg = x_t 16807^(v_begin + g R + 64 wid + 1), the draw of this wave's first
+    // evaluation row in group g; xsg advances it by one group of this workgroup, xsk by one tile
+    uint32_t xg = 0, xsg = 0, xsk = 0;
+    if (!REF) {
+        xg = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + (uint64_t)g * R + 64u * wid + 1u));
+        xsg = minstd_pow_tab((uint64_t)gridDim.x * R);
+        xsk = minstd_pow_tab(64u * (uint64_t)nwaves);
+    }
     const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
     for (uint32_t i = threadIdx.x; i < R * NW; i += blockDim.x) smask[i] = 0;
     if (threadIdx.x == 0) {
@@ -1531,9 +1550,11 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     __amdgpu_buffer_rsrc_t gr = tile_group_rsrc(a, gclamp);
     const uint16_t* __restrict__ gcol = a.tcol + a.gbase[gclamp];
     uint4 v[kTileU];
+    uint32_t nq0 = 0;   // scan_stats: quads of the first prefetch (counted after the barrier below)
 #pragma unroll
     for (int u = 0; u < kTileU; u++) {
         const uint32_t pu = fpos + 8u * L * u;
+        nq0 += pu < fend ? 1u : 0u;
         v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the staging below the first quads
@@ -1554,6 +1575,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // DMA + staging landed
     MCMC_PHASE(a, 1);
+    if ((DG && a.scan_stats) && nq0) atomicAdd(&sh.st_quads, nq0);
 
     while (g < a.ngroups) {
         if (timing) tmark = __builtin_readcyclecounter();
@@ -1584,7 +1606,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         }
         const uint32_t kslot = kpair % 3u;
         // the group's last pair: its last block, every row already full, or the drain
-        const bool last = (b + 1 == nb) || allfull || drain || (a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
+        const bool last = (b + 1 == nb) || allfull || drain || (DG && a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
         // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
         if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
@@ -1598,6 +1620,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         const uint32_t pg = nvalid ? ng : g, pb = nvalid ? nbn : b;
         uint32_t npos, nend, npads;
         tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend, npads);
+        npos += 8u * li;
         const __amdgpu_buffer_rsrc_t ngr = tile_group_rsrc(a, pg);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
         const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + buf * SB;
@@ -1642,6 +1665,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
 #pragma unroll
             for (int u = 0; u < kTileU; u++) {
                 const uint32_t pu = pos + 8u * L * u;
+                if ((DG && a.scan_stats) && row < rows && pu < end) atomicAdd(&sh.st_quads, 1u);
                 v[u] = tile_load(gr, gcol, (row < rows && pu < end) ? 2u * pu : kTileOOB);
             }
         } else if (EXIT && b > 0 && row < rows) {
@@ -1649,7 +1673,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
             if (is_full(base)) end = pos;
         }
-        if (a.scan_stats && threadIdx.x == 0) sh.st_pairs++;
+        if ((DG && a.scan_stats) && threadIdx.x == 0) sh.st_pairs++;
         // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
         // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
         // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
@@ -1687,7 +1711,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                        \
                 const uint32_t pu = npos2 + 8u * L * u;                                                 \
                 const bool ld = nrow < rows && pu < nend2;                                              \
-                if (a.scan_stats && ld) atomicAdd(&sh.st_quads, 1u);                                    \
+                if ((DG && a.scan_stats) && ld) atomicAdd(&sh.st_quads, 1u);                                    \
                 NXT[u] = tile_load(gr, gcol, ld ? 2u * pu : kTileOOB);                                  \
             }                                                                                           \
             _Pragma("unroll") for (int u = 0; u < kTileU; u++)                                          \
@@ -1753,16 +1777,17 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // the next pair's first quads: in flight across the boundary (and the evaluation)
         gr = ngr;
         gcol = ngcol;
-        fpos = npos + 8u * li;
+        fpos = npos;
         fend = nend;
         fpads = npads;
 #pragma unroll
         for (int u = 0; u < kTileU; u++) {
             const uint32_t pu = fpos + 8u * L * u;
+            if ((DG && a.scan_stats) && pu < fend) atomicAdd(&sh.st_quads, 1u);
             v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
         }
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_scan += t1 - tmark; tmark = t1; }
-        if (last) {
+        if (last && REF) {
             MCMC_LDS_BARRIER();   // every wave's mask ORs of the group are in
             // every wave evaluates a share of the group's rows and clears their masks for the next group
             for (uint32_t e0 = wid * min(q, 64u); e0 < rows; e0 += nwaves * min(q, 64u)) {
@@ -1774,23 +1799,63 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
                     if ((uint32_t)lane < cnt) smask[idx] = 0;
                 }
-                if (REF)
-                    evaluate_ref_tile<NW>(a, C, Cs, t, r0 + e0, cnt, acc, lane, p_lds, hist_lds);
-                else
-                    wave_viol += evaluate_tile<NW>(a, st, C, Cs, x_t, r0 + e0, cnt, acc,
-                                                   lane, wave_ev, vf);
+                evaluate_ref_tile<NW>(a, C, Cs, t, r0 + e0, cnt, acc, lane, p_lds, hist_lds);
+            }
+            if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
+        } else if (last) {
+            // Wave w evaluates rows w * 64 + k * 1024 (64-row tiles) and clears their masks for the
+            // next group. Each tile's own colours and taboo counters are loaded one tile ahead (the
+            // first before the barrier); u_v's minstd state comes from the wave's running base
+            // xg = x_t 16807^(v + 1) of its first row (no per-tile power).
+            const uint32_t tstride = nwaves * 64u;
+            const uint32_t lpow = kMinstdLanePow[lane];
+            uint32_t e0 = wid * 64u, cv = 0, tab = 0;
+            if (e0 + (uint32_t)lane < rows) {
+                cv = C[a.v_begin + r0 + e0 + lane];
+                if (a.taboo) tab = a.taboo[r0 + e0 + lane];
+            }
+            // every wave's mask ORs of the group are in, and this wave's DMA of the next pair has
+            // landed (the DMA precedes the 6 first-row loads; vmcnt(6) also covers the loads above):
+            // the pair's barrier after the evaluation then waits for LDS only, so the evaluation's
+            // stores and the next pair's first quads stay in flight across it
+            MCMC_PAIR_BARRIER();
+            uint32_t xk = xg;
+            for (; e0 < rows; e0 += tstride) {
+                const uint32_t cnt = min(64u, rows - e0);
+                const uint32_t e1 = e0 + tstride;
+                uint32_t cv1 = 0, tab1 = 0;
+                if (e1 + (uint32_t)lane < rows) {
+                    cv1 = C[a.v_begin + r0 + e1 + lane];
+                    if (a.taboo) tab1 = a.taboo[r0 + e1 + lane];
+                }
+                uint32_t acc[NW];
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    const uint32_t idx = (e0 + lane) * NW + i;
+                    acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
+                    if ((uint32_t)lane < cnt) smask[idx] = 0;
+                }
+                wave_viol += evaluate_core<NW>(a, st, Cs, r0 + e0, cnt, acc, lane, wave_ev, vf, cv, tab,
+                                               minstd_mulmod(xk, lpow));
+                cv = cv1;
+                tab = tab1;
+                xk = minstd_mulmod(xk, xsk);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         }
-        MCMC_PAIR_BARRIER();   // pair k+1's DMA landed everywhere; buffer k&1 and the masks are free
+        // pair k+1's DMA landed everywhere (the evaluation's barrier waited for it); buffer k&1 and
+        // the masks are free
+        if (!REF && last) MCMC_LDS_BARRIER();
+        else MCMC_PAIR_BARRIER();
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_wait += t1 - tmark; }
         if (REF && !RES && nbn == 0) gpar ^= 1u;   // the next pair starts a new group
+        if (!REF && last) xg = minstd_mulmod(xg, xsg);
         g = ng;
         b = nbn;
         buf ^= 1u;
         kpair++;
     }
-    if (a.scan_stats) {   // diagnostics: quads loaded and pairs staged by this workgroup
+    if ((DG && a.scan_stats)) {   // diagnostics: quads loaded and pairs staged by this workgroup
         __syncthreads();
         if (threadIdx.x == 0) {
             atomicAdd(&a.scan_stats[0], (unsigned long long)sh.st_quads);
@@ -1903,13 +1968,13 @@ hipError_t allow_lds_blocked(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_blocked_kernel<NW>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-template <int NW, bool RES, bool REF = false, bool EX = false>
+template <int NW, bool RES, bool REF = false, bool EX = false, bool DG = false>
 void launch_tiled(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
-    sweep_tiled_kernel<NW, RES, REF, EX><<<g, b, lds, s>>>(a);
+    sweep_tiled_kernel<NW, RES, REF, EX, DG><<<g, b, lds, s>>>(a);
 }
-template <int NW, bool RES, bool REF = false, bool EX = false>
+template <int NW, bool RES, bool REF = false, bool EX = false, bool DG = false>
 hipError_t allow_lds_tiled(size_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES, REF, EX>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&sweep_tiled_kernel<NW, RES, REF, EX, DG>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 template <int NW, bool LDSC>
@@ -1954,6 +2019,7 @@ struct mcmc_ctx {
     uint64_t initDraws = 0;
     mcmc_run_stats last{};
     SweepLaunch sweep = nullptr;
+    SweepLaunch sweep_diag = nullptr;   // tiled early exit (streaming): the diagnostics instantiation
     dim3 grid, block;
     size_t lds = 0;             // dynamic LDS of the sweep kernel (colour replica staging)
     uint32_t* wave_start = nullptr;
@@ -2180,9 +2246,15 @@ int ensure_constants() {
     return MCMC_OK;
 }
 
+// The sweep launch for these arguments: the diagnostics instantiation when they ask for it.
+void launch_tiled_or_diag(mcmc_ctx* c, const SweepArgs& a) {
+    const bool diag = a.scan_stats || a.phase_ts || a.dbg_max_pairs;
+    (diag && c->sweep_diag ? c->sweep_diag : c->sweep)(a, c->grid, c->block, c->lds, c->stream);
+}
+
 // Host launch of one (sweep, commit) pair on the context stream.
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
-    c->sweep(a, c->grid, c->block, c->lds, c->stream);
+    launch_tiled_or_diag(c, a);
     if (a.fused) return;
     if (c->wide) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
@@ -2566,6 +2638,16 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 c->sweep = tab[wi];
                 ea = wi == 0 ? allow_lds_tiled<1, false, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, false, false, true>(c->lds)
                    : wi == 2 ? allow_lds_tiled<4, false, false, true>(c->lds) : allow_lds_tiled<8, false, false, true>(c->lds);
+                static const SweepLaunch tabd[4] = {launch_tiled<1, false, false, true, true>,
+                                                    launch_tiled<2, false, false, true, true>,
+                                                    launch_tiled<4, false, false, true, true>,
+                                                    launch_tiled<8, false, false, true, true>};
+                c->sweep_diag = tabd[wi];
+                if (ea == hipSuccess)
+                    ea = wi == 0 ? allow_lds_tiled<1, false, false, true, true>(c->lds)
+                       : wi == 1 ? allow_lds_tiled<2, false, false, true, true>(c->lds)
+                       : wi == 2 ? allow_lds_tiled<4, false, false, true, true>(c->lds)
+                                 : allow_lds_tiled<8, false, false, true, true>(c->lds);
             }
         } else if (resident) {
             static const SweepLaunch tab[4] = {launch_tiled<1, true>, launch_tiled<2, true>, launch_tiled<4, true>,
@@ -3410,7 +3492,7 @@ int mcmc_part_sweep_async(mcmc_ctx* c) {
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
     c->ran = true;
     SweepArgs a = make_args(c, 1);
-    c->sweep(a, c->grid, c->block, c->lds, c->stream);
+    launch_tiled_or_diag(c, a);
     if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;

@@ -521,3 +521,4 @@ def test_early_exit_drain_matches_oracle(M, monkeypatch, drain, rows, stream):
     monkeypatch.setenv("MCMC_FULL_SCAN", "1")
     col2, st2, _ = gpu_run(M, off, idx, ncol, seed, 0, maxRip=5)
     assert_same(col2, st2, r)
+
