@@ -389,23 +389,28 @@ def main() -> int:
         # result cannot change; MCMC_FULL_SCAN=1 scans every arc): the bytes one launch moves are
         # counted on the device (mcmc_set_scan_stats, 3 sweeps outside the timed region) -- id quads,
         # the staged (group, block) pairs' table rows and colour slices, own colour read + write
-        q, pr, tot2, ker2 = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        q, qu, pr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        tot2, ker2 = ctypes.c_double(), ctypes.c_double()
         sctx = col._ctx if dist is None else drv._ctx
         check(lib().mcmc_set_scan_stats(sctx, 1))
         if dist is None:
             check(lib().mcmc_bench_sweeps(col._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
         else:
             check(lib().mcmc_part_run(arr, 1, 3, ctypes.byref(st)))
-        check(lib().mcmc_get_scan_stats(sctx, ctypes.byref(q), ctypes.byref(pr)))
+        check(lib().mcmc_get_scan_stats_ex(sctx, ctypes.byref(q), ctypes.byref(qu), ctypes.byref(pr)))
         check(lib().mcmc_set_scan_stats(sctx, 0))
-        quads, pairs = q.value / 3.0, pr.value / 3.0
+        # algorithmic: the quads whose ids the scan gathered (the exact early exit needs them);
+        # issued: every quad loaded, incl. those fetched ahead for a row that filled up first
+        quads, quads_issued, pairs = qu.value / 3.0, q.value / 3.0, pr.value / 3.0
         R = info["grp_rows"]
         table = 4 * ((R + 4) & ~3)
-        slice_b = 0 if info["resident"] else min(65536, ((g.nNodes + 15) // 16) * 16)
+        slice_b = 0 if info["resident"] else min(1 << info["block_log2"], ((g.nNodes + 15) // 16) * 16)
         nloc = g.nNodes if dist is None else int(bounds[rank + 1] - bounds[rank])
         b_alg = 16 * quads + pairs * (table + slice_b) + 2 * nloc
         scan = {"early_exit": info.get("early", True), "quads_per_sweep": quads, "pairs_per_sweep": pairs,
                 "id_bytes": 16 * quads, "table_bytes": pairs * table, "slice_bytes": pairs * slice_b,
+                "quads_issued_per_sweep": quads_issued,
+                "issued_bytes": 16 * quads_issued + pairs * (table + slice_b) + 2 * nloc,
                 "layout_bytes_full_scan": b_fmt,
                 "note": "exact early exit: a row's scan stops once its mask holds all nCol colours "
                         "(count_free_colors cannot change); a group skips its remaining column blocks once "

@@ -174,6 +174,10 @@ int mcmc_set_bench_mode(mcmc_ctx* c, int on);
  * MCMC_FULL_SCAN=1 in the environment at mcmc_create scans every arc instead. */
 int mcmc_set_scan_stats(mcmc_ctx* c, int on);
 int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs);
+/* The same counters plus `used` (may be NULL): the quads whose ids the scan gathered. `quads` also
+ * counts loads issued ahead for a row that filled up before they were needed (the scan keeps two
+ * steps in flight), so `used` is the bytes the exact early exit needs, `quads` what it issued. */
+int mcmc_get_scan_stats_ex(mcmc_ctx* c, uint64_t* quads, uint64_t* used, uint64_t* pairs);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

@@ -72,6 +72,7 @@ int get_tiled_layout(mcmc_graph* gh, uint32_t v_begin, uint32_t v_end, uint32_t 
                      hipStream_t s, const TiledLayout** out);
 // Default rows per group of a tiled layout on nloc rows (mcmc_create and the generator agree).
 uint32_t tiled_default_rows(uint32_t nloc, uint32_t cus, uint32_t rmax);
+constexpr uint32_t kTileRowsMax = 8191;      // tiled groups: dlist/claims are 16-bit row indices
 constexpr uint32_t kTileGenRowsMax = 1792;   // generator layouts: fits the streaming LDS for nCol <= 64
 // CSR (ascending rows) of a generated graph with a full-range layout.
 int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx);

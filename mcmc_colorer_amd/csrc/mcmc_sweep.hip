@@ -142,7 +142,8 @@ struct SweepArgs {
     int early;
     uint32_t dbg_max_pairs;     // diagnostics only (MCMC_DEBUG_MAX_PAIRS): cut every group after k pairs (wrong results)
     uint32_t drain_rows;        // tiled early exit: a group with at most this many rows left drains them (<= 256)
-    unsigned long long* scan_stats;   // diagnostics (MCMC_SCAN_STATS): [0] quads loaded, [1] pairs staged
+    unsigned long long* scan_stats;   // diagnostics (MCMC_SCAN_STATS): [0] quads loaded, [1] pairs staged,
+                                      // [2] quads whose ids were gathered (the scan needed them)
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
     uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
     uint32_t* evcnt;            // wide: their number per workgroup [nblk] (written every sweep)
@@ -857,7 +858,7 @@ struct TailShared {
     uint32_t cursor[2];   // tiled: per-pair row cursor (double-buffered with the pair buffers)
     uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
     uint32_t dn[2];       // tiled sparse pairs / drain: rows listed (by pair-buffer parity)
-    uint32_t st_quads, st_pairs;   // diagnostics (scan_stats): quads loaded, pairs staged by the workgroup
+    uint32_t st_quads, st_pairs, st_used;   // diagnostics (scan_stats): quads loaded, pairs staged, quads gathered
     uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
 };
@@ -1241,8 +1242,9 @@ __device__ __forceinline__ void evaluate_ref_tile(const SweepArgs& a, const uint
     atomicAdd(&hist_lds[star], 1u);
 }
 
-// Streaming mode: the colour slice of a pair (2^16 vertices at most) per LDS buffer.
-constexpr uint32_t kSliceBytes = 65536;
+// Streaming mode: the colour slice of a pair (2^block_log2 vertices, at most 2^16) per LDS buffer of
+// max(2^block_log2, 16 KiB) bytes (the DMA lands whole wave-instructions: 16 waves x 1 KiB).
+__host__ __device__ inline uint32_t tile_slice_buf(uint32_t block_log2) { return 1u << (block_log2 > 14u ? block_log2 : 14u); }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // register-promotable 16 B
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
@@ -1275,8 +1277,9 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
     if (!RES) {
         const uint32_t lo = b << a.block_log2;
         const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
-#pragma unroll
-        for (uint32_t k = 0; k < kSliceBytes / 16u / 64u / 16u; k++) {   // 4 wave-instructions per wave
+        // the slice buffer (tile_slice_buf: 16-64 KiB): 1-4 wave-instructions per wave
+        const uint32_t kn = tile_slice_buf(a.block_log2) / 1024u / nwaves;
+        for (uint32_t k = 0; k < kn; k++) {
             const uint32_t piece = (k * nwaves + wid) * 64u;
             const uint32_t q = min(piece + (uint32_t)lane, nq16 - 1u);
             glds16(C + (lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
@@ -1401,7 +1404,7 @@ __device__ __forceinline__ void tile_open_rows(uint32_t rows, const uint32_t* sm
     __syncthreads();
 }
 
-template <int NW>
+template <int NW, bool DG>
 __device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g, uint32_t b,
                                            uint32_t na, uint32_t* smask, TailShared& sh, const uint32_t* fullw,
                                            int lane) {
@@ -1432,6 +1435,10 @@ __device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __
                     const uint4 v1 = *reinterpret_cast<const uint4*>(gids + (q2 < s1 ? q2 : q));
                     drain_quad<NW>(cb, v0, true, m);
                     drain_quad<NW>(cb, v1, q2 < s1, m);
+                    if (DG && a.scan_stats) {   // drain quads: loaded and gathered alike
+                        atomicAdd(&sh.st_quads, q2 < s1 ? 2u : 1u);
+                        atomicAdd(&sh.st_used, q2 < s1 ? 2u : 1u);
+                    }
                 }
             }
 #pragma unroll
@@ -1477,7 +1484,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     uint8_t* lbase = reinterpret_cast<uint8_t*>(lds_raw);
     const uint32_t R = a.grp_rows, nb = a.nblocks;
-    const uint32_t SB = RES ? a.slice_bytes : kSliceBytes;             // bytes per colour buffer
+    const uint32_t SB = RES ? a.slice_bytes : tile_slice_buf(a.block_log2);   // bytes per colour buffer
     uint8_t* seg_base = lbase + (RES ? SB : 2u * SB);
     const uint32_t SEGB = a.seg_buf_bytes;                              // bytes per table buffer
     uint32_t* smask = reinterpret_cast<uint32_t*>(seg_base + 2u * SEGB);
@@ -1538,7 +1545,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         return f;
     };
     uint32_t nfull_run = 0, kpair = 0;   // rows of the current group known full; pair counter
-    if (threadIdx.x == 0) sh.st_quads = sh.st_pairs = 0;
+    if (threadIdx.x == 0) sh.st_quads = sh.st_pairs = sh.st_used = 0;
     if (g < a.ngroups) {
         tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
         if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
@@ -1759,10 +1766,14 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     do {                                                                                                \
         if (REF) tile_gather_ref<NW>(scb, Q, OK, m, oc, QPOS, tend, whi, a.v_begin + r0 + row, cmode, ecnt); \
         else tile_gather<NW>(scb, Q, OK, m);                                                            \
+        if (DG && a.scan_stats) {                                                                       \
+            const uint64_t ub = __ballot(OK);                                                           \
+            if (lane == 0 && ub) atomicAdd(&sh.st_used, (uint32_t)__popcll(ub));                        \
+        }                                                                                               \
     } while (0)
         uint4 v1[kTileU];
         if (drain) {
-            tile_drain<NW>(a, C, g, b, nlist, smask, sh, fullw, lane);
+            tile_drain<NW, DG>(a, C, g, b, nlist, smask, sh, fullw, lane);
         } else if (!allfull && __ballot(row < rows)) {
             for (;;) {
                 bool c0, c1;
@@ -1860,6 +1871,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         if (threadIdx.x == 0) {
             atomicAdd(&a.scan_stats[0], (unsigned long long)sh.st_quads);
             atomicAdd(&a.scan_stats[1], (unsigned long long)sh.st_pairs);
+            atomicAdd(&a.scan_stats[2], (unsigned long long)sh.st_used);
         }
     }
     MCMC_PHASE(a, 3);
@@ -2545,20 +2557,20 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         // Resident (replica + two segment-table buffers + masks fit one workgroup's LDS): replica
         // staged once. Otherwise (streaming) two 64 KiB colour-slice buffers. One 1024-thread
         // workgroup per CU either way. Groups of R rows: about one group per workgroup, at most
-        // what the LDS holds (rmax) and 4095 (a table row = one DMA instruction per wave).
+        // what the LDS holds (rmax) and kTileRowsMax.
         const size_t rep = lds_bytes;
         const char* gr = getenv("MCMC_GROUP_ROWS");
         // REF adds [p: 1 KiB][histogram][2 own-colour buffers of own_bytes(rows) (streaming)]
         auto own_bytes = [](uint32_t rows) -> size_t { return ((size_t)rows + 47u + 1023u) & ~(size_t)1023u; };
         auto lds_need = [&](bool res, uint32_t rows) -> size_t {
             const size_t segb = ((size_t)tseg_stride(rows) * 4u + 1023u) & ~(size_t)1023u;
-            const size_t base = (res ? rep : 2u * (size_t)kSliceBytes) + 2u * segb;
+            const size_t base = (res ? rep : 2u * (size_t)tile_slice_buf(c->block_log2)) + 2u * segb;
             if (!ref) return base + (size_t)rows * c->nw * 4u;
             return base + (((size_t)rows * c->nw * 4u + 15u) & ~(size_t)15u) + 1024u + 4u * kHistWords +
                    (res ? 0u : 2u * own_bytes(rows));
         };
         auto rmax_for = [&](bool res) -> uint32_t {
-            uint32_t r = 4095;
+            uint32_t r = kTileRowsMax;
             while (r > 1 && lds_need(res, r) > kMaxLdsBytes) r -= 1;
             return lds_need(res, r) <= kMaxLdsBytes ? r : 0u;
         };
@@ -2976,24 +2988,29 @@ int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
 int mcmc_set_scan_stats(mcmc_ctx* c, int on) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 2 * sizeof(unsigned long long)));
-    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 2 * sizeof(unsigned long long)));
+    if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 3 * sizeof(unsigned long long)));
+    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 3 * sizeof(unsigned long long)));
     c->scan_stats_on = on != 0;
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
     return MCMC_OK;
 }
 
-int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs) {
+int mcmc_get_scan_stats_ex(mcmc_ctx* c, uint64_t* quads, uint64_t* used, uint64_t* pairs) {
     if (!c || !quads || !pairs) return fail(MCMC_E_ARG, "NULL argument");
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[3] = {0, 0, 0};
     if (c->scan_stats) {
         MCMC_HIP_TRY(hipSetDevice(c->g->device));
         MCMC_HIP_TRY(hipMemcpy(h, c->scan_stats, sizeof(h), hipMemcpyDeviceToHost));
     }
     *quads = h[0];
+    if (used) *used = h[2];
     *pairs = h[1];
     return MCMC_OK;
+}
+
+int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs) {
+    return mcmc_get_scan_stats_ex(c, quads, nullptr, pairs);
 }
 
 int mcmc_set_bench_mode(mcmc_ctx* c, int on) {

@@ -1,12 +1,12 @@
 """Folds rocprofv3 PMC passes (scripts/gpu_prof.sh: pass 1 FETCH_SIZE, pass 2 WRITE_SIZE) into
 profiles/pmc_summary.json, which bench.py reads for roofline.traffic.
 
-  python profiles/make_pmc_summary.py <prof_dir> <key> [kernel-substring[,...]] [last-K]
+  python profiles/make_pmc_summary.py <prof_dir> <key> [kernel-substring[;...]] [last-K]
 
 FETCH_SIZE / WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read (MI355X_MICROARCH.md, HBM/rocprofv3 section), so it is doubled;
 WRITE_SIZE is taken as is. Values are averaged over the kernel's profiled launches; a
-comma-separated kernel list (one sweep made of several launches, e.g. the wide sweep) sums the
+semicolon-separated kernel list (one sweep made of several launches, e.g. the wide sweep) sums the
 per-launch means of each. last-K: only each kernel's last K launches (the bench's timed sweeps,
 not the convergence run's early exits before them).
 """
@@ -32,7 +32,7 @@ def main() -> None:
     last = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     fetch_kib = write_kib = 0.0
     nf = nw = 0
-    for k in kernel.split(","):
+    for k in kernel.split(";"):
         f, n1 = mean_counter(prof / "pmc1" / "run_counter_collection.csv", "FETCH_SIZE", k, last)
         w, n2 = mean_counter(prof / "pmc2" / "run_counter_collection.csv", "WRITE_SIZE", k, last)
         fetch_kib, write_kib, nf, nw = fetch_kib + f, write_kib + w, max(nf, n1), max(nw, n2)
