@@ -57,7 +57,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 KERNELS = {"lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
-           "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)"}
+           "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)",
+           "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
 
 def load_traffic(key: str):

@@ -120,8 +120,12 @@ struct SweepArgs {
     // reference-GPU-semantics mode (REF instantiations of the tiled sweep, refmode.hip)
     uint32_t* xw0;              // XORWOW states of sweep parity 0 / 1: SoA {v0..v4, d} x nloc
     uint32_t* xw1;
-    uint32_t* hist;             // [2][kHistWords] colour histograms of C_t by parity (C_t[v] <= nCol)
+    uint32_t* hist;             // [2][hist_words] colour histograms of C_t by parity (C_t[v] <= nCol)
+    uint32_t hist_words;        // kHistWords (uint8 REF), nCol + 1 rounded up (REF wide, ref_wide.h)
     float ref_hi;               // 1 - (nCol - 1) * eps (coloringMCMC_balance.cu:132)
+    uint32_t* rw_cnt;           // REF wide: [4] list lengths (ref_wide.h kRw*)
+    uint32_t* rw_lists;         // REF wide: [4][n] listed violators / long rows
+    float* ptab;                // REF wide: p of every colour for the running sweep (genDynamicDistribution)
     uint32_t own_buf_bytes;     // streaming REF: LDS bytes of one own-colour buffer
     // wide sweep (nCol > 256, uint16 replicas; sweep_wide.h)
     uint64_t arc_begin, arc_count;   // the local rows' arcs: col_idx[arc_begin, arc_begin + arc_count)
@@ -446,12 +450,14 @@ __device__ uint32_t wide_block_events(const SweepArgs& a, uint32_t Eg, uint32_t*
 // iterations (maxRip sweeps) the loop ends without that test, and this sweep is the count-only
 // pass whose count is the last sweep's "nuovi conflitti" (:229). Accepting flips the parity of
 // the colours, XORWOW states and histograms, and clears the histogram sweep t+1 accumulates into.
-__device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long long ecnt) {
+// copy_from (REF wide): the histogram sweep t+1 accumulates into starts as this copy, not zeroed.
+__device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long long ecnt,
+                                   const uint32_t* copy_from = nullptr) {
     DevState* st = a.st;
     const unsigned long long c = ecnt;
     if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = c;
     const uint32_t cap = a.maxRip > 0 ? a.maxRip : 1u;   // do { ... } while (rip < maxRip): >= 1 sweep
-    if (t == cap || c <= a.z) {
+    if (t == cap || (!a.bench && c <= a.z)) {   // throughput mode: no convergence stop
         if (threadIdx.x == 0) {
             const uint32_t rip = (t == cap) ? cap : t + 1u;
             st->done = 1;
@@ -462,8 +468,8 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
         }
         return;
     }
-    uint32_t* h = a.hist + (t & 1u) * kHistWords;
-    for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x) h[i] = 0;
+    uint32_t* h = a.hist + (t & 1u) * a.hist_words;
+    for (uint32_t i = threadIdx.x; i < a.hist_words; i += blockDim.x) h[i] = copy_from ? copy_from[i] : 0u;
     if (threadIdx.x == 0) {
         st->t = t + 1;
         st->arrive_viol = 0;
@@ -1494,7 +1500,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint8_t* own_base = reinterpret_cast<uint8_t*>(hist_lds + kHistWords);
     if (REF) {
         // genDynamicDistribution (coloringMCMC_utils.cu:64-70) from C_t's histogram
-        const uint32_t* __restrict__ H = a.hist + (t & 1u) * kHistWords;
+        const uint32_t* __restrict__ H = a.hist + (t & 1u) * a.hist_words;
         for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x) hist_lds[i] = 0;
         for (uint32_t c = threadIdx.x; c < a.nCol; c += blockDim.x)
             p_lds[c] = (1.0f - ((float)H[c] / (float)a.n)) / (float)(a.nCol - 1u);
@@ -1883,7 +1889,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     __syncthreads();   // the commit may reuse the colour-slice LDS for its sort
     if (REF) {
         // C_(t+1)'s histogram: this workgroup's counts; its same-colour arcs ride the arrival
-        uint32_t* __restrict__ Hn = a.hist + ((t + 1u) & 1u) * kHistWords;
+        uint32_t* __restrict__ Hn = a.hist + ((t + 1u) & 1u) * a.hist_words;
         for (uint32_t c = threadIdx.x; c <= a.nCol; c += blockDim.x)
             if (hist_lds[c]) atomicAdd(&Hn[c], hist_lds[c]);
         uint32_t x = ecnt;
@@ -1952,6 +1958,7 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
 }
 
 #include "sweep_wide.h"
+#include "ref_wide.h"
 
 // ----------------------------------------------------------------------------------------------
 using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
@@ -1966,6 +1973,16 @@ void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
     else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     wide_eval_kernel<<<a.evnblk + kWalkBlocks, 256, 0, s>>>(a);
+}
+// REF wide (ref_wide.h): grid = 8 blocks per CU (g.x = CUs) for the list kernels; masks of nCol bits
+// per violator in LDS (at most 32 KiB per 256-thread block)
+void launch_ref_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
+    const uint32_t wstride = (((a.nCol + 31u) >> 5) + 3u) & ~3u;
+    refw_scan_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, g.x * 16u)), 256, 0, s>>>(a);
+    refw_rows_kernel<16><<<g.x * 8u, 256, 0, s>>>(a, kRwLong);
+    refw_rows_kernel<1024><<<g.x, 1024, 0, s>>>(a, kRwHub);
+    refw_walk_kernel<1><<<g.x * 8u, 64u * kRefwWalkWaves, sizeof(uint32_t) * kRefwWalkWaves * wstride, s>>>(a, kRwViol);
+    refw_walk_kernel<16><<<g.x, 1024, sizeof(uint32_t) * wstride, s>>>(a, kRwViolBig);
 }
 template <int NW, bool LDSC>
 void launch_sweep(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
@@ -2072,7 +2089,12 @@ struct mcmc_ctx {
     bool ref = false;
     mcmc_gpurand* rand = nullptr;   // caller-owned per-vertex XORWOW states
     uint32_t rand_base = 0;         // the states' parity when the run started
-    uint32_t* hist = nullptr;       // [2][kHistWords]
+    uint32_t* hist = nullptr;       // [2][hist_words]
+    uint32_t hist_words = kHistWords;
+    bool refwide = false;           // REF with nCol > 255 (variant 5: uint16 replicas over the CSR, ref_wide.h)
+    uint32_t* rw_cnt = nullptr;
+    uint32_t* rw_lists = nullptr;
+    float* ptab = nullptr;
     uint32_t own_buf_bytes = 0;
     // wide sweep (variant 4: nCol > 256, uint16 colour replicas; sweep_wide.h)
     bool wide = false;
@@ -2175,6 +2197,13 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.xw0 = c->rand->states[c->rand_base];
         a.xw1 = c->rand->states[c->rand_base ^ 1u];
         a.hist = c->hist;
+        a.hist_words = c->hist_words;
+        a.rw_cnt = c->rw_cnt;
+        a.rw_lists = c->rw_lists;
+        if (c->refwide) {
+            a.etab = c->etab;
+            a.ptab = c->ptab;
+        }
         // nvcc contracts 1.0f - (nCol - 1) * eps into one fma (coloringMCMC_balance.cu:132)
         a.ref_hi = std::fma(-(float)(c->p.nCol - 1u), c->p.epsilon, 1.0f);
         a.own_buf_bytes = c->own_buf_bytes;
@@ -2268,7 +2297,8 @@ void launch_tiled_or_diag(mcmc_ctx* c, const SweepArgs& a) {
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     launch_tiled_or_diag(c, a);
     if (a.fused) return;
-    if (c->wide) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
+    if (c->refwide) refw_commit_kernel<<<1, 1024, 0, c->stream>>>(a);
+    else if (c->wide) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
@@ -2327,25 +2357,25 @@ int run_tailcut_ref(mcmc_ctx* c, const DevState& h, uint64_t cc, uint64_t* final
     uint8_t* C = c->colors[h.t & 1u];
     *passes = 0;
     *finalConf = h.finalViol;
-    std::vector<uint8_t> hc(n);
+    std::vector<uint8_t> hc((size_t)n * c->cbytes);
     int rc = download_colors(c, C, hc.data());
     if (rc) return rc;
     std::vector<uint32_t> stats(std::max(n, nCol) + 1u, 0u);
-    for (uint8_t v : hc) stats[v]++;
+    for (uint32_t v = 0; v < n; v++) stats[c->cbytes == 2 ? reinterpret_cast<const uint16_t*>(hc.data())[v] : hc[v]]++;
     std::vector<uint32_t> ordered(nCol);
     for (uint32_t i = 0; i < nCol; i++) ordered[i] = i;
     std::sort(&ordered[0], &ordered[0] + nCol, [&](int i, int j) { return stats[i] < stats[j]; });
     MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ordered.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice,
                                 c->stream));
     const TailView tv = tail_view(c);
-    rc = tail_count(tv, C, 1u, c->vflags, c->tc_count, c->stream, true);
+    rc = tail_count(tv, C, c->cbytes, c->vflags, c->tc_count, c->stream, true);
     if (rc) return rc;
     while (cc > 0 && *passes < c->tailcut_max) {
         rc = tail_select(c->vflags, n, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream);
         if (rc) return rc;
-        rc = tail_repair(tv, C, 1u, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, true, cc);
+        rc = tail_repair(tv, C, c->cbytes, c->tc_list, c->tc_len, c->tc_colorIdx, nCol, c->stream, true, cc);
         if (rc) return rc;
-        rc = tail_count(tv, C, 1u, c->vflags, c->tc_count, c->stream, true);
+        rc = tail_count(tv, C, c->cbytes, c->vflags, c->tc_count, c->stream, true);
         if (rc) return rc;
         unsigned long long hv = 0;
         MCMC_HIP_TRY(hipMemcpyAsync(&hv, c->tc_count, sizeof(hv), hipMemcpyDeviceToHost, c->stream));
@@ -2441,15 +2471,14 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     // nCol > 256: the wide sweep (uint16 replicas, sweep_wide.h); MCMC_GATHER=wide forces it
     const char* gv = getenv("MCMC_GATHER");
     const std::string gsel = gv ? gv : "";
-    const bool wide = p->nCol > 256 || (gsel == "wide" && !ref);
+    // REF: a colour may equal nCol (initColoring at u = 1.0f), so uint8 replicas hold nCol <= 255
+    const bool wide = ref ? p->nCol > 255 : (p->nCol > 256 || gsel == "wide");
     if (wide) {
         if (p->nCol > kWideMaxCol) return fail(MCMC_E_ARG, "nCol > 65535 is not supported (uint16 colour replicas)");
-        if (ref) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
         if (!gd.row_off) return fail(MCMC_E_ARG, "nCol > 256 needs a CSR graph (mcmc_graph_upload / _simulate)");
     }
     if (ref) {
-        // a colour may equal nCol (initColoring at u = 1.0f): it must fit the uint8 replicas
-        if (p->nCol < 2 || p->nCol > 255) return fail(MCMC_E_ARG, "reference-GPU mode: 2 <= nCol <= 255");
+        if (p->nCol < 2) return fail(MCMC_E_ARG, "reference-GPU mode: nCol >= 2");
         if (v_begin != 0 || v_end != gd.n) return fail(MCMC_E_ARG, "reference-GPU mode: whole-graph contexts");
         if (ref->n != gd.n || ref->device != gd.device)
             return fail(MCMC_E_ARG, "reference-GPU mode: the XORWOW states do not match the graph");
@@ -2479,7 +2508,14 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
     if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
     if (!gd.row_off || ref) c->variant = 3;   // generated graph / REF: tiled layout only
-    if (wide) {
+    if (wide && ref) {   // REF over the CSR with uint16 replicas (ref_wide.h)
+        c->variant = 5;
+        c->refwide = true;
+        c->cbytes = 2;
+        c->fused = 0;
+        c->sweep = launch_ref_wide;
+        c->hist_words = (p->nCol + 1u + 63u) & ~63u;
+    } else if (wide) {
         c->variant = 4;
         c->wide = true;
         c->cbytes = 2;
@@ -2505,8 +2541,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->lds = (size_t)(1u << c->block_log2) + (size_t)c->chunk_rows * c->nw * 4u;
         ea = wi == 0 ? allow_lds_blocked<1>(c->lds) : wi == 1 ? allow_lds_blocked<2>(c->lds)
            : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
-    } else if (c->variant == 4) {
-        c->sweep = launch_wide;   // geometry and tables below
+    } else if (c->variant == 4 || c->variant == 5) {
+        // geometry and tables below
     } else if (c->variant == 3) {
         const char* bl = getenv("MCMC_BLOCK_LOG2");
         c->block_log2 = (bl && gd.row_off) ? (uint32_t)std::max(4, std::min(16, atoi(bl))) : 16u;
@@ -2753,6 +2789,22 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("wide sweep setup: ") + hipGetErrorString(ew));
         }
+    } else if (c->variant == 5) {
+        c->grid = dim3((uint32_t)cus);   // launch_ref_wide scales it per kernel
+        c->block = dim3(256);
+        hipError_t ew = hipMalloc(&c->rw_cnt, 4 * sizeof(uint32_t));
+        if (ew == hipSuccess) ew = hipMalloc(&c->rw_lists, 4 * sizeof(uint32_t) * std::max<size_t>(nloc, 1));
+        if (ew == hipSuccess) ew = hipMemsetAsync(c->rw_cnt, 0, 4 * sizeof(uint32_t), c->stream);
+        std::vector<float> et((size_t)p->nCol + 1);   // E[k] = k eps in fp32 (refw_walk_own)
+        eps_table(p->epsilon, p->nCol, et.data());
+        if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
+        if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
+        if (ew == hipSuccess) ew = hipMalloc(&c->ptab, sizeof(float) * p->nCol);
+        if (ew == hipSuccess) ew = hipStreamSynchronize(c->stream);
+        if (ew != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("reference-GPU wide setup: ") + hipGetErrorString(ew));
+        }
     } else if (c->variant != 2) {
         c->block = dim3(1024);
         c->grid = dim3((uint32_t)cus);
@@ -2760,7 +2812,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->block = dim3(256);
         c->grid = dim3((uint32_t)cus * 8u);
     }
-    if (c->variant != 3 && c->variant != 4) {
+    if (c->variant != 3 && c->variant != 4 && c->variant != 5) {
         const uint32_t W = c->variant == 1 ? c->grid.x : c->grid.x * (c->block.x / 64);
         hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
         if (ew != hipSuccess) {
@@ -2794,7 +2846,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             return fail(MCMC_E_HIP, std::string("segments: ") + hipGetErrorString(es));
         }
     }
-    if (ref && hipMalloc(&c->hist, sizeof(uint32_t) * 2u * kHistWords) != hipSuccess) {
+    if (ref && hipMalloc(&c->hist, sizeof(uint32_t) * 2u * c->hist_words) != hipSuccess) {
         mcmc_destroy(c);
         return fail(MCMC_E_NOMEM, "histogram allocation");
     }
@@ -3050,12 +3102,21 @@ int mcmc_ref_init(mcmc_ctx* c) {
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }   // states moved
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
     c->batch = c->bench_n = 0;
-    MCMC_HIP_TRY(hipMemsetAsync(c->hist, 0, sizeof(uint32_t) * 2u * kHistWords, c->stream));
+    MCMC_HIP_TRY(hipMemsetAsync(c->hist, 0, sizeof(uint32_t) * 2u * c->hist_words, c->stream));
     if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * n, c->stream));
     int rc = upload_state(c, 0);
     if (rc) return rc;
     const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 2048u));
-    ref_init_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], c->rand->states[c->rand_base], n, nCol, c->hist);
+    if (c->refwide) {
+        refw_init_kernel<<<blocks, 256, 0, c->stream>>>(reinterpret_cast<uint16_t*>(c->colors[0]),
+                                                        c->rand->states[c->rand_base], n, nCol, c->hist);
+        const SweepArgs a = make_args(c, 1);
+        refw_ptab_kernel<<<std::max<uint32_t>(1u, (nCol + 255u) / 256u), 256, 0, c->stream>>>(a, 0u);
+        // sweep 0 adjusts a copy of C_0's histogram (refw_hist_move)
+        MCMC_HIP_TRY(hipMemcpyAsync(c->hist + c->hist_words, c->hist, sizeof(uint32_t) * c->hist_words,
+                                    hipMemcpyDeviceToDevice, c->stream));
+    } else
+        ref_init_kernel<<<blocks, 256, 0, c->stream>>>(c->colors[0], c->rand->states[c->rand_base], n, nCol, c->hist);
     MCMC_HIP_TRY(hipGetLastError());
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     c->initialized = true;
@@ -3141,7 +3202,7 @@ int mcmc_get_coloring(mcmc_ctx* c, uint32_t* out) {
     std::vector<uint8_t> tmp((size_t)c->n * c->cbytes);
     int rc = download_colors(c, c->colors[which], tmp.data());
     if (rc) return rc;
-    if (c->wide)
+    if (c->cbytes == 2)
         for (uint32_t v = 0; v < c->n; v++) out[v] = reinterpret_cast<const uint16_t*>(tmp.data())[v];
     else
         for (uint32_t v = 0; v < c->n; v++) out[v] = tmp[v];
@@ -3278,6 +3339,10 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         i.layout_bytes = 4ull * kWideChunk * c->xs->chunks + 4ull * c->xs->chunks;
         i.sweep_bytes = i.layout_bytes + 2 * (uint64_t)c->n + 5 * nloc + taboo +
                         (c->xs->mode == 1 ? (uint64_t)c->n : 0);   // LDS mode: the fingerprint array
+    } else if (c->refwide) {
+        // CSR; colour replica read once, own colours read and written (2 B each), both histograms
+        i.layout_bytes = 8 * (nloc + 1) + 4 * mloc;
+        i.sweep_bytes = i.layout_bytes + 2 * (uint64_t)c->n + 4 * nloc + taboo + 48 * nloc + 8ull * c->hist_words;
     } else if (c->wide) {
         // CSR + per-chunk row table; colour replica read once + own colours + write (2 B each)
         i.layout_bytes = 8 * (nloc + 1) + 4 * mloc + 4ull * (c->nchunks + 1);
@@ -3313,6 +3378,9 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->tc_count);
     (void)hipFree(c->tc_tmp);
     (void)hipFree(c->hist);
+    (void)hipFree(c->rw_cnt);
+    (void)hipFree(c->rw_lists);
+    (void)hipFree(c->ptab);
     (void)hipFree(c->chunk_row);
     (void)hipFree(c->wflag);
     (void)hipFree(c->wfp[0]);

@@ -119,3 +119,50 @@ def test_ref_mode_multigraph_unsorted_rows(M):
     off[1:] = np.cumsum([len(r) for r in rows])
     idx = np.array([w for r in rows for w in r], dtype=np.uint32)
     compare(M, off, idx, M.Graph.from_csr(off, idx), 7, 5, maxrip=25, tailcut=True)
+
+
+def hub_graph(n, hubs, hub_deg, extra, seed):
+    """Symmetric CSR: `hubs` vertices joined to hub_deg random others each, plus `extra` random
+    edges (rows of every size class of the wide REF sweep: lane, wave and workgroup rows)."""
+    rng = np.random.default_rng(seed)
+    edges = set()
+    for h in range(hubs):
+        for w in rng.choice(n, size=hub_deg, replace=False):
+            if int(w) != h:
+                edges.add((min(h, int(w)), max(h, int(w))))
+    for _ in range(extra):
+        a, b = (int(x) for x in rng.integers(0, n, 2))
+        if a != b:
+            edges.add((min(a, b), max(a, b)))
+    rows = [[] for _ in range(n)]
+    for a, b in edges:
+        rows[a].append(b)
+        rows[b].append(a)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    idx = np.array([w for r in rows for w in sorted(r)], dtype=np.uint32)
+    return off, idx
+
+
+WIDE_CASES = [
+    # graph, nCol (0: maxDeg), seed, maxRip, taboo, tailcut
+    ("rnd2", 0, 1, 40, 0, False),       # setupRnd2 G(1500, 0.3): nCol = maxDeg (~500), wave rows
+    ("rnd2", 256, 2, 25, 2, True),      # the first colour count past the uint8 replicas; taboo
+    ("hubs", 300, 3, 20, 0, False),     # 2500-arc hubs: workgroup rows and workgroup violator walks
+    ("hubs", 0, 4, 15, 1, True),        # nCol = maxDeg, taboo, the tail cut on uint16 colours
+    ("hubs", 4000, 5, 10, 0, False),    # more colours than any row has neighbours
+]
+
+
+@pytest.mark.parametrize("graph,ncol,seed,maxrip,taboo,tailcut", WIDE_CASES)
+def test_ref_mode_wide_matches_oracle(M, graph, ncol, seed, maxrip, taboo, tailcut):
+    """--mcmcgpu-ref past 255 colours (uint16 replicas, csrc/ref_wide.h): colouring, per-sweep
+    conflicting-edge counts, rip, sweeps, tail cut and the XORWOW states equal the oracle's."""
+    if graph == "rnd2":
+        O.srand(1)
+        off, idx = O.setup_rnd2(1500, 0.3)
+    else:
+        off, idx = hub_graph(6000, 6, 2500, 30000, seed)
+    nc = ncol or O.max_deg(off)
+    g = M.Graph.from_csr(off, idx)
+    compare(M, off, idx, g, nc, seed, maxrip=maxrip, taboo=taboo, tailcut=tailcut)
