@@ -340,7 +340,8 @@ void mcmc_gpurand_destroy(mcmc_gpurand* r);
  * (coloringMCMC_main.cu:271-290) for at most tail_max_passes passes (the reference's is unbounded).
  * Stats: iter = rip, maxIterReached = (rip == maxRip), finalViol = conflicting EDGES of the
  * returned colouring, sweepsRun = sweeps, trajLen = counts of C_0 .. C_last (mcmc_get_trajectory).
- * The states advance as the reference's do; repetitions pass the same `rand`. 2 <= nCol <= 255.
+ * The states advance as the reference's do; repetitions pass the same `rand`. 2 <= nCol <= 65535
+ * (nCol > 255: uint16 replicas over the CSR, csrc/ref_wide.h).
  * Parity unpinned against CUDA. */
 int mcmc_ref_create(const mcmc_graph* g, const mcmc_params* p, mcmc_gpurand* rand, mcmc_ctx** out);
 int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats);

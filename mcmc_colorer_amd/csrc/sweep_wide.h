@@ -40,7 +40,10 @@ constexpr uint32_t kWideMaxCol = 65535;
 constexpr int kWideWalkThreads = 256;
 constexpr int kWideEvalPer = 8;           // vertices per evaluation lane
 constexpr uint32_t kSplitArcs = 2048;     // arcs per task of a split walk (SweepArgs::split_arcs)
-constexpr uint32_t kWalkBlocks = 256;     // walk workgroups beside the evaluation
+#ifndef MCMC_WALK_BLOCKS
+#define MCMC_WALK_BLOCKS 1024   // 4 per CU: the violator-heavy C5 sweep 0.44 -> 0.32 ms (256 / 512 / 1024 measured), none idle when converged
+#endif
+constexpr uint32_t kWalkBlocks = MCMC_WALK_BLOCKS;   // walk workgroups beside the evaluation
 constexpr uint32_t kSplitMax = 64;        // violators with a global occupancy mask (split walks)
 constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
 
