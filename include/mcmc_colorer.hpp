@@ -309,6 +309,130 @@ private:
     int lastRepetition{0};
 };
 
+// ---- ColoringMCMC_CPU's class surface (graph_coloring/coloringMCMC_CPU.h:15-31) ----------------
+// The reference's --mcmccpu colorer, run by the same HIP sweep as ColoringMCMC (its semantics ARE
+// the CPU colorer's: bit-identical colouring, iteration count and glibc stream). Kept: the ctor
+// (graph, params, seed -- main.cu:171 passes seed + repetition), run(), show_histogram(),
+// violation_count() (on the GPU: mcmc_count_violations of the given colouring), saveStats() and
+// saveColor() in the reference's layout (coloringMCMC_CPUutils.cpp:70-109), getC(). The per-vertex
+// GoogleTest hooks of the reference (count_free_colors, fill_p, extract_new_color, fill_qstar) act on
+// the CPU class's private buffers and have no counterpart: the sweep computes them in registers.
+template <typename nodeW, typename edgeW>
+class ColoringMCMC_CPU {
+public:
+    ColoringMCMC_CPU(Graph<nodeW, edgeW>* g, ColoringMCMCParams params, uint32_t seed)
+        : graph(g), param(params), seed(seed) {}
+    ~ColoringMCMC_CPU() {
+        if (ctx) mcmc_destroy(ctx);
+    }
+
+    void run() {
+        if (ctx) mcmc_destroy(ctx);
+        ctx = nullptr;
+        mcmc_params p = to_params();
+        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
+        MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));   // rand(): the process stream
+        if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(ctx, param.tailcutRepair));
+        MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
+        MCMC_CHECK(mcmc_run(ctx, 0, &stats));
+        MCMC_CHECK(mcmc_get_glibc_window(ctx, mcmc::glibc_global().w));
+        C.resize(graph->getNNodes());
+        MCMC_CHECK(mcmc_get_coloring(ctx, C.data()));
+        iter = stats.iter;
+        maxIterReached = stats.maxIterReached != 0;
+    }
+
+    void show_histogram() const {
+        std::vector<size_t> hist(param.nCol, 0);
+        for (uint32_t c : C) hist[c]++;
+        for (size_t i = 0; i < hist.size(); i++) std::cout << i << ": " << hist[i] << std::endl;
+    }
+
+    // Vertices with a neighbour of their own colour in `currentColoring` (coloringMCMC_CPU.cpp:329-351),
+    // their flags in `violations`; counted on the GPU.
+    size_t violation_count(const std::vector<uint32_t>& currentColoring, std::vector<bool>& violations) {
+        mcmc_params p = to_params();
+        mcmc_ctx* vc = nullptr;
+        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &vc));
+        MCMC_CHECK(mcmc_init_coloring(vc, currentColoring.data()));
+        uint64_t count = 0;
+        std::vector<uint8_t> flags(graph->getNNodes());
+        MCMC_CHECK(mcmc_count_violations(vc, &count, flags.data()));
+        mcmc_destroy(vc);
+        violations.assign(flags.begin(), flags.end());
+        return (size_t)count;
+    }
+
+    void saveStats(size_t it, float duration, std::ofstream& outFile) const {
+        const uint32_t nCol = param.nCol;
+        outFile << "MCMC Colorer - CPU version - Report" << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "GRAPH INFO" << std::endl;
+        outFile << "Nodes: " << graph->getNNodes() << " - Edges: " << graph->getNEdges() << std::endl;
+        outFile << "Max deg: " << graph->getMaxNodeDeg() << " - Min deg: " << graph->getMinNodeDeg()
+                << " - Avg deg: " << graph->getMeanNodeDeg() << std::endl;
+        outFile << "Edge probability (for randomly generated graphs): " << graph->prob << std::endl;
+        outFile << "Seed: " << seed << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "EXECUTION INFO" << std::endl;
+        outFile << "Repetition: " << it << std::endl;
+        outFile << "Execution time: " << duration << std::endl;
+        outFile << "Iteration performed: " << iter << std::endl;
+        outFile << "Max iteration reached: " << (maxIterReached ? "yes" : "no") << std::endl;
+        outFile << "-------------------------------------------" << std::endl;
+        outFile << "Color histogram:" << std::endl;
+        std::vector<size_t> hist(nCol, 0);
+        for (uint32_t c : C) hist[c]++;
+        size_t used = 0;
+        for (size_t i = 0; i < nCol; i++) {
+            outFile << i << ": " << hist[i] << std::endl;
+            if (hist[i]) used++;
+        }
+        outFile << "Number of colors: " << nCol << " - Used colors: " << used << std::endl;
+        outFile << "Color ratio: " << param.numColorRatio << std::endl;
+        size_t total = 0;
+        for (size_t h : hist) total += h;
+        const float mean = (float)(int)total / (float)nCol;   // std::accumulate(..., 0): an int sum
+        float var = 0;
+        for (size_t h : hist) var += ((h - mean) * (h - mean));
+        var /= (float)nCol;
+        outFile << "Average number of nodes for each color: " << mean << std::endl;
+        outFile << "Variance: " << var << std::endl;
+        outFile << "StD: " << std::sqrt(var) << std::endl;
+    }
+
+    void saveColor(std::ofstream& outfile) const {
+        for (size_t i = 0; i < C.size(); i++) outfile << i << " " << C[i] << std::endl;
+    }
+
+    std::vector<uint32_t>* getC() { return &C; }
+    const mcmc_run_stats& getStats() const { return stats; }
+
+private:
+    mcmc_params to_params() const {
+        mcmc_params p{};
+        p.nCol = param.nCol;
+        p.epsilon = param.epsilon;
+        p.lambda = param.lambda;
+        p.ratioFreezed = param.ratioFreezed;
+        p.numColorRatio = param.numColorRatio;
+        p.maxRip = param.maxRip;
+        p.tabooIteration = param.tabooIteration;
+        p.tailcut = param.tailcut;
+        p.seed = seed;
+        return p;
+    }
+
+    Graph<nodeW, edgeW>* graph;
+    ColoringMCMCParams param;
+    uint32_t seed;
+    mcmc_ctx* ctx{nullptr};
+    mcmc_run_stats stats{};
+    std::vector<uint32_t> C;
+    uint32_t iter{0};
+    bool maxIterReached{false};
+};
+
 // ---- reference-GPU-semantics mode -------------------------------------
 // GPURand's per-vertex curandStates (GPURandomizer.cu:85-101), shared by every repetition.
 class CurandStates {

@@ -10,7 +10,8 @@
 //   --tailcutRepair: after the loop, run the reference's tail cut (coloringMCMC_CPU.cpp:272-311)
 //   with its inner loop fixed (k++; the reference's never returns), at most 1000 passes
 // Outputs <outDir>/<graphName>-MCMC_GPU-<i>.log and -colors.txt per repetition.
-// --mcmccpu is served by the test-infrastructure oracle (oracle/build/mcmc_cpu_ref, same flags);
+// --mcmccpu: ColoringMCMC_CPU's surface (-MCMC_CPU-<i> files, seed + i), run by the same HIP sweep --
+// the CPU colorer's results, bit for bit (the oracle, oracle/build/mcmc_cpu_ref, is test infrastructure);
 // --lubygpu (ColoringLuby), --grdffgpu (ColoringGreedyFF) and --vffgpu (ColoringVFF) write
 // <graphName>-LUBY-<i> / -GFF-<i> / -VFF-<i> .log and -colors.txt.
 #include <getopt.h>
@@ -110,6 +111,7 @@ void help(const char* argv0) {
               << "                       for n where the reference's O(n^2) generator is infeasible (1e7)\n"
               << "  --mcmcgpu            MCMC colorer on the MI355X (default)\n"
               << "  --mcmcgpu-ref        the reference's GPU colorer semantics (XORWOW, balance-dynamic)\n"
+              << "  --mcmccpu            ColoringMCMC_CPU's outputs (-MCMC_CPU- files), computed by the same GPU sweep\n"
               << "  --grdffgpu           parallel greedy first-fit colorer (ColoringGreedyFF)\n"
               << "  --lubygpu            Luby independent-set colorer (ColoringLuby::run_fast)\n"
               << "  --vffgpu             greedy first fit + vertex-first-fit rebalancing (ColoringVFF)\n"
@@ -190,16 +192,11 @@ int main(int argc, char** argv) {
         std::cout << "Graph file undefined (--graph). Specify a graph file or enable simulation mode." << std::endl;
         return 255;
     }
-    if (mcmccpu) {
-        std::cout << "--mcmccpu: the CPU colorer is the test-infrastructure oracle: oracle/build/mcmc_cpu_ref (same flags)"
-                  << std::endl;
-        return 255;
-    }
     if (mcmcgpu && mcmcgpuref) {
         std::cout << "--mcmcgpu and --mcmcgpu-ref write the same files: choose one" << std::endl;
         return 255;
     }
-    if (!mcmcgpu && !mcmcgpuref && !greedyff && !lubygpu && !vffgpu) {
+    if (!mcmcgpu && !mcmcgpuref && !mcmccpu && !greedyff && !lubygpu && !vffgpu) {
         std::cout << "No coloring algorithm specified: enabling MCMC GPU (--mcmcgpu)" << std::endl;
         mcmcgpu = true;
     }
@@ -228,8 +225,9 @@ int main(int argc, char** argv) {
     mkdir(outDir.c_str(), 0775);
 
     const float numColorRatio = 1.0f / (float)numColRatio;        // main.cu:53
-    if (gpus > 1 && (mcmcgpuref || greedyff || lubygpu || vffgpu || tailcutRepair)) {
-        std::cout << "--gpus > 1 partitions --mcmcgpu only (no --mcmcgpu-ref, other colorers or --tailcutRepair)" << std::endl;
+    if (gpus > 1 && (mcmcgpuref || mcmccpu || greedyff || lubygpu || vffgpu || tailcutRepair)) {
+        std::cout << "--gpus > 1 partitions --mcmcgpu only (no --mcmcgpu-ref, --mcmccpu, other colorers or --tailcutRepair)"
+                  << std::endl;
         return 255;
     }
     Graph<float, float>* g;
@@ -313,7 +311,7 @@ int main(int argc, char** argv) {
             std::ofstream vffFileColors(outDir + "/" + graphName + "-VFF-" + std::to_string(i) + "-colors.txt");
             balanced.saveColor(vffFileColors);
         }
-        if (!mcmcgpu && !mcmcgpuref) continue;
+        if (!mcmcgpu && !mcmcgpuref && !mcmccpu) continue;
         ColoringMCMCParams params;                                   // main.cu:160-168
         params.numColorRatio = numColorRatio;
         params.nCol = (nCol != 0) ? nCol : (col_sz)(g->getMaxNodeDeg() * numColorRatio);
@@ -324,6 +322,18 @@ int main(int argc, char** argv) {
         params.tabooIteration = tabooIteration;
         params.tailcut = tailcut;
         params.tailcutRepair = tailcutRepair ? 1000u : 0u;
+        if (mcmccpu) {   // main.cu:170-190: before the GPU colorer, on the same glibc stream
+            ColoringMCMC_CPU<float, float> mcmcCpu(g, params, seed + i);
+            const auto s0 = std::chrono::steady_clock::now();
+            mcmcCpu.run();
+            const float duration = (float)std::chrono::duration<double>(std::chrono::steady_clock::now() - s0).count();
+            std::cout << "MCMC_CPU elapsed time: " << duration << std::endl;
+            std::ofstream cpuFileLog(outDir + "/" + graphName + "-MCMC_CPU-" + std::to_string(i) + ".log");
+            mcmcCpu.saveStats(i, duration, cpuFileLog);
+            std::ofstream cpuFileColors(outDir + "/" + graphName + "-MCMC_CPU-" + std::to_string(i) + "-colors.txt");
+            mcmcCpu.saveColor(cpuFileColors);
+        }
+        if (!mcmcgpu && !mcmcgpuref) continue;
         if (mcmcgpuref) {
             ColoringMCMCGpuRef<float, float> colRef(g, curand, params);
             colRef.setDirectoryPath(outDir + "/" + graphName + "-MCMC_GPU-" + std::to_string(i));

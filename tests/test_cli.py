@@ -118,3 +118,26 @@ def test_cli_mcmcgpu_ref(tmp_path):
         assert log.count("***** Tentativo numero:") == res.res.sweeps + res.res.tailcutPasses
         assert ("---> TailCutting" in log) == (res.res.tailcutPasses > 0)
         assert f"Max iteration reached {'yes' if res.res.maxIterReached else 'no'}" in log
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--mcmcgpu"]])
+def test_cli_mcmccpu_surface(tmp_path, extra):
+    """--mcmccpu through the product (ColoringMCMC_CPU's surface, run by the HIP sweep) writes the
+    oracle CLI's -MCMC_CPU- files: colours and the whole report except the wall time, for every
+    repetition (seed + i, one glibc stream); with --mcmcgpu beside it the CPU colorer runs first."""
+    args = ["--simulate", "0.05", "-n", "1500", "--nCol", "20", "--tabooIteration", "1", "--repet", "2", "--seed", "3"]
+    po, oo = tmp_path / "gpu", tmp_path / "cpu"
+    r1 = subprocess.run([str(CLI), "--mcmccpu", *extra, *args, "--outDir", str(po)], capture_output=True, text=True,
+                        timeout=600)
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    assert "MCMC_CPU elapsed time" in r1.stdout
+    r2 = subprocess.run([str(ORACLE), "--mcmccpu", *args, "--outDir", str(oo)], capture_output=True, text=True,
+                        timeout=600)
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    name = "1500_0.050000_1.000000"
+    strip = lambda t: re.sub(r"Execution time: .*", "", t)
+    for i in range(2):
+        assert (po / f"{name}-MCMC_CPU-{i}-colors.txt").read_text() == (oo / f"{name}-MCMC_CPU-{i}-colors.txt").read_text()
+        assert strip((po / f"{name}-MCMC_CPU-{i}.log").read_text()) == strip((oo / f"{name}-MCMC_CPU-{i}.log").read_text())
+        assert (po / f"{name}-MCMC_GPU-{i}.log").exists() == bool(extra)
