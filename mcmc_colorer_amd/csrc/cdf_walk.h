@@ -179,6 +179,21 @@ MCMC_HD int first_of_64(Pred pred) {
 #endif
 }
 
+// Length of the run of colours of one kind (`bit`: 1 occupied, 0 free) from colour c, across words,
+// capped at nCol.
+MCMC_HD uint32_t mask_run_len(const uint32_t* mask, uint32_t nCol, uint32_t c, uint32_t bit) {
+    uint32_t r = 0, x = c;
+    while (x < nCol) {
+        const uint32_t wv = bit ? ~mask[x >> 5] : mask[x >> 5];   // set bits: the other kind
+        const uint32_t rest = wv >> (x & 31u);
+        const uint32_t len = rest ? (uint32_t)__builtin_ctz(rest) : 32u - (x & 31u);
+        r += len;
+        x += len;
+        if (rest) break;
+    }
+    return r < nCol - c ? r : nCol - c;
+}
+
 // walk_mask with word prefix counts pre[w] = occupied colours in words < w (NWW + 1 entries),
 // for a whole wave. Inside a binade with non-tying increments dE, dP the mantissa integer after
 // colour x is k0 + occ(c..x) dE + free(c..x) dP: monotone, so the first colour whose sum passes
@@ -198,10 +213,16 @@ MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32
         const uint32_t bc = f32_bits(cdf);
         const uint32_t E = bc >> 23;
         uint32_t dE = 0, dP = 0;
-        if (E == 0u || !binade_inc(eps, E, dE) || !binade_inc(pf, E, dP)) {   // one exact step
-            cdf += ((mask[c >> 5] >> (c & 31u)) & 1u) ? eps : pf;
-            if (cdf > u) return c;
-            c++;
+        if (E == 0u || !binade_inc(eps, E, dE) || !binade_inc(pf, E, dP)) {
+            // cdf = 0 or a tying increment: the run of equal addends from c (colours of one kind,
+            // across words) by cdf_run, exact step by step where the rounding depends on the sum's
+            // parity (a violator with few free colours crosses a tie binade over thousands of
+            // occupied ones: colour-by-colour steps cost ~90 us there)
+            const uint32_t bit = (mask[c >> 5] >> (c & 31u)) & 1u;
+            const uint32_t r = mask_run_len(mask, nCol, c, bit);
+            const uint32_t s = cdf_run(cdf, bit ? eps : pf, r, u);
+            if (s) return c + s - 1u;
+            c += r;
             continue;
         }
         if (dE == 0u && dP == 0u) return nCol;   // every further sum rounds back to cdf (<= u)

@@ -101,6 +101,30 @@ def test_cdf_walk_prefix_wave_large_ncol(case):
     assert not mism, mism[:5]
 
 
+def test_cdf_walk_tie_binades_long_runs():
+    """A violator with few free colours (long runs of occupied ones): where an addend's increment
+    ties (x / ulp a half-integer) the walk steps runs with cdf_run instead of colour by colour; every
+    case against the literal float32 walk, pf with odd and even mantissas, u up to just below 1."""
+    rng = np.random.default_rng(4242)
+    mism, odd = [], 0
+    for it in range(24):
+        ncol = int(rng.integers(2000, 30000))
+        gap = int(rng.integers(50, 900))
+        bits = np.ones(ncol, dtype=bool)
+        bits[rng.integers(0, gap)::gap] = False
+        pop = int(bits.sum())
+        eps = [1e-8, 3e-7, 2.0 ** -30 * 3][it % 3]
+        pf = np.float32((np.float32(1.0) - np.float32(eps) * np.float32(pop)) / np.float32(ncol - pop))
+        odd += int(np.frombuffer(pf.tobytes(), dtype=np.uint32)[0] & 1)
+        for u in (np.float32(1.0) - np.float32(2.0 ** -24), canon(int(rng.integers(1, 2**31 - 1))),
+                  np.float32(pf * np.float32(rng.integers(1, 6)))):
+            a, b = lib_walk(bits, ncol, 0, eps, pf, u), naive_walk(bits, ncol, eps, pf, u)
+            if a != b:
+                mism.append((ncol, gap, eps, float(pf), float(u), a, b))
+    assert odd > 0
+    assert not mism, mism[:5]
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU parity
 
