@@ -1370,7 +1370,11 @@ __device__ __forceinline__ void tile_first_row(const SweepArgs& a, uint32_t g, u
 // the next pair's 2 first-row bounds and 4 first quads) has landed, this wave's LDS traffic is
 // done, then a raw barrier -- the loads issued after the DMA stay in flight across it (a
 // __syncthreads() would drain them).
-#define MCMC_PAIR_BARRIER() asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#define MCMC_STR2(x) #x
+#define MCMC_STR(x) MCMC_STR2(x)
+#define MCMC_PAIR_VMCNT (2 + MCMC_TILE_U)   // the next pair's 2 first-row bounds + its kTileU first quads
+#define MCMC_PAIR_BARRIER() \
+    asm volatile("s_waitcnt vmcnt(" MCMC_STR(MCMC_PAIR_VMCNT) ") lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define MCMC_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Drain (early exit): the group's rows whose masks are still not full (at most drain_rows, few once
@@ -2646,13 +2650,15 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         while (sl < 6 && 2.0 * (double)(1u << sl) * kTileU < quads) sl++;
         if (c->early && !ref) {
             // early exit: a row scans about min(its segment, the ids that fill its mask -- the coupon
-            // collector's nCol H(nCol)) per block; the smallest L whose step covers 3/4 of that
-            // (measured: C3 L = 2 1.63 ms vs L = 4 1.75; C2 L = 1, 2 22.7 us vs L = 8 30.7)
+            // collector's nCol H(nCol)) per block; the smallest L whose step covers that, so a segment
+            // takes one step (the scan is instruction-issue bound: SQ_ACTIVE_INST_ANY ~ 1 issue per
+            // SIMD cycle, every masked slot costs its wave instruction; measured r02: C3 L = 2 / 4 / 8
+            // 1.345 / 1.257 / 1.671 ms, C2 L = 1 / 2 / 4 23.6 / 23.8 / 25.5 us)
             double hn = 0.0;
             for (uint32_t k = 1; k <= p->nCol; k++) hn += 1.0 / k;
             const double scan_ids = std::min(8.0 * quads, (double)p->nCol * hn);
             sl = 0;
-            while (sl < 6 && 8.0 * (double)(1u << sl) * kTileU < 0.75 * scan_ids) sl++;
+            while (sl < 6 && 8.0 * (double)(1u << sl) * kTileU < scan_ids) sl++;
         }
         const char* sv = getenv("MCMC_SUB_LOG2");
         if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));
