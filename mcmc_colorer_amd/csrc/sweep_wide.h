@@ -805,6 +805,68 @@ static void plan_pieces(const std::vector<uint32_t>& chunk0, uint32_t nwg, std::
     wgp[nwg] = (uint32_t)(pieces.size() / 3);
 }
 
+// XCD-aware variant (default when nwg is a multiple of kXSlabs): the row space is cut into kXSlabs
+// ranges of equal chunk counts (quantiles of the chunks' base rows), and range x goes to the
+// workgroups b with b % kXSlabs == x, which share one XCD under round-robin dispatch. A workgroup's
+// row-fingerprint windows then stay inside its XCD's range (0.5 MiB of fingerprints at C5: resident
+// in that XCD's 4 MiB L2 across all 32 slabs) instead of every XCD sweeping all n fingerprints once
+// per slab. Inside an XCD, each slab's chunks of the range are cut into pieces of about the
+// XCD's chunks / workgroups and dealt largest first (LPT) as plan_pieces does.
+static void plan_pieces_xcd(const std::vector<uint32_t>& chunk0, const std::vector<uint32_t>& base, uint32_t nwg,
+                            std::vector<uint32_t>& pieces, std::vector<uint32_t>& wgp) {
+    const uint32_t ns = (uint32_t)chunk0.size() - 1u, C = chunk0[ns], X = kXSlabs, per_x = nwg / X;
+    std::vector<uint32_t> sorted_base(base.begin(), base.begin() + C);
+    std::sort(sorted_base.begin(), sorted_base.end());
+    std::vector<uint32_t> bound(X + 1, 0u);   // row ranges [bound[x], bound[x+1])
+    for (uint32_t x = 1; x < X; x++) bound[x] = sorted_base[(size_t)C * x / X];
+    bound[X] = 0xFFFFFFFFu;
+    std::vector<std::vector<uint32_t>> per(nwg);
+    std::vector<std::array<uint32_t, 3>> all;
+    for (uint32_t x = 0; x < X; x++) {
+        std::vector<std::array<uint32_t, 3>> cells;   // (slab, lo, hi) of this row range
+        uint64_t tot = 0;
+        for (uint32_t s = 0; s < ns; s++) {
+            const auto b0 = base.begin() + chunk0[s], b1 = base.begin() + chunk0[s + 1];
+            // chunks of slab s ascend by base row: the range's chunks are one run
+            const uint32_t lo = chunk0[s] + (uint32_t)(std::lower_bound(b0, b1, bound[x]) - b0);
+            const uint32_t hi = x + 1 == X ? chunk0[s + 1] : chunk0[s] + (uint32_t)(std::lower_bound(b0, b1, bound[x + 1]) - b0);
+            if (hi > lo) { cells.push_back({s, lo, hi}); tot += hi - lo; }
+        }
+        const double T = std::max(1.0, (double)tot / per_x);
+        std::vector<std::array<uint32_t, 3>> pc;
+        for (const auto& c : cells) {
+            const uint32_t cs = c[2] - c[1];
+            const uint32_t p = std::max<uint32_t>(1u, (uint32_t)std::llround(cs / T));
+            for (uint32_t k = 0; k < p; k++) {
+                const uint32_t a = c[1] + (uint32_t)((uint64_t)cs * k / p), b = c[1] + (uint32_t)((uint64_t)cs * (k + 1) / p);
+                if (b > a) pc.push_back({c[0], a, b});
+            }
+        }
+        std::stable_sort(pc.begin(), pc.end(), [](const std::array<uint32_t, 3>& p, const std::array<uint32_t, 3>& q) {
+            return p[2] - p[1] > q[2] - q[1];
+        });
+        std::vector<std::pair<uint64_t, uint32_t>> heap;   // (load, workgroup), min-heap over the XCD's workgroups
+        for (uint32_t k = 0; k < per_x; k++) heap.push_back({0, x + k * X});
+        auto cmp = [](const std::pair<uint64_t, uint32_t>& p, const std::pair<uint64_t, uint32_t>& q) { return p > q; };
+        std::make_heap(heap.begin(), heap.end(), cmp);
+        for (const auto& p : pc) {
+            std::pop_heap(heap.begin(), heap.end(), cmp);
+            auto& h = heap.back();
+            per[h.second].push_back((uint32_t)all.size());
+            all.push_back(p);
+            h.first += p[2] - p[1];
+            std::push_heap(heap.begin(), heap.end(), cmp);
+        }
+    }
+    pieces.clear();
+    wgp.assign(nwg + 1, 0);
+    for (uint32_t w = 0; w < nwg; w++) {
+        wgp[w] = (uint32_t)(pieces.size() / 3);
+        for (uint32_t i : per[w]) pieces.insert(pieces.end(), all[i].begin(), all[i].end());
+    }
+    wgp[nwg] = (uint32_t)(pieces.size() / 3);
+}
+
 // The slab layout of rows [vb, ve) in `mode` (0: 8 L2 slabs, 1: 2^17-vertex LDS tiles over `nwg`
 // workgroups), built on first use and cached on the graph. *out stays nullptr (and MCMC_OK is
 // returned) when the layout does not apply: no CSR, no arcs, uint32 entry positions or row deltas
@@ -935,7 +997,14 @@ int get_xslab(mcmc_graph* gh, uint32_t vb, uint32_t ve, uint32_t mode, uint32_t 
     XTRY(hipStreamSynchronize(st));
     if (!h[1] && mode == 1) {
         std::vector<uint32_t> pc, wgp;
-        plan_pieces(L->chunk0_h, nwg, pc, wgp);
+        const char* pe = getenv("MCMC_TSCAN_PLAN");   // "lpt": the XCD-blind plan (A/B)
+        if (nwg % kXSlabs == 0 && !(pe && std::string(pe) == "lpt")) {
+            std::vector<uint32_t> bh(L->chunks);
+            XTRY(hipMemcpy(bh.data(), L->base, sizeof(uint32_t) * bh.size(), hipMemcpyDeviceToHost));
+            plan_pieces_xcd(L->chunk0_h, bh, nwg, pc, wgp);
+        } else {
+            plan_pieces(L->chunk0_h, nwg, pc, wgp);
+        }
         L->nwg = nwg;
         L->npieces = (uint32_t)(pc.size() / 3);
         XTRY(hipMalloc(&L->pieces, sizeof(uint32_t) * std::max<size_t>(pc.size(), 3)));
