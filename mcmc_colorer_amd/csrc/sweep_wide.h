@@ -38,7 +38,10 @@ constexpr uint32_t kWideChunk = 256;      // entries (arcs) per wave chunk: 64 l
 constexpr uint32_t kWideMaskWords = 2048; // nCol <= 65536
 constexpr uint32_t kWideMaxCol = 65535;
 constexpr int kWideWalkThreads = 256;
-constexpr int kWideEvalPer = 8;           // vertices per evaluation lane
+#ifndef MCMC_WIDE_EVAL_PER
+#define MCMC_WIDE_EVAL_PER 8
+#endif
+constexpr int kWideEvalPer = MCMC_WIDE_EVAL_PER;   // vertices per evaluation lane
 constexpr uint32_t kSplitArcs = 2048;     // arcs per task of a split walk (SweepArgs::split_arcs)
 #ifndef MCMC_WALK_BLOCKS
 #define MCMC_WALK_BLOCKS 1024   // 4 per CU: the violator-heavy C5 sweep 0.44 -> 0.32 ms (256 / 512 / 1024 measured), none idle when converged
@@ -146,6 +149,10 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 constexpr uint32_t kTsLog = 17;                                  // 2^17 vertices per LDS tile
 constexpr int kTscanThreads = 1024;
 constexpr uint32_t kTsUnroll = 3;                               // chunks per wave step
+#ifndef MCMC_TS_DEPTH
+#define MCMC_TS_DEPTH 2
+#endif
+constexpr uint32_t kTsDepth = MCMC_TS_DEPTH;                     // chunk sets in flight per wave (2 or 3)
 constexpr uint32_t kTsCand = 1024;                              // LDS candidate list (8 KiB)
 constexpr uint32_t kTsWin = 1024;                               // row-fingerprint window per wave (bytes)
 constexpr size_t kTscanLds = (size_t)1 << kTsLog;                // 128 KiB of fingerprints
@@ -218,26 +225,32 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
         uint32_t ch = c0 + wave;
         if (ch < c1) {
             const uint4 pad4 = make_uint4(kXsPad, kXsPad, kXsPad, kXsPad);
-            uint4 q[kTsUnroll];
-            uint32_t bs[kTsUnroll];
+            const uint32_t S = kTsUnroll * nwave;   // chunks from one set of this wave to its next
+            // set `cs` (chunks cs, cs + nwave, ...) into (Y, BY); chunks past the piece are padding
+            auto load_set = [&](uint4 (&Y)[kTsUnroll], uint32_t (&BY)[kTsUnroll], uint32_t cs) {
 #pragma unroll
-            for (uint32_t u = 0; u < kTsUnroll; u++) {
-                const uint32_t c = ch + u * nwave;
-                q[u] = pad4;
-                bs[u] = 0;
-                if (c < c1) {
-                    q[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
-                    bs[u] = a.xs_base[c];
+                for (uint32_t u = 0; u < kTsUnroll; u++) {
+                    const uint32_t c = cs + u * nwave;
+                    Y[u] = pad4;
+                    BY[u] = 0;
+                    if (c < c1) {
+                        Y[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
+                        BY[u] = a.xs_base[c];
+                    }
                 }
-            }
-            for (;;) {
+            };
+            // one step: set `ch` from (X, BX); the set MCMC_TS_DEPTH - 1 ahead is loaded into (Y, BY)
+            // behind this step's fingerprint gathers. Returns false once the piece is done.
+            auto step = [&](uint4 (&X)[kTsUnroll], uint32_t (&BX)[kTsUnroll], uint4 (&Y)[kTsUnroll],
+                            uint32_t (&BY)[kTsUnroll]) -> bool {
+                if (ch >= c1) return false;
                 uint32_t e[4 * kTsUnroll], r[4 * kTsUnroll], fr[4 * kTsUnroll], fc[4 * kTsUnroll];
 #pragma unroll
                 for (uint32_t u = 0; u < kTsUnroll; u++) {
-                    e[4 * u] = q[u].x;
-                    e[4 * u + 1] = q[u].y;
-                    e[4 * u + 2] = q[u].z;
-                    e[4 * u + 3] = q[u].w;
+                    e[4 * u] = X[u].x;
+                    e[4 * u + 1] = X[u].y;
+                    e[4 * u + 2] = X[u].z;
+                    e[4 * u + 3] = X[u].w;
                 }
                 // row fingerprints: each chunk's rows ascend from its base, so one 16-byte load per
                 // lane fetches a 1 KiB window of them (from base rounded down to 16); entries past
@@ -246,26 +259,15 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
                 uint32_t w0[kTsUnroll];
 #pragma unroll
                 for (uint32_t u = 0; u < kTsUnroll; u++) {
-                    w0[u] = (vb + bs[u]) & ~15u;
+                    w0[u] = (vb + BX[u]) & ~15u;
                     wv[u] = *reinterpret_cast<const uint4*>(fp + w0[u] + 16u * lane);   // fp has 2 KiB of slack
                 }
 #pragma unroll
                 for (uint32_t i = 0; i < 4 * kTsUnroll; i++) {
-                    r[i] = bs[i / 4] + (e[i] >> kTsLog);
+                    r[i] = BX[i / 4] + (e[i] >> kTsLog);
                     fc[i] = e[i] != kXsPad ? (uint32_t)lfp[e[i] & cmask] : 1u;
                 }
-                const uint32_t nx = ch + kTsUnroll * nwave;
-                const bool more = nx < c1;
-#pragma unroll
-                for (uint32_t u = 0; u < kTsUnroll; u++) {   // the next set, behind the gathers
-                    const uint32_t c = nx + u * nwave;
-                    q[u] = pad4;
-                    bs[u] = 0;
-                    if (more && c < c1) {
-                        q[u] = *reinterpret_cast<const uint4*>(ent + (size_t)c * kWideChunk);
-                        bs[u] = a.xs_base[c];
-                    }
-                }
+                load_set(Y, BY, ch + (kTsDepth - 1u) * S);   // behind the gathers
 #pragma unroll
                 for (uint32_t u = 0; u < kTsUnroll; u++) {   // the wave's window slot: its own LDS ops stay in order
                     *reinterpret_cast<uint4*>(win + 16u * lane) = wv[u];
@@ -291,9 +293,28 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
                         }
                     }
                 }
-                if (!more) break;
-                ch = nx;
+                ch += S;
+                return true;
+            };
+            // register sets rotate by expansion, never by copy (a copy would wait for its loads)
+            uint4 qa[kTsUnroll], qb[kTsUnroll];
+            uint32_t ba[kTsUnroll], bb[kTsUnroll];
+            load_set(qa, ba, ch);
+#if MCMC_TS_DEPTH == 3
+            uint4 qc[kTsUnroll];
+            uint32_t bc[kTsUnroll];
+            load_set(qb, bb, ch + S);
+            for (;;) {
+                if (!step(qa, ba, qc, bc)) break;
+                if (!step(qb, bb, qa, ba)) break;
+                if (!step(qc, bc, qb, bb)) break;
             }
+#else
+            for (;;) {
+                if (!step(qa, ba, qb, bb)) break;
+                if (!step(qb, bb, qa, ba)) break;
+            }
+#endif
         }
         __syncthreads();
         const uint32_t nc = min(ncand, kTsCand);
