@@ -139,6 +139,23 @@ public:
     const mcmc_graph* handle() const { return h_; }
     int device() const { return device_; }
     float prob{0.0f};
+    // Row-partial graphs (ErFast with a row range: one rank's rows) describe only their rows; the
+    // whole graph's statistics (sum of arcs, max / min degree over every rank's rows) make the
+    // default nCol (main.cu:162) and the reports equal the one-GPU run's.
+    static void mergePartitionStats(const std::vector<Graph*>& parts) {
+        uint64_t m = 0;
+        node mx = 0, mn = ~node(0);
+        for (const Graph* p : parts) {
+            m += p->m_;
+            mx = std::max(mx, p->maxDeg_);
+            mn = std::min(mn, p->minDeg_);
+        }
+        for (Graph* p : parts) {
+            p->m_ = m;
+            p->maxDeg_ = mx;
+            p->minDeg_ = parts.empty() ? 0 : mn;
+        }
+    }
 
 private:
     void info() { MCMC_CHECK(mcmc_graph_info(h_, &n_, &m_, &maxDeg_, &minDeg_)); }
@@ -183,8 +200,12 @@ public:
         }
         std::vector<int> devs;
         for (auto* g : parts) devs.push_back(g->device());
-        comms.resize(parts.size());
-        MCMC_CHECK(mcmc_comm_init_all(devs.data(), (uint32_t)devs.size(), comms.data()));
+        comms.assign(parts.size(), nullptr);
+        // ranks sharing one device run over the library's loopback transport (device copies; RCCL
+        // refuses two ranks on one GPU) -- a rehearsal of the partitioned run on a single GPU
+        const bool one_device = std::all_of(devs.begin(), devs.end(), [&](int x) { return x == devs[0]; });
+        if (!one_device || devs.size() == 1)
+            MCMC_CHECK(mcmc_comm_init_all(devs.data(), (uint32_t)devs.size(), comms.data()));
     }
     ~ColoringMCMC() {
         if (ctx) mcmc_destroy(ctx);
@@ -217,16 +238,13 @@ public:
             MCMC_CHECK(mcmc_run(ctx, 0, &stats));
             res = ctx;
         } else {
-            if (param.tailcutRepair) {
-                std::fprintf(stderr, "ColoringMCMC: the tail-cut repair runs on one GPU\n");
-                std::abort();
-            }
             for (auto* c : pctx) mcmc_destroy(c);
             pctx.assign(parts.size(), nullptr);
             const uint32_t world = (uint32_t)parts.size();
             for (uint32_t r = 0; r < world; r++) {
                 MCMC_CHECK(mcmc_part_create(parts[r]->handle(), &p, world, r, bounds.data(), comms[r], &pctx[r]));
                 MCMC_CHECK(mcmc_set_glibc_window(pctx[r], mcmc::glibc_global().w));
+                if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(pctx[r], param.tailcutRepair));
                 MCMC_CHECK(mcmc_init_coloring(pctx[r], nullptr));
             }
             std::vector<mcmc_run_stats> st(world);

@@ -60,7 +60,7 @@ typedef struct {
     uint32_t iter;             /* "Iteration performed"                                          */
     int32_t  maxIterReached;   /* "Max iteration reached"                                        */
     uint64_t finalViol;        /* conflicting vertices of the returned coloring                  */
-    uint64_t trajLen;          /* = iter + 1 entries of per-sweep Cviol (mcmc_get_trajectory)    */
+    uint64_t trajLen;          /* per-sweep Cviol entries kept = min(iter + 1, 2^20) (mcmc_get_trajectory) */
     uint64_t glibcDraws;       /* rand() draws consumed by CDF-overflow events                   */
     uint64_t initDraws;        /* engine draws of the initial coloring (n + rejections)          */
     double   loopMs;           /* device time of the sweep loop (hipEvent)                       */

@@ -273,8 +273,16 @@ int gff_color(const GraphDev& gd, uint32_t* A, uint32_t* B, uint32_t* forb, uint
     const uint32_t n = gd.n;
     DevBuf<uint8_t> fresh;
     MCMC_HIP_TRY(fresh.alloc(n));
+    // sym: the conflict pass may scan only the rows coloured this round (gff_conflict_kernel). The
+    // check needs ascending rows; it never reorders the caller's graph: an unsorted CSR (or one the
+    // check cannot handle) takes the conservative pass over every coloured row, correct either way.
     bool sym = false;
-    if (int rc = csr_symmetric(const_cast<GraphDev&>(gd), 0, n, 0, &sym)) return rc;
+    if (gd.sym >= 0) {
+        sym = gd.sym == 1;
+    } else if (gd.sorted) {
+        GraphDev probe = gd;   // csr_symmetric caches into its argument: keep the caller's handle const
+        if (csr_symmetric(probe, 0, n, 0, &sym) != MCMC_OK) sym = false;
+    }
     const uint32_t maxColors = gd.maxDeg + 1;   // :17 (getMaxNodeDeg() + 1)
     const uint32_t W = (maxColors + 31u) / 32u;
     MCMC_HIP_TRY(hipMemset(A, 0, sizeof(uint32_t) * n));

@@ -125,6 +125,7 @@ void help(const char* argv0) {
               << "  --outDir D           output directory\n"
               << "  --device D           HIP device (default 0)\n"
               << "  --gpus N             --mcmcgpu vertex-partitioned over devices D .. D+N-1 of this node\n"
+              << "  --loopback           with --gpus N: all N ranks on device D, exchanged by device copies (rehearsal)\n"
               << "                       (RCCL inside the library; arc-balanced plan for CSR graphs)\n";
 }
 
@@ -138,6 +139,7 @@ int main(int argc, char** argv) {
          tailcutRepair = false, mcmcgpuref = false, greedyff = false, lubygpu = false, vffgpu = false;
     uint64_t erSeed = 1;
     int device = 0, gpus = 1;
+    bool loopback = false;
     const struct option longopts[] = {
         {"graph", required_argument, 0, 'g'},    {"outDir", required_argument, 0, 'o'},
         {"simulate", required_argument, 0, 's'}, {"nodes", required_argument, 0, 'n'},
@@ -149,7 +151,7 @@ int main(int argc, char** argv) {
         {"seed", required_argument, 0, 'S'},     {"help", no_argument, 0, 'h'},
         {"device", required_argument, 0, 'D'},   {"simulate-fast", required_argument, 0, 'F'},
         {"er-seed", required_argument, 0, 'E'},  {"tailcutRepair", no_argument, 0, 'X'},
-        {"mcmcgpu-ref", no_argument, 0, 'G'},    {"gpus", required_argument, 0, 'P'},
+        {"mcmcgpu-ref", no_argument, 0, 'G'},    {"gpus", required_argument, 0, 'P'}, {"loopback", no_argument, 0, 'L'},
         {0, 0, 0, 0}};
     int c;
     while ((c = getopt_long(argc, argv, "g:o:s:n:12345k:r:t:lR:S:hD:", longopts, nullptr)) != -1) {
@@ -180,6 +182,7 @@ int main(int argc, char** argv) {
                 case 'X': tailcutRepair = true; break;
                 case 'G': mcmcgpuref = true; break;
                 case 'P': if (std::stoi(optarg) < 1) throw 1; gpus = std::stoi(optarg); break;
+                case 'L': loopback = true; break;
                 case 'h': help(argv[0]); return 0;
                 default: break;
             }
@@ -225,9 +228,8 @@ int main(int argc, char** argv) {
     mkdir(outDir.c_str(), 0775);
 
     const float numColorRatio = 1.0f / (float)numColRatio;        // main.cu:53
-    if (gpus > 1 && (mcmcgpuref || mcmccpu || greedyff || lubygpu || vffgpu || tailcutRepair)) {
-        std::cout << "--gpus > 1 partitions --mcmcgpu only (no --mcmcgpu-ref, --mcmccpu, other colorers or --tailcutRepair)"
-                  << std::endl;
+    if (gpus > 1 && (mcmcgpuref || mcmccpu || greedyff || lubygpu || vffgpu)) {
+        std::cout << "--gpus > 1 partitions --mcmcgpu only (no --mcmcgpu-ref, --mcmccpu or other colorers)" << std::endl;
         return 255;
     }
     Graph<float, float>* g;
@@ -239,8 +241,9 @@ int main(int argc, char** argv) {
             bounds.resize((size_t)gpus + 1);
             MCMC_CHECK(mcmc_part_plan_rows(n, (uint32_t)gpus, bounds.data()));
             for (int r = 0; r < gpus; r++)
-                parts.push_back(new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device + r,
-                                                        bounds[r], bounds[r + 1]));
+                parts.push_back(new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed,
+                                                        device + (loopback ? 0 : r), bounds[r], bounds[r + 1]));
+            Graph<float, float>::mergePartitionStats(parts);   // default nCol and reports: whole-graph stats
             g = parts[0];
         } else {
             g = new Graph<float, float>(Graph<float, float>::ErFast{}, n, (float)prob, erSeed, device);
@@ -249,7 +252,7 @@ int main(int argc, char** argv) {
         const mcmc::GlibcWindow w0 = mcmc::glibc_global();
         for (int r = 0; r < gpus; r++) {   // the exact graph on every device, from the same stream position
             mcmc::glibc_global() = w0;
-            parts.push_back(new Graph<float, float>(n, (float)prob, seed, device + r));
+            parts.push_back(new Graph<float, float>(n, (float)prob, seed, device + (loopback ? 0 : r)));
         }
         g = parts[0];
     } else {
@@ -258,7 +261,7 @@ int main(int argc, char** argv) {
         if (!import_edge_list(graphFilename, off, idx)) return 255;
         const uint32_t nn = (uint32_t)(off.size() - 1);
         const float p = (float)idx.size() / (float)(nn * nn);      // main.cu:68 (uint32 product, as the reference)
-        for (int r = 0; r < gpus; r++) parts.push_back(new Graph<float, float>(off, idx, p, device + r));
+        for (int r = 0; r < gpus; r++) parts.push_back(new Graph<float, float>(off, idx, p, device + (loopback ? 0 : r)));
         g = parts[0];
     }
     if (gpus > 1 && bounds.empty()) {   // CSR graphs: arc-balanced plan from the degree prefix

@@ -81,7 +81,9 @@ int tiled_to_csr(const mcmc_graph* gh, uint64_t* row_off, uint32_t* col_idx);
 namespace mcmc {
 // Row access for the tail cut (tailcut.hip): the CSR when the graph has one, else the tiled layout.
 struct TailView {
-    uint32_t n = 0;
+    uint32_t n = 0;                // rows (a partitioned context: its local rows)
+    uint32_t vb = 0;               // vertex of local row 0 (the replica's index of row l is vb + l)
+    uint32_t csr_row0 = 0;         // CSR row of local row 0 (row_off is the whole graph's; tiled: local)
     const uint64_t* row_off = nullptr;
     const uint32_t* col_idx = nullptr;
     const uint16_t* tcol = nullptr;
@@ -144,7 +146,11 @@ struct PartDesc {
     mcmc_comm* comm;             // nullptr: exchanged by the caller / the loopback transport
     uint32_t* events;            // the rank's sorted list of a paused (spill) sweep
     uint32_t maxRip;
+    uint32_t* dlt[2];            // delta slots (world x kDeltaWords words), sweep t's at dlt[(t+1) & 1]
+    bool delta_ok;               // the context can run delta-mode steps (tiled sweep with delta slots)
+    uint32_t tailcut_max;        // mcmc_set_tailcut_repair pass cap (0: off)
 };
+constexpr uint32_t kPartDeltaWords = 4096;   // = kDeltaWords (mcmc_sweep.hip): one rank's delta slot
 int part_desc(mcmc_ctx* c, PartDesc* d);
 // Hands a native partitioned context its buffers (one allocation, freed by mcmc_destroy), its own
 // stream (destroyed there too) and its communicator (borrowed).
@@ -153,6 +159,25 @@ int part_adopt(mcmc_ctx* c, void* mem, hipStream_t own_stream, mcmc_comm* comm);
 int part_spill_buffer(mcmc_ctx* c, uint32_t stride, uint32_t** buf);
 // Refreshes and returns the context's run summary (mcmc_part_state + the stats of mcmc_run).
 int part_stats(mcmc_ctx* c, mcmc_run_stats* s);
+// Delta exchange (native driver): the context's delta slot buffers (world x kPartDeltaWords words
+// each, owned by the caller's allocation); whether delta-mode steps are possible; a step's sweep
+// (delta: append changed vertices), its commit (mode 1 delta, 0 full, -1 full-mode resumption of
+// a paused sweep; spill: the gathered full event lists or nullptr), and the remote-range sync that
+// precedes delta mode after full-mode steps.
+int part_set_delta(mcmc_ctx* c, uint32_t* d0, uint32_t* d1);
+bool part_delta_ok(const mcmc_ctx* c);
+const void* part_state_ptr(const mcmc_ctx* c);   // device state: {t, done, x_t, err} in its first 16 bytes
+int part_sweep(mcmc_ctx* c, bool delta);
+int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride);
+int part_sync_remote(mcmc_ctx* c);
+int part_run_begin(mcmc_ctx* c);   // a run's start: this rank's delta slots empty, no tail-cut result
+// Partitioned tail cut (mcmc_sweep.hip): state and colorIdx at loop exit (global Cviol, the final t,
+// the final colouring's buffer); one rank's repair of its flagged rows; its recount (device sum
+// word); the result for the run summary.
+int part_tail_init(mcmc_ctx* c, uint64_t* cviol, uint32_t* t_final, uint8_t** colors);
+int part_tail_repair(mcmc_ctx* c, uint8_t* C, uint32_t t_final, bool first);
+int part_tail_count(mcmc_ctx* c, const uint8_t* C, unsigned long long** count);
+void part_tail_done(mcmc_ctx* c, uint64_t cviol, uint32_t passes);
 }  // namespace mcmc
 
 struct mcmc_graph {

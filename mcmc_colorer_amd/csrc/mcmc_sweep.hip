@@ -163,8 +163,20 @@ struct SweepArgs {
     uint32_t xs_S, xs_cbits;    // slab width (vertices), bits of the slab-local column
     uint32_t xs_nwg;            // LDS mode: workgroups of the scan launch
     uint32_t xs_sym;            // 1: one entry per local edge, flags both ends; 0: every arc, flags its row
+    // partitioned delta exchange (native driver, multi.hip): this rank's delta slots of parity 0 / 1
+    // ([0] pairs appended, [1] 0, then (v, c) pairs); dcap > 0: the sweep appends (delta mode)
+    uint32_t* dlt0;
+    uint32_t* dlt1;
+    uint32_t dcap;
+    const uint32_t* dall0;      // commit: every rank's slots of parity 0 / 1 (world x kDeltaWords)
+    const uint32_t* dall1;
+    int part_delta;             // commit: 1 delta mode (remote changes arrive as pairs, applied to both
+                                //   replicas), 0 full mode, -1 full-mode resumption of a paused sweep
 };
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
+constexpr uint32_t kDeltaWords = 4096;  // MCMC delta slot per rank: head + (v, c) pairs (16 KiB)
+constexpr uint32_t kDeltaHead = 2;
+constexpr uint32_t kDeltaPairs = (kDeltaWords - kDeltaHead) / 2;
 
 // Phase timestamps of the last sweep, 8 slots per workgroup (wall_clock64, 100 MHz): 0 start,
 // 1 first scan begins, 2 scans done, 3 evaluation done, 4 tail done (last workgroup: commit done).
@@ -356,6 +368,8 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             const uint32_t v = s[i];
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
             Cs[v] = (CT)c;
+            // delta mode: both replicas carry C_t+1 on the remote rows (part_commit_kernel)
+            if (a.part_delta > 0 && (v < a.v_begin || v >= a.v_end)) const_cast<CT*>(C)[v] = (CT)c;
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                 a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
@@ -519,6 +533,9 @@ constexpr uint32_t kFootFatal = 1u, kFootSpill = 2u;
 // DevState::err bits: 1 fatal, 2 paused for a spill exchange (st->done is set meanwhile, so every
 // kernel of the steps a driver enqueued before it noticed returns at once).
 constexpr uint32_t kErrFatal = 1u, kErrSpill = 2u;
+// bit 2: paused because some rank's delta slot overflowed (delta mode): the driver exchanges the
+// sweep's colour ranges instead and resumes with a full-mode commit (multi.hip)
+constexpr uint32_t kErrDelta = 4u;
 
 __device__ __forceinline__ uint32_t* rank_footer(const SweepArgs& a, uint32_t t, uint32_t r) {
     return ((t & 1) ? a.foot0 : a.foot1) + (size_t)r * kFooterWords;   // next-colour parity
@@ -572,18 +589,21 @@ template <typename CT>
 __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a, const uint32_t* spill,
                                                                      uint32_t stride) {
     __shared__ uint32_t lds[kLdsSortCap];
-    __shared__ uint32_t sh_go, sh_t, sh_E, sh_err, sh_spill;
+    __shared__ uint32_t sh_go, sh_t, sh_E, sh_err, sh_spill, sh_dovf;
     __shared__ unsigned long long sh_viol;
     __shared__ uint32_t sh_off[kMaxWorld + 1];
+    __shared__ uint32_t sh_dn[kMaxWorld];
     DevState* st = a.st;
     if (threadIdx.x == 0) {
         const uint32_t t0 = st->t;
-        // spill == nullptr: the step's own commit (skipped once done); else the resumption of a
-        // loop paused for this sweep's spill exchange
-        sh_go = spill ? ((st->err & kErrSpill) != 0u) : (st->done == 0u);
+        // spill == nullptr and not resuming: the step's own commit (skipped once done); else the
+        // resumption of a loop paused for this sweep's spill or delta-overflow exchange
+        const bool resume = spill != nullptr || (a.part_delta < 0);
+        sh_go = resume ? ((st->err & (kErrSpill | kErrDelta)) != 0u) : (st->done == 0u);
         sh_t = t0;
         unsigned long long v = 0;
-        uint32_t E = 0, err = st->err & kErrFatal, sp = 0;
+        uint32_t E = 0, err = st->err & kErrFatal, sp = 0, dovf = 0;
+        const uint32_t* dall = (t0 & 1) ? a.dall0 : a.dall1;   // next-colour parity, like the footers
         for (uint32_t r = 0; r < a.world; r++) {
             const uint32_t* f = rank_footer(a, t0, r);
             v += (unsigned long long)f[0] | ((unsigned long long)f[1] << 32);
@@ -591,24 +611,31 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
             E += spill ? f[2] : min(f[2], kFooterEvents);
             err |= f[3] & kFootFatal;
             sp |= f[3] & kFootSpill;
+            sh_dn[r] = 0;
+            if (a.part_delta > 0) {
+                const uint32_t k = dall[(size_t)r * kDeltaWords];
+                dovf |= k > kDeltaPairs ? 1u : 0u;
+                sh_dn[r] = min(k, kDeltaPairs);
+            }
         }
         sh_off[a.world] = E;
         sh_viol = v;
         sh_E = E;
         sh_err = err;
-        sh_spill = sp;
-        if (sh_go && spill) {
+        sh_spill = spill ? 0u : sp;
+        sh_dovf = dovf;
+        if (sh_go && resume) {
             st->done = 0;
-            st->err &= ~kErrSpill;
+            st->err &= ~(kErrSpill | kErrDelta);
         }
     }
     __syncthreads();
     if (!sh_go) return;
     const uint32_t t = sh_t;
     const bool stop = t == a.maxRip + 1 || (!a.bench && sh_viol <= a.z);
-    if (!spill && sh_spill && !stop && !sh_err) {   // pause: the driver gathers the full lists
+    if ((sh_spill || sh_dovf) && !stop && !sh_err) {   // pause: the driver gathers lists / colour ranges
         if (threadIdx.x == 0) {
-            st->err |= kErrSpill;
+            st->err |= (sh_spill ? kErrSpill : 0u) | (sh_dovf ? kErrDelta : 0u);
             st->done = 1;
         }
         return;
@@ -619,9 +646,53 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
             const uint32_t Er = sh_off[r + 1] - sh_off[r];
             for (uint32_t i = threadIdx.x; i < Er; i += blockDim.x) a.events[sh_off[r] + i] = src[i];
         }
+        if (a.part_delta > 0) {
+            // the other ranks' changed vertices into both replicas: C_t+1 (this sweep's output)
+            // and the C_t buffer, which sweep t+1 overwrites only on this rank's rows -- so after
+            // every delta-mode commit both replicas hold C_t+1 outside the local range
+            CT* B = reinterpret_cast<CT*>((t & 1) ? a.colors0 : a.colors1);
+            CT* A = reinterpret_cast<CT*>((t & 1) ? a.colors1 : a.colors0);
+            const uint32_t* dall = (t & 1) ? a.dall0 : a.dall1;
+            for (uint32_t r = 0; r < a.world; r++) {
+                if (r == a.rank) continue;
+                const uint32_t* d = dall + (size_t)r * kDeltaWords + kDeltaHead;
+                for (uint32_t i = threadIdx.x; i < sh_dn[r]; i += blockDim.x) {
+                    const uint32_t v = d[2u * i];
+                    const CT c = (CT)d[2u * i + 1u];
+                    B[v] = c;
+                    A[v] = c;
+                }
+            }
+        }
+        // this rank's slot for sweep t + 1 starts empty
+        if (threadIdx.x == 0 && a.dlt0) ((t & 1) ? a.dlt1 : a.dlt0)[0] = 0u;
     }
     __syncthreads();
     commit_control<CT>(a, t, sh_viol, sh_E, sh_err, lds, kLdsSortCap);
+}
+
+// Delta mode needs both replicas equal outside this rank's rows: after a full-mode step (or at the
+// start of a run) the next-colour buffer's remote part is set to the current colouring's.
+template <typename CT>
+__global__ __launch_bounds__(256) void part_sync_remote_kernel(SweepArgs a) {
+    const DevState* st = a.st;
+    if (st->done) return;
+    const uint32_t t = st->t;
+    const uint8_t* src = (t & 1) ? a.colors1 : a.colors0;   // C_t
+    uint8_t* dst = (t & 1) ? a.colors0 : a.colors1;
+    const size_t cb = sizeof(CT);
+    const size_t r0[2] = {0, (size_t)a.v_end * cb};
+    const size_t r1[2] = {(size_t)a.v_begin * cb, (size_t)a.n * cb};
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < 2; k++) {
+        const size_t b0 = r0[k], b1 = r1[k];
+        if (b1 <= b0) continue;
+        const size_t q0 = (b0 + 15) & ~(size_t)15, q1 = (b1 & ~(size_t)15) > q0 ? (b1 & ~(size_t)15) : q0;
+        for (size_t i = q0 + 16 * tid; i < q1; i += 16 * nth)
+            *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+        for (size_t i = b0 + tid; i < (q0 < b1 ? q0 : b1); i += nth) dst[i] = src[i];
+        for (size_t i = q1 + tid; i < b1; i += nth) dst[i] = src[i];
+    }
 }
 
 // The wide sweep's partitioned footer (its kernels have no fused last-workgroup step): this
@@ -706,6 +777,25 @@ __device__ __forceinline__ uint32_t evaluate_core(const SweepArgs& a, DevState* 
             if (a.taboo != nullptr) a.taboo[l] = (newc == cv) ? a.tabooIteration : 0u;
         } else {
             Cs[v] = (uint8_t)cv;   // placeholder, overwritten by the commit's glibc replay
+        }
+    }
+
+    // partitioned delta exchange (a.dcap > 0): this rank's vertices whose colour changed, as (v, c)
+    // pairs in its delta slot of the next-colour parity; overflow events are left out (every rank
+    // replays them), so a slot lists exactly the other vertices where C_t+1 differs from C_t
+    if (a.dcap) {
+        const bool chg = valid && tab == 0 && !event && newc != cv;
+        const uint64_t cb = __ballot(chg);
+        if (cb) {
+            uint32_t* dl = (Cs == a.colors1) ? a.dlt1 : a.dlt0;
+            uint32_t based = 0;
+            if (lane == 0) based = atomicAdd(dl, (uint32_t)__popcll(cb));
+            based = __shfl(based, 0, 64);
+            const uint32_t idx = based + (uint32_t)__popcll(cb & ((1ull << lane) - 1ull));
+            if (chg && idx < a.dcap) {
+                dl[kDeltaHead + 2u * idx] = v;
+                dl[kDeltaHead + 2u * idx + 1u] = newc;
+            }
         }
     }
 
@@ -2073,6 +2163,10 @@ struct mcmc_ctx {
     uint32_t world = 1, rank = 0;
     std::vector<uint32_t> bounds;            // partitioned: rank r sweeps rows [bounds[r], bounds[r+1])
     uint32_t* foot[2] = {nullptr, nullptr};  // partitioned: footer buffers, world x kFooterWords each
+    uint32_t* dlt[2] = {nullptr, nullptr};   // native partitioned: delta slots, world x kDeltaWords each
+    bool tail_done = false;                  // partitioned tail cut ran after the loop (multi.hip)
+    uint32_t tail_passes = 0;
+    uint64_t tail_viol = 0;
     void* own_part = nullptr;                // native partitioned contexts: their own colour + footer buffers
     mcmc_comm* comm = nullptr;               // native partitioned contexts: the RCCL communicator (borrowed)
     uint32_t* spill = nullptr;               // native spill exchange: gathered lists, world x spill_stride
@@ -2192,6 +2286,12 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.foot0 = c->foot[0];
         a.foot1 = c->foot[1];
         a.rank = c->rank;
+        if (c->dlt[0]) {
+            a.dall0 = c->dlt[0];
+            a.dall1 = c->dlt[1];
+            a.dlt0 = c->dlt[0] + (size_t)c->rank * kDeltaWords;
+            a.dlt1 = c->dlt[1] + (size_t)c->rank * kDeltaWords;
+        }
     }
     a.world = c->world;
     a.lds_sort_cap = (uint32_t)(c->lds / 4);
@@ -2335,10 +2435,12 @@ int ensure_tail_buffers(mcmc_ctx* c) {
 
 TailView tail_view(const mcmc_ctx* c) {
     TailView tv;
-    tv.n = c->n;
+    tv.n = c->v_end - c->v_begin;   // a partitioned context's own rows
+    tv.vb = c->v_begin;
     if (c->g->row_off) {
         tv.row_off = c->g->row_off;
         tv.col_idx = c->g->col_idx;
+        tv.csr_row0 = c->v_begin;
     } else {
         tv.tcol = c->tl->tcol;
         tv.gbase = c->tl->gbase;
@@ -2990,14 +3092,14 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
         s.iter = h.iter;
         s.maxIterReached = (int32_t)h.maxIterReached;
         s.finalViol = h.finalViol;
-        s.trajLen = (uint64_t)h.iter + 1;
+        s.trajLen = std::min<uint64_t>((uint64_t)h.iter + 1, c->traj_cap);   // entries kept
         s.sweepsRun = h.iter + 1;
     } else {
         // early stop (max_sweeps): h.t sweeps accepted, no final count
         s.iter = h.t;
         s.maxIterReached = 0;
         s.finalViol = ~0ull;
-        s.trajLen = h.t;
+        s.trajLen = std::min<uint64_t>(h.t, c->traj_cap);
         s.sweepsRun = h.t;
     }
     s.glibcDraws = h.glibc_draws;
@@ -3080,8 +3182,8 @@ int mcmc_set_bench_mode(mcmc_ctx* c, int on) {
 
 int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
-    if (c->part || c->v_begin != 0 || c->v_end != c->n)
-        return fail(MCMC_E_STATE, "tail cutting runs on whole-graph contexts (mcmc_run)");
+    if (!c->part && (c->v_begin != 0 || c->v_end != c->n))
+        return fail(MCMC_E_STATE, "tail cutting runs on whole-graph (mcmc_run) or partitioned (mcmc_part_run) contexts");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (max_passes) {
         int rc = ensure_tail_buffers(c);
@@ -3169,7 +3271,7 @@ int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats) {
     st.iter = h.iter;                             // rip
     st.maxIterReached = (int32_t)h.maxIterReached;
     st.finalViol = h.finalViol;                   // conflicting edges of the returned colouring
-    st.trajLen = (uint64_t)h.t + 1;
+    st.trajLen = std::min<uint64_t>((uint64_t)h.t + 1, c->traj_cap);
     st.sweepsRun = (h.t == cap) ? cap : h.t;      // selectStar launches of the reference
     st.initDraws = c->n;
     st.loopMs = ms;
@@ -3431,6 +3533,10 @@ int part_desc(mcmc_ctx* c, PartDesc* d) {
     d->comm = c->comm;
     d->events = c->events;
     d->maxRip = c->p.maxRip;
+    d->dlt[0] = c->dlt[0];
+    d->dlt[1] = c->dlt[1];
+    d->delta_ok = part_delta_ok(c);
+    d->tailcut_max = c->tailcut_max;
     return MCMC_OK;
 }
 
@@ -3450,6 +3556,123 @@ int part_stats(mcmc_ctx* c, mcmc_run_stats* s) {
     if (rc) return rc;
     *s = c->last;
     return MCMC_OK;
+}
+
+int part_set_delta(mcmc_ctx* c, uint32_t* d0, uint32_t* d1) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "not a partitioned context");
+    c->dlt[0] = d0;
+    c->dlt[1] = d1;
+    return MCMC_OK;
+}
+
+bool part_delta_ok(const mcmc_ctx* c) { return c && c->part && c->dlt[0] && !c->wide; }
+
+const void* part_state_ptr(const mcmc_ctx* c) { return c->st; }
+static_assert(kDeltaWords == kPartDeltaWords, "delta slot size");
+static_assert(offsetof(DevState, t) == 0 && offsetof(DevState, done) == 4 && offsetof(DevState, err) == 12,
+              "part_state_ptr readers take {t, done, x_t, err} from the first 16 bytes");
+
+int part_sweep(mcmc_ctx* c, bool delta) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
+    if (delta && !part_delta_ok(c)) return fail(MCMC_E_STATE, "delta exchange: tiled partitioned contexts only");
+    c->ran = true;
+    SweepArgs a = make_args(c, 1);
+    a.dcap = delta ? kDeltaPairs : 0u;
+    launch_tiled_or_diag(c, a);
+    if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
+}
+
+int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    if (mode > 0 && !part_delta_ok(c)) return fail(MCMC_E_STATE, "delta exchange: tiled partitioned contexts only");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    SweepArgs a = make_args(c, 1);
+    a.part_delta = mode;
+    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a, spill, stride);
+    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a, spill, stride);
+    MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
+}
+
+int part_sync_remote(mcmc_ctx* c) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    SweepArgs a = make_args(c, 1);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, ((uint64_t)c->n * c->cbytes / 16 + 255) / 256 + 1);
+    if (c->wide) part_sync_remote_kernel<uint16_t><<<blocks, 256, 0, c->stream>>>(a);
+    else part_sync_remote_kernel<uint8_t><<<blocks, 256, 0, c->stream>>>(a);
+    MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
+}
+
+int part_run_begin(mcmc_ctx* c) {
+    c->tail_done = false;
+    if (!part_delta_ok(c)) return MCMC_OK;
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    for (int k = 0; k < 2; k++)
+        MCMC_HIP_TRY(hipMemsetAsync(c->dlt[k] + (size_t)c->rank * kDeltaWords, 0, sizeof(uint32_t) * kDeltaHead,
+                                    c->stream));
+    return MCMC_OK;
+}
+
+// ---- partitioned tail cut (coloringMCMC_CPU.cpp:272-311, corrected), driven by multi.hip --------
+// The reference's repair pass is sequential in ascending vertex order; ranks own ascending ranges,
+// so a pass runs rank by rank: rank r repairs its flagged rows on its replica (seeing the colours
+// earlier ranks repaired in this pass), then its range is broadcast; the recount is per rank plus a
+// sum. Exactly the single-context pass (tests/test_multi.py::test_native_loopback_tailcut*).
+int part_tail_init(mcmc_ctx* c, uint64_t* cviol, uint32_t* t_final, uint8_t** colors) {
+    if (!c || !c->part || !c->tailcut_max) return fail(MCMC_E_STATE, "partitioned context with tail cutting");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    DevState h{};
+    if (int rc = download_state(c, &h)) return rc;
+    if (!h.done || (h.err & (kErrFatal | kErrSpill | kErrDelta))) return fail(MCMC_E_STATE, "the loop has not finished");
+    *cviol = h.finalViol;
+    *t_final = h.t;
+    *colors = c->colors[h.t & 1u];
+    const uint32_t nCol = c->p.nCol;
+    std::vector<size_t> colorIdx(nCol);   // identity (:131-132), by ascending histogram when z > 0 (:272-278)
+    for (uint32_t i = 0; i < nCol; i++) colorIdx[i] = i;
+    if (c->z > 0) {
+        std::vector<uint8_t> hc((size_t)c->n * c->cbytes);
+        if (int rc = download_colors(c, *colors, hc.data())) return rc;
+        std::vector<size_t> histBins(nCol, 0);
+        for (uint32_t v = 0; v < c->n; v++)
+            histBins[c->cbytes == 2 ? reinterpret_cast<const uint16_t*>(hc.data())[v] : hc[v]]++;
+        std::sort(colorIdx.begin(), colorIdx.end(), [&](int i, int j) { return histBins[i] < histBins[j]; });
+    }
+    std::vector<uint32_t> ci(colorIdx.begin(), colorIdx.end());
+    MCMC_HIP_TRY(hipMemcpyAsync(c->tc_colorIdx, ci.data(), sizeof(uint32_t) * nCol, hipMemcpyHostToDevice, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    c->tail_traj.clear();
+    return MCMC_OK;
+}
+
+// One rank's share of a pass: its flagged rows (first pass: the flags of the colouring before the
+// last accepted sweep, as run_tailcut) repaired in order on the replica `C`.
+int part_tail_repair(mcmc_ctx* c, uint8_t* C, uint32_t t_final, bool first) {
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    const uint32_t nloc = c->v_end - c->v_begin;
+    const uint8_t* flags = c->vflags + (first ? (size_t)(t_final >= 1 ? (t_final - 1u) & 1u : 0u) * nloc : 0);
+    if (int rc = tail_select(flags, nloc, c->tc_list, c->tc_len, &c->tc_tmp, &c->tc_tmp_bytes, c->stream)) return rc;
+    return tail_repair(tail_view(c), C, c->cbytes, c->tc_list, c->tc_len, c->tc_colorIdx, c->p.nCol, c->stream, false,
+                       ~0ull);
+}
+
+// The recount of this rank's rows (:308) into its flags; *count: the device word holding the sum.
+int part_tail_count(mcmc_ctx* c, const uint8_t* C, unsigned long long** count) {
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    *count = c->tc_count;
+    return tail_count(tail_view(c), C, c->cbytes, c->vflags, c->tc_count, c->stream, false);
+}
+
+void part_tail_done(mcmc_ctx* c, uint64_t cviol, uint32_t passes) {
+    c->tail_done = true;
+    c->tail_passes = passes;
+    c->tail_viol = cviol;
 }
 
 int part_spill_buffer(mcmc_ctx* c, uint32_t stride, uint32_t** buf) {
@@ -3577,27 +3800,9 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t*
     return MCMC_OK;
 }
 
-int mcmc_part_sweep_async(mcmc_ctx* c) {
-    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
-    MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
-    c->ran = true;
-    SweepArgs a = make_args(c, 1);
-    launch_tiled_or_diag(c, a);
-    if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
-    MCMC_HIP_TRY(hipGetLastError());
-    return MCMC_OK;
-}
+int mcmc_part_sweep_async(mcmc_ctx* c) { return part_sweep(c, false); }
 
-int mcmc_part_commit_async(mcmc_ctx* c) {
-    if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
-    MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    SweepArgs a = make_args(c, 1);
-    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a, nullptr, 0u);
-    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a, nullptr, 0u);
-    MCMC_HIP_TRY(hipGetLastError());
-    return MCMC_OK;
-}
+int mcmc_part_commit_async(mcmc_ctx* c) { return part_commit(c, 0, nullptr, 0u); }
 
 int mcmc_part_spill_counts(mcmc_ctx* c, uint32_t* counts) {
     if (!c || !c->part || !counts) return fail(MCMC_E_STATE, "partitioned context and counts required");
@@ -3627,12 +3832,7 @@ int mcmc_part_spill_local(mcmc_ctx* c, void* dst, uint32_t* count) {
 
 int mcmc_part_spill_commit_async(mcmc_ctx* c, const uint32_t* gathered, uint32_t stride) {
     if (!c || !c->part || !gathered) return fail(MCMC_E_ARG, "NULL argument");
-    MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    SweepArgs a = make_args(c, 1);
-    if (c->wide) part_commit_kernel<uint16_t><<<1, kCommitThreads, 0, c->stream>>>(a, gathered, stride);
-    else part_commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a, gathered, stride);
-    MCMC_HIP_TRY(hipGetLastError());
-    return MCMC_OK;
+    return part_commit(c, 0, gathered, stride);
 }
 
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {
@@ -3641,7 +3841,7 @@ int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {
     DevState h{};
     int rc = download_state(c, &h);
     if (rc) return rc;
-    const bool fin = h.done && !(h.err & kErrSpill);   // paused for a spill exchange: not done
+    const bool fin = h.done && !(h.err & (kErrSpill | kErrDelta));   // paused for an exchange: not done
     if (done) *done = fin ? 1 : 0;
     if (t) *t = h.t;
     if (err) *err = h.err;
@@ -3649,11 +3849,13 @@ int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {
         c->last.iter = h.iter;
         c->last.maxIterReached = (int32_t)h.maxIterReached;
         c->last.finalViol = h.finalViol;
-        c->last.trajLen = (uint64_t)h.iter + 1;
+        c->last.trajLen = std::min<uint64_t>((uint64_t)h.iter + 1, c->traj_cap);
         c->last.sweepsRun = h.iter + 1;
+        c->last.tailcutPasses = c->tail_done ? c->tail_passes : 0u;
+        if (c->tail_done) c->last.finalViol = c->tail_viol;
     } else {
         c->last.iter = h.t;
-        c->last.trajLen = h.t;
+        c->last.trajLen = std::min<uint64_t>(h.t, c->traj_cap);
         c->last.finalViol = ~0ull;
     }
     c->last.glibcDraws = h.glibc_draws;

@@ -56,13 +56,30 @@ uint32_t equal_stride(const PartDesc& d) {
     return S;
 }
 
-// MCMC_EXCHANGE = p2p (default) | allgather. xGMI is a full mesh of point-to-point links: every
-// rank's range goes to each peer over its own link, all links at once (7 x n/8 bytes per rank at
-// 8 GPUs); the ring all-gather (equal-stride plans only) moves the same bytes through 7 hops.
+// MCMC_EXCHANGE = delta (default) | p2p | allgather.
+//   delta: a step sends only this rank's changed vertices (its delta slot, 16 KiB) and footer to
+//          every peer; a slot that overflows pauses that sweep, which is then exchanged in full,
+//          and the next kFullAfterOverflow steps run in full mode before delta mode resumes;
+//   p2p:   every step sends this rank's whole row range to every peer (xGMI is a full mesh of
+//          point-to-point links: each range rides its own link, all links at once);
+//   allgather: equal-stride plans only, one in-place all-gather of the replica per step.
 int exchange_mode() {
     const char* e = getenv("MCMC_EXCHANGE");
-    return (e && !strcmp(e, "allgather")) ? 2 : 1;
+    if (e && !strcmp(e, "allgather")) return 2;
+    if (e && !strcmp(e, "p2p")) return 1;
+    return 0;
 }
+constexpr uint32_t kFullAfterOverflow = 16;
+constexpr uint32_t kStepsPerPoll = 8;   // steps enqueued per batch; the host polls one batch behind
+
+// hipEvent owned for a scope (every early return releases it).
+struct EventGuard {
+    hipEvent_t e = nullptr;
+    int device = 0;
+    ~EventGuard() {
+        if (e) { (void)hipSetDevice(device); (void)hipEventDestroy(e); }
+    }
+};
 
 struct Driver {
     std::vector<mcmc_ctx*> ctx;
@@ -71,10 +88,17 @@ struct Driver {
     bool rccl = false;
     uint32_t world = 1;
     int mode = 0;
+    bool delta_ok = false;        // every local context can run delta-mode steps
+    bool synced = false;          // delta invariant: both replicas hold the current colouring off the local rows
+    hipStream_t poll = nullptr;   // side stream of ctx[0]'s device: reads the device state while steps run
+    uint32_t* pinned = nullptr;   // host-pinned copy of the state's first words {t, done, x_t, err}
 
     ~Driver() {
         for (size_t i = 0; i < ev.size(); i++)
             if (ev[i]) { (void)hipSetDevice(d[i].device); (void)hipEventDestroy(ev[i]); }
+        if (!d.empty()) (void)hipSetDevice(d[0].device);
+        if (poll) (void)hipStreamDestroy(poll);
+        if (pinned) (void)hipHostFree(pinned);
     }
 
     int setup(mcmc_ctx** cs, uint32_t k) {
@@ -101,53 +125,80 @@ struct Driver {
             }
         }
         mode = exchange_mode();
+        // delta mode needs the same decision on every rank: it depends only on the sweep kind
+        // (uint8 tiled sweep), which every rank of a partition shares
+        delta_ok = mode == 0 && world > 1;
+        for (auto& x : d) delta_ok = delta_ok && x.delta_ok;
+        MCMC_HIP_TRY(hipSetDevice(d[0].device));
+        MCMC_HIP_TRY(hipStreamCreateWithFlags(&poll, hipStreamNonBlocking));
+        MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pinned), 16, hipHostMallocDefault));
+        for (auto* c : ctx)
+            if (int rc = part_run_begin(c)) return rc;
         return MCMC_OK;
     }
 
-    int exchange(uint32_t t) {
+    // Step t's exchange. delta: footers + delta slots; else footers + the row ranges.
+    int exchange(uint32_t t, bool delta) {
         const uint32_t nb = (t + 1) & 1u;
         if (rccl) {
+            if (world == 1) return MCMC_OK;   // nothing leaves the rank
             const uint32_t S = equal_stride(d[0]);
-            const bool ag = S != 0 && mode == 2;   // equal-stride ranges may take one in-place all-gather
-            if (world > 1) {
+            if (!delta && S != 0 && mode == 2) {   // equal-stride ranges: two in-place all-gathers
                 MCMC_NCCL_TRY(ncclGroupStart());
                 for (auto& x : d) {
                     uint8_t* C = x.colors[nb];
-                    ncclComm_t cm = x.comm->comm;
-                    if (ag) {
-                        MCMC_NCCL_TRY(ncclAllGather(C + (size_t)x.rank * S * x.cbytes, C, (size_t)S * x.cbytes, ncclUint8,
-                                                    cm, x.stream));
-                        continue;
-                    }
-                    const size_t b0 = x.bounds[x.rank], len = x.bounds[x.rank + 1] - b0;
-                    for (uint32_t q = 0; q < world; q++) {
-                        if (q == x.rank) continue;
+                    MCMC_NCCL_TRY(ncclAllGather(C + (size_t)x.rank * S * x.cbytes, C, (size_t)S * x.cbytes, ncclUint8,
+                                                x.comm->comm, x.stream));
+                    MCMC_NCCL_TRY(ncclAllGather(x.foot[nb] + (size_t)x.rank * MCMC_FOOTER_WORDS, x.foot[nb],
+                                                MCMC_FOOTER_WORDS, ncclUint32, x.comm->comm, x.stream));
+                }
+                MCMC_NCCL_TRY(ncclGroupEnd());
+                return MCMC_OK;
+            }
+            // one group of point-to-point transfers: to every peer this rank's footer slot and
+            // either its delta slot or its row range; from every peer the same
+            MCMC_NCCL_TRY(ncclGroupStart());
+            for (auto& x : d) {
+                ncclComm_t cm = x.comm->comm;
+                const size_t b0 = x.bounds[x.rank], len = x.bounds[x.rank + 1] - b0;
+                for (uint32_t q = 0; q < world; q++) {
+                    if (q == x.rank) continue;
+                    MCMC_NCCL_TRY(ncclSend(x.foot[nb] + (size_t)x.rank * MCMC_FOOTER_WORDS, MCMC_FOOTER_WORDS, ncclUint32,
+                                           (int)q, cm, x.stream));
+                    MCMC_NCCL_TRY(ncclRecv(x.foot[nb] + (size_t)q * MCMC_FOOTER_WORDS, MCMC_FOOTER_WORDS, ncclUint32,
+                                           (int)q, cm, x.stream));
+                    if (delta) {
+                        MCMC_NCCL_TRY(ncclSend(x.dlt[nb] + (size_t)x.rank * kPartDeltaWords, kPartDeltaWords, ncclUint32,
+                                               (int)q, cm, x.stream));
+                        MCMC_NCCL_TRY(ncclRecv(x.dlt[nb] + (size_t)q * kPartDeltaWords, kPartDeltaWords, ncclUint32,
+                                               (int)q, cm, x.stream));
+                    } else {
+                        uint8_t* C = x.colors[nb];
                         MCMC_NCCL_TRY(ncclSend(C + b0 * x.cbytes, len * x.cbytes, ncclUint8, (int)q, cm, x.stream));
                         const size_t c0 = x.bounds[q], clen = x.bounds[q + 1] - c0;
                         MCMC_NCCL_TRY(ncclRecv(C + c0 * x.cbytes, clen * x.cbytes, ncclUint8, (int)q, cm, x.stream));
                     }
                 }
-                MCMC_NCCL_TRY(ncclGroupEnd());
             }
-            // footers: one in-place all-gather (also at world 1, where it is the only collective)
-            MCMC_NCCL_TRY(ncclGroupStart());
-            for (auto& x : d)
-                MCMC_NCCL_TRY(ncclAllGather(x.foot[nb] + (size_t)x.rank * MCMC_FOOTER_WORDS, x.foot[nb], MCMC_FOOTER_WORDS,
-                                            ncclUint32, x.comm->comm, x.stream));
             MCMC_NCCL_TRY(ncclGroupEnd());
             return MCMC_OK;
         }
-        // loopback: rank r copies its rows and footer slot into every peer's buffers on its own
-        // stream; every peer's commit waits for all of them
+        // loopback: rank r copies its footer slot and its delta slot or rows into every peer's
+        // buffers on its own stream; every peer's commit waits for all of them
         for (uint32_t r = 0; r < world; r++) {
             const PartDesc& x = d[r];
             MCMC_HIP_TRY(hipSetDevice(x.device));
             const size_t b0 = x.bounds[r], len = x.bounds[r + 1] - b0;
             for (uint32_t q = 0; q < world; q++) {
                 if (q == r) continue;
-                if (len)
+                if (delta) {
+                    MCMC_HIP_TRY(hipMemcpyAsync(d[q].dlt[nb] + (size_t)r * kPartDeltaWords,
+                                                x.dlt[nb] + (size_t)r * kPartDeltaWords, 4u * kPartDeltaWords,
+                                                hipMemcpyDefault, x.stream));
+                } else if (len) {
                     MCMC_HIP_TRY(hipMemcpyAsync(d[q].colors[nb] + b0 * x.cbytes, x.colors[nb] + b0 * x.cbytes,
                                                 len * x.cbytes, hipMemcpyDefault, x.stream));
+                }
                 MCMC_HIP_TRY(hipMemcpyAsync(d[q].foot[nb] + (size_t)r * MCMC_FOOTER_WORDS,
                                             x.foot[nb] + (size_t)r * MCMC_FOOTER_WORDS, kFootBytes, hipMemcpyDefault,
                                             x.stream));
@@ -162,12 +213,28 @@ struct Driver {
         return MCMC_OK;
     }
 
-    // The paused sweep's full lists: all-gathered with stride = the longest, then committed.
-    int spill() {
+    // One step: sweep (every local rank) -> exchange -> commit. A delta-mode step after full-mode
+    // ones first makes both replicas equal off the local rows (part_sync_remote).
+    int step(uint32_t t, bool delta) {
+        if (delta && !synced) {
+            for (auto* c : ctx)
+                if (int rc = part_sync_remote(c)) return rc;
+        }
+        synced = delta;
+        for (auto* c : ctx)
+            if (int rc = part_sweep(c, delta)) return rc;
+        if (int rc = exchange(t, delta)) return rc;
+        for (auto* c : ctx)
+            if (int rc = part_commit(c, delta ? 1 : 0, nullptr, 0u)) return rc;
+        return MCMC_OK;
+    }
+
+    // The paused sweep's full lists: all-gathered with stride = the longest (rank order).
+    int spill_gather(std::vector<uint32_t*>& buf, uint32_t* stride_out) {
         std::vector<uint32_t> cnt(world, 0);
         if (int rc = mcmc_part_spill_counts(ctx[0], cnt.data())) return rc;
         const uint32_t stride = std::max<uint32_t>(1u, *std::max_element(cnt.begin(), cnt.end()));
-        std::vector<uint32_t*> buf(d.size());
+        buf.assign(d.size(), nullptr);
         for (size_t i = 0; i < d.size(); i++) {
             MCMC_HIP_TRY(hipSetDevice(d[i].device));
             if (int rc = part_spill_buffer(ctx[i], stride, &buf[i])) return rc;
@@ -178,22 +245,119 @@ struct Driver {
                 MCMC_NCCL_TRY(ncclAllGather(d[i].events, buf[i], stride, ncclUint32, d[i].comm->comm, d[i].stream));
             MCMC_NCCL_TRY(ncclGroupEnd());
         } else {
-            for (uint32_t r = 0; r < world; r++) {   // rare: plain synchronous copies
-                MCMC_HIP_TRY(hipSetDevice(d[r].device));
-                MCMC_HIP_TRY(hipStreamSynchronize(d[r].stream));
-            }
             for (uint32_t q = 0; q < world; q++)
                 for (uint32_t r = 0; r < world; r++)
                     if (cnt[r])
                         MCMC_HIP_TRY(hipMemcpy(buf[q] + (size_t)r * stride, d[r].events, sizeof(uint32_t) * cnt[r],
                                                hipMemcpyDefault));
         }
-        for (size_t i = 0; i < d.size(); i++)
-            if (int rc = mcmc_part_spill_commit_async(ctx[i], buf[i], stride)) return rc;
+        *stride_out = stride;
         return MCMC_OK;
     }
-};
 
+    int drain() {
+        for (auto& x : d) {
+            MCMC_HIP_TRY(hipSetDevice(x.device));
+            MCMC_HIP_TRY(hipStreamSynchronize(x.stream));
+        }
+        return MCMC_OK;
+    }
+
+    // A sweep paused at td (err bits 2 spill, 4 delta overflow; the queue drained): the full event
+    // lists and/or the sweep's row ranges, then its commit. delta_step: td ran in delta mode.
+    int resume(uint32_t td, uint32_t err, bool delta_step) {
+        std::vector<uint32_t*> buf;
+        uint32_t stride = 0;
+        if ((err & 2u) && (rc_ = spill_gather(buf, &stride))) return rc_;
+        const bool full = (err & 4u) != 0;   // a delta slot overflowed: the rows travel in full
+        if (full && (rc_ = exchange(td, false))) return rc_;
+        for (size_t i = 0; i < d.size(); i++) {
+            const int m = full ? -1 : (delta_step ? 1 : 0);
+            if (buf.empty() && m >= 0) return fail(MCMC_E_STATE, "nothing to resume");
+            if ((rc_ = part_commit(ctx[i], m, buf.empty() ? nullptr : buf[i], stride))) return rc_;
+        }
+        synced = delta_step && !full;
+        return MCMC_OK;
+    }
+
+    // ctx[0]'s {t, done, err} read on the side stream once `e` (end of a batch) has passed; the
+    // steps enqueued after it keep the GPU busy meanwhile.
+    int peek(hipEvent_t e, uint32_t* t, uint32_t* done, uint32_t* err) {
+        MCMC_HIP_TRY(hipSetDevice(d[0].device));
+        MCMC_HIP_TRY(hipStreamWaitEvent(poll, e, 0));
+        MCMC_HIP_TRY(hipMemcpyAsync(pinned, part_state_ptr(ctx[0]), 16, hipMemcpyDeviceToHost, poll));
+        MCMC_HIP_TRY(hipStreamSynchronize(poll));
+        *t = pinned[0];
+        *done = pinned[1];
+        *err = pinned[3];
+        return MCMC_OK;
+    }
+
+    // The corrected tail cut after the loop, rank by rank in ascending order (part_tail_*).
+    int tailcut() {
+        std::vector<uint64_t> cv(d.size());
+        std::vector<uint32_t> tf(d.size());
+        std::vector<uint8_t*> C(d.size());
+        for (size_t i = 0; i < d.size(); i++)
+            if ((rc_ = part_tail_init(ctx[i], &cv[i], &tf[i], &C[i]))) return rc_;
+        uint64_t cviol = cv[0];
+        uint32_t passes = 0;
+        const uint32_t cap = d[0].tailcut_max;
+        unsigned long long* hsum = reinterpret_cast<unsigned long long*>(pinned);
+        while (cviol > 0 && passes < cap) {
+            for (uint32_t r = 0; r < world; r++) {
+                for (size_t i = 0; i < d.size(); i++)
+                    if (d[i].rank == r && (rc_ = part_tail_repair(ctx[i], C[i], tf[i], passes == 0))) return rc_;
+                // rank r's rows as repaired: to every other rank before the next rank's turn
+                const size_t b0 = d[0].bounds[r], len = d[0].bounds[r + 1] - b0;
+                if (world == 1 || len == 0) continue;
+                if (rccl) {
+                    MCMC_NCCL_TRY(ncclGroupStart());
+                    for (size_t i = 0; i < d.size(); i++)
+                        MCMC_NCCL_TRY(ncclBroadcast(C[i] + b0 * d[i].cbytes, C[i] + b0 * d[i].cbytes, len * d[i].cbytes,
+                                                    ncclUint8, (int)r, d[i].comm->comm, d[i].stream));
+                    MCMC_NCCL_TRY(ncclGroupEnd());
+                } else {
+                    if ((rc_ = drain())) return rc_;
+                    for (uint32_t q = 0; q < world; q++)
+                        if (q != r)
+                            MCMC_HIP_TRY(hipMemcpy(C[q] + b0 * d[q].cbytes, C[r] + b0 * d[r].cbytes, len * d[r].cbytes,
+                                                   hipMemcpyDefault));
+                }
+            }
+            // recount (:308): every rank its rows, summed over the ranks
+            uint64_t tot = 0;
+            std::vector<unsigned long long*> cnt(d.size());
+            for (size_t i = 0; i < d.size(); i++)
+                if ((rc_ = part_tail_count(ctx[i], C[i], &cnt[i]))) return rc_;
+            if (rccl) {
+                if (world > 1) {
+                    MCMC_NCCL_TRY(ncclGroupStart());
+                    for (size_t i = 0; i < d.size(); i++)
+                        MCMC_NCCL_TRY(ncclAllReduce(cnt[i], cnt[i], 1, ncclUint64, ncclSum, d[i].comm->comm, d[i].stream));
+                    MCMC_NCCL_TRY(ncclGroupEnd());
+                }
+                MCMC_HIP_TRY(hipSetDevice(d[0].device));
+                MCMC_HIP_TRY(hipMemcpyAsync(hsum, cnt[0], sizeof(unsigned long long), hipMemcpyDeviceToHost, d[0].stream));
+                MCMC_HIP_TRY(hipStreamSynchronize(d[0].stream));
+                tot = *hsum;
+            } else {
+                for (size_t i = 0; i < d.size(); i++) {
+                    MCMC_HIP_TRY(hipSetDevice(d[i].device));
+                    MCMC_HIP_TRY(hipMemcpyAsync(hsum, cnt[i], sizeof(unsigned long long), hipMemcpyDeviceToHost, d[i].stream));
+                    MCMC_HIP_TRY(hipStreamSynchronize(d[i].stream));
+                    tot += *hsum;
+                }
+            }
+            cviol = tot;
+            passes++;
+        }
+        for (auto* c : ctx) part_tail_done(c, cviol, passes);
+        return MCMC_OK;
+    }
+
+    int rc_ = MCMC_OK;
+};
 }  // namespace
 
 extern "C" {
@@ -269,11 +433,12 @@ int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, 
     const size_t S = world > 1 ? bounds[1] : n;
     const size_t cols = (std::max<size_t>((size_t)n + 256, (size_t)world * S + 256) * cb + 255) & ~(size_t)255;
     const size_t foot = (size_t)world * 4u * MCMC_FOOTER_WORDS;
+    const size_t dlt = (size_t)world * 4u * kPartDeltaWords;   // delta slots (delta-mode exchange)
     void* mem = nullptr;
     hipStream_t st = nullptr;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipMalloc(&mem, 2 * cols + 2 * foot);
-    if (e == hipSuccess) e = hipMemset(mem, 0, 2 * cols + 2 * foot);
+    if (e == hipSuccess) e = hipMalloc(&mem, 2 * cols + 2 * foot + 2 * dlt);
+    if (e == hipSuccess) e = hipMemset(mem, 0, 2 * cols + 2 * foot + 2 * dlt);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e != hipSuccess) {
         (void)hipFree(mem);
@@ -283,6 +448,9 @@ int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, 
     uint8_t* b = static_cast<uint8_t*>(mem);
     int rc = mcmc_part_attach(c, world, rank, bounds, b, b + cols, cols, b + 2 * cols, b + 2 * cols + foot, st);
     if (!rc) rc = part_adopt(c, mem, st, comm);
+    if (!rc)
+        rc = part_set_delta(c, reinterpret_cast<uint32_t*>(b + 2 * cols + 2 * foot),
+                            reinterpret_cast<uint32_t*>(b + 2 * cols + 2 * foot + dlt));
     if (rc) {
         (void)hipFree(mem);
         (void)hipStreamDestroy(st);
@@ -298,55 +466,84 @@ int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
     Driver D;
     if (int rc = D.setup(ctxs, k)) return rc;
     const uint32_t limit = max_sweeps ? max_sweeps : D.d[0].maxRip + 2;   // + the final count pass (sweeps)
-    const uint32_t check_every = 8;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    EventGuard e0, e1;
+    EventGuard batch_ev[2];
+    e0.device = e1.device = batch_ev[0].device = batch_ev[1].device = D.d[0].device;
     MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
-    MCMC_HIP_TRY(hipEventCreate(&e0));
-    MCMC_HIP_TRY(hipEventCreate(&e1));
-    MCMC_HIP_TRY(hipEventRecord(e0, D.d[0].stream));
+    MCMC_HIP_TRY(hipEventCreate(&e0.e));
+    MCMC_HIP_TRY(hipEventCreate(&e1.e));
+    for (auto& b : batch_ev) MCMC_HIP_TRY(hipEventCreateWithFlags(&b.e, hipEventDisableTiming));
+    MCMC_HIP_TRY(hipEventRecord(e0.e, D.d[0].stream));
     // the loop continues from the device's sweep counter (a second call resumes where the first
     // stopped: the exchange's buffer parity is the device's)
     int32_t dn0 = 0;
     uint32_t t = 0, err0 = 0;
-    int rc = mcmc_part_state(D.ctx[0], &dn0, &t, &err0);
-    if (rc) return rc;
-    if (err0 & 2u) return fail(MCMC_E_STATE, "a spill exchange is pending");
+    if (int rc = mcmc_part_state(D.ctx[0], &dn0, &t, &err0)) return rc;
+    if (err0 & 6u) return fail(MCMC_E_STATE, "an exchange of a paused sweep is pending");
     const uint32_t t_begin = t;
-    bool done = dn0 != 0;
-    while (!rc && !done && t - t_begin < limit) {
-        const uint32_t kk = std::min(check_every, limit - (t - t_begin));
-        for (uint32_t s = 0; s < kk && !rc; s++, t++) {
-            for (auto* c : D.ctx)
-                if ((rc = mcmc_part_sweep_async(c))) break;
-            if (!rc) rc = D.exchange(t);
-            for (auto* c : D.ctx)
-                if (!rc && (rc = mcmc_part_commit_async(c))) break;
+    // host-side exchange policy, identical on every rank (it sees the same device decisions)
+    uint32_t full_left = 0;                // steps to run in full mode after a delta overflow
+    std::vector<uint8_t> was_delta;        // mode of every enqueued step (index t - t_begin)
+    auto enqueue = [&](uint32_t steps) -> int {
+        for (uint32_t s = 0; s < steps; s++, t++) {
+            const bool delta = D.delta_ok && full_left == 0;
+            if (full_left) full_left--;
+            was_delta.push_back(delta ? 1 : 0);
+            if (int rc = D.step(t, delta)) return rc;
         }
-        if (rc) break;
-        int32_t dn = 0;
-        uint32_t td = 0, err = 0;
-        if ((rc = mcmc_part_state(D.ctx[0], &dn, &td, &err))) break;
-        if (err & 1u) { rc = fail(MCMC_E_DEVICE, "partitioned sweep: device error flag"); break; }
-        if (err & 2u) {   // spill pause at sweep td: resume from it
-            if ((rc = D.spill())) break;
-            if ((rc = mcmc_part_state(D.ctx[0], &dn, &td, &err))) break;
-            t = td;
+        return MCMC_OK;
+    };
+    // Batches of kStepsPerPoll steps; after enqueuing batch j + 1 the host waits for batch j's end
+    // and reads ctx[0]'s state on a side stream, so the device never idles for the host's poll.
+    bool done = dn0 != 0;
+    uint32_t inflight = 0;                 // batches enqueued and not yet polled (0..2)
+    uint32_t cur = 0;                      // batch_ev slot of the oldest unpolled batch
+    while (!done) {
+        const uint32_t left = limit - std::min(limit, t - t_begin);
+        if (left && inflight < 2) {
+            if (int rc = enqueue(std::min(kStepsPerPoll, left))) return rc;
+            MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
+            MCMC_HIP_TRY(hipEventRecord(batch_ev[(cur + inflight) & 1].e, D.d[0].stream));
+            inflight++;
+            if (inflight < 2 && t - t_begin < limit) continue;   // keep one batch queued ahead
+        }
+        if (!inflight) break;   // the step limit is reached and every batch was polled
+        uint32_t td = 0, dn = 0, err = 0;
+        if (int rc = D.peek(batch_ev[cur].e, &td, &dn, &err)) return rc;
+        cur ^= 1u;
+        inflight--;
+        if (err & 1u) return fail(MCMC_E_DEVICE, "partitioned sweep: device error flag");
+        if (err & 6u) {   // paused at sweep td: drain the no-op steps behind it, exchange, resume
+            if (int rc = D.drain()) return rc;
+            int32_t dn2 = 0;
+            uint32_t err2 = 0;
+            if (int rc = mcmc_part_state(D.ctx[0], &dn2, &td, &err2)) return rc;
+            if (int rc = D.resume(td, err2, td - t_begin < was_delta.size() && was_delta[td - t_begin])) return rc;
+            if (err2 & 4u) full_left = kFullAfterOverflow;
+            t = td + 1;
+            was_delta.resize(t - t_begin);
+            inflight = 0;
+            cur = 0;
+            continue;
         }
         done = dn != 0;
     }
-    if (!rc) {
-        MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
-        MCMC_HIP_TRY(hipEventRecord(e1, D.d[0].stream));
-        MCMC_HIP_TRY(hipEventSynchronize(e1));
+    if (int rc = D.drain()) return rc;
+    int32_t dnf = 0;
+    uint32_t tf = 0, errf = 0;
+    if (int rc = mcmc_part_state(D.ctx[0], &dnf, &tf, &errf)) return rc;
+    if (errf & 1u) return fail(MCMC_E_DEVICE, "partitioned sweep: device error flag");
+    if (dnf && D.d[0].tailcut_max) {
+        if (int rc = D.tailcut()) return rc;
     }
+    MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
+    MCMC_HIP_TRY(hipEventRecord(e1.e, D.d[0].stream));
+    MCMC_HIP_TRY(hipEventSynchronize(e1.e));
     float ms = 0;
-    if (!rc) (void)hipEventElapsedTime(&ms, e0, e1);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (rc) return rc;
+    (void)hipEventElapsedTime(&ms, e0.e, e1.e);
     for (uint32_t i = 0; i < k; i++) {
         mcmc_run_stats s{};
-        if ((rc = part_stats(D.ctx[i], &s))) return rc;
+        if (int rc = part_stats(D.ctx[i], &s)) return rc;
         s.loopMs = ms;
         if (stats) stats[i] = s;
     }

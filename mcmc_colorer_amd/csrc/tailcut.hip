@@ -44,7 +44,7 @@ namespace {
 template <bool SKIP_PADS = false, class F>
 __device__ __forceinline__ void for_neighbours(const TailView& g, uint32_t l, uint32_t part, uint32_t parts, F&& f) {
     if (g.row_off) {
-        const uint64_t rs = g.row_off[l], re = g.row_off[l + 1];
+        const uint64_t rs = g.row_off[g.csr_row0 + l], re = g.row_off[g.csr_row0 + l + 1];
         for (uint64_t k = rs + part; k < re; k += parts) f(g.col_idx[k]);
         return;
     }
@@ -73,10 +73,10 @@ __global__ __launch_bounds__(256) void tail_count_kernel(TailView g, const CT* _
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
     unsigned long long wave_total = 0;
     for (uint32_t l = gw; l < g.n; l += nw) {
-        const CT cv = C[l];
+        const CT cv = C[g.vb + l];
         uint32_t hits = 0;
         if (EDGES) {
-            for_neighbours<true>(g, l, lane, 64u, [&](uint32_t w) { hits += (C[w] == cv && w > l) ? 1u : 0u; });
+            for_neighbours<true>(g, l, lane, 64u, [&](uint32_t w) { hits += (C[w] == cv && w > g.vb + l) ? 1u : 0u; });
             for (int off = 32; off > 0; off >>= 1) hits += __shfl_xor(hits, off, 64);
         } else {
             bool hit = false;
@@ -114,17 +114,18 @@ __global__ __launch_bounds__(kRepairThreads) void tail_repair_kernel(TailView g,
     // colour thread 0 stored for an earlier vertex of the list
     const volatile CT* Cv = C;
     for (uint32_t k = 0; k < L; k++) {
-        const uint32_t i = list[k];
+        const uint32_t li = list[k];   // local row; i: its vertex (the replica's index)
+        const uint32_t i = g.vb + li;
         for (uint32_t w = tid; w < words; w += blockDim.x) mask[w] = 0;
         __syncthreads();
         if (WIDE) {
-            for_neighbours(g, i, tid, kRepairThreads, [&](uint32_t w) {
+            for_neighbours(g, li, tid, kRepairThreads, [&](uint32_t w) {
                 const uint32_t c = Cv[w];
                 if (c < nCol) atomicOr(&mask[c >> 5], 1u << (c & 31));
             });
         } else {
             uint32_t m[kMaskWords] = {};
-            for_neighbours(g, i, tid, kRepairThreads, [&](uint32_t w) {
+            for_neighbours(g, li, tid, kRepairThreads, [&](uint32_t w) {
                 const uint32_t c = Cv[w];
 #pragma unroll
                 for (int q = 0; q < kMaskWords; q++) m[q] |= (c >> 5) == (uint32_t)q ? 1u << (c & 31) : 0u;

@@ -67,6 +67,27 @@ def plan(graph: Graph, world: int, balance: bool = True) -> np.ndarray:
     return b
 
 
+def group_default_ncol(graph, params: ColoringMCMCParams, group=None) -> int:
+    """main.cu:162's default nCol (maxDeg * numColorRatio) over a partitioned group: a rank may hold
+    only its own rows (Graph.er_fast(rows=...)), so the max degree is all-reduced (MAX) first and
+    every rank samples the same colour range as the one-GPU run."""
+    import torch
+    import torch.distributed as dist
+
+    mx = torch.tensor([int(graph.getMaxNodeDeg())], dtype=torch.int64)
+    if dist.get_backend(group) == "nccl":
+        mx = mx.cuda()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+
+    class _Whole:   # default_ncol reads only the max degree
+        maxDeg = int(mx.item())
+
+        def getMaxNodeDeg(self):
+            return self.maxDeg
+
+    return default_ncol(_Whole(), params)
+
+
 class HipRank:
     """This rank's share of the sweep on its GPU, over the caller-exchanged C ABI (mcmc_part_*),
     with torch tensors as the exchange buffers."""
@@ -184,7 +205,7 @@ class PartitionedColoringMCMC:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if params.nCol == 0:
-            params = ColoringMCMCParams(**{**params.__dict__, "nCol": default_ncol(graph, params)})
+            params = ColoringMCMCParams(**{**params.__dict__, "nCol": group_default_ncol(graph, params, group)})
         self.param = params
         self.rand = randStates
         self.check_every = max(1, check_every)
@@ -280,7 +301,7 @@ class NativePartitionedColoringMCMC:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if params.nCol == 0:
-            params = ColoringMCMCParams(**{**params.__dict__, "nCol": default_ncol(graph, params)})
+            params = ColoringMCMCParams(**{**params.__dict__, "nCol": group_default_ncol(graph, params, group)})
         self.param = params
         self.rand = randStates
         self.graph = graph
@@ -306,6 +327,8 @@ class NativePartitionedColoringMCMC:
         self._cparams.seed = seed & 0xFFFFFFFF
         check(lib().mcmc_part_create(self.graph.handle, ctypes.byref(self._cparams), self.world, self.rank,
                                      u32ptr(self.bounds), self._comm, ctypes.byref(self._ctx)))
+        if self.param.tailcutRepair:
+            check(lib().mcmc_set_tailcut_repair(self._ctx, int(self.param.tailcutRepair)))
 
     def init(self, iteration: int = 0) -> None:
         self._make(self.rand.seed + iteration)
@@ -364,6 +387,8 @@ class LoopbackPartition:
         for r in range(self.world):
             check(lib().mcmc_part_create(self.graphs[r].handle, ctypes.byref(self._cparams), self.world, r,
                                          u32ptr(self.bounds), None, ctypes.byref(self._ctx[r])))
+            if params.tailcutRepair:   # the corrected tail cut after the loop, rank by rank (multi.hip)
+                check(lib().mcmc_set_tailcut_repair(self._ctx[r], int(params.tailcutRepair)))
 
     def run(self, glibc: GlibcRand, max_sweeps: int = 0) -> list:
         for c in self._ctx:

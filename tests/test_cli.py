@@ -141,3 +141,31 @@ def test_cli_mcmccpu_surface(tmp_path, extra):
         assert (po / f"{name}-MCMC_CPU-{i}-colors.txt").read_text() == (oo / f"{name}-MCMC_CPU-{i}-colors.txt").read_text()
         assert strip((po / f"{name}-MCMC_CPU-{i}.log").read_text()) == strip((oo / f"{name}-MCMC_CPU-{i}.log").read_text())
         assert (po / f"{name}-MCMC_GPU-{i}.log").exists() == bool(extra)
+
+
+def _run_cli(out, args):
+    r = subprocess.run([str(CLI), "--mcmcgpu", *args, "--outDir", str(out)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--tailcut", "--tailcutRepair"]])
+def test_cli_gpus_loopback_equals_one_gpu(tmp_path, extra):
+    """--gpus 3 --loopback --simulate-fast (every rank generates only its own rows, all three on the
+    one device): default nCol, report and colours equal the one-GPU run's -- the whole graph's
+    statistics (maxDeg/minDeg/Edges from every rank's rows, not rank 0's), and with
+    --tailcut --tailcutRepair the partitioned tail cut."""
+    n, p = 70000, 0.002
+    args = ["--simulate-fast", str(p), "-n", str(n), "--er-seed", "3", "--seed", "5", *extra]
+    out1 = _run_cli(tmp_path / "one", args)
+    out3 = _run_cli(tmp_path / "three", [*args, "--gpus", "3", "--loopback"])
+    name = f"{n}_{p:.6f}_1.000000_er3"
+    for suffix in ("-MCMC_GPU-0-colors.txt",):
+        assert (tmp_path / "one" / (name + suffix)).read_text() == (tmp_path / "three" / (name + suffix)).read_text()
+    strip = lambda t: [l for l in t.splitlines() if not l.startswith("Execution time")]
+    assert strip((tmp_path / "one" / f"{name}-MCMC_GPU-0.log").read_text()) == \
+        strip((tmp_path / "three" / f"{name}-MCMC_GPU-0.log").read_text())
+    deg = lambda o: re.search(r"Min Degree: (\d+) - Max Degree: (\d+)", o).groups()
+    assert deg(out1) == deg(out3)
+    assert re.search(r"Edges: (\d+)", out1).group(1) == re.search(r"Edges: (\d+)", out3).group(1)

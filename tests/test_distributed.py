@@ -126,3 +126,37 @@ def test_partitioned_driver_gloo_matches_oracle(world, case):
 def plan_rows_py(n, world):
     S = ((n + world - 1) // world + 63) // 64 * 64
     return [min(r * S, n) for r in range(world)] + [n]
+
+
+def _ncol_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mcmc_colorer_amd import colorer as M
+        from mcmc_colorer_amd.distributed import group_default_ncol
+
+        class _Rows:   # a rank's row-partial graph: its own rows' max degree only
+            def getMaxNodeDeg(self):
+                return [37, 120, 64][rank]
+
+        q.put((rank, group_default_ncol(_Rows(), M.ColoringMCMCParams(nCol=0)),
+               group_default_ncol(_Rows(), M.ColoringMCMCParams(nCol=0, numColorRatio=0.5))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_default_ncol_uses_whole_graph_max_degree():
+    """with per-rank graphs (Graph.er_fast(rows=...)) every rank must take main.cu:162's
+    nCol from the WHOLE graph's max degree, not its own rows'."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ncol_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = dict((x[0], x[1:]) for x in (q.get(timeout=300) for _ in range(world)))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(res[r] == (120, 60) for r in range(world)), res

@@ -4,7 +4,9 @@ GPU (one MI355X): the partitioned colorer run inside one C call (mcmc_part_run) 
   * the loopback transport (every rank in this process on the one GPU, exchanged by device copies,
     otherwise the exact sequence of the RCCL path) for worlds 1..8: equal-row and arc-balanced
     plans, the wide sweep (nCol > 256), per-rank generated graphs, and sweeps whose overflow events
-    outgrow a rank's footer (the spill exchange);
+    outgrow a rank's footer (the spill exchange); the default delta exchange (changed vertices
+    only), its overflow fallback (full ranges, then delta again), the full-range exchange
+    (MCMC_EXCHANGE=p2p), and the corrected tail cut run rank by rank;
   * RCCL at world 1 through the C ABI: mcmc_comm_init_all and mcmc_comm_unique_id +
     mcmc_comm_init_rank, and the torch.distributed front end (NativePartitionedColoringMCMC);
   * the Python-exchanged protocol (HipRank in lock-step) on arc-balanced plans and spills.
@@ -261,3 +263,71 @@ def test_lockstep_arc_balanced_and_spill(M, world):
     assert ranks[0].spills >= 1
     for b in ranks:
         assert b.coloring().tolist() == r.colors.tolist() and b.trajectory().tolist() == r.traj.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["delta", "p2p"])
+@pytest.mark.parametrize("world", [2, 5])
+def test_native_loopback_exchange_modes(M, monkeypatch, exchange, world):
+    """Both exchange forms give the oracle's run: delta (a rank sends the vertices whose colour
+    changed; replicas kept equal off its rows) and p2p (whole row ranges every sweep)."""
+    from mcmc_colorer_amd.distributed import plan_rows
+
+    monkeypatch.setenv("MCMC_EXCHANGE", exchange)
+    off, idx, nc, r = oracle_case(3000, 0.02, 16, 41, maxRip=40)
+    lp, st, _ = loopback(M, off, idx, nc, 41, plan_rows(3000, world), 3000 * 3001 // 2, maxRip=40)
+    assert_native(lp, st, r, world)
+    lp.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_loopback_delta_overflow(M, world):
+    """A sparse graph with few colours: thousands of vertices change colour per rank in the first
+    sweeps, more than a delta slot holds (2047 pairs) -- those sweeps pause, travel as full row
+    ranges, 16 full-mode steps follow, then delta mode resumes (after syncing the replicas); the
+    run still equals the oracle's. Events (eps 0.05) ride along."""
+    from mcmc_colorer_amd.distributed import plan_rows
+
+    off, idx = circulant(60000, 4)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 5, 17, epsilon=0.05, maxRip=60, nthreads=8)
+    lp, st, _ = loopback(M, off, idx, 5, 17, plan_rows(60000, world), 0, epsilon=0.05, maxRip=60)
+    assert_native(lp, st, r, world)
+    lp.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("ncol,maxrip,tailcut", [(24, 250, True), (40, 3, False), (16, 6, False)])
+def test_native_loopback_tailcut(M, world, ncol, maxrip, tailcut):
+    """The corrected tail cut (coloringMCMC_CPU.cpp:272-311, k++) on a partitioned run: rank by rank
+    in ascending order (each rank's repaired rows broadcast before the next rank's turn), recount
+    summed over the ranks -- colouring, final Cviol and pass count equal the oracle's (the last
+    case cannot repair: every pass up to the 1000-pass cap)."""
+    from mcmc_colorer_amd.distributed import plan_rows
+
+    n, p, seed = 2500, 0.02, 1
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, maxRip=maxrip, tailcut=tailcut, tailcutRepair=True)
+    assert r.res.tailcutPasses >= 1
+    lp, st, _ = loopback(M, off, idx, nc, seed, plan_rows(n, world), n * (n + 1) // 2, maxRip=maxrip,
+                         tailcut=tailcut, tailcutRepair=1000)
+    assert_native(lp, st, r, world)
+    assert all(s.tailcutPasses == r.res.tailcutPasses for s in st)
+    lp.close()
+
+
+@pytest.mark.gpu
+def test_native_loopback_tailcut_generated_rows(M):
+    """Tail cut over per-rank generated layouts (no CSR: rows through each rank's tiled layout)."""
+    n, p, ncol, seed = 140000, 0.0004, 120, 9
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, tailcut=True, tailcutRepair=True, nthreads=8)
+    assert r.res.tailcutPasses >= 1
+    b = np.array([0, 50048, 90048, n], dtype=np.uint32)
+    graphs = [M.Graph.er_fast(n, p, seed, rows=(int(b[k]), int(b[k + 1]))) for k in range(3)]
+    lp, st, _ = loopback(M, off, idx, ncol, seed, b, 0, graphs=graphs, tailcut=True, tailcutRepair=1000)
+    assert_native(lp, st, r, 3)
+    assert all(s.tailcutPasses == r.res.tailcutPasses for s in st)
+    lp.close()
