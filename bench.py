@@ -113,6 +113,10 @@ def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window:
     v1, k1, r1 = sample(1, max_seconds)
     w1 = time.perf_counter() - t0
     info = host_info()
+    # The GPU pool gives one GPU's job a share of the host's CPUs (OMP_NUM_THREADS = 16 on the box;
+    # the affinity mask still lists every CPU of the machine, which other jobs use): the OpenMP leg
+    # runs on that share, and its per-thread rate scaled to every usable CPU is reported beside it
+    # as an upper bound for the CPU path on the whole host (linear scaling assumed, not measured)
     threads = int(os.environ.get("OMP_NUM_THREADS") or info["usable_cpus"] or 1)
     t0 = time.perf_counter()
     vN, kN, rN = sample(threads, max_seconds / 2)
@@ -129,7 +133,14 @@ def cpu_baseline(off: np.ndarray, idx: np.ndarray, ncol: int, seed: int, window:
                       "sample": f"first {kN} sweeps, OpenMP variant of the oracle on {threads} threads (same "
                                 f"colouring as the single-thread run; loop 2 / fill_qstar, output-dead, skipped); "
                                 f"{wN:.1f} s wall",
-                      "identical_trajectory_prefix": bool(np.array_equal(r1.traj[:min(k1, kN)], rN.traj[:min(k1, kN)]))},
+                      "identical_trajectory_prefix": bool(np.array_equal(r1.traj[:min(k1, kN)], rN.traj[:min(k1, kN)])),
+                      "cpu_share_note": "threads = the job's CPU share on the GPU box (OMP_NUM_THREADS); the "
+                                        "pool's rules reserve the other CPUs of the machine for other jobs"},
+        "all_usable_cpus_extrapolated": {
+            "value": vN / threads * (info["usable_cpus"] or threads), "cores": info["usable_cpus"],
+            "kind": "extrapolation",
+            "note": f"all_cores' per-thread rate x {info['usable_cpus']} usable CPUs (linear scaling assumed, "
+                    f"an upper bound for the CPU path on this host; not measured)"},
     }
 
 

@@ -108,6 +108,7 @@ struct SweepArgs {
     uint32_t slice_bytes;       // tiled: colour bytes a pair's slice can hold (resident: the replica)
     uint32_t seg_buf_bytes;     // tiled: LDS bytes of one segment-table buffer (1 KiB multiple)
     unsigned long long* phase_ts;   // diagnostics (MCMC_PHASE_DUMP): per-workgroup phase timestamps
+    unsigned long long* pair_trace; // diagnostics (MCMC_PAIR_TRACE): per workgroup and pair, kPairTraceRec words
     // partitioned runs: colour replicas stay in vertex order; every rank's footer (kFooterWords:
     // local Cviol, event count, flags, sorted events) sits in slot `rank` of the footer buffer of
     // the next-colour parity (sweep t: foot[(t + 1) & 1], like colors[(t + 1) & 1])
@@ -173,6 +174,8 @@ struct SweepArgs {
     int part_delta;             // commit: 1 delta mode (remote changes arrive as pairs, applied to both
                                 //   replicas), 0 full mode, -1 full-mode resumption of a paused sweep
 };
+constexpr uint32_t kPairTraceMax = 256;   // pairs traced per workgroup (MCMC_PAIR_TRACE)
+constexpr uint32_t kPairTraceRec = 8;     // {start, scan end min, scan end max, eval end, barrier end, info, 0, 0}
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
 constexpr uint32_t kDeltaWords = 4096;  // MCMC delta slot per rank: head + (v, c) pairs (16 KiB)
 constexpr uint32_t kDeltaHead = 2;
@@ -957,6 +960,7 @@ struct TailShared {
     uint32_t st_quads, st_pairs, st_used;   // diagnostics (scan_stats): quads loaded, pairs staged, quads gathered
     uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
+    unsigned long long tr[2][3];   // diagnostics (pair trace): scan end min / max over waves, eval end max
 };
 
 __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, TailShared& sh, uint32_t wave_viol,
@@ -1611,6 +1615,8 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t lds0 = lds_addr(lbase), seg_lds0 = lds_addr(seg_base);
     uint32_t wave_viol = 0, wave_ev = 0;
     const bool timing = DG && a.phase_ts != nullptr;
+    const bool ptrace = DG && a.pair_trace != nullptr;
+    unsigned long long tr_start = 0;
     uint64_t cyc_wait = 0, cyc_scan = 0, cyc_eval = 0, tmark = 0;
 
     uint32_t g = blockIdx.x, b = 0, buf = 0;
@@ -1686,6 +1692,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
 
     while (g < a.ngroups) {
         if (timing) tmark = __builtin_readcyclecounter();
+        if (ptrace && threadIdx.x == 0) {
+            tr_start = wall_clock64();
+            sh.tr[(kpair + 1u) & 1u][0] = ~0ull;
+            sh.tr[(kpair + 1u) & 1u][1] = 0;
+            sh.tr[(kpair + 1u) & 1u][2] = 0;
+        }
         const uint32_t r0 = g * R;
         const uint32_t rows = min(R, nloc - r0);
         const uint32_t q = (rows + nwaves - 1) / nwaves;   // evaluation share per wave
@@ -1898,6 +1910,11 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             v[u] = tile_load(gr, gcol, pu < fend ? 2u * pu : kTileOOB);
         }
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_scan += t1 - tmark; tmark = t1; }
+        if (ptrace && lane == 0) {
+            const unsigned long long w = wall_clock64();
+            atomicMin(&sh.tr[kpair & 1u][0], w);
+            atomicMax(&sh.tr[kpair & 1u][1], w);
+        }
         if (last && REF) {
             MCMC_LDS_BARRIER();   // every wave's mask ORs of the group are in
             // every wave evaluates a share of the group's rows and clears their masks for the next group
@@ -1953,12 +1970,26 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 xk = minstd_mulmod(xk, xsk);
             }
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
+            if (ptrace && lane == 0) atomicMax(&sh.tr[kpair & 1u][2], (unsigned long long)wall_clock64());
         }
         // pair k+1's DMA landed everywhere (the evaluation's barrier waited for it); buffer k&1 and
         // the masks are free
         if (!REF && last) MCMC_LDS_BARRIER();
         else MCMC_PAIR_BARRIER();
         if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_wait += t1 - tmark; }
+        if (ptrace && threadIdx.x == 0 && kpair < kPairTraceMax) {
+            unsigned long long* rec = a.pair_trace + ((size_t)blockIdx.x * kPairTraceMax + kpair) * kPairTraceRec;
+            rec[0] = tr_start;
+            rec[1] = sh.tr[kpair & 1u][0];
+            rec[2] = sh.tr[kpair & 1u][1];
+            rec[3] = sh.tr[kpair & 1u][2];
+            rec[4] = wall_clock64();
+            // info: block | open rows at the pair's top << 16 | drain, sparse, last, allfull << 40 | group << 44
+            const uint32_t nopen = EXIT ? rows - min(nfull_run, rows) : rows;
+            rec[5] = (unsigned long long)b | ((unsigned long long)nopen << 16) | ((unsigned long long)drain << 40) |
+                     ((unsigned long long)sparse << 41) | ((unsigned long long)last << 42) |
+                     ((unsigned long long)allfull << 43) | ((unsigned long long)g << 44);
+        }
         if (REF && !RES && nbn == 0) gpar ^= 1u;   // the next pair starts a new group
         if (!REF && last) xg = minstd_mulmod(xg, xsg);
         g = ng;
@@ -2153,6 +2184,7 @@ struct mcmc_ctx {
     uint32_t sub_log2 = 0, slice_bytes = 0;
     bool variant_res = false;          // variant 3: replica LDS-resident
     unsigned long long* phase_ts = nullptr;   // MCMC_PHASE_DUMP diagnostics
+    unsigned long long* pair_trace = nullptr; // MCMC_PAIR_TRACE diagnostics (tiled sweep)
     int fused = 1;              // commit runs inside the sweep kernel (last workgroup)
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
@@ -2360,6 +2392,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         }
     }
     a.phase_ts = c->phase_ts;
+    a.pair_trace = c->pair_trace;
     a.tile = 32;  // vertices per wave-tile (evaluation batch)
     a.wave_start = c->wave_start;
     return a;
@@ -2393,7 +2426,7 @@ int ensure_constants() {
 
 // The sweep launch for these arguments: the diagnostics instantiation when they ask for it.
 void launch_tiled_or_diag(mcmc_ctx* c, const SweepArgs& a) {
-    const bool diag = a.scan_stats || a.phase_ts || a.dbg_max_pairs;
+    const bool diag = a.scan_stats || a.phase_ts || a.dbg_max_pairs || a.pair_trace;
     (diag && c->sweep_diag ? c->sweep_diag : c->sweep)(a, c->grid, c->block, c->lds, c->stream);
 }
 
@@ -2685,6 +2718,11 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     chk(hipMalloc(&c->evdraw, sizeof(uint32_t) * pcap));
     chk(hipMalloc(&c->st, sizeof(DevState)));
     chk(hipMalloc(&c->traj, sizeof(unsigned long long) * c->traj_cap));
+    if (getenv("MCMC_PAIR_TRACE")) {
+        const size_t words = (size_t)kPairTraceRec * kPairTraceMax * 4096u;
+        chk(hipMalloc(&c->pair_trace, sizeof(unsigned long long) * words));
+        chk(hipMemset(c->pair_trace, 0, sizeof(unsigned long long) * words));
+    }
     if (getenv("MCMC_PHASE_DUMP")) {
         chk(hipMalloc(&c->phase_ts, sizeof(unsigned long long) * 8u * 4096u));
         chk(hipMemset(c->phase_ts, 0, sizeof(unsigned long long) * 8u * 4096u));
@@ -3378,6 +3416,14 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
     if (total_ms) *total_ms = tot;
     if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
+    if (c->pair_trace) {   // diagnostics: the last sweep's per-pair records, gridDim x kPairTraceMax x kPairTraceRec
+        std::vector<unsigned long long> h_tr((size_t)kPairTraceRec * kPairTraceMax * c->grid.x);
+        MCMC_HIP_TRY(hipMemcpy(h_tr.data(), c->pair_trace, h_tr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("MCMC_PAIR_TRACE"), "wb")) {
+            fwrite(h_tr.data(), sizeof(unsigned long long), h_tr.size(), f);
+            fclose(f);
+        }
+    }
     if (c->phase_ts) {   // diagnostics: the last sweep's per-workgroup phase timestamps (+ commit stamps)
         std::vector<unsigned long long> h_ts((size_t)8 * 4096u);
         MCMC_HIP_TRY(hipMemcpy(h_ts.data(), c->phase_ts, h_ts.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -3479,6 +3525,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wave_start);
     (void)hipFree(c->seg);
     (void)hipFree(c->phase_ts);
+    (void)hipFree(c->pair_trace);
     (void)hipFree(c->vflags);
     (void)hipFree(c->tc_list);
     (void)hipFree(c->tc_len);

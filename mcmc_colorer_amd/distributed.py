@@ -413,6 +413,11 @@ class LoopbackPartition:
             check(lib().mcmc_get_trajectory(self._ctx[r], u64ptr(out), k.value, ctypes.byref(k)))
         return out
 
+    def info(self, r: int = 0) -> dict:
+        i = MCMCCtxInfo()
+        check(lib().mcmc_get_info(self._ctx[r], ctypes.byref(i)))
+        return i.as_dict()
+
     def close(self) -> None:
         for c in self._ctx:
             if c:

@@ -13,13 +13,17 @@ column blocks, layout indices far past 2^32) and checked against the oracle with
     (count_free_colors / fill_p / extract_new_color, coloringMCMC_CPU.cpp:361-528) from C_t on its
     regenerated row and u_v = engine draw K0 + t n + v + 1 (:139); the per-vertex violation flags
     of the tail cut's recount kernel (a second code path over the layout) equal the oracle's for
-    the sampled rows; the recount's total equals the sweep's fused Cviol_t (the trajectory).
+    the sampled rows; the recount's total equals the sweep's fused Cviol_t (the trajectory);
+  * sweeps 0..2, EVERY vertex: C_1..C_3 equal tests/c3_expect.py's restatement of the all-full case
+    (pinned against the oracle's one-vertex update), overflow events replayed from glibc in vertex
+    order -- at the default eps and at eps = 1e-3 (about 3% of the vertices change colour per sweep).
 """
 import time
 
 import numpy as np
 import pytest
 
+import c3_expect as X
 import oracle_ref as O
 
 N, P, SEED, NCOL, EPS = 10_000_000, 0.001, 1, 32, 1e-8
@@ -80,5 +84,42 @@ def test_c3_full_size_rows_and_sweeps(hip_lib):
                 checked += 1
     print(f"checked {checked} vertex updates ({events} CDF overflows skipped)", flush=True)
     assert checked >= 2900
+    t1 = time.perf_counter()
+    X.pin_walk(NCOL, EPS)
+    E, k0e, evs = X.expected(3, EPS)
+    assert k0e == k0
+    for t in range(4):
+        bad = np.nonzero(C[t] != E[t])[0]
+        assert len(bad) == 0, f"C_{t}: {len(bad)} vertices differ, first {bad[:5].tolist()}"
+    print(f"every vertex of C_1..C_3 equals the all-full restatement ({evs} overflow events; "
+          f"{time.perf_counter() - t1:.1f} s)", flush=True)
+    col.close()
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c3_full_size_every_vertex_eps_1e3(hip_lib):
+    """eps = 1e-3: about 3% of the vertices leave their colour each sweep (u < own colour x eps walks
+    to a lower colour), so the walk's every branch position is exercised on all 1e7 vertices."""
+    import mcmc_colorer_amd.colorer as M
+
+    eps = 1e-3
+    X.pin_walk(NCOL, eps)
+    E, k0, evs = X.expected(3, eps)
+    g = M.Graph.er_fast(N, P, SEED)
+    col = M.ColoringMCMC(g, M.GPURand(N, SEED, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=NCOL, epsilon=eps))
+    col.init(0)
+    got = [col.coloring()]
+    for _ in range(3):
+        col.step(1)
+        got.append(col.coloring())
+    changed = [int((E[t + 1] != E[t]).sum()) for t in range(3)]
+    print(f"\nchanged colours per sweep {changed}, overflow events {evs}", flush=True)
+    assert min(changed) > 100_000
+    for t in range(4):
+        bad = np.nonzero(got[t] != E[t])[0]
+        assert len(bad) == 0, f"C_{t}: {len(bad)} vertices differ, first {bad[:5].tolist()}"
+    assert col.trajectory().tolist()[:3] == [N, N, N]
     col.close()
     g.close()

@@ -211,3 +211,13 @@ def test_vertex_update_equals_one_oracle_sweep(ncol, eps):
         else:
             assert c == r1.colors[v], v
     assert events == r1.res.glibcDraws
+
+
+def test_c3_expect_walk_pinned():
+    """tests/c3_expect.py's vectorised all-full CDF walk (the full-size C3/C4 checks' expectation)
+    equals the oracle's one-vertex update, at the default eps and at 1e-3."""
+    import c3_expect as X
+
+    X.pin_walk(32, 1e-8)
+    X.pin_walk(32, 1e-3)
+    X.pin_walk(16, 3.3e6, k=500)
