@@ -94,6 +94,14 @@ struct SweepArgs {
                                 //                          2 = packs this rank's footer (partitioned)
     uint32_t world;
     uint32_t lds_sort_cap;      // words of the sweep kernel's dynamic LDS reusable by the commit sort
+    int olist_on;               // tiled early exit: the LDS holds an R-entry open-row list (listed pairs)
+    // tiled early exit, tail queue (tq_dense > 0): a group's blocks [0, tq_dense) run as pairs; its
+    // rows still open then wait in this workgroup's queue (global) and finish block by block after
+    // the workgroup's last group, rows of all its groups together (tile_tail)
+    uint32_t tq_dense;
+    uint32_t tq_cap;            // queue entries per workgroup and queue
+    uint32_t* tq_l;             // [grid][2][tq_cap] local rows
+    uint32_t* tq_m;             // [grid][2][tq_cap][NW] their occupancy masks
     const uint32_t* seg;        // blocked: per-(block, local row) segment offsets, (nb+1) x nloc
     uint32_t nblocks;           // blocked: column blocks of 2^block_log2 vertices
     uint32_t block_log2;        // blocked: log2 of the column block (17: 128 KiB of uint8 colours)
@@ -724,13 +732,13 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
 // ----------------------------------------------------------------------------------------------
 // evaluate_core: the caller has loaded lane j's own colour cv and taboo counter tab and computed
 // x = the minstd state after draw v + 1 of this sweep (x_t 16807^(v+1) mod 2^31-1).
+// evaluate_lane: lane-wise form -- this lane evaluates local row l when `valid` (any rows per lane,
+// not necessarily consecutive: the tail queue's entries); every lane of the wave calls it.
 template <int NW>
-__device__ __forceinline__ uint32_t evaluate_core(const SweepArgs& a, DevState* __restrict__ st,
-                                                  uint8_t* __restrict__ Cs, uint32_t l0, uint32_t cnt,
+__device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* __restrict__ st,
+                                                  uint8_t* __restrict__ Cs, bool valid, uint32_t l,
                                                   const uint32_t (&acc)[NW], int lane, uint32_t& ev_flag,
                                                   uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x) {
-    const bool valid = (uint32_t)lane < cnt;
-    const uint32_t l = l0 + lane;
     const uint32_t v = a.v_begin + l;
     uint32_t pop = 0;
 #pragma unroll
@@ -816,6 +824,14 @@ __device__ __forceinline__ uint32_t evaluate_core(const SweepArgs& a, DevState* 
         }
     }
     return nviol;
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t evaluate_core(const SweepArgs& a, DevState* __restrict__ st,
+                                                  uint8_t* __restrict__ Cs, uint32_t l0, uint32_t cnt,
+                                                  const uint32_t (&acc)[NW], int lane, uint32_t& ev_flag,
+                                                  uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x) {
+    return evaluate_lane<NW>(a, st, Cs, (uint32_t)lane < cnt, l0 + lane, acc, lane, ev_flag, vf, cv, tab, x);
 }
 
 // Per-vertex evaluation of one tile, after the occupancy masks are built: lane j < cnt holds the
@@ -961,6 +977,7 @@ struct TailShared {
     uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
     unsigned long long tr[2][3];   // diagnostics (pair trace): scan end min / max over waves, eval end max
+    uint32_t qn[2];       // tiled tail queue: entries of the two queues
 };
 
 __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, TailShared& sh, uint32_t wave_viol,
@@ -1387,6 +1404,19 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
     }
 }
 
+// DMA of column block b's colour slice alone (the tail queue's blocks; no segment table).
+__device__ __forceinline__ void tile_dma_slice(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t b,
+                                               uint32_t slice_lds, uint32_t wid, uint32_t nwaves, int lane) {
+    const uint32_t lo = b << a.block_log2;
+    const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
+    const uint32_t kn = tile_slice_buf(a.block_log2) / 1024u / nwaves;
+    for (uint32_t k = 0; k < kn; k++) {
+        const uint32_t piece = (k * nwaves + wid) * 64u;
+        const uint32_t q = min(piece + (uint32_t)lane, nq16 - 1u);
+        glds16(C + (lo + 16u * q), __builtin_amdgcn_readfirstlane(slice_lds + piece * 16u));
+    }
+}
+
 // REF, streaming: DMA of group g's own colours (the rows' bytes, from the 16-byte boundary at or
 // below the group's first vertex) into an own-colour buffer (a multiple of 1 KiB: every wave
 // instruction lands 64 x 16 B).
@@ -1491,18 +1521,29 @@ __device__ __forceinline__ void drain_quad(const uint8_t* __restrict__ cb, const
     for (int e = 0; e < 8; e++) set_color_bit<NW>(m, c[e]);
 }
 
-// The group's rows whose masks are not full yet, into sh.dlist (any order); *count = sh.dn[par]
-// (zeroed at the top of the previous pair). All threads; a barrier follows.
+// The group's rows whose masks are not full yet, into `list` (at most `cap`; ascending inside each
+// wave's 64-row chunk, chunks in arrival order); *count = sh.dn[par] (zeroed at the top of the
+// previous pair). Ballot compaction, one LDS atomic per wave and chunk. All threads; a barrier follows.
 template <int NW>
 __device__ __forceinline__ void tile_open_rows(uint32_t rows, const uint32_t* smask, TailShared& sh,
-                                               const uint32_t* fullw, uint32_t par) {
-    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
-        bool f = true;
+                                               const uint32_t* fullw, uint32_t par, uint16_t* list, uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t r0 = threadIdx.x & ~63u; r0 < rows; r0 += blockDim.x) {
+        const uint32_t r = r0 + lane;
+        bool open = false;
+        if (r < rows) {
+            bool f = true;
 #pragma unroll
-        for (int i = 0; i < NW; i++) f = f && ((smask[r * NW + i] & fullw[i]) == fullw[i]);
-        if (!f) {
-            const uint32_t k = atomicAdd(&sh.dn[par], 1u);
-            if (k < 256u) sh.dlist[k] = (uint16_t)r;
+            for (int i = 0; i < NW; i++) f = f && ((smask[r * NW + i] & fullw[i]) == fullw[i]);
+            open = !f;
+        }
+        const uint64_t bm = __ballot(open);
+        uint32_t base = 0;
+        if (lane == 0 && bm) base = atomicAdd(&sh.dn[par], (uint32_t)__popcll(bm));
+        base = __shfl(base, 0, 64);
+        if (open) {
+            const uint32_t k = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+            if (k < cap) list[k] = (uint16_t)r;
         }
     }
     __syncthreads();
@@ -1560,6 +1601,249 @@ __device__ __forceinline__ void tile_drain(const SweepArgs& a, const uint8_t* __
     }
 }
 
+// ---- tail queue (phase B of the early-exit sweep) ---------------------------------------------
+// After its last group a workgroup finishes the rows its groups left open after the dense blocks,
+// block by block: block b's slice is staged ONCE, then the queue is streamed through it in chunks
+// (entries: local row, its mask; per chunk the rows' segment bounds of block b are read into LDS),
+// sub-groups claiming entries exactly as rows of a pair (one-ahead loads, ping-pong register sets).
+// A row whose mask filled up, or whose blocks ran out, is evaluated (lane per entry, u_v by minstd
+// skip-ahead); the others are queued for block b + 1. Rows of ~22 groups share every block: the
+// per-group tail pairs (few open rows each: one exposed memory round trip after another, C3 pair 2
+// 9.7 us for 737 rows, pair 3 4.8 us, the drain 8.9 us) become a few dense passes.
+template <int NW, bool DG>
+__device__ __forceinline__ void tail_scan(const SweepArgs& a, const uint8_t* __restrict__ sc,
+                                          const uint64_t* E_base, const uint32_t* E_s0, const uint32_t* E_s1,
+                                          uint32_t* E_m, uint32_t k, TailShared& sh, const uint32_t (&fullw)[NW],
+                                          int lane) {
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t L = 1u << a.sub_log2, nsub = 64u >> a.sub_log2;
+    const uint32_t sub = (uint32_t)lane >> a.sub_log2, li = (uint32_t)lane & (L - 1u);
+    const uint32_t step = 8u * L * kTileU;
+    const uint16_t* __restrict__ tc = a.tcol;
+    auto is_full = [&](const uint32_t (&x)[NW]) -> bool {
+        bool f = true;
+#pragma unroll
+        for (int i = 0; i < NW; i++) f = f && ((x[i] & fullw[i]) == fullw[i]);
+        return f;
+    };
+    uint32_t e = wid * nsub + sub, pos = 0, end = 0;
+    const uint16_t* rb = tc;
+    uint32_t base[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) base[i] = 0;
+    if (e < k) {
+        pos = E_s0[e] + 8u * li;
+        end = E_s1[e];
+        rb = tc + E_base[e];
+#pragma unroll
+        for (int i = 0; i < NW; i++) base[i] = E_m[e * NW + i];
+    }
+    uint32_t claim = 0;
+    if (li == 0) claim = atomicAdd(&sh.cursor[0], 1u);
+    uint4 v0[kTileU], v1[kTileU];
+#pragma unroll
+    for (int u = 0; u < kTileU; u++) {
+        const uint32_t pu = pos + 8u * L * u;
+        const bool ld = e < k && pu < end;
+        if ((DG && a.scan_stats) && ld) atomicAdd(&sh.st_quads, 1u);
+        v0[u] = *reinterpret_cast<const uint4*>(ld ? rb + pu : tc);
+    }
+    uint32_t m[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) m[i] = 0;
+    bool rowfull = false;
+#define MCMC_TQ_STEP(CUR, NXT, CONT)                                                                    \
+    {                                                                                                   \
+        const bool act = e < k;                                                                         \
+        uint32_t npos2 = pos + step, ne = e, nend2 = end;                                               \
+        const uint16_t* nrb = rb;                                                                       \
+        uint32_t nbase[NW];                                                                             \
+        _Pragma("unroll") for (int i = 0; i < NW; i++) nbase[i] = base[i];                              \
+        const bool fin = act && (npos2 - 8u * li >= end || rowfull);                                    \
+        if (__ballot(fin)) {                                                                            \
+            const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
+            if (fin) {                                                                                  \
+                ne = got;                                                                               \
+                if (ne < k) {                                                                           \
+                    npos2 = E_s0[ne] + 8u * li;                                                         \
+                    nend2 = E_s1[ne];                                                                   \
+                    nrb = tc + E_base[ne];                                                              \
+                    _Pragma("unroll") for (int i = 0; i < NW; i++) nbase[i] = E_m[ne * NW + i];         \
+                }                                                                                       \
+                if (li == 0) claim = atomicAdd(&sh.cursor[0], 1u);                                      \
+            }                                                                                           \
+        }                                                                                               \
+        CONT = __ballot(ne < k) != 0;                                                                   \
+        if (CONT) {                                                                                     \
+            _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                        \
+                const uint32_t pu = npos2 + 8u * L * u;                                                 \
+                const bool ld = ne < k && pu < nend2;                                                   \
+                if ((DG && a.scan_stats) && ld) atomicAdd(&sh.st_quads, 1u);                            \
+                NXT[u] = *reinterpret_cast<const uint4*>(ld ? nrb + pu : tc);                           \
+            }                                                                                           \
+        }                                                                                               \
+        _Pragma("unroll") for (int u = 0; u < kTileU; u++) {                                            \
+            const bool ok = act && !rowfull && pos + 8u * L * u < end;                                  \
+            tile_gather<NW>(sc, CUR[u], ok, m);                                                         \
+            if (DG && a.scan_stats) {                                                                   \
+                const uint64_t ub = __ballot(ok);                                                       \
+                if (lane == 0 && ub) atomicAdd(&sh.st_used, (uint32_t)__popcll(ub));                    \
+            }                                                                                           \
+        }                                                                                               \
+        const bool chk = act && !fin;                                                                   \
+        if (__ballot(fin || chk)) {                                                                     \
+            uint32_t red[NW];                                                                           \
+            _Pragma("unroll") for (int i = 0; i < NW; i++) {                                            \
+                uint32_t x = m[i];                                                                      \
+                for (uint32_t off = 1; off < L; off <<= 1) x |= __shfl_xor(x, (int)off, 64);            \
+                red[i] = x;                                                                             \
+            }                                                                                           \
+            if (fin) {                                                                                  \
+                if (li == 0) {                                                                          \
+                    _Pragma("unroll") for (int i = 0; i < NW; i++)                                      \
+                        if (red[i]) atomicOr(&E_m[e * NW + i], red[i]);                                 \
+                }                                                                                       \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) m[i] = 0;                                \
+            } else if (chk) {                                                                           \
+                uint32_t nm[NW];                                                                        \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) nm[i] = red[i] | base[i];                \
+                rowfull = is_full(nm);                                                                  \
+            }                                                                                           \
+        }                                                                                               \
+        if (fin) rowfull = false;                                                                       \
+        _Pragma("unroll") for (int i = 0; i < NW; i++) base[i] = nbase[i];                              \
+        e = ne;                                                                                         \
+        pos = npos2;                                                                                    \
+        end = nend2;                                                                                    \
+        rb = nrb;                                                                                       \
+    }
+    if (__ballot(e < k)) {
+        for (;;) {
+            bool c0, c1;
+            MCMC_TQ_STEP(v0, v1, c0)
+            if (!c0) break;
+            MCMC_TQ_STEP(v1, v0, c1)
+            if (!c1) break;
+        }
+    }
+#undef MCMC_TQ_STEP
+}
+
+template <int NW, bool DG>
+__device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restrict__ st, const uint8_t* __restrict__ C,
+                                       uint8_t* __restrict__ Cs, uint8_t* __restrict__ vf, uint8_t* lbase,
+                                       uint32_t SB, TailShared& sh, const uint32_t (&fullw)[NW], uint32_t x_t,
+                                       int lane, uint32_t& wave_viol, uint32_t& wave_ev, uint32_t kpair) {
+    const bool ptrace = DG && a.pair_trace != nullptr;
+    auto stamp = [&](unsigned long long* rec, int k) {
+        if (ptrace && threadIdx.x == 0) rec[k] = wall_clock64();
+    };
+    const uint32_t R = a.grp_rows, nb = a.nblocks, TS = tseg_stride(R);
+    const uint32_t wid = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+    const uint32_t nsub = 64u >> a.sub_log2;
+    auto is_full = [&](const uint32_t (&x)[NW]) -> bool {
+        bool f = true;
+#pragma unroll
+        for (int i = 0; i < NW; i++) f = f && ((x[i] & fullw[i]) == fullw[i]);
+        return f;
+    };
+    // chunk entries in slice buffer 1: base (8 B), s0, s1, row (4 B each), mask (4 NW B)
+    const uint32_t CH = min(2048u, (SB / (20u + 4u * NW)) & ~63u);
+    uint64_t* E_base = reinterpret_cast<uint64_t*>(lbase + SB);
+    uint32_t* E_s0 = reinterpret_cast<uint32_t*>(E_base + CH);
+    uint32_t* E_s1 = E_s0 + CH;
+    uint32_t* E_l = E_s1 + CH;
+    uint32_t* E_m = E_l + CH;
+    uint32_t* Q_l = a.tq_l + (size_t)blockIdx.x * 2u * a.tq_cap;
+    uint32_t* Q_m = a.tq_m + (size_t)blockIdx.x * 2u * a.tq_cap * NW;
+    const uint32_t lds0 = lds_addr(lbase);
+    uint32_t qs = 0;
+    for (uint32_t bb = a.tq_dense; bb < nb; bb++) {
+        __syncthreads();
+        const uint32_t qn = sh.qn[qs];
+        if (qn == 0) break;
+        __syncthreads();   // every wave has read qn
+        if (threadIdx.x == 0) sh.qn[qs ^ 1u] = 0;
+        unsigned long long* rec = (ptrace && kpair < kPairTraceMax)
+                                      ? a.pair_trace + ((size_t)blockIdx.x * kPairTraceMax + kpair) * kPairTraceRec
+                                      : nullptr;
+        if (rec) stamp(rec, 0);
+        tile_dma_slice(a, C, bb, lds0, wid, nwaves, lane);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the slice landed
+        if (rec) stamp(rec, 1);
+        uint64_t t_load = 0, t_scan = 0, t_cls = 0;
+        if ((DG && a.scan_stats) && threadIdx.x == 0) sh.st_pairs++;
+        const uint32_t* Ql = Q_l + (size_t)qs * a.tq_cap;
+        const uint32_t* Qm = Q_m + (size_t)qs * a.tq_cap * NW;
+        uint32_t* Pl = Q_l + (size_t)(qs ^ 1u) * a.tq_cap;
+        uint32_t* Pm = Q_m + (size_t)(qs ^ 1u) * a.tq_cap * NW;
+        const bool lastb = bb + 1 == nb;
+        for (uint32_t c0 = 0; c0 < qn; c0 += CH) {
+            const uint32_t k = min(CH, qn - c0);
+            for (uint32_t e = threadIdx.x; e < k; e += blockDim.x) {
+                const uint32_t l = Ql[c0 + e];
+                const uint32_t g = l / R, r = l - g * R;
+                const uint32_t* ts = a.tseg + ((size_t)g * nb + bb) * TS;
+                E_base[e] = a.gbase[g];
+                E_s0[e] = ts[r] & kTsegPos;
+                E_s1[e] = ts[r + 1] & kTsegPos;
+                E_l[e] = l;
+#pragma unroll
+                for (int i = 0; i < NW; i++) E_m[e * NW + i] = Qm[(size_t)(c0 + e) * NW + i];
+            }
+            if (threadIdx.x == 0) sh.cursor[0] = nwaves * nsub;
+            const uint64_t w0 = ptrace ? wall_clock64() : 0;
+            __syncthreads();
+            const uint64_t w1 = ptrace ? wall_clock64() : 0;
+            tail_scan<NW, DG>(a, lbase, E_base, E_s0, E_s1, E_m, k, sh, fullw, lane);
+            __syncthreads();
+            const uint64_t w2 = ptrace ? wall_clock64() : 0;
+            t_load += w1 - w0;
+            t_scan += w2 - w1;
+            // full (or out of blocks): evaluate; else queue for block bb + 1
+            for (uint32_t e0 = wid * 64u; e0 < k; e0 += nwaves * 64u) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                const bool in = e < k;
+                uint32_t acc[NW];
+#pragma unroll
+                for (int i = 0; i < NW; i++) acc[i] = in ? E_m[e * NW + i] : 0u;
+                const uint32_t l = in ? E_l[e] : 0u;
+                const bool done = in && (lastb || is_full(acc));
+                const bool keep = in && !done;
+                const uint64_t km = __ballot(keep);
+                if (km) {
+                    uint32_t qb = 0;
+                    if (lane == 0) qb = atomicAdd(&sh.qn[qs ^ 1u], (uint32_t)__popcll(km));
+                    qb = __shfl(qb, 0, 64);
+                    if (keep) {
+                        const uint32_t idx = qb + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
+                        Pl[idx] = l;
+#pragma unroll
+                        for (int i = 0; i < NW; i++) Pm[(size_t)idx * NW + i] = acc[i];
+                    }
+                }
+                uint32_t cv = 0, tab = 0, x = 0;
+                if (done) {
+                    cv = C[a.v_begin + l];
+                    if (a.taboo) tab = a.taboo[l];
+                    x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + l + 1u));
+                }
+                wave_viol += evaluate_lane<NW>(a, st, Cs, done, l, acc, lane, wave_ev, vf, cv, tab, x);
+            }
+            __syncthreads();
+            if (ptrace) t_cls += wall_clock64() - w2;
+        }
+        if (rec && threadIdx.x == 0) {   // tail block: slice staged, entry loads, scans, classify (durations)
+            rec[2] = t_load;
+            rec[3] = t_scan;
+            rec[4] = t_cls;
+            rec[5] = (unsigned long long)bb | ((unsigned long long)qn << 16) | (1ull << 39);
+        }
+        kpair++;
+        qs ^= 1u;
+    }
+}
+
 // RES: the whole replica is LDS-resident; otherwise the colour slice of each pair. One 1024-thread
 // workgroup per CU (two smaller ones per CU were measured to split the CU's issue unevenly: the
 // younger finished 30% later and the tail ran at half occupancy). A workgroup walks its
@@ -1592,6 +1876,8 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     uint8_t* seg_base = lbase + (RES ? SB : 2u * SB);
     const uint32_t SEGB = a.seg_buf_bytes;                              // bytes per table buffer
     uint32_t* smask = reinterpret_cast<uint32_t*>(seg_base + 2u * SEGB);
+    // early exit, listed pairs: the group's open rows (R entries) after the masks (a.olist_on)
+    uint16_t* olist = reinterpret_cast<uint16_t*>(smask + R * NW);
     // REF: [dynamic distribution p (256 floats)][new-colour histogram][2 own-colour buffers]
     float* p_lds = reinterpret_cast<float*>(seg_base + 2u * SEGB + ((R * NW * 4u + 15u) & ~15u));
     uint32_t* hist_lds = reinterpret_cast<uint32_t*>(p_lds + 256);
@@ -1614,6 +1900,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint32_t nbytes16 = (a.n + 15u) & ~15u;
     const uint32_t lds0 = lds_addr(lbase), seg_lds0 = lds_addr(seg_base);
     uint32_t wave_viol = 0, wave_ev = 0;
+    const uint32_t lpow = REF ? 0u : kMinstdLanePow[lane];   // 16807^lane: read once, before any scan load
     const bool timing = DG && a.phase_ts != nullptr;
     const bool ptrace = DG && a.pair_trace != nullptr;
     unsigned long long tr_start = 0;
@@ -1634,10 +1921,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         sh.cursor[0] = nwaves * nsub;
         sh.nfull[0] = sh.nfull[1] = sh.nfull[2] = 0;
         sh.dn[0] = sh.dn[1] = 0;
+        sh.qn[0] = sh.qn[1] = 0;
     }
     // Early exit (not REF: its scan counts arcs): a row whose mask holds all nCol colours is done --
     // its later segments are skipped, and once every row of a group is done its remaining pairs are.
     const bool EXIT = EX && !REF && a.early;   // EX = false: the full-scan instantiation (no early-exit code)
+    const bool TQ = EXIT && !RES && a.tq_dense != 0 && a.tq_dense < nb;   // the tail queue (tile_tail)
     uint32_t fullw[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) {
@@ -1711,21 +2000,30 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             const uint32_t nopen = rows - min(nfull_run, rows);
             // few rows left: they finish every remaining block here (tile_drain), no more pairs
             drain = !allfull && b > 0 && nopen <= a.drain_rows && b + 1 < nb;
-            // a sparse pair: only the listed open rows are claimed (not every row of the group)
-            sparse = !allfull && !drain && b > 0 && nopen <= 256u;
+            // a listed pair: only the open rows are claimed (not every row of the group) -- few open
+            // rows (the 256-entry list), or (a.olist_on) a tenth of the rows or more full: claiming
+            // full rows broke the one-row-ahead load pipeline (every open row behind a full one
+            // waited a whole memory round trip; C3 pair 2: 12.2 us with 737 of 1776 rows open)
+            sparse = !allfull && !drain && b > 0 && (nopen <= 256u || (a.olist_on && 10u * nopen < 9u * rows));
             if (threadIdx.x == 0) {
                 sh.nfull[(kpair + 1u) % 3u] = 0;
                 sh.dn[buf ^ 1u] = 0;   // the next pair's list counter (its last use: the previous pair)
             }
         }
+        // tail queue: the group's last dense pair -- its full rows are evaluated at its end, the open
+        // ones queued for tile_tail
+        const bool split = TQ && b + 1 == a.tq_dense && !allfull && !drain;
         uint32_t nlist = 0;
+        uint16_t* dl = sh.dlist;
         if (drain || sparse) {
-            tile_open_rows<NW>(rows, smask, sh, fullw, buf);
-            nlist = min(sh.dn[buf], 256u);
+            const bool big = sparse && a.olist_on;   // the R-entry list (any number of open rows)
+            dl = big ? olist : sh.dlist;
+            tile_open_rows<NW>(rows, smask, sh, fullw, buf, dl, big ? R : 256u);
+            nlist = min(sh.dn[buf], big ? R : 256u);
         }
         const uint32_t kslot = kpair % 3u;
         // the group's last pair: its last block, every row already full, or the drain
-        const bool last = (b + 1 == nb) || allfull || drain || (DG && a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
+        const bool last = (b + 1 == nb) || allfull || drain || split || (DG && a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
         // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
         if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
@@ -1773,7 +2071,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             // sub-groups (their first quads reloaded: the prefetched ones are the static rows'),
             // the rest claimed (the cursor starts past them)
             const uint32_t s = wid * nsub + sub;
-            row = s < nlist ? (uint32_t)sh.dlist[s] : rows;
+            row = s < nlist ? (uint32_t)dl[s] : rows;
             if (row < rows) {
                 const uint32_t sraw = sseg[row];
                 pos = (sraw & kTsegPos) + 8u * li;
@@ -1810,7 +2108,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             const uint32_t got = __shfl(claim, (int)(sub << a.sub_log2), 64);                           \
             if (fin) {                                                                                  \
                 nrow = got;                                                                             \
-                if (sparse) nrow = (got < nlist) ? (uint32_t)sh.dlist[got] : rows;                      \
+                if (sparse) nrow = (got < nlist) ? (uint32_t)dl[got] : rows;                            \
                 if (nrow < rows) {                                                                      \
                     const uint32_t sraw = sseg[nrow];                                                   \
                     npos2 = (sraw & kTsegPos) + 8u * li;                                                \
@@ -1897,6 +2195,22 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         }
 #undef MCMC_TILE_STEP
 #undef MCMC_TILE_GATHER
+        // the evaluation's own colours and taboo counters of this wave's first two tiles, loaded
+        // BEFORE the next pair's first quads: vmcnt retires loads in order, so a load issued after
+        // those quads would make the evaluation wait for their HBM round trip (C3: 6 us per group)
+        const uint32_t tstride = nwaves * 64u;
+        uint32_t cvA = 0, tabA = 0, cvB = 0, tabB = 0;
+        if (!REF && last) {
+            const uint32_t ea = wid * 64u + (uint32_t)lane, eb = ea + tstride;
+            if (ea < rows) {
+                cvA = C[a.v_begin + r0 + ea];
+                if (a.taboo) tabA = a.taboo[r0 + ea];
+            }
+            if (eb < rows) {
+                cvB = C[a.v_begin + r0 + eb];
+                if (a.taboo) tabB = a.taboo[r0 + eb];
+            }
+        }
         // the next pair's first quads: in flight across the boundary (and the evaluation)
         gr = ngr;
         gcol = ngcol;
@@ -1932,16 +2246,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             if (timing) { const uint64_t t1 = __builtin_readcyclecounter(); cyc_eval += t1 - tmark; tmark = t1; }
         } else if (last) {
             // Wave w evaluates rows w * 64 + k * 1024 (64-row tiles) and clears their masks for the
-            // next group. Each tile's own colours and taboo counters are loaded one tile ahead (the
-            // first before the barrier); u_v's minstd state comes from the wave's running base
-            // xg = x_t 16807^(v + 1) of its first row (no per-tile power).
-            const uint32_t tstride = nwaves * 64u;
-            const uint32_t lpow = kMinstdLanePow[lane];
-            uint32_t e0 = wid * 64u, cv = 0, tab = 0;
-            if (e0 + (uint32_t)lane < rows) {
-                cv = C[a.v_begin + r0 + e0 + lane];
-                if (a.taboo) tab = a.taboo[r0 + e0 + lane];
-            }
+            // next group. Each tile's own colours and taboo counters are loaded two tiles ahead (the
+            // first two before the next pair's quads); u_v's minstd state comes from the wave's
+            // running base xg = x_t 16807^(v + 1) of its first row (no per-tile power).
+            uint32_t e0 = wid * 64u, cv = cvA, tab = tabA;
             // every wave's mask ORs of the group are in, and this wave's DMA of the next pair has
             // landed (the DMA precedes the 6 first-row loads; vmcnt(6) also covers the loads above):
             // the pair's barrier after the evaluation then waits for LDS only, so the evaluation's
@@ -1950,11 +2258,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             uint32_t xk = xg;
             for (; e0 < rows; e0 += tstride) {
                 const uint32_t cnt = min(64u, rows - e0);
-                const uint32_t e1 = e0 + tstride;
-                uint32_t cv1 = 0, tab1 = 0;
-                if (e1 + (uint32_t)lane < rows) {
-                    cv1 = C[a.v_begin + r0 + e1 + lane];
-                    if (a.taboo) tab1 = a.taboo[r0 + e1 + lane];
+                const uint32_t e2 = e0 + 2u * tstride;
+                uint32_t cv1 = cvB, tab1 = tabB;
+                cvB = 0;
+                tabB = 0;
+                if (e2 + (uint32_t)lane < rows) {
+                    cvB = C[a.v_begin + r0 + e2 + lane];
+                    if (a.taboo) tabB = a.taboo[r0 + e2 + lane];
                 }
                 uint32_t acc[NW];
 #pragma unroll
@@ -1963,7 +2273,25 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     acc[i] = ((uint32_t)lane < cnt) ? smask[idx] : 0u;
                     if ((uint32_t)lane < cnt) smask[idx] = 0;
                 }
-                wave_viol += evaluate_core<NW>(a, st, Cs, r0 + e0, cnt, acc, lane, wave_ev, vf, cv, tab,
+                bool okv = (uint32_t)lane < cnt;
+                if (split) {   // open rows wait in the tail queue (queue 0), with their masks
+                    const bool open = okv && !is_full(acc);
+                    const uint64_t om = __ballot(open);
+                    if (om) {
+                        uint32_t qb = 0;
+                        if (lane == 0) qb = atomicAdd(&sh.qn[0], (uint32_t)__popcll(om));
+                        qb = __shfl(qb, 0, 64);
+                        if (open) {
+                            const uint32_t idx = qb + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
+                            a.tq_l[(size_t)blockIdx.x * 2u * a.tq_cap + idx] = r0 + e0 + lane;
+#pragma unroll
+                            for (int i = 0; i < NW; i++)
+                                a.tq_m[((size_t)blockIdx.x * 2u * a.tq_cap + idx) * NW + i] = acc[i];
+                        }
+                    }
+                    okv = okv && !open;
+                }
+                wave_viol += evaluate_lane<NW>(a, st, Cs, okv, r0 + e0 + lane, acc, lane, wave_ev, vf, cv, tab,
                                                minstd_mulmod(xk, lpow));
                 cv = cv1;
                 tab = tab1;
@@ -1997,6 +2325,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         buf ^= 1u;
         kpair++;
     }
+    if (TQ) tile_tail<NW, DG>(a, st, C, Cs, vf, lbase, SB, sh, fullw, x_t, lane, wave_viol, wave_ev, kpair);
     if ((DG && a.scan_stats)) {   // diagnostics: quads loaded and pairs staged by this workgroup
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2189,6 +2518,10 @@ struct mcmc_ctx {
     bool part = false;          // attached to a partitioned run (caller-owned buffers and stream)
     int bench_mode = 0;         // mcmc_set_bench_mode: no convergence stop (throughput timing)
     int early = 1;              // tiled: early-exit scan (MCMC_FULL_SCAN=1: every arc)
+    int olist_on = 0;           // tiled early exit: R-entry open-row list in LDS (listed pairs)
+    uint32_t tq_dense = 0, tq_cap = 0;       // tiled early exit: tail queue (dense blocks, entries per queue)
+    uint32_t* tq_l = nullptr;                // [grid][2][tq_cap] rows
+    uint32_t* tq_m = nullptr;                // [grid][2][tq_cap][nw] masks
     uint32_t drain_rows = 32;   // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256; C3: 32 best)
     unsigned long long* scan_stats = nullptr;   // mcmc_set_scan_stats: [quads loaded, pairs staged]
     bool scan_stats_on = false;
@@ -2306,6 +2639,11 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.check_done = check_done;
     a.bench = c->bench_mode;
     a.early = c->early;
+    a.olist_on = c->olist_on;
+    a.tq_dense = c->tq_l ? c->tq_dense : 0u;
+    a.tq_cap = c->tq_cap;
+    a.tq_l = c->tq_l;
+    a.tq_m = c->tq_m;
     a.drain_rows = c->drain_rows;
     if (const char* dm = getenv("MCMC_DEBUG_MAX_PAIRS")) a.dbg_max_pairs = (uint32_t)atoi(dm);
     a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
@@ -2804,6 +3142,29 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));
         c->sub_log2 = sl;
         c->lds = lds_need(resident, R);
+        if (!ref && c->early && !getenv("MCMC_NO_OLIST")) {   // the open-row list of listed pairs, if it fits
+            const size_t lb = ((size_t)R * 2u + 15u) & ~(size_t)15u;
+            if (c->lds + lb <= kMaxLdsBytes) {
+                c->lds += lb;
+                c->olist_on = 1;
+            }
+        }
+        // the tail queue (streaming early exit with more blocks than the dense ones): every
+        // workgroup's queues hold all rows of its groups
+        const char* tqe = getenv("MCMC_TQ_DENSE");
+        const uint32_t tqd = tqe ? (uint32_t)std::max(0, atoi(tqe)) : 2u;
+        if (!ref && c->early && !resident && tqd > 0 && tqd < c->nblocks && c->tl->ngroups > 0) {
+            const uint32_t gpw = (c->tl->ngroups + c->grid.x - 1) / c->grid.x;
+            c->tq_cap = gpw * R;
+            const size_t ents = (size_t)c->grid.x * 2u * c->tq_cap;
+            hipError_t qe = hipMalloc(&c->tq_l, sizeof(uint32_t) * ents);
+            if (qe == hipSuccess) qe = hipMalloc(&c->tq_m, sizeof(uint32_t) * ents * c->nw);
+            if (qe != hipSuccess) {
+                mcmc_destroy(c);
+                return fail(MCMC_E_NOMEM, std::string("tail queue: ") + hipGetErrorString(qe));
+            }
+            c->tq_dense = tqd;
+        }
         c->own_buf_bytes = resident ? 0u : (uint32_t)own_bytes(R);
         if (ref) {
             if (resident) {
@@ -3525,6 +3886,8 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->wave_start);
     (void)hipFree(c->seg);
     (void)hipFree(c->phase_ts);
+    (void)hipFree(c->tq_l);
+    (void)hipFree(c->tq_m);
     (void)hipFree(c->pair_trace);
     (void)hipFree(c->vflags);
     (void)hipFree(c->tc_list);
@@ -3614,6 +3977,10 @@ int part_set_delta(mcmc_ctx* c, uint32_t* d0, uint32_t* d1) {
 
 bool part_delta_ok(const mcmc_ctx* c) { return c && c->part && c->dlt[0] && !c->wide; }
 
+// A partition of one rank (world 1) steps exactly like a whole-graph context: the sweep commits in
+// its last workgroup (no footer, no exchange, no commit launch). Not for the reference-semantics mode.
+static bool part_solo(const mcmc_ctx* c) { return c->world == 1 && !c->ref && !getenv("MCMC_PART_SOLO_OFF"); }
+
 const void* part_state_ptr(const mcmc_ctx* c) { return c->st; }
 static_assert(kDeltaWords == kPartDeltaWords, "delta slot size");
 static_assert(offsetof(DevState, t) == 0 && offsetof(DevState, done) == 4 && offsetof(DevState, err) == 12,
@@ -3627,14 +3994,22 @@ int part_sweep(mcmc_ctx* c, bool delta) {
     c->ran = true;
     SweepArgs a = make_args(c, 1);
     a.dcap = delta ? kDeltaPairs : 0u;
-    launch_tiled_or_diag(c, a);
-    if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (part_solo(c)) {
+        // world 1: nothing to exchange -- the one-GPU step (the last workgroup commits, or the
+        // wide sweep's commit launch); the step's part_commit is then a no-op
+        a.fused = c->wide ? 0 : 1;
+        launch_pair(c, a);
+    } else {
+        launch_tiled_or_diag(c, a);
+        if (c->wide) wide_footer_kernel<<<1, kCommitThreads, 0, c->stream>>>(a);
+    }
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
 }
 
 int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride) {
     if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
+    if (part_solo(c)) return MCMC_OK;   // world 1: the sweep committed (part_sweep)
     if (mode > 0 && !part_delta_ok(c)) return fail(MCMC_E_STATE, "delta exchange: tiled partitioned contexts only");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     SweepArgs a = make_args(c, 1);

@@ -16,6 +16,8 @@ for path in sys.argv[1:]:
     nwg = len(t)
     recs = t.reshape(-1, REC)
     recs = recs[recs[:, 0] > 0]
+    tail = recs[(recs[:, 5] >> 39) & 1 == 1]     # tail-queue blocks (tile_tail): durations in slots 2-4
+    recs = recs[(recs[:, 5] >> 39) & 1 == 0]
     info = recs[:, 5]
     b = info & 0xFFFF
     nopen = (info >> 16) & 0xFFFFFF
@@ -39,6 +41,16 @@ for path in sys.argv[1:]:
               f"{np.median(ev[m][last[m] == 1]) if (last[m] == 1).any() else 0:6.2f} {np.median(bar[m]):6.2f}")
     tot = scan.sum() + ev.sum() + bar.sum()
     print(f"  share: scan {scan.sum() / tot:.2f}  eval {ev.sum() / tot:.2f}  barrier {bar.sum() / tot:.2f}")
+    if len(tail):
+        tb = tail[:, 5] & 0xFFFF
+        tq = (tail[:, 5] >> 16) & 0xFFFFFF
+        print("  tail queue: block  workgroups  entries(med)  stage  load  scan  classify   (median us)")
+        for k in np.unique(tb):
+            m = tb == k
+            print(f"              {k:5d} {m.sum():11d} {np.median(tq[m]):13.0f} {np.median(us(tail[m, 1] - tail[m, 0])):6.2f} "
+                  f"{np.median(us(tail[m, 2])):5.2f} {np.median(us(tail[m, 3])):5.2f} {np.median(us(tail[m, 4])):9.2f}")
+        per_wg = (us(tail[:, 1] - tail[:, 0]) + us(tail[:, 2]) + us(tail[:, 3]) + us(tail[:, 4])).sum() / nwg
+        print(f"  tail queue total {per_wg:.1f} us per workgroup")
     for k in range(int(b.max()) + 1):
         m = b == k
         if m.any():

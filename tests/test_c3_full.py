@@ -23,7 +23,7 @@ import time
 import numpy as np
 import pytest
 
-import c3_expect as X
+import c3_expect as C3X
 import oracle_ref as O
 
 N, P, SEED, NCOL, EPS = 10_000_000, 0.001, 1, 32, 1e-8
@@ -85,8 +85,8 @@ def test_c3_full_size_rows_and_sweeps(hip_lib):
     print(f"checked {checked} vertex updates ({events} CDF overflows skipped)", flush=True)
     assert checked >= 2900
     t1 = time.perf_counter()
-    X.pin_walk(NCOL, EPS)
-    E, k0e, evs = X.expected(3, EPS)
+    C3X.pin_walk(NCOL, EPS)
+    E, k0e, evs = C3X.expected(3, EPS)
     assert k0e == k0
     for t in range(4):
         bad = np.nonzero(C[t] != E[t])[0]
@@ -105,8 +105,8 @@ def test_c3_full_size_every_vertex_eps_1e3(hip_lib):
     import mcmc_colorer_amd.colorer as M
 
     eps = 1e-3
-    X.pin_walk(NCOL, eps)
-    E, k0, evs = X.expected(3, eps)
+    C3X.pin_walk(NCOL, eps)
+    E, k0, evs = C3X.expected(3, eps)
     g = M.Graph.er_fast(N, P, SEED)
     col = M.ColoringMCMC(g, M.GPURand(N, SEED, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=NCOL, epsilon=eps))
     col.init(0)
