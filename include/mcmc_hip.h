@@ -258,7 +258,8 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t*
 int mcmc_part_sweep_async(mcmc_ctx* c);
 int mcmc_part_commit_async(mcmc_ctx* c);
 /* Synchronises the stream; *done = 1 once the loop is over (colouring/trajectory then final);
- * *err: bit 0 a fatal device error, bit 1 a spill exchange is pending (then *t is the paused sweep). */
+ * *err: bit 0 a fatal device error, bit 1 a spill exchange is pending, bit 2 a delta slot overflowed
+ * (then *t is the paused sweep). */
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
 /* Spill exchange of a paused sweep: every rank's list length (from the exchanged footers), this
  * rank's sorted list copied to device memory dst (NULL: the count only), and the resumption from
@@ -266,6 +267,28 @@ int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err);
 int mcmc_part_spill_counts(mcmc_ctx* c, uint32_t* counts /* world */);
 int mcmc_part_spill_local(mcmc_ctx* c, void* dst, uint32_t* count);
 int mcmc_part_spill_commit_async(mcmc_ctx* c, const uint32_t* gathered, uint32_t stride);
+/* Delta exchange (what mcmc_part_run does by default at world > 1): a step sends, instead of the
+ * rank's rows, its delta slot -- MCMC_DELTA_WORDS uint32 at dlt[(t+1)&1] + rank * MCMC_DELTA_WORDS:
+ * [0] pairs appended (may exceed the slot's (MCMC_DELTA_WORDS - 2) / 2), [1] 0, then (vertex, colour)
+ * pairs of the rank's vertices whose colour changed (overflow events excepted: every rank replays
+ * them). The commit applies every other rank's pairs to BOTH replicas, so outside its own rows a
+ * rank's replicas stay equal; after full-mode steps (or at a run's start) mcmc_part_sync_remote_async
+ * restores that before the next delta step. A slot that overflowed pauses the sweep on every rank
+ * (mcmc_part_state err bit 2): exchange its rows as in full mode, then resume with mode -1 (and the
+ * gathered lists if err bit 1 is set too). dlt0/dlt1: caller-owned device buffers of world *
+ * MCMC_DELTA_WORDS uint32 each (mcmc_part_create's contexts own theirs). Tiled sweeps only (nCol <=
+ * 256): mcmc_part_delta_ok. Modes of mcmc_part_commit_mode_async: 1 delta, 0 full, -1 full-mode
+ * resumption of a paused sweep (gathered/stride as mcmc_part_spill_commit_async, or NULL/0). */
+#define MCMC_DELTA_WORDS 4096
+int mcmc_part_attach_delta(mcmc_ctx* c, void* dlt0, void* dlt1);
+int mcmc_part_delta_ok(mcmc_ctx* c);
+int mcmc_part_sweep_mode_async(mcmc_ctx* c, int delta);
+int mcmc_part_commit_mode_async(mcmc_ctx* c, int mode, const uint32_t* gathered, uint32_t stride);
+int mcmc_part_sync_remote_async(mcmc_ctx* c);
+/* Exchange statistics of the context's last mcmc_part_run: steps exchanged in delta and in full
+ * mode, delta-slot overflows (paused sweeps), and the bytes this rank sent to its peers. */
+int mcmc_part_exchange_stats(mcmc_ctx* c, uint64_t* delta_steps, uint64_t* full_steps, uint64_t* overflows,
+                             uint64_t* bytes_sent);
 
 /* Native runs (csrc/multi.hip): RCCL communicators behind the ABI. One process per GPU:
  * rank 0 calls mcmc_comm_unique_id and hands the bytes to the others (any channel), every rank

@@ -68,6 +68,13 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_part_spill_counts": (c_int, [c_void_p, _u32p]),
     "mcmc_part_spill_local": (c_int, [c_void_p, c_void_p, _u32p]),
     "mcmc_part_spill_commit_async": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "mcmc_part_attach_delta": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mcmc_part_delta_ok": (c_int, [c_void_p]),
+    "mcmc_part_sweep_mode_async": (c_int, [c_void_p, c_int]),
+    "mcmc_part_commit_mode_async": (c_int, [c_void_p, c_int, c_void_p, c_uint32]),
+    "mcmc_part_sync_remote_async": (c_int, [c_void_p]),
+    "mcmc_part_exchange_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64),
+                                         POINTER(c_uint64)]),
     "mcmc_comm_unique_id": (c_int, [c_void_p]),
     "mcmc_comm_init_rank": (c_int, [c_void_p, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "mcmc_comm_init_all": (c_int, [POINTER(c_int), c_uint32, POINTER(c_void_p)]),

@@ -170,7 +170,8 @@ const void* part_state_ptr(const mcmc_ctx* c);   // device state: {t, done, x_t,
 int part_sweep(mcmc_ctx* c, bool delta);
 int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride);
 int part_sync_remote(mcmc_ctx* c);
-int part_run_begin(mcmc_ctx* c);   // a run's start: this rank's delta slots empty, no tail-cut result
+int part_run_begin(mcmc_ctx* c);   // a run's start: this rank's delta slots empty, no tail-cut result, stats zero
+void part_add_xstats(mcmc_ctx* c, uint64_t delta_steps, uint64_t full_steps, uint64_t ovf, uint64_t bytes);
 // Partitioned tail cut (mcmc_sweep.hip): state and colorIdx at loop exit (global Cviol, the final t,
 // the final colouring's buffer); one rank's repair of its flagged rows; its recount (device sum
 // word); the result for the run summary.

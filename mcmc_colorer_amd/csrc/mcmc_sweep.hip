@@ -100,8 +100,13 @@ struct SweepArgs {
     // the workgroup's last group, rows of all its groups together (tile_tail)
     uint32_t tq_dense;
     uint32_t tq_cap;            // queue entries per workgroup and queue
-    uint32_t* tq_l;             // [grid][2][tq_cap] local rows
+    uint32_t* tq_l;             // [grid][2][tq_cap][3] local row, its u_v minstd state, own colour | taboo << 8
     uint32_t* tq_m;             // [grid][2][tq_cap][NW] their occupancy masks
+    uint32_t eown_off;          // tiled early exit: LDS byte offset of the evaluated group's own colours (0: none)
+    // the own-colour walk in closed form (fill_p cases (i)/(iii)): ewalk[c] = {E[c], fl(E[c] + hi)} with
+    // E[c] the c-fold fp32 sum of eps; nullptr where the host found the form inexact (ewalk_table)
+    const float2* ewalk;
+    uint32_t ewalk_off;         // tiled: LDS byte offset of its copy (0: none)
     const uint32_t* seg;        // blocked: per-(block, local row) segment offsets, (nb+1) x nloc
     uint32_t nblocks;           // blocked: column blocks of 2^block_log2 vertices
     uint32_t block_log2;        // blocked: log2 of the column block (17: 128 KiB of uint8 colours)
@@ -734,11 +739,17 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
 // x = the minstd state after draw v + 1 of this sweep (x_t 16807^(v+1) mod 2^31-1).
 // evaluate_lane: lane-wise form -- this lane evaluates local row l when `valid` (any rows per lane,
 // not necessarily consecutive: the tail queue's entries); every lane of the wave calls it.
+// ew (LDS, or nullptr): the closed-form own-colour walk (SweepArgs::ewalk) -- for fill_p's cases
+// (i)/(iii) the CDF before colour c < cv is E[c+1], at cv it is S = fl(E[cv] + hi), and after it adding
+// eps leaves S unchanged (checked on the host for every colour), so once u >= E[cv] the walk's answer
+// is cv when S > u, else a CDF overflow; below E[cv] (probability ~E[cv], < 3e-6 at eps 1e-8) the
+// step-by-step walk runs. Bit-identical to the loop.
 template <int NW>
 __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* __restrict__ st,
                                                   uint8_t* __restrict__ Cs, bool valid, uint32_t l,
                                                   const uint32_t (&acc)[NW], int lane, uint32_t& ev_flag,
-                                                  uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x) {
+                                                  uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x,
+                                                  const float2* ew = nullptr) {
     const uint32_t v = a.v_begin + l;
     uint32_t pop = 0;
 #pragma unroll
@@ -766,7 +777,15 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
     }
     // extract_new_color: cdf += p[c]; break on cdf > u (strict).
     uint32_t newc = a.nCol;
-    if (valid && tab == 0) {
+    bool walked = false;
+    if (ew != nullptr && valid && tab == 0 && !(viol && Zvcomp > 0)) {
+        const float2 es = ew[cv];
+        if (u >= es.x) {
+            newc = (es.y > u) ? cv : a.nCol;
+            walked = true;
+        }
+    }
+    if (valid && tab == 0 && !walked) {
         float cdf = 0.0f;
 #pragma unroll
         for (int i = 0; i < NW; i++) {
@@ -976,7 +995,8 @@ struct TailShared {
     uint32_t st_quads, st_pairs, st_used;   // diagnostics (scan_stats): quads loaded, pairs staged, quads gathered
     uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
-    unsigned long long tr[2][3];   // diagnostics (pair trace): scan end min / max over waves, eval end max
+    unsigned long long tr[2][4];   // diagnostics (pair trace): scan end min / max over waves, eval end max,
+                                   // the evaluation's barrier passed (max)
     uint32_t qn[2];       // tiled tail queue: entries of the two queues
 };
 
@@ -1733,7 +1753,8 @@ template <int NW, bool DG>
 __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restrict__ st, const uint8_t* __restrict__ C,
                                        uint8_t* __restrict__ Cs, uint8_t* __restrict__ vf, uint8_t* lbase,
                                        uint32_t SB, TailShared& sh, const uint32_t (&fullw)[NW], uint32_t x_t,
-                                       int lane, uint32_t& wave_viol, uint32_t& wave_ev, uint32_t kpair) {
+                                       int lane, uint32_t& wave_viol, uint32_t& wave_ev, uint32_t kpair,
+                                       const float2* ew) {
     const bool ptrace = DG && a.pair_trace != nullptr;
     auto stamp = [&](unsigned long long* rec, int k) {
         if (ptrace && threadIdx.x == 0) rec[k] = wall_clock64();
@@ -1747,14 +1768,17 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
         for (int i = 0; i < NW; i++) f = f && ((x[i] & fullw[i]) == fullw[i]);
         return f;
     };
-    // chunk entries in slice buffer 1: base (8 B), s0, s1, row (4 B each), mask (4 NW B)
-    const uint32_t CH = min(2048u, (SB / (20u + 4u * NW)) & ~63u);
+    // chunk entries in slice buffer 1: base (8 B), s0, s1, row, u_v state, own colour | taboo << 8
+    // (4 B each), mask (4 NW B)
+    const uint32_t CH = min(2048u, (SB / (28u + 4u * NW)) & ~63u);
     uint64_t* E_base = reinterpret_cast<uint64_t*>(lbase + SB);
     uint32_t* E_s0 = reinterpret_cast<uint32_t*>(E_base + CH);
     uint32_t* E_s1 = E_s0 + CH;
     uint32_t* E_l = E_s1 + CH;
-    uint32_t* E_m = E_l + CH;
-    uint32_t* Q_l = a.tq_l + (size_t)blockIdx.x * 2u * a.tq_cap;
+    uint32_t* E_x = E_l + CH;
+    uint32_t* E_c = E_x + CH;
+    uint32_t* E_m = E_c + CH;
+    uint32_t* Q_l = a.tq_l + (size_t)blockIdx.x * 2u * a.tq_cap * 3u;
     uint32_t* Q_m = a.tq_m + (size_t)blockIdx.x * 2u * a.tq_cap * NW;
     const uint32_t lds0 = lds_addr(lbase);
     uint32_t qs = 0;
@@ -1773,15 +1797,17 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
         if (rec) stamp(rec, 1);
         uint64_t t_load = 0, t_scan = 0, t_cls = 0;
         if ((DG && a.scan_stats) && threadIdx.x == 0) sh.st_pairs++;
-        const uint32_t* Ql = Q_l + (size_t)qs * a.tq_cap;
+        const uint32_t* Ql = Q_l + (size_t)qs * a.tq_cap * 3u;
         const uint32_t* Qm = Q_m + (size_t)qs * a.tq_cap * NW;
-        uint32_t* Pl = Q_l + (size_t)(qs ^ 1u) * a.tq_cap;
+        uint32_t* Pl = Q_l + (size_t)(qs ^ 1u) * a.tq_cap * 3u;
         uint32_t* Pm = Q_m + (size_t)(qs ^ 1u) * a.tq_cap * NW;
         const bool lastb = bb + 1 == nb;
         for (uint32_t c0 = 0; c0 < qn; c0 += CH) {
             const uint32_t k = min(CH, qn - c0);
             for (uint32_t e = threadIdx.x; e < k; e += blockDim.x) {
-                const uint32_t l = Ql[c0 + e];
+                const uint32_t l = Ql[(size_t)(c0 + e) * 3u];
+                E_x[e] = Ql[(size_t)(c0 + e) * 3u + 1u];
+                E_c[e] = Ql[(size_t)(c0 + e) * 3u + 2u];
                 const uint32_t g = l / R, r = l - g * R;
                 const uint32_t* ts = a.tseg + ((size_t)g * nb + bb) * TS;
                 E_base[e] = a.gbase[g];
@@ -1817,18 +1843,21 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
                     qb = __shfl(qb, 0, 64);
                     if (keep) {
                         const uint32_t idx = qb + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
-                        Pl[idx] = l;
+                        Pl[(size_t)idx * 3u] = l;
+                        Pl[(size_t)idx * 3u + 1u] = E_x[e];
+                        Pl[(size_t)idx * 3u + 2u] = E_c[e];
 #pragma unroll
                         for (int i = 0; i < NW; i++) Pm[(size_t)idx * NW + i] = acc[i];
                     }
                 }
                 uint32_t cv = 0, tab = 0, x = 0;
-                if (done) {
-                    cv = C[a.v_begin + l];
-                    if (a.taboo) tab = a.taboo[l];
-                    x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + l + 1u));
+                if (done) {   // everything from the entry: no global load in this loop
+                    const uint32_t ct = E_c[e];
+                    cv = ct & 0xFFu;
+                    tab = ct >> 8;
+                    x = E_x[e];
                 }
-                wave_viol += evaluate_lane<NW>(a, st, Cs, done, l, acc, lane, wave_ev, vf, cv, tab, x);
+                wave_viol += evaluate_lane<NW>(a, st, Cs, done, l, acc, lane, wave_ev, vf, cv, tab, x, ew);
             }
             __syncthreads();
             if (ptrace) t_cls += wall_clock64() - w2;
@@ -1871,6 +1900,13 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     uint8_t* lbase = reinterpret_cast<uint8_t*>(lds_raw);
+    // the closed-form own-colour walk's table in LDS (landed by the first barrier below)
+    const float2* ew = nullptr;
+    if (!REF && a.ewalk_off && a.ewalk) {
+        float2* ewl = reinterpret_cast<float2*>(lbase + a.ewalk_off);
+        for (uint32_t i = threadIdx.x; i < a.nCol; i += blockDim.x) ewl[i] = a.ewalk[i];
+        ew = ewl;
+    }
     const uint32_t R = a.grp_rows, nb = a.nblocks;
     const uint32_t SB = RES ? a.slice_bytes : tile_slice_buf(a.block_log2);   // bytes per colour buffer
     uint8_t* seg_base = lbase + (RES ? SB : 2u * SB);
@@ -1986,6 +2022,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             sh.tr[(kpair + 1u) & 1u][0] = ~0ull;
             sh.tr[(kpair + 1u) & 1u][1] = 0;
             sh.tr[(kpair + 1u) & 1u][2] = 0;
+            sh.tr[(kpair + 1u) & 1u][3] = 0;
         }
         const uint32_t r0 = g * R;
         const uint32_t rows = min(R, nloc - r0);
@@ -2029,6 +2066,9 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
         const uint32_t ng = last ? g + gridDim.x : g, nbn = last ? 0u : b + 1;
         const bool nvalid = ng < a.ngroups;
+        // the evaluated group's own colours by LDS-DMA now, so the evaluation at the pair's end finds
+        // them landed (a register load there waited one loaded-HBM round trip, ~5 us per group)
+        if (!REF && last && a.eown_off) tile_dma_own(a, C, g, lds0 + a.eown_off, wid, nwaves, lane);
         if (nvalid) {
             tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane);
             if (REF && !RES && nbn == 0)
@@ -2200,14 +2240,15 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // those quads would make the evaluation wait for their HBM round trip (C3: 6 us per group)
         const uint32_t tstride = nwaves * 64u;
         uint32_t cvA = 0, tabA = 0, cvB = 0, tabB = 0;
+        const uint8_t* eown = lbase + a.eown_off + ((a.v_begin + r0) & 15u);   // a.eown_off: own colours in LDS
         if (!REF && last) {
             const uint32_t ea = wid * 64u + (uint32_t)lane, eb = ea + tstride;
             if (ea < rows) {
-                cvA = C[a.v_begin + r0 + ea];
+                if (!a.eown_off) cvA = C[a.v_begin + r0 + ea];
                 if (a.taboo) tabA = a.taboo[r0 + ea];
             }
             if (eb < rows) {
-                cvB = C[a.v_begin + r0 + eb];
+                if (!a.eown_off) cvB = C[a.v_begin + r0 + eb];
                 if (a.taboo) tabB = a.taboo[r0 + eb];
             }
         }
@@ -2255,6 +2296,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             // the pair's barrier after the evaluation then waits for LDS only, so the evaluation's
             // stores and the next pair's first quads stay in flight across it
             MCMC_PAIR_BARRIER();
+            if (ptrace && lane == 0) atomicMax(&sh.tr[kpair & 1u][3], (unsigned long long)wall_clock64());
             uint32_t xk = xg;
             for (; e0 < rows; e0 += tstride) {
                 const uint32_t cnt = min(64u, rows - e0);
@@ -2263,9 +2305,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                 cvB = 0;
                 tabB = 0;
                 if (e2 + (uint32_t)lane < rows) {
-                    cvB = C[a.v_begin + r0 + e2 + lane];
+                    if (!a.eown_off) cvB = C[a.v_begin + r0 + e2 + lane];
                     if (a.taboo) tabB = a.taboo[r0 + e2 + lane];
                 }
+                if (a.eown_off && e0 + (uint32_t)lane < rows) cv = eown[e0 + lane];
                 uint32_t acc[NW];
 #pragma unroll
                 for (int i = 0; i < NW; i++) {
@@ -2281,9 +2324,12 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                         uint32_t qb = 0;
                         if (lane == 0) qb = atomicAdd(&sh.qn[0], (uint32_t)__popcll(om));
                         qb = __shfl(qb, 0, 64);
-                        if (open) {
+                        if (open) {   // the entry carries what its evaluation needs: u_v's state, own colour, taboo
                             const uint32_t idx = qb + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
-                            a.tq_l[(size_t)blockIdx.x * 2u * a.tq_cap + idx] = r0 + e0 + lane;
+                            uint32_t* q = a.tq_l + ((size_t)blockIdx.x * 2u * a.tq_cap + idx) * 3u;
+                            q[0] = r0 + e0 + lane;
+                            q[1] = minstd_mulmod(xk, lpow);
+                            q[2] = cv | (tab << 8);
 #pragma unroll
                             for (int i = 0; i < NW; i++)
                                 a.tq_m[((size_t)blockIdx.x * 2u * a.tq_cap + idx) * NW + i] = acc[i];
@@ -2292,7 +2338,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     okv = okv && !open;
                 }
                 wave_viol += evaluate_lane<NW>(a, st, Cs, okv, r0 + e0 + lane, acc, lane, wave_ev, vf, cv, tab,
-                                               minstd_mulmod(xk, lpow));
+                                               minstd_mulmod(xk, lpow), ew);
                 cv = cv1;
                 tab = tab1;
                 xk = minstd_mulmod(xk, xsk);
@@ -2312,6 +2358,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             rec[2] = sh.tr[kpair & 1u][1];
             rec[3] = sh.tr[kpair & 1u][2];
             rec[4] = wall_clock64();
+            rec[6] = sh.tr[kpair & 1u][3];
             // info: block | open rows at the pair's top << 16 | drain, sparse, last, allfull << 40 | group << 44
             const uint32_t nopen = EXIT ? rows - min(nfull_run, rows) : rows;
             rec[5] = (unsigned long long)b | ((unsigned long long)nopen << 16) | ((unsigned long long)drain << 40) |
@@ -2325,7 +2372,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         buf ^= 1u;
         kpair++;
     }
-    if (TQ) tile_tail<NW, DG>(a, st, C, Cs, vf, lbase, SB, sh, fullw, x_t, lane, wave_viol, wave_ev, kpair);
+    if (TQ) tile_tail<NW, DG>(a, st, C, Cs, vf, lbase, SB, sh, fullw, x_t, lane, wave_viol, wave_ev, kpair, ew);
     if ((DG && a.scan_stats)) {   // diagnostics: quads loaded and pairs staged by this workgroup
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2520,6 +2567,9 @@ struct mcmc_ctx {
     int early = 1;              // tiled: early-exit scan (MCMC_FULL_SCAN=1: every arc)
     int olist_on = 0;           // tiled early exit: R-entry open-row list in LDS (listed pairs)
     uint32_t tq_dense = 0, tq_cap = 0;       // tiled early exit: tail queue (dense blocks, entries per queue)
+    uint32_t eown_off = 0;                   // tiled early exit: LDS offset of the evaluated group's own colours
+    float2* ewalk = nullptr;                 // closed-form own-colour walk table (nullptr: the form is inexact)
+    uint32_t ewalk_off = 0;                  // tiled: LDS offset of its copy
     uint32_t* tq_l = nullptr;                // [grid][2][tq_cap] rows
     uint32_t* tq_m = nullptr;                // [grid][2][tq_cap][nw] masks
     uint32_t drain_rows = 32;   // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256; C3: 32 best)
@@ -2530,6 +2580,7 @@ struct mcmc_ctx {
     uint32_t* foot[2] = {nullptr, nullptr};  // partitioned: footer buffers, world x kFooterWords each
     uint32_t* dlt[2] = {nullptr, nullptr};   // native partitioned: delta slots, world x kDeltaWords each
     bool tail_done = false;                  // partitioned tail cut ran after the loop (multi.hip)
+    uint64_t xs_delta = 0, xs_full = 0, xs_ovf = 0, xs_bytes = 0;   // mcmc_part_run's exchange statistics
     uint32_t tail_passes = 0;
     uint64_t tail_viol = 0;
     void* own_part = nullptr;                // native partitioned contexts: their own colour + footer buffers
@@ -2644,6 +2695,9 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.tq_cap = c->tq_cap;
     a.tq_l = c->tq_l;
     a.tq_m = c->tq_m;
+    a.eown_off = c->eown_off;
+    a.ewalk = c->ewalk;
+    a.ewalk_off = c->ewalk_off;
     a.drain_rows = c->drain_rows;
     if (const char* dm = getenv("MCMC_DEBUG_MAX_PAIRS")) a.dbg_max_pairs = (uint32_t)atoi(dm);
     a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
@@ -2977,6 +3031,28 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     if (const char* fs = getenv("MCMC_FULL_SCAN")) c->early = atoi(fs) ? 0 : 1;
     if (const char* dr = getenv("MCMC_DRAIN_ROWS")) c->drain_rows = std::min<uint32_t>(256u, (uint32_t)atoi(dr));
     if (ref) c->fused = 1;
+    // The closed-form own-colour walk (evaluate_lane): E[c] = c-fold fp32 sum of eps, S[c] = fl(E[c] +
+    // hi), exact when E never decreases and adding eps to every S[c] leaves it unchanged (standard
+    // eps: S ~ 1, eps below half an ulp). Same fp32 operations as the device walk (-ffp-contract=off).
+    if (!ref && !wide && p->nCol >= 1 && p->nCol <= 256 && !getenv("MCMC_NO_EWALK")) {
+        const float eps = p->epsilon, hi = 1.0f - (float)(p->nCol - 1) * eps;
+        std::vector<float2> tab(p->nCol);
+        bool ok = eps >= 0.0f;
+        float E = 0.0f;
+        for (uint32_t k = 0; k < p->nCol && ok; k++) {
+            const float S = E + hi;
+            ok = (S + eps) == S;
+            tab[k] = make_float2(E, S);
+            const float En = E + eps;
+            ok = ok && En >= E;
+            E = En;
+        }
+        if (ok) {
+            hipError_t ee = hipMalloc(&c->ewalk, sizeof(float2) * p->nCol);
+            if (ee == hipSuccess) ee = hipMemcpy(c->ewalk, tab.data(), sizeof(float2) * p->nCol, hipMemcpyHostToDevice);
+            if (ee != hipSuccess) { (void)hipFree(c->ewalk); c->ewalk = nullptr; }
+        }
+    }
     // Variant: the tiled layout (16-bit block-local ids, replica LDS-resident when it fits, else
     // streamed 64 KiB slices) -- fastest on every measured shape. The CSR variants stay selectable
     // for A/B runs and parity tests. Knobs: MCMC_GATHER=tiled|lds|blocked|global, MCMC_BLOCK_LOG2,
@@ -3149,6 +3225,19 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 c->olist_on = 1;
             }
         }
+        // the closed-form own-colour walk's table (evaluate_lane), LDS copy
+        if (!ref && c->ewalk && c->lds + ((8u * (size_t)p->nCol + 15u) & ~(size_t)15u) <= kMaxLdsBytes) {
+            c->ewalk_off = (uint32_t)c->lds;
+            c->lds += (8u * (size_t)p->nCol + 15u) & ~(size_t)15u;
+        }
+        // the evaluated group's own colours, LDS-DMA'd at its last pair's top (early exit, streaming)
+        if (!ref && c->early && !resident) {
+            const size_t ob = own_bytes(R);
+            if (c->lds + ob <= kMaxLdsBytes) {
+                c->eown_off = (uint32_t)c->lds;
+                c->lds += ob;
+            }
+        }
         // the tail queue (streaming early exit with more blocks than the dense ones): every
         // workgroup's queues hold all rows of its groups
         const char* tqe = getenv("MCMC_TQ_DENSE");
@@ -3157,7 +3246,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             const uint32_t gpw = (c->tl->ngroups + c->grid.x - 1) / c->grid.x;
             c->tq_cap = gpw * R;
             const size_t ents = (size_t)c->grid.x * 2u * c->tq_cap;
-            hipError_t qe = hipMalloc(&c->tq_l, sizeof(uint32_t) * ents);
+            hipError_t qe = hipMalloc(&c->tq_l, sizeof(uint32_t) * 3u * ents);
             if (qe == hipSuccess) qe = hipMalloc(&c->tq_m, sizeof(uint32_t) * ents * c->nw);
             if (qe != hipSuccess) {
                 mcmc_destroy(c);
@@ -3887,6 +3976,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->seg);
     (void)hipFree(c->phase_ts);
     (void)hipFree(c->tq_l);
+    (void)hipFree(c->ewalk);
     (void)hipFree(c->tq_m);
     (void)hipFree(c->pair_trace);
     (void)hipFree(c->vflags);
@@ -3982,7 +4072,7 @@ bool part_delta_ok(const mcmc_ctx* c) { return c && c->part && c->dlt[0] && !c->
 static bool part_solo(const mcmc_ctx* c) { return c->world == 1 && !c->ref && !getenv("MCMC_PART_SOLO_OFF"); }
 
 const void* part_state_ptr(const mcmc_ctx* c) { return c->st; }
-static_assert(kDeltaWords == kPartDeltaWords, "delta slot size");
+static_assert(kDeltaWords == kPartDeltaWords && kDeltaWords == MCMC_DELTA_WORDS, "delta slot size");
 static_assert(offsetof(DevState, t) == 0 && offsetof(DevState, done) == 4 && offsetof(DevState, err) == 12,
               "part_state_ptr readers take {t, done, x_t, err} from the first 16 bytes");
 
@@ -4031,8 +4121,16 @@ int part_sync_remote(mcmc_ctx* c) {
     return MCMC_OK;
 }
 
+void part_add_xstats(mcmc_ctx* c, uint64_t delta_steps, uint64_t full_steps, uint64_t ovf, uint64_t bytes) {
+    c->xs_delta += delta_steps;
+    c->xs_full += full_steps;
+    c->xs_ovf += ovf;
+    c->xs_bytes += bytes;
+}
+
 int part_run_begin(mcmc_ctx* c) {
     c->tail_done = false;
+    c->xs_delta = c->xs_full = c->xs_ovf = c->xs_bytes = 0;
     if (!part_delta_ok(c)) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     for (int k = 0; k < 2; k++)
@@ -4255,6 +4353,32 @@ int mcmc_part_spill_local(mcmc_ctx* c, void* dst, uint32_t* count) {
 int mcmc_part_spill_commit_async(mcmc_ctx* c, const uint32_t* gathered, uint32_t stride) {
     if (!c || !c->part || !gathered) return fail(MCMC_E_ARG, "NULL argument");
     return part_commit(c, 0, gathered, stride);
+}
+
+int mcmc_part_attach_delta(mcmc_ctx* c, void* dlt0, void* dlt1) {
+    if (!c || !dlt0 || !dlt1) return fail(MCMC_E_ARG, "NULL argument");
+    return part_set_delta(c, static_cast<uint32_t*>(dlt0), static_cast<uint32_t*>(dlt1));
+}
+
+int mcmc_part_delta_ok(mcmc_ctx* c) { return part_delta_ok(c) ? 1 : 0; }
+
+int mcmc_part_sweep_mode_async(mcmc_ctx* c, int delta) { return part_sweep(c, delta != 0); }
+
+int mcmc_part_commit_mode_async(mcmc_ctx* c, int mode, const uint32_t* gathered, uint32_t stride) {
+    if (mode < -1 || mode > 1) return fail(MCMC_E_ARG, "mode: 1 delta, 0 full, -1 full-mode resumption");
+    return part_commit(c, mode, gathered, stride);
+}
+
+int mcmc_part_sync_remote_async(mcmc_ctx* c) { return part_sync_remote(c); }
+
+int mcmc_part_exchange_stats(mcmc_ctx* c, uint64_t* delta_steps, uint64_t* full_steps, uint64_t* overflows,
+                             uint64_t* bytes_sent) {
+    if (!c || !c->part) return fail(MCMC_E_STATE, "not a partitioned context");
+    if (delta_steps) *delta_steps = c->xs_delta;
+    if (full_steps) *full_steps = c->xs_full;
+    if (overflows) *overflows = c->xs_ovf;
+    if (bytes_sent) *bytes_sent = c->xs_bytes;
+    return MCMC_OK;
 }
 
 int mcmc_part_state(mcmc_ctx* c, int32_t* done, uint32_t* t, uint32_t* err) {

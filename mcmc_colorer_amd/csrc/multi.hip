@@ -213,9 +213,18 @@ struct Driver {
         return MCMC_OK;
     }
 
+    // bytes this rank sends per step in each mode (to world - 1 peers)
+    uint64_t step_bytes(const PartDesc& x, bool delta) const {
+        if (world < 2) return 0;
+        const uint64_t rows = (uint64_t)x.bounds[x.rank + 1] - x.bounds[x.rank];
+        const uint64_t per = 4ull * MCMC_FOOTER_WORDS + (delta ? 4ull * kPartDeltaWords : rows * x.cbytes);
+        return per * (world - 1);
+    }
+
     // One step: sweep (every local rank) -> exchange -> commit. A delta-mode step after full-mode
     // ones first makes both replicas equal off the local rows (part_sync_remote).
     int step(uint32_t t, bool delta) {
+        for (size_t i = 0; i < d.size(); i++) part_add_xstats(ctx[i], delta ? 1 : 0, delta ? 0 : 1, 0, step_bytes(d[i], delta));
         if (delta && !synced) {
             for (auto* c : ctx)
                 if (int rc = part_sync_remote(c)) return rc;
@@ -271,6 +280,8 @@ struct Driver {
         if ((err & 2u) && (rc_ = spill_gather(buf, &stride))) return rc_;
         const bool full = (err & 4u) != 0;   // a delta slot overflowed: the rows travel in full
         if (full && (rc_ = exchange(td, false))) return rc_;
+        if (full)
+            for (size_t i = 0; i < d.size(); i++) part_add_xstats(ctx[i], 0, 0, 1, step_bytes(d[i], false));
         for (size_t i = 0; i < d.size(); i++) {
             const int m = full ? -1 : (delta_step ? 1 : 0);
             if (buf.empty() && m >= 0) return fail(MCMC_E_STATE, "nothing to resume");

@@ -42,6 +42,9 @@ from .colorer import ColoringMCMCParams, GlibcRand, GPURand, Graph, default_ncol
 
 FOOTER_WORDS = 1024   # MCMC_FOOTER_WORDS
 FOOTER_EVENTS = FOOTER_WORDS - 4
+DELTA_WORDS = 4096    # MCMC_DELTA_WORDS: a rank's delta slot ([0] pairs appended, [1] 0, (v, colour) pairs)
+DELTA_PAIRS = (DELTA_WORDS - 2) // 2
+FULL_AFTER_OVERFLOW = 16   # full-mode steps after a delta slot overflowed (csrc/multi.hip kFullAfterOverflow)
 COMM_ID_BYTES = 128   # MCMC_COMM_ID_BYTES
 
 
@@ -107,6 +110,7 @@ class HipRank:
         size = (self.n + 256) * self.cb
         self.colors = [torch.zeros(size, dtype=torch.uint8, device=device) for _ in range(2)]
         self.foot = [torch.zeros(world * FOOTER_WORDS, dtype=torch.int32, device=device) for _ in range(2)]
+        self.dlt = [torch.zeros(world * DELTA_WORDS, dtype=torch.int32, device=device) for _ in range(2)]
         self._ctx = ctypes.c_void_p()
         self._size = size
         self._make(seed)
@@ -122,17 +126,27 @@ class HipRank:
         check(lib().mcmc_part_attach(self._ctx, self.world, self.rank, u32ptr(self.bounds), self.colors[0].data_ptr(),
                                      self.colors[1].data_ptr(), self._size, self.foot[0].data_ptr(),
                                      self.foot[1].data_ptr(), ctypes.c_void_p(stream)))
+        check(lib().mcmc_part_attach_delta(self._ctx, ctypes.c_void_p(self.dlt[0].data_ptr()),
+                                           ctypes.c_void_p(self.dlt[1].data_ptr())))
 
     def init(self, seed: int, glibc: GlibcRand) -> None:
         self._make(seed)
         check(lib().mcmc_set_glibc_window(self._ctx, u32ptr(glibc.window)))
         check(lib().mcmc_init_coloring(self._ctx, None))
 
-    def sweep(self) -> None:
-        check(lib().mcmc_part_sweep_async(self._ctx))
+    def delta_ok(self) -> bool:
+        return bool(lib().mcmc_part_delta_ok(self._ctx))
 
-    def commit(self) -> None:
-        check(lib().mcmc_part_commit_async(self._ctx))
+    def sweep(self, delta: bool = False) -> None:
+        check(lib().mcmc_part_sweep_mode_async(self._ctx, 1 if delta else 0))
+
+    def commit(self, mode: int = 0, spill=None, stride: int = 0) -> None:
+        """mode 1 delta, 0 full, -1 full-mode resumption of a paused sweep; spill: the gathered lists."""
+        check(lib().mcmc_part_commit_mode_async(self._ctx, mode, ctypes.c_void_p(spill.data_ptr()) if spill is not None
+                                                else None, stride))
+
+    def sync_remote(self) -> None:
+        check(lib().mcmc_part_sync_remote_async(self._ctx))
 
     def state(self) -> tuple[bool, int, int]:
         done, t, err = ctypes.c_int32(), ctypes.c_uint32(), ctypes.c_uint32()
@@ -140,10 +154,11 @@ class HipRank:
         return bool(done.value), t.value, err.value
 
     def exchange_buffers(self, t: int):
-        """(next-colour buffer, [(byte range of rank r's rows)], next footer buffer) of sweep t."""
+        """(next-colour buffer, [(byte range of rank r's rows)], next footer buffer, next delta-slot
+        buffer) of sweep t."""
         nb = (t + 1) & 1
         rngs = [(int(self.bounds[r]) * self.cb, int(self.bounds[r + 1]) * self.cb) for r in range(self.world)]
-        return self.colors[nb], rngs, self.foot[nb]
+        return self.colors[nb], rngs, self.foot[nb], self.dlt[nb]
 
     def spill_counts(self) -> np.ndarray:
         c = np.zeros(self.world, dtype=np.uint32)
@@ -195,7 +210,7 @@ class PartitionedColoringMCMC:
     ``run(iteration)`` is bit-identical to ``ColoringMCMC.run(iteration)`` on one GPU."""
 
     def __init__(self, graph: Graph, randStates: GPURand, params: ColoringMCMCParams, group=None,
-                 backend=None, check_every: int = 8, bounds: Optional[np.ndarray] = None):
+                 backend=None, check_every: int = 8, bounds: Optional[np.ndarray] = None, exchange: str = "delta"):
         import torch
         import torch.distributed as dist
 
@@ -215,7 +230,11 @@ class PartitionedColoringMCMC:
         self.b = backend
         self.sweeps = 0
         self.spills = 0
+        self.overflows = 0
         self.nccl = dist.get_backend(group) == "nccl"
+        # exchange: "delta" (changed vertices only, as mcmc_part_run; ranks agree: the mode depends only
+        # on the sweep kind every rank shares) or "full" (every rank's rows every step)
+        self.delta = exchange == "delta" and self.world > 1 and backend_delta_ok(self.b)
 
     def _bcast(self, seg, src: int) -> None:
         if seg.numel() == 0:
@@ -238,25 +257,39 @@ class PartitionedColoringMCMC:
         else:
             self.dist.all_gather_into_tensor(out, mine.clone(), group=self.group)
 
-    def _exchange(self, t: int) -> None:
-        C, rngs, F = self.b.exchange_buffers(t)
-        for r, (lo, hi) in enumerate(rngs):   # every rank's rows to every rank
-            self._bcast(C[lo:hi], r)
+    def _exchange(self, t: int, delta: bool = False) -> None:
+        C, rngs, F, D = self.b.exchange_buffers(t)
+        if delta:   # every rank's delta slot to every rank
+            self._allgather(D, D[self.rank * DELTA_WORDS:(self.rank + 1) * DELTA_WORDS])
+        else:
+            for r, (lo, hi) in enumerate(rngs):   # every rank's rows to every rank
+                self._bcast(C[lo:hi], r)
         self._allgather(F, F[self.rank * FOOTER_WORDS:(self.rank + 1) * FOOTER_WORDS])
 
-    def _step(self, t: int) -> None:
-        self.b.sweep()
-        self._exchange(t)
-        self.b.commit()
+    def _step(self, t: int, delta: bool) -> None:
+        if delta and not self._synced:   # replicas equal off the local rows before a delta step
+            self.b.sync_remote()
+        self._synced = delta
+        self.b.sweep(delta)
+        self._exchange(t, delta)
+        self.b.commit(1 if delta else 0)
 
-    def _spill(self) -> None:
-        """The paused sweep's full lists: all-gathered with a common stride, then committed."""
-        stride = int(max(1, self.b.spill_counts().max()))
-        mine = self.b.spill_local(stride)
-        gathered = self.torch.zeros(self.world * stride, dtype=mine.dtype, device=mine.device)
-        self._allgather(gathered, mine)
-        self.b.spill_commit(gathered, stride)
-        self.spills += 1
+    def _resume(self, tdev: int, err: int, delta_step: bool) -> None:
+        """A sweep paused at tdev: the full lists (err bit 1, the spill exchange) and/or its rows in full
+        (err bit 2, a delta slot overflowed), then its commit."""
+        gathered, stride = None, 0
+        if err & 2:
+            stride = int(max(1, self.b.spill_counts().max()))
+            mine = self.b.spill_local(stride)
+            gathered = self.torch.zeros(self.world * stride, dtype=mine.dtype, device=mine.device)
+            self._allgather(gathered, mine)
+            self.spills += 1
+        full = bool(err & 4)
+        if full:
+            self._exchange(tdev, False)
+            self.overflows += 1
+        self.b.commit(-1 if full else (1 if delta_step else 0), gathered, stride)
+        self._synced = delta_step and not full
 
     def run(self, iteration: int = 0, max_sweeps: int = 0):
         """max_sweeps > 0: stop after that many sweeps (bounded samples), as ColoringMCMC.run."""
@@ -265,18 +298,27 @@ class PartitionedColoringMCMC:
         limit = max_sweeps if max_sweeps else self.param.maxRip + 2
         t = 0
         done = False
+        self._synced = False
+        full_left = 0
+        modes = []
         while t < limit and not done:
             k = min(self.check_every, limit - t)
             for _ in range(k):
-                self._step(t)
+                d = self.delta and full_left == 0
+                full_left = max(0, full_left - 1)
+                modes.append(d)
+                self._step(t, d)
                 t += 1
             done, tdev, err = b.state()
             if err & 1:
                 raise RuntimeError("partitioned sweep: device error flag")
-            if err & 2:   # spill pause at sweep tdev (later steps were no-ops): resume from it
-                self._spill()
+            if err & 6:   # paused at sweep tdev (later steps were no-ops): exchange, resume from it
+                self._resume(tdev, err, modes[tdev] if tdev < len(modes) else False)
+                if err & 4:
+                    full_left = FULL_AFTER_OVERFLOW
                 done, tdev, err = b.state()
                 t = tdev
+                del modes[t:]
         _, tdev, _ = b.state()
         self.sweeps = tdev + 1 if done else tdev   # sweeps the device ran (incl. the final count pass)
         b.glibc_window(self.rand.glibc)
@@ -287,6 +329,12 @@ class PartitionedColoringMCMC:
 
     def trajectory(self) -> np.ndarray:
         return self.b.trajectory()
+
+
+def backend_delta_ok(backend) -> bool:
+    """Whether a rank backend runs delta-mode steps (HipRank: the tiled sweep; NumpyRank: always)."""
+    f = getattr(backend, "delta_ok", None)
+    return bool(f()) if f is not None else False
 
 
 class NativePartitionedColoringMCMC:

@@ -28,17 +28,19 @@ for path in sys.argv[1:]:
     skew = us(smax - smin)
     ev = np.where(last == 1, us(np.maximum(eend, smax) - smax), 0.0)
     bar = us(bend - np.where(last == 1, np.maximum(eend, smax), smax))
+    ebar = np.where((last == 1) & (recs[:, 6] > 0), us(recs[:, 6] - smax), 0.0)   # eval: its barrier passed
     span = us(t[:, :, 4].max(axis=1) - t[:, 0, 0])
     print(f"{path}: {nwg} workgroups, {len(recs)} pairs ({len(recs) / nwg:.1f} per workgroup), "
           f"workgroup span med {np.median(span):.1f} max {span.max():.1f} us")
-    print("   b  pairs  open(med)  drain sparse allfull   scan   skew   eval    bar   (median us)")
+    print("   b  pairs  open(med)  drain sparse allfull   scan   skew   eval (bar)    bar   (median us)")
     for k in range(int(b.max()) + 1):
         m = b == k
         if not m.any():
             continue
         print(f"{k:4d} {m.sum():6d} {np.median(nopen[m]):9.0f} {drain[m].sum():6d} {sparse[m].sum():6d} "
               f"{allfull[m].sum():7d} {np.median(scan[m]):6.2f} {np.median(skew[m]):6.2f} "
-              f"{np.median(ev[m][last[m] == 1]) if (last[m] == 1).any() else 0:6.2f} {np.median(bar[m]):6.2f}")
+              f"{np.median(ev[m][last[m] == 1]) if (last[m] == 1).any() else 0:6.2f} "
+              f"({np.median(ebar[m][last[m] == 1]) if (last[m] == 1).any() else 0:5.2f}) {np.median(bar[m]):6.2f}")
     tot = scan.sum() + ev.sum() + bar.sum()
     print(f"  share: scan {scan.sum() / tot:.2f}  eval {ev.sum() / tot:.2f}  barrier {bar.sum() / tot:.2f}")
     if len(tail):

@@ -1,7 +1,8 @@
 """Multi-rank path on CPU (gloo): the product's PartitionedColoringMCMC driver with the numpy rank
 backend (tests/partition_ref.py), world sizes 2 and 3, against the unpartitioned oracle: equal-row
 and arc-balanced plans (mcmc_part_plan_csr), events on every rank, and more events per rank than a
-footer holds (the spill exchange)."""
+footer holds (the spill exchange) -- with the full-range exchange and with the delta exchange
+(changed vertices only; a slot that overflows pauses the sweep, which then travels in full)."""
 import os
 import socket
 
@@ -19,6 +20,7 @@ CASES = [
     ("simulate", 80, 0.3, 300, 5, 1e-3, 0, 6, "rows"),      # nCol > 256: the wide sweep's 2-byte colours
     ("skewed", 2000, 0.0, 12, 6, 1e-8, 0, 12, "arcs"),      # arc-balanced plan of a skewed graph
     ("circulant", 10500, 0.0, 3, 21, 3e7, 0, 3, "rows"),    # > 1020 events per rank in sweep 0: spill
+    ("circulant", 20000, 0.0, 5, 17, 0.05, 0, 20, "rows"),  # > 2047 changed vertices per rank: delta overflow
 ]
 
 
@@ -55,7 +57,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, exchange="full"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -74,20 +76,21 @@ def _worker(rank, world, port, case, q):
             nNodes = n
 
         params = M.ColoringMCMCParams(nCol=ncol, epsilon=eps, maxRip=maxrip, tabooIteration=taboo)
-        drv = PartitionedColoringMCMC(_G(), rs, params, backend=backend, check_every=3)
+        drv = PartitionedColoringMCMC(_G(), rs, params, backend=backend, check_every=3, exchange=exchange)
         out = []
         for it in range(2):                    # two repetitions: seed + i, shared glibc stream
             drv.run(it)
             out.append((drv.coloring().tolist(), drv.trajectory().tolist(), backend.iter,
-                        rs.glibc.window.tolist(), drv.spills, bounds.tolist()))
+                        rs.glibc.window.tolist(), drv.spills, bounds.tolist(), drv.overflows))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("exchange", ["full", "delta"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1]}-{c[8]}")
-def test_partitioned_driver_gloo_matches_oracle(world, case):
+def test_partitioned_driver_gloo_matches_oracle(world, case, exchange):
     kind, n, p, ncol, seed, eps, taboo, maxrip, pl = case
     off, idx = make_graph(kind, n, p)
     O.srand(1)
@@ -98,7 +101,7 @@ def test_partitioned_driver_gloo_matches_oracle(world, case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, exchange)) for r in range(world)]
     for pr in procs:
         pr.start()
     results = dict(q.get(timeout=600) for _ in range(world))
@@ -107,15 +110,17 @@ def test_partitioned_driver_gloo_matches_oracle(world, case):
         assert pr.exitcode == 0
     for rank in range(world):
         for i, ref in enumerate(refs):
-            colors, traj, it, _, spills, bounds = results[rank][i]
+            colors, traj, it, _, spills, bounds, _ = results[rank][i]
             assert colors == ref.colors.tolist(), (rank, i)
             assert traj == ref.traj.tolist(), (rank, i)
             assert it == ref.res.iter
     assert refs[0].res.glibcDraws + refs[1].res.glibcDraws > 0 or eps < 1
     # replicas leave the glibc stream at the same position
     assert len({tuple(results[r][1][3]) for r in range(world)}) == 1
-    if kind == "circulant":
+    if kind == "circulant" and n == 10500:
         assert results[0][0][4] >= 1, "the case must exercise the spill exchange"
+    if kind == "circulant" and n == 20000 and exchange == "delta":
+        assert results[0][0][6] >= 2, "the case must overflow delta slots (and return to delta mode)"
     if pl == "arcs":
         b = results[0][0][5]
         deg = np.diff(off.astype(np.int64))

@@ -228,8 +228,8 @@ def _lockstep_exchange(ranks, t):
     from mcmc_colorer_amd.distributed import FOOTER_WORDS
 
     bufs = [b.exchange_buffers(t) for b in ranks]
-    for q, (Cq, _, Fq) in enumerate(bufs):
-        for r, (Cr, rngs, Fr) in enumerate(bufs):
+    for q, (Cq, _, Fq, _) in enumerate(bufs):
+        for r, (Cr, rngs, Fr, _) in enumerate(bufs):
             if r != q:
                 lo, hi = rngs[r]
                 Cq[lo:hi].copy_(Cr[lo:hi])
