@@ -1403,7 +1403,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 template <bool RES>
 __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
                                               uint32_t b, uint32_t seg_lds, uint32_t slice_lds, uint32_t wid,
-                                              uint32_t nwaves, int lane) {
+                                              uint32_t nwaves, int lane, bool slice = true) {
     const uint32_t TS = tseg_stride(a.grp_rows);
     const uint32_t np = TS / 4u;   // 16-B pieces of the table row
     const uint32_t* gs = a.tseg + ((size_t)g * a.nblocks + b) * TS;
@@ -1411,7 +1411,7 @@ __device__ __forceinline__ void tile_dma_pair(const SweepArgs& a, const uint8_t*
         const uint32_t p = min(w * 64u + (uint32_t)lane, np - 1u);
         glds16(gs + 4u * p, __builtin_amdgcn_readfirstlane(seg_lds + w * 1024u));
     }
-    if (!RES) {
+    if (!RES && slice) {
         const uint32_t lo = b << a.block_log2;
         const uint32_t nq16 = min(a.slice_bytes, ((a.n + 15u) & ~15u) - lo) >> 4;
         // the slice buffer (tile_slice_buf: 16-64 KiB): 1-4 wave-instructions per wave
@@ -1963,6 +1963,9 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     // its later segments are skipped, and once every row of a group is done its remaining pairs are.
     const bool EXIT = EX && !REF && a.early;   // EX = false: the full-scan instantiation (no early-exit code)
     const bool TQ = EXIT && !RES && a.tq_dense != 0 && a.tq_dense < nb;   // the tail queue (tile_tail)
+    // with the tail queue's two dense blocks, their slices stay in the two slice buffers for all of
+    // phase A (every group's pairs read the same two slices): pairs stage their tables only
+    const bool RS = TQ && a.tq_dense == 2u;
     uint32_t fullw[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) {
@@ -1979,6 +1982,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     if (threadIdx.x == 0) sh.st_quads = sh.st_pairs = sh.st_used = 0;
     if (g < a.ngroups) {
         tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
+        if (RS) tile_dma_slice(a, C, 1, lds0 + SB, wid, nwaves, lane);   // block 1's slice, resident too
         if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
     }
     // the first pair's first quads (bounds from the global table), then the resident replica
@@ -2070,7 +2074,8 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // them landed (a register load there waited one loaded-HBM round trip, ~5 us per group)
         if (!REF && last && a.eown_off) tile_dma_own(a, C, g, lds0 + a.eown_off, wid, nwaves, lane);
         if (nvalid) {
-            tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane);
+            tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane,
+                               !RS);
             if (REF && !RES && nbn == 0)
                 tile_dma_own(a, C, ng, lds_addr(own_base) + (gpar ^ 1u) * a.own_buf_bytes, wid, nwaves, lane);
         }
@@ -2080,7 +2085,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         npos += 8u * li;
         const __amdgpu_buffer_rsrc_t ngr = tile_group_rsrc(a, pg);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
-        const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + buf * SB;
+        const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + (RS ? (b & 1u) : buf) * SB;
         const uint32_t* __restrict__ sseg = reinterpret_cast<const uint32_t*>(seg_base + buf * SEGB);
         // sub-group state: current row, this lane's next quad, the row's end (ids from the group
         // base); the first step's quads are already in v. Rows after the first come from the pair's
