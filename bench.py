@@ -401,7 +401,6 @@ def main() -> int:
         # result cannot change; MCMC_FULL_SCAN=1 scans every arc): the bytes one launch moves are
         # counted on the device (mcmc_set_scan_stats, 3 sweeps outside the timed region) -- id quads,
         # the staged (group, block) pairs' table rows and colour slices, own colour read + write
-        q, qu, pr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         tot2, ker2 = ctypes.c_double(), ctypes.c_double()
         sctx = col._ctx if dist is None else drv._ctx
         check(lib().mcmc_set_scan_stats(sctx, 1))
@@ -409,24 +408,32 @@ def main() -> int:
             check(lib().mcmc_bench_sweeps(col._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
         else:
             check(lib().mcmc_part_run(arr, 1, 3, ctypes.byref(st)))
-        check(lib().mcmc_get_scan_stats_ex(sctx, ctypes.byref(q), ctypes.byref(qu), ctypes.byref(pr)))
+        sv = (ctypes.c_uint64 * 6)()
+        check(lib().mcmc_get_scan_stats_v2(sctx, sv))
         check(lib().mcmc_set_scan_stats(sctx, 0))
         # algorithmic: the quads whose ids the scan gathered (the exact early exit needs them);
-        # issued: every quad loaded, incl. those fetched ahead for a row that filled up first
-        quads, quads_issued, pairs = qu.value / 3.0, q.value / 3.0, pr.value / 3.0
+        # issued: every quad loaded, incl. those fetched ahead for a row that filled up first; plus
+        # the segment tables of the pairs, the colour slices staged (the tail queue keeps the two
+        # dense blocks' slices resident: 2 per workgroup, then one per tail block), the tail queue's
+        # entries (16 B written, 16 B read + 16 B of segment bounds / group base per read)
+        quads_issued, pairs, quads, slices, qw, qr = [x / 3.0 for x in sv]
         R = info["grp_rows"]
         table = 4 * ((R + 4) & ~3)
         slice_b = 0 if info["resident"] else min(1 << info["block_log2"], ((g.nNodes + 15) // 16) * 16)
         nloc = g.nNodes if dist is None else int(bounds[rank + 1] - bounds[rank])
-        b_alg = 16 * quads + pairs * (table + slice_b) + 2 * nloc
+        rest = pairs * table + slices * slice_b + 16 * qw + 32 * qr + 2 * nloc
+        b_alg = 16 * quads + rest
         scan = {"early_exit": info.get("early", True), "quads_per_sweep": quads, "pairs_per_sweep": pairs,
-                "id_bytes": 16 * quads, "table_bytes": pairs * table, "slice_bytes": pairs * slice_b,
+                "id_bytes": 16 * quads, "table_bytes": pairs * table, "slices_per_sweep": slices,
+                "slice_bytes": slices * slice_b, "tail_queue_entries_written": qw, "tail_queue_entries_read": qr,
+                "tail_queue_bytes": 16 * qw + 32 * qr,
                 "quads_issued_per_sweep": quads_issued,
-                "issued_bytes": 16 * quads_issued + pairs * (table + slice_b) + 2 * nloc,
+                "issued_bytes": 16 * quads_issued + rest,
                 "layout_bytes_full_scan": b_fmt,
                 "note": "exact early exit: a row's scan stops once its mask holds all nCol colours "
-                        "(count_free_colors cannot change); a group skips its remaining column blocks once "
-                        "every row is full. Bit-identical results (tests/test_gpu_parity.py)."}
+                        "(count_free_colors cannot change); rows still open after the two dense blocks wait "
+                        "in the workgroup's tail queue and finish block by block after its last group. "
+                        "Bit-identical results (tests/test_gpu_parity.py, tests/test_c3_full.py)."}
         if dist is None and not a.no_full_scan:
             # the same sweep scanning every arc (MCMC_FULL_SCAN=1): the layout-bound reference point
             os.environ["MCMC_FULL_SCAN"] = "1"

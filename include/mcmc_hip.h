@@ -178,6 +178,10 @@ int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs);
  * counts loads issued ahead for a row that filled up before they were needed (the scan keeps two
  * steps in flight), so `used` is the bytes the exact early exit needs, `quads` what it issued. */
 int mcmc_get_scan_stats_ex(mcmc_ctx* c, uint64_t* quads, uint64_t* used, uint64_t* pairs);
+/* All counters: [0] quads loaded, [1] pairs (a segment table each), [2] quads gathered, [3] colour
+ * slices staged (the tail queue's resident dense slices and its blocks included), [4] / [5] tail-queue
+ * entries written / read (16 B each, plus a row's 8 B segment bounds and 8 B group base per read). */
+int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

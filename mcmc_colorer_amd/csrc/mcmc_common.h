@@ -170,6 +170,15 @@ const void* part_state_ptr(const mcmc_ctx* c);   // device state: {t, done, x_t,
 int part_sweep(mcmc_ctx* c, bool delta);
 int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride);
 int part_sync_remote(mcmc_ctx* c);
+// Per-context driver resources, created on first use and kept until mcmc_destroy (a run then pays no
+// stream / pinned-memory / event creation): a side stream, 16 pinned bytes, and events (0: the
+// loopback transport's, 1-2: loop start/end, 3-4: batch ends).
+struct PartRes {
+    hipStream_t poll = nullptr;
+    uint32_t* pinned = nullptr;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+};
+int part_resources(mcmc_ctx* c, PartRes** out);
 int part_run_begin(mcmc_ctx* c);   // a run's start: this rank's delta slots empty, no tail-cut result, stats zero
 void part_add_xstats(mcmc_ctx* c, uint64_t delta_steps, uint64_t full_steps, uint64_t ovf, uint64_t bytes);
 // Partitioned tail cut (mcmc_sweep.hip): state and colorIdx at loop exit (global Cviol, the final t,

@@ -993,6 +993,7 @@ struct TailShared {
     uint32_t nfull[3];    // tiled early exit: rows of the group whose mask filled up, per pair (mod 3)
     uint32_t dn[2];       // tiled sparse pairs / drain: rows listed (by pair-buffer parity)
     uint32_t st_quads, st_pairs, st_used;   // diagnostics (scan_stats): quads loaded, pairs staged, quads gathered
+    uint32_t st_slices, st_qw, st_qr;       // colour slices staged, tail-queue entries written / read
     uint16_t dlist[256];  // tiled sparse pairs / drain: the group's rows whose masks are not full yet
     unsigned long long viol;
     unsigned long long tr[2][4];   // diagnostics (pair trace): scan end min / max over waves, eval end max,
@@ -1796,7 +1797,10 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the slice landed
         if (rec) stamp(rec, 1);
         uint64_t t_load = 0, t_scan = 0, t_cls = 0;
-        if ((DG && a.scan_stats) && threadIdx.x == 0) sh.st_pairs++;
+        if ((DG && a.scan_stats) && threadIdx.x == 0) {
+            sh.st_slices++;
+            sh.st_qr += qn;
+        }
         const uint32_t* Ql = Q_l + (size_t)qs * a.tq_cap * 3u;
         const uint32_t* Qm = Q_m + (size_t)qs * a.tq_cap * NW;
         uint32_t* Pl = Q_l + (size_t)(qs ^ 1u) * a.tq_cap * 3u;
@@ -1840,6 +1844,7 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
                 if (km) {
                     uint32_t qb = 0;
                     if (lane == 0) qb = atomicAdd(&sh.qn[qs ^ 1u], (uint32_t)__popcll(km));
+                    if ((DG && a.scan_stats) && lane == 0) atomicAdd(&sh.st_qw, (uint32_t)__popcll(km));
                     qb = __shfl(qb, 0, 64);
                     if (keep) {
                         const uint32_t idx = qb + (uint32_t)__popcll(km & ((1ull << lane) - 1ull));
@@ -1979,7 +1984,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         return f;
     };
     uint32_t nfull_run = 0, kpair = 0;   // rows of the current group known full; pair counter
-    if (threadIdx.x == 0) sh.st_quads = sh.st_pairs = sh.st_used = 0;
+    if (threadIdx.x == 0) {
+        sh.st_quads = sh.st_pairs = sh.st_used = sh.st_qw = sh.st_qr = 0;
+        sh.st_slices = (RS && g < a.ngroups) ? 2u : 0u;   // the resident dense slices
+    }
     if (g < a.ngroups) {
         tile_dma_pair<RES>(a, C, g, 0, seg_lds0, lds0, wid, nwaves, lane);
         if (RS) tile_dma_slice(a, C, 1, lds0 + SB, wid, nwaves, lane);   // block 1's slice, resident too
@@ -2135,7 +2143,10 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
             if (is_full(base)) end = pos;
         }
-        if ((DG && a.scan_stats) && threadIdx.x == 0) sh.st_pairs++;
+        if ((DG && a.scan_stats) && threadIdx.x == 0) {
+            sh.st_pairs++;
+            if (!RS && !RES) sh.st_slices++;
+        }
         // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
         // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
         // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
@@ -2328,6 +2339,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
                     if (om) {
                         uint32_t qb = 0;
                         if (lane == 0) qb = atomicAdd(&sh.qn[0], (uint32_t)__popcll(om));
+                        if ((DG && a.scan_stats) && lane == 0) atomicAdd(&sh.st_qw, (uint32_t)__popcll(om));
                         qb = __shfl(qb, 0, 64);
                         if (open) {   // the entry carries what its evaluation needs: u_v's state, own colour, taboo
                             const uint32_t idx = qb + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
@@ -2384,6 +2396,9 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             atomicAdd(&a.scan_stats[0], (unsigned long long)sh.st_quads);
             atomicAdd(&a.scan_stats[1], (unsigned long long)sh.st_pairs);
             atomicAdd(&a.scan_stats[2], (unsigned long long)sh.st_used);
+            atomicAdd(&a.scan_stats[3], (unsigned long long)sh.st_slices);
+            atomicAdd(&a.scan_stats[4], (unsigned long long)sh.st_qw);
+            atomicAdd(&a.scan_stats[5], (unsigned long long)sh.st_qr);
         }
     }
     MCMC_PHASE(a, 3);
@@ -2586,6 +2601,7 @@ struct mcmc_ctx {
     uint32_t* dlt[2] = {nullptr, nullptr};   // native partitioned: delta slots, world x kDeltaWords each
     bool tail_done = false;                  // partitioned tail cut ran after the loop (multi.hip)
     uint64_t xs_delta = 0, xs_full = 0, xs_ovf = 0, xs_bytes = 0;   // mcmc_part_run's exchange statistics
+    PartRes* pres = nullptr;                 // mcmc_part_run's stream, pinned word and events (part_resources)
     uint32_t tail_passes = 0;
     uint64_t tail_viol = 0;
     void* own_part = nullptr;                // native partitioned contexts: their own colour + footer buffers
@@ -3641,8 +3657,8 @@ int mcmc_count_violations(mcmc_ctx* c, uint64_t* count, uint8_t* flags) {
 int mcmc_set_scan_stats(mcmc_ctx* c, int on) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
-    if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 3 * sizeof(unsigned long long)));
-    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 3 * sizeof(unsigned long long)));
+    if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 6 * sizeof(unsigned long long)));
+    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 6 * sizeof(unsigned long long)));
     c->scan_stats_on = on != 0;
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
@@ -3664,6 +3680,17 @@ int mcmc_get_scan_stats_ex(mcmc_ctx* c, uint64_t* quads, uint64_t* used, uint64_
 
 int mcmc_get_scan_stats(mcmc_ctx* c, uint64_t* quads, uint64_t* pairs) {
     return mcmc_get_scan_stats_ex(c, quads, nullptr, pairs);
+}
+
+int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
+    if (c->scan_stats) {
+        MCMC_HIP_TRY(hipSetDevice(c->g->device));
+        MCMC_HIP_TRY(hipMemcpy(h, c->scan_stats, sizeof(h), hipMemcpyDeviceToHost));
+    }
+    for (int i = 0; i < 6; i++) out[i] = h[i];
+    return MCMC_OK;
 }
 
 int mcmc_set_bench_mode(mcmc_ctx* c, int on) {
@@ -4009,6 +4036,15 @@ void mcmc_destroy(mcmc_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
+    if (c->pres) {   // the driver's stream, pinned word and events
+        (void)hipSetDevice(c->g->device);
+        if (c->pres->poll) (void)hipStreamSynchronize(c->pres->poll);
+        for (hipEvent_t e : c->pres->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (c->pres->poll) (void)hipStreamDestroy(c->pres->poll);
+        if (c->pres->pinned) (void)hipHostFree(c->pres->pinned);
+        delete c->pres;
+    }
     if (c->own_part) {   // native partitioned contexts: their buffers and their own stream
         if (c->stream) (void)hipStreamSynchronize(c->stream);
         (void)hipFree(c->own_part);
@@ -4123,6 +4159,23 @@ int part_sync_remote(mcmc_ctx* c) {
     if (c->wide) part_sync_remote_kernel<uint16_t><<<blocks, 256, 0, c->stream>>>(a);
     else part_sync_remote_kernel<uint8_t><<<blocks, 256, 0, c->stream>>>(a);
     MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
+}
+
+int part_resources(mcmc_ctx* c, PartRes** out) {
+    if (!c->pres) {
+        MCMC_HIP_TRY(hipSetDevice(c->g->device));
+        std::unique_ptr<PartRes> r(new PartRes());
+        MCMC_HIP_TRY(hipStreamCreateWithFlags(&r->poll, hipStreamNonBlocking));
+        MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&r->pinned), 16, hipHostMallocDefault));
+        MCMC_HIP_TRY(hipEventCreateWithFlags(&r->ev[0], hipEventDisableTiming));
+        MCMC_HIP_TRY(hipEventCreate(&r->ev[1]));
+        MCMC_HIP_TRY(hipEventCreate(&r->ev[2]));
+        MCMC_HIP_TRY(hipEventCreateWithFlags(&r->ev[3], hipEventDisableTiming));
+        MCMC_HIP_TRY(hipEventCreateWithFlags(&r->ev[4], hipEventDisableTiming));
+        c->pres = r.release();
+    }
+    *out = c->pres;
     return MCMC_OK;
 }
 

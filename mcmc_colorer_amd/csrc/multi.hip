@@ -72,15 +72,6 @@ int exchange_mode() {
 constexpr uint32_t kFullAfterOverflow = 16;
 constexpr uint32_t kStepsPerPoll = 8;   // steps enqueued per batch; the host polls one batch behind
 
-// hipEvent owned for a scope (every early return releases it).
-struct EventGuard {
-    hipEvent_t e = nullptr;
-    int device = 0;
-    ~EventGuard() {
-        if (e) { (void)hipSetDevice(device); (void)hipEventDestroy(e); }
-    }
-};
-
 struct Driver {
     std::vector<mcmc_ctx*> ctx;
     std::vector<PartDesc> d;
@@ -90,16 +81,10 @@ struct Driver {
     int mode = 0;
     bool delta_ok = false;        // every local context can run delta-mode steps
     bool synced = false;          // delta invariant: both replicas hold the current colouring off the local rows
-    hipStream_t poll = nullptr;   // side stream of ctx[0]'s device: reads the device state while steps run
-    uint32_t* pinned = nullptr;   // host-pinned copy of the state's first words {t, done, x_t, err}
-
-    ~Driver() {
-        for (size_t i = 0; i < ev.size(); i++)
-            if (ev[i]) { (void)hipSetDevice(d[i].device); (void)hipEventDestroy(ev[i]); }
-        if (!d.empty()) (void)hipSetDevice(d[0].device);
-        if (poll) (void)hipStreamDestroy(poll);
-        if (pinned) (void)hipHostFree(pinned);
-    }
+    PartRes* res0 = nullptr;      // ctx[0]'s resources: side stream reading the device state while steps
+                                  // run, pinned copy of the state's first words {t, done, x_t, err}, events
+    hipStream_t poll = nullptr;
+    uint32_t* pinned = nullptr;
 
     int setup(mcmc_ctx** cs, uint32_t k) {
         ctx.assign(cs, cs + k);
@@ -120,8 +105,9 @@ struct Driver {
                 if (d[i].rank != i) return fail(MCMC_E_ARG, "loopback transport: contexts in rank order");
             ev.assign(k, nullptr);
             for (uint32_t i = 0; i < k; i++) {
-                MCMC_HIP_TRY(hipSetDevice(d[i].device));
-                MCMC_HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+                PartRes* r = nullptr;
+                if (int rc = part_resources(ctx[i], &r)) return rc;
+                ev[i] = r->ev[0];
             }
         }
         mode = exchange_mode();
@@ -129,9 +115,9 @@ struct Driver {
         // (uint8 tiled sweep), which every rank of a partition shares
         delta_ok = mode == 0 && world > 1;
         for (auto& x : d) delta_ok = delta_ok && x.delta_ok;
-        MCMC_HIP_TRY(hipSetDevice(d[0].device));
-        MCMC_HIP_TRY(hipStreamCreateWithFlags(&poll, hipStreamNonBlocking));
-        MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pinned), 16, hipHostMallocDefault));
+        if (int rc = part_resources(ctx[0], &res0)) return rc;
+        poll = res0->poll;
+        pinned = res0->pinned;
         for (auto* c : ctx)
             if (int rc = part_run_begin(c)) return rc;
         return MCMC_OK;
@@ -477,13 +463,10 @@ int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
     Driver D;
     if (int rc = D.setup(ctxs, k)) return rc;
     const uint32_t limit = max_sweeps ? max_sweeps : D.d[0].maxRip + 2;   // + the final count pass (sweeps)
-    EventGuard e0, e1;
-    EventGuard batch_ev[2];
-    e0.device = e1.device = batch_ev[0].device = batch_ev[1].device = D.d[0].device;
+    struct Ev { hipEvent_t e; };   // the context's cached events (part_resources)
+    Ev e0{D.res0->ev[1]}, e1{D.res0->ev[2]};
+    Ev batch_ev[2] = {{D.res0->ev[3]}, {D.res0->ev[4]}};
     MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
-    MCMC_HIP_TRY(hipEventCreate(&e0.e));
-    MCMC_HIP_TRY(hipEventCreate(&e1.e));
-    for (auto& b : batch_ev) MCMC_HIP_TRY(hipEventCreateWithFlags(&b.e, hipEventDisableTiming));
     MCMC_HIP_TRY(hipEventRecord(e0.e, D.d[0].stream));
     // the loop continues from the device's sweep counter (a second call resumes where the first
     // stopped: the exchange's buffer parity is the device's)
