@@ -3156,11 +3156,11 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     if (getenv("MCMC_PAIR_TRACE")) {
         const size_t words = (size_t)kPairTraceRec * kPairTraceMax * 4096u;
         chk(hipMalloc(&c->pair_trace, sizeof(unsigned long long) * words));
-        chk(hipMemset(c->pair_trace, 0, sizeof(unsigned long long) * words));
+        chk(hipMemsetAsync(c->pair_trace, 0, sizeof(unsigned long long) * words, c->stream));
     }
     if (getenv("MCMC_PHASE_DUMP")) {
         chk(hipMalloc(&c->phase_ts, sizeof(unsigned long long) * 8u * 4096u));
-        chk(hipMemset(c->phase_ts, 0, sizeof(unsigned long long) * 8u * 4096u));
+        chk(hipMemsetAsync(c->phase_ts, 0, sizeof(unsigned long long) * 8u * 4096u, c->stream));
     }
     if (e != hipSuccess) {
         mcmc_destroy(c);
@@ -3398,7 +3398,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             if (c->xs && c->xs->mode == 1) {
                 for (int q = 0; q < 2 && ew == hipSuccess; q++) {   // slack: tile staging and row windows
                     ew = hipMalloc(&c->wfp[q], (size_t)gd.n + 2048);
-                    if (ew == hipSuccess) ew = hipMemset(c->wfp[q], 0, (size_t)gd.n + 2048);
+                    if (ew == hipSuccess) ew = hipMemsetAsync(c->wfp[q], 0, (size_t)gd.n + 2048, c->stream);
                 }
             }
         }
@@ -3466,6 +3466,12 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     if (ref && hipMalloc(&c->hist, sizeof(uint32_t) * 2u * c->hist_words) != hipSuccess) {
         mcmc_destroy(c);
         return fail(MCMC_E_NOMEM, "histogram allocation");
+    }
+    // the tables' null-stream uploads (hipMemcpy) do not order against the context's non-blocking
+    // stream: the device is idle before the first sweep can read them
+    if (hipError_t ed = hipDeviceSynchronize(); ed != hipSuccess) {
+        mcmc_destroy(c);
+        return fail(MCMC_E_HIP, std::string("context setup: ") + hipGetErrorString(ed));
     }
     *out = c;
     return MCMC_OK;
@@ -3658,7 +3664,7 @@ int mcmc_set_scan_stats(mcmc_ctx* c, int on) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 6 * sizeof(unsigned long long)));
-    if (on) MCMC_HIP_TRY(hipMemset(c->scan_stats, 0, 6 * sizeof(unsigned long long)));
+    if (on) MCMC_HIP_TRY(hipMemsetAsync(c->scan_stats, 0, 6 * sizeof(unsigned long long), c->stream));
     c->scan_stats_on = on != 0;
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
@@ -4370,6 +4376,9 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t*
     c->rank = rank;
     c->part = true;
     // the caller's stream as given: 0 is the legacy null stream (torch's default current stream)
+    // the context's uploads so far ran on its own (non-blocking) stream: finish them before the
+    // caller's stream takes over, or the first sweep could overtake them
+    if (c->stream) MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
     c->stream = static_cast<hipStream_t>(stream);
     c->borrowed_stream = true;

@@ -435,8 +435,11 @@ int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, 
     hipStream_t st = nullptr;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipMalloc(&mem, 2 * cols + 2 * foot + 2 * dlt);
-    if (e == hipSuccess) e = hipMemset(mem, 0, 2 * cols + 2 * foot + 2 * dlt);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    // zeroed on the partition's own stream: a null-stream hipMemset does not order against a
+    // non-blocking stream, and could land after mcmc_init_coloring wrote C_0 into these buffers
+    if (e == hipSuccess) e = hipMemsetAsync(mem, 0, 2 * cols + 2 * foot + 2 * dlt, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         (void)hipFree(mem);
         mcmc_destroy(c);
