@@ -228,7 +228,7 @@ def main() -> int:
                          "c3: configs[2]/[3] (n 1e7, p 0.001, 32 colours, the build's G(n,p) generator; "
                          "N > 1 partitions the same graph: strong scaling)")
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--vertices", type=int, default=100000, help="n of --simulate (per GPU under weak scaling)")
     ap.add_argument("--prob", type=float, default=0.01)
     ap.add_argument("--ncol", type=int, default=16)
