@@ -501,6 +501,20 @@ def main() -> int:
                             "value": g.nNodes * sv.sweepsRun / (sv.loopMs * 1e-3),
                             "trajectory": [int(x) for x in cv.trajectory()]}
         cv.close()
+        # the three C5 rates side by side: `value` (sweeps of a converged colouring, throughput
+        # mode), the violator-heavy loop above, and the reference loop itself at nCol = maxDeg from
+        # C_0 (its sweeps: the violators of C_0, then the sweep that finds Cviol = 0 and stops)
+        out["headline"] = {
+            "converged_sweeps": {"value": value, "ms_per_sweep": wall * 1e3 / a.steps},
+            "violator_sweeps": {"value": out["violators"]["value"], "ms_per_sweep": out["violators"]["ms_per_sweep"],
+                                "nCol": nc4},
+            "note": "value = converged-colouring sweeps; violator_sweeps = nCol maxDeg/4, every sweep with "
+                    "violators and walks; reference_loop = run() from C_0 at nCol = maxDeg"}
+        if conv is not None and conv["sweeps_run"]:
+            out["headline"]["reference_loop"] = {
+                "value": g.nNodes * conv["sweeps_run"] / (conv["loop_ms"] * 1e-3),
+                "ms_per_sweep": conv["loop_ms"] / conv["sweeps_run"], "sweeps": conv["sweeps_run"],
+                "trajectory": conv["trajectory"]}
     if scan is not None:
         out["scan"] = scan
     # CPU and refstruct legs: on the benchmarked graph for c2; for c3 (no CSR can exist: 400 GB) on

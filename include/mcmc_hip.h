@@ -103,8 +103,10 @@ int mcmc_graph_er_fast_part(uint32_t n, double prob, uint64_t seed, uint32_t wor
 int mcmc_graph_er_fast_rows(uint32_t n, double prob, uint64_t seed, uint32_t v_begin, uint32_t v_end, int device,
                             mcmc_graph** out);
 /* The CSR (uint64 offsets, uint32 ids; rows in layout order, not sorted) of a graph generated with
- * mcmc_graph_er_fast, built on the device from its tiled layout and kept on the handle (then
- * mcmc_graph_device_ptrs works). For the refstruct baseline at full occupancy (bench.py). */
+ * mcmc_graph_er_fast(_rows / _part), built on the device from its tiled layout and kept on the
+ * handle (then mcmc_graph_device_ptrs works; a row-partial graph's rows outside its range are
+ * empty). For the refstruct baseline at full occupancy (bench.py); mcmc_create calls it for
+ * nCol > 256 (the wide sweep scans a CSR). MCMC_E_NOMEM with the byte counts when it does not fit. */
 int mcmc_graph_materialize_csr(mcmc_graph* g);
 /* R-MAT power-law graph (configs[4] stand-in: SNAP LiveJournal / Reddit are not available; SURVEY.md
  * §8d C5), generated on the device as a CSR with ascending neighbour lists: 2^scale vertices,

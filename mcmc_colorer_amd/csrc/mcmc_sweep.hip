@@ -160,6 +160,9 @@ struct SweepArgs {
     int early;
     uint32_t dbg_max_pairs;     // diagnostics only (MCMC_DEBUG_MAX_PAIRS): cut every group after k pairs (wrong results)
     uint32_t drain_rows;        // tiled early exit: a group with at most this many rows left drains them (<= 256)
+    // tiled early exit: a group's next pair (its next block) is staged at the END of the current
+    // pair's scan, and only while some row is still open (rows expected to fill inside a block: C2)
+    int late_stage;
     unsigned long long* scan_stats;   // diagnostics (MCMC_SCAN_STATS): [0] quads loaded, [1] pairs staged,
                                       // [2] quads whose ids were gathered (the scan needed them)
     const float* etab;          // wide: E[k] = k-fold fp32 sum of eps, k = 0..nCol (walk_own_tab)
@@ -1984,6 +1987,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         return f;
     };
     uint32_t nfull_run = 0, kpair = 0;   // rows of the current group known full; pair counter
+    bool pstaged = true;                 // this pair's table and slice were staged (late staging skips some)
     if (threadIdx.x == 0) {
         sh.st_quads = sh.st_pairs = sh.st_used = sh.st_qw = sh.st_qr = 0;
         sh.st_slices = (RS && g < a.ngroups) ? 2u : 0u;   // the resident dense slices
@@ -2078,19 +2082,26 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
         const uint32_t ng = last ? g + gridDim.x : g, nbn = last ? 0u : b + 1;
         const bool nvalid = ng < a.ngroups;
+        // late staging: the group's next pair is staged after this pair's scan, and not at all once
+        // every row is full (the next pair then reads neither buffer); its first-row bounds are read
+        // after that DMA too, so the boundary's counted vmcnt still covers it
+        const bool late = EXIT && a.late_stage && !last && nvalid && !RES;
         // the evaluated group's own colours by LDS-DMA now, so the evaluation at the pair's end finds
         // them landed (a register load there waited one loaded-HBM round trip, ~5 us per group)
         if (!REF && last && a.eown_off) tile_dma_own(a, C, g, lds0 + a.eown_off, wid, nwaves, lane);
-        if (nvalid) {
+        if (nvalid && !late) {
             tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves, lane,
                                !RS);
             if (REF && !RES && nbn == 0)
                 tile_dma_own(a, C, ng, lds_addr(own_base) + (gpar ^ 1u) * a.own_buf_bytes, wid, nwaves, lane);
         }
         const uint32_t pg = nvalid ? ng : g, pb = nvalid ? nbn : b;
-        uint32_t npos, nend, npads;
-        tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend, npads);
-        npos += 8u * li;
+        uint32_t npos = 0, nend = 0, npads = 0;
+        if (!late) {
+            tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend, npads);
+            npos += 8u * li;
+            if (!nvalid) nend = npos;   // no next pair: its "first quads" load nothing
+        }
         const __amdgpu_buffer_rsrc_t ngr = tile_group_rsrc(a, pg);
         const uint16_t* __restrict__ ngcol = a.tcol + a.gbase[pg];
         const uint8_t* __restrict__ scb = RES ? lbase + (b << a.block_log2) : lbase + (RS ? (b & 1u) : buf) * SB;
@@ -2143,10 +2154,11 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
             for (int i = 0; i < NW; i++) base[i] = smask[row * NW + i];
             if (is_full(base)) end = pos;
         }
-        if ((DG && a.scan_stats) && threadIdx.x == 0) {
+        if ((DG && a.scan_stats) && threadIdx.x == 0 && pstaged) {
             sh.st_pairs++;
             if (!RS && !RES) sh.st_slices++;
         }
+        bool nstaged = true;
         // One step: gathers of CUR (this step's quads), loads of the next step into NXT. Expanded
         // twice over ping-pong register sets (a `v = vn` copy at the back-edge made hipcc wait
         // vmcnt(0) before the copy: a one-step-deep pipeline). The wave's last step issues no
@@ -2251,6 +2263,20 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         }
 #undef MCMC_TILE_STEP
 #undef MCMC_TILE_GATHER
+        if (late) {
+            // rows full so far (monotone: a count that reaches `rows` is final) -- every row full means
+            // the next pair is all-full and reads neither buffer
+            const uint32_t fnow = __builtin_amdgcn_readfirstlane(
+                nfull_run + __hip_atomic_load(&sh.nfull[kslot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            const bool af = fnow >= rows;
+            nstaged = !af;
+            if (!af)
+                tile_dma_pair<RES>(a, C, ng, nbn, seg_lds0 + (buf ^ 1u) * SEGB, lds0 + (buf ^ 1u) * SB, wid, nwaves,
+                                   lane, !RS);
+            tile_first_row(a, pg, pb, nloc, wid, nwaves, sub, npos, nend, npads);
+            npos += 8u * li;
+            if (af) nend = npos;
+        }
         // the evaluation's own colours and taboo counters of this wave's first two tiles, loaded
         // BEFORE the next pair's first quads: vmcnt retires loads in order, so a load issued after
         // those quads would make the evaluation wait for their HBM round trip (C3: 6 us per group)
@@ -2388,6 +2414,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         b = nbn;
         buf ^= 1u;
         kpair++;
+        pstaged = nstaged;
     }
     if (TQ) tile_tail<NW, DG>(a, st, C, Cs, vf, lbase, SB, sh, fullw, x_t, lane, wave_viol, wave_ev, kpair, ew);
     if ((DG && a.scan_stats)) {   // diagnostics: quads loaded and pairs staged by this workgroup
@@ -2593,6 +2620,7 @@ struct mcmc_ctx {
     uint32_t* tq_l = nullptr;                // [grid][2][tq_cap] rows
     uint32_t* tq_m = nullptr;                // [grid][2][tq_cap][nw] masks
     uint32_t drain_rows = 32;   // tiled early exit: drain threshold (MCMC_DRAIN_ROWS, 0 = off, <= 256; C3: 32 best)
+    int late_stage = 0;         // tiled early exit: stage a group's next pair after the scan, if a row is open
     unsigned long long* scan_stats = nullptr;   // mcmc_set_scan_stats: [quads loaded, pairs staged]
     bool scan_stats_on = false;
     uint32_t world = 1, rank = 0;
@@ -2720,6 +2748,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.ewalk = c->ewalk;
     a.ewalk_off = c->ewalk_off;
     a.drain_rows = c->drain_rows;
+    a.late_stage = c->late_stage;
     if (const char* dm = getenv("MCMC_DEBUG_MAX_PAIRS")) a.dbg_max_pairs = (uint32_t)atoi(dm);
     a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
@@ -3027,7 +3056,14 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     const bool wide = ref ? p->nCol > 255 : (p->nCol > 256 || gsel == "wide");
     if (wide) {
         if (p->nCol > kWideMaxCol) return fail(MCMC_E_ARG, "nCol > 65535 is not supported (uint16 colour replicas)");
-        if (!gd.row_off) return fail(MCMC_E_ARG, "nCol > 256 needs a CSR graph (mcmc_graph_upload / _simulate)");
+        // the wide sweep scans a CSR (its slab layout and violator walks are built from one): a
+        // generated graph gets its CSR from the tiled layout here, when it fits beside the layout
+        // (the reference's default nCol = maxDeg, main.cu:162, on --simulate graphs); C3 on one
+        // device does not (4.0e11 B of ids + 2.2e11 B of layout > 288 GB) and fails with the sizes
+        if (!gd.row_off) {
+            int mr = mcmc_graph_materialize_csr(const_cast<mcmc_graph*>(g));
+            if (mr) return fail(mr, std::string("nCol > 256 on a generated graph: ") + mcmc_last_error());
+        }
     }
     if (ref) {
         if (p->nCol < 2) return fail(MCMC_E_ARG, "reference-GPU mode: nCol >= 2");
@@ -3234,6 +3270,12 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             const double scan_ids = std::min(8.0 * quads, (double)p->nCol * hn);
             sl = 0;
             while (sl < 6 && 8.0 * (double)(1u << sl) * kTileU < scan_ids) sl++;
+            // late staging where a mean segment leaves a row open with probability < 1%
+            // (nCol (1 - 1/nCol)^d, d ids): C2's 500-id segments fill 16 colours inside block 0, so its
+            // block-1 pair (slice, table, first quads) was staged for nothing; C3 (65 of ~130 ids) keeps
+            // staging ahead. A wrong guess costs one exposed DMA round trip, never a result.
+            c->late_stage = 8.0 * quads >= (double)p->nCol * std::log(100.0 * p->nCol) ? 1 : 0;
+            if (const char* ls = getenv("MCMC_LATE_STAGE")) c->late_stage = atoi(ls) ? 1 : 0;
         }
         const char* sv = getenv("MCMC_SUB_LOG2");
         if (sv) sl = (uint32_t)std::max(0, std::min(6, atoi(sv)));

@@ -550,42 +550,55 @@ extern "C" int mcmc_graph_rows(const mcmc_graph* g, const uint32_t* rows, uint32
     return MCMC_OK;
 }
 
-// The CSR of a generated graph (uint64 offsets, uint32 ids), built on the device from its
-// full-range tiled layout: for callers that need the reference's layout itself (the refstruct
-// baseline at full occupancy). Rows keep layout order (not sorted: above 2^31 arcs the segmented
-// sort does not apply); the sweep and the layout are unaffected.
+// The CSR of a generated graph (uint64 offsets, uint32 ids), built on the device from its tiled
+// layout: for callers that need the reference's layout itself (the refstruct baseline at full
+// occupancy, the wide sweep's slab layout and walks when nCol > 256). A row-partial graph (a rank's
+// rows, mcmc_graph_er_fast_rows) gets a whole-graph offset array whose rows outside its layout are
+// empty. Rows keep layout order (not sorted: above 2^31 arcs the segmented sort does not apply);
+// the sweep and the layout are unaffected. Fails with the byte counts when the CSR does not fit in
+// free device memory (C3: 4.0e11 B of ids beside the 2.2e11 B layout on a 288 GB device).
 extern "C" int mcmc_graph_materialize_csr(mcmc_graph* g) {
     if (!g) return fail(MCMC_E_ARG, "NULL graph");
     if (g->g.row_off) return MCMC_OK;
     const TiledLayout* L = nullptr;
     for (auto& t : g->tiles)
-        if (t->v_begin == 0 && t->v_end == g->g.n) L = t.get();
-    if (!L) return fail(MCMC_E_STATE, "graph has no full-range tiled layout");
+        if (!L || t->v_end - t->v_begin > L->v_end - L->v_begin) L = t.get();
+    if (!L) return fail(MCMC_E_STATE, "graph has no tiled layout");
     MCMC_HIP_TRY(hipSetDevice(g->g.device));
-    const uint32_t n = g->g.n;
+    const uint32_t n = g->g.n, vb = L->v_begin, nloc = L->v_end - L->v_begin;
+    {
+        size_t fr = 0, tot = 0;
+        MCMC_HIP_TRY(hipMemGetInfo(&fr, &tot));
+        const uint64_t need = 4ull * (L->arcs + 4) + 16ull * ((uint64_t)n + 1) + (64ull << 20);
+        if (need > fr)
+            return fail(MCMC_E_NOMEM, "materialize CSR: " + std::to_string(L->arcs) + " arcs need " +
+                                          std::to_string(need) + " B of device memory, " + std::to_string(fr) +
+                                          " B free (the tiled layout holds " + std::to_string(2ull * L->ids) + " B)");
+    }
     uint64_t *deg = nullptr, *off = nullptr;
     uint32_t* idx = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     hipError_t e = hipMalloc(&deg, sizeof(uint64_t) * ((size_t)n + 1));
     if (e == hipSuccess) e = hipMalloc(&off, sizeof(uint64_t) * ((size_t)n + 1));
-    const uint32_t blocks = (n + 255) / 256;
-    if (e == hipSuccess) {
+    if (e == hipSuccess) e = hipMemset(deg, 0, sizeof(uint64_t) * ((size_t)n + 1));
+    const uint32_t blocks = (nloc + 255) / 256;
+    if (e == hipSuccess && nloc) {   // local row i of the layout is vertex vb + i
         tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2,
-                                          nullptr, n, nullptr, deg, nullptr, nullptr);
-        e = hipMemset(deg + n, 0, sizeof(uint64_t));
+                                          nullptr, nloc, nullptr, deg + vb, nullptr, nullptr);
+        e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, deg, off, n + 1);
     if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tmp_bytes, 16));
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, deg, off, n + 1);
     uint64_t m = 0;
     if (e == hipSuccess) e = hipMemcpy(&m, off + n, sizeof(uint64_t), hipMemcpyDeviceToHost);
-    if (e == hipSuccess && m != g->g.m) e = hipErrorInvalidValue;
+    if (e == hipSuccess && (m != g->g.m || m != L->arcs)) e = hipErrorInvalidValue;
     if (e == hipSuccess) e = hipMalloc(&idx, sizeof(uint32_t) * (m + 4));
     if (e == hipSuccess) e = hipMemset(idx, 0, sizeof(uint32_t) * (m + 4));
-    if (e == hipSuccess) {
+    if (e == hipSuccess && nloc) {
         tile_rows_kernel<<<blocks, 256>>>(L->tcol, L->gbase, L->tseg, L->grp_rows, L->nblocks, L->block_log2,
-                                          nullptr, n, off, nullptr, idx, nullptr);
+                                          nullptr, nloc, off + vb, nullptr, idx, nullptr);
         e = hipDeviceSynchronize();
     }
     (void)hipFree(deg);

@@ -169,6 +169,24 @@ def test_native_loopback_er_fast_rows(M):
     lp.close()
 
 
+@pytest.mark.gpu
+def test_native_loopback_wide_er_fast_rows(M):
+    """configs[3]'s shape at the reference's default nCol = maxDeg (> 256): every rank generates
+    only its rows (mcmc_graph_er_fast_rows), the wide sweep materialises each rank's row-partial
+    CSR from its layout, and the native driver's run equals the oracle's whole-graph run."""
+    n, p, seed = 8000, 0.06, 5
+    off, idx = O.er_fast(n, p, seed)
+    ncol = O.max_deg(off)
+    assert ncol > 256
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=10)
+    b = np.array([0, 2560, 5120, n], dtype=np.uint32)
+    graphs = [M.Graph.er_fast(n, p, seed, rows=(int(b[k]), int(b[k + 1]))) for k in range(3)]
+    lp, st, _ = loopback(M, off, idx, ncol, seed, b, 0, graphs=graphs, maxRip=10)
+    assert_native(lp, st, r, 3)
+    lp.close()
+
+
 def _rccl_world1(M, off, idx, nc, seed, draws, use_id):
     import ctypes
 

@@ -165,6 +165,33 @@ def test_wide_default_ncol_maxdeg_dense():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,p,seed", [(4000, 0.1, 7), (9000, 0.04, 3)])
+def test_wide_generated_graph_default_ncol(n, p, seed):
+    """The reference's default nCol = maxDeg (main.cu:162) on a graph of the build's generator
+    (--simulate at C3/C4 scale, no CSR until the wide sweep asks for one): mcmc_create builds the
+    CSR from the tiled layout (mcmc_graph_materialize_csr) and runs the wide sweep; colouring,
+    trajectory and loop state equal the oracle's run on the oracle's restatement of the same graph."""
+    import mcmc_colorer_amd.colorer as M
+
+    off, idx = O.er_fast(n, p, seed)
+    ncol = O.max_deg(off)
+    assert ncol > 256
+    g = M.Graph.er_fast(n, p, seed)
+    assert g.maxDeg == ncol and g.nEdges == len(idx)
+    params = M.ColoringMCMCParams(nCol=M.default_ncol(g, M.ColoringMCMCParams(nCol=0)), maxRip=40)
+    assert params.nCol == ncol
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), params)
+    st = col.run(0)
+    assert col.info()["variant"] == "wide"
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=40)
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, st.finalViol, st.glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+    col.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ncol,eps,taboo,tailcut", [(300, 1e-8, 0, False), (1000, 1e-8, 2, False),
                                                      (700, 1e-3, 0, False), (4000, 1e-8, 0, True),
                                                      (65535, 1e-8, 0, False)])
