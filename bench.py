@@ -351,11 +351,13 @@ def main() -> int:
         if a.warmup:
             check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
         check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
+        inc0 = None if ref else col.wide_inc_stats()
         t0 = time.perf_counter()
         check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
         wall = time.perf_counter() - t0
         kernel_ms = ker.value
         info = col.info()
+        inc1 = None if ref else col.wide_inc_stats()
     else:
         import torch
 
@@ -448,6 +450,25 @@ def main() -> int:
                                  "achieved_GBs": b_fmt / (ker2.value * 1e-3) / 1e9,
                                  "frac": b_fmt / (ker2.value * 1e-3) / 1e9 / HBM_PEAK_GBS}
             cf.close()
+    wide_inc = None
+    if dist is None and not ref and variant == "wide" and inc1 and inc1["enabled"]:
+        # incremental violation counts (sweep_wide.h wide_inc_*): a sweep moves the counts by the rows
+        # that changed colour instead of scanning the slab layout, so it is priced by what it reads:
+        # per vertex its flag and colour (3 B), per changed row its offsets, list entries and the
+        # replica / fingerprint sync (30 B), per changed arc its id and both colour reads (8 B); a
+        # full recount sweep (the first, or after many changes) by the layout's B_fmt
+        d = {k: inc1[k] - inc0[k] for k in ("incremental_sweeps", "full_sweeps", "changed_rows", "changed_arcs")}
+        S = max(1, d["incremental_sweeps"] + d["full_sweeps"])
+        b_alg = (3.0 * g.nNodes * d["incremental_sweeps"] + 30.0 * d["changed_rows"] + 8.0 * d["changed_arcs"]
+                 + b_fmt * d["full_sweeps"]) / S
+        wide_inc = dict(d, sweeps_counted=S, changed_rows_per_sweep=d["changed_rows"] / S,
+                        changed_arcs_per_sweep=d["changed_arcs"] / S, bytes_per_sweep=b_alg,
+                        layout_bytes_full_sweep=b_fmt,
+                        note="exact incremental violation counts: each sweep moves every row's same-colour "
+                             "count by the rows that changed colour (a full recount over the slab layout when "
+                             "many change); bit-identical to the full scan (tests/test_wide.py::"
+                             "test_wide_incremental_counts). The roofline prices the sweep by these bytes: it "
+                             "is bound by launch and dependent-latency chains, not by HBM.")
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9
     key = f"{a.config}/{variant}" if (world == 1 and (a.config in ("c3", "c5") or n_req == 100000)) else None
     if key and ref:
@@ -490,6 +511,8 @@ def main() -> int:
     }
     if conv is not None:
         out["convergence"] = conv
+    if wide_inc is not None:
+        out["wide_inc"] = wide_inc
     if dist is None and a.config == "c5" and not a.no_convergence:
         # the wide sweep WITH violators in every timed sweep (nCol = maxDeg / 4 does not converge):
         # the reference loop capped at 20 sweeps, device time per sweep and the per-sweep Cviol

@@ -184,6 +184,13 @@ int mcmc_get_scan_stats_ex(mcmc_ctx* c, uint64_t* quads, uint64_t* used, uint64_
  * slices staged (the tail queue's resident dense slices and its blocks included), [4] / [5] tail-queue
  * entries written / read (16 B each, plus a row's 8 B segment bounds and 8 B group base per read). */
 int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]);
+/* The wide sweep's incremental violation counts (no reference counterpart; the reference recounts
+ * every row each sweep, coloringMCMC_CPU.cpp:329-351): [0] 1 if the context keeps them (a whole-graph
+ * context over a symmetric CSR without repeated arcs, nCol > 256), then since mcmc_init_coloring
+ * [1] sweeps that moved the counts by the rows that changed, [2] full recounts, [3] rows that
+ * changed colour, [4] their arcs. Results are the same either way; MCMC_WIDE_INC=0 at mcmc_create
+ * turns it off. */
+int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

@@ -296,6 +296,15 @@ class ColoringMCMC:
         check(lib().mcmc_get_info(self._ctx, ctypes.byref(i)))
         return i.as_dict()
 
+    def wide_inc_stats(self) -> dict:
+        """The wide sweep's incremental violation counts since the colouring was initialised
+        (mcmc_get_wide_inc_stats): whether the context keeps them, sweeps that moved them by the rows
+        that changed, full recounts, changed rows and their arcs."""
+        out = (ctypes.c_uint64 * 5)()
+        check(lib().mcmc_get_wide_inc_stats(self._ctx, out))
+        return {"enabled": bool(out[0]), "incremental_sweeps": int(out[1]), "full_sweeps": int(out[2]),
+                "changed_rows": int(out[3]), "changed_arcs": int(out[4])}
+
     def save(self, iteration: int) -> None:
         d = self.directory
         Path(d).parent.mkdir(parents=True, exist_ok=True)

@@ -118,6 +118,7 @@ struct XSlabLayout {
     uint32_t mode = 0;
     uint32_t S = 0, cbits = 0;
     uint32_t sym = 0;                  // 1: one entry per local edge (symmetric CSR); 0: every arc
+    uint32_t simple = 0;               // sym and no row lists a neighbour twice (incremental counts apply)
     uint32_t nslabs = 0, chunks = 0;
     std::vector<uint32_t> chunk0_h;    // first chunk of every slab (nslabs + 1)
     uint64_t entries = 0;              // kept arcs (unpadded)

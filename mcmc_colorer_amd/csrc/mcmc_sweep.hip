@@ -169,6 +169,8 @@ struct SweepArgs {
     uint32_t* evblk;            // wide: per evaluation workgroup, its overflow events ascending [nblk][kEvSlot]
     uint32_t* evcnt;            // wide: their number per workgroup [nblk] (written every sweep)
     uint32_t evnblk;            // wide: evaluation workgroups
+    const uint32_t* evpow;      // wide: [evnblk][4] 16807^(v + 1) of each evaluation wave's first vertex
+    uint32_t a256;              // 16807^256 mod (2^31 - 1)
     // wide: XCD-slab edge layout of the violation scan (sweep_wide.h, get_xslab); xs_ent == nullptr
     // -> the CSR arc scan
     const uint32_t* xs_ent;     // [xs_chunk0[8] * 256] entries (row delta << cbits | slab-local column)
@@ -189,7 +191,124 @@ struct SweepArgs {
     const uint32_t* dall1;
     int part_delta;             // commit: 1 delta mode (remote changes arrive as pairs, applied to both
                                 //   replicas), 0 full mode, -1 full-mode resumption of a paused sweep
+    // wide sweep, incremental violation counts (sweep_wide.h, wide_inc_*; a whole-graph context over a
+    // symmetric CSR without repeated arcs, LDS tile scan): nullptr = every sweep's tile scan flags.
+    // The writers of sweep t list the rows they change (C_t -> C_t+1) in lists of parity q = (t+1) & 1,
+    // each in its own slot (no shared counter: a device-scope atomic on one word serialises at ~90
+    // per us): evaluation workgroup eb in eslot[q][eb], walk workgroup b in wslot[q][b], the commit in
+    // cchg[q]; rows above inc_hub_arcs arcs in hub[q] (rare; one atomic each). A slot holds its count and
+    // the rows' arcs in its first two words. The evaluation also lists the violators of C_t it saw
+    // (vslot[p][eb], p = t & 1): the next sweep's flag pass starts from them.
+    uint32_t* inc;              // [kIncWords] control words
+    uint32_t* inc_vcnt;         // [nloc] same-colour arcs of every row in C_t
+    uint32_t* inc_hub;          // [2][nloc] changed rows above inc_hub_arcs arcs
+    uint32_t* inc_tch;          // [2][nloc] rows whose count left 0 in sweep t's delta pass
+    uint32_t* inc_eslot;        // [2][evnblk][2 + inc_slot] evaluation workgroups' changed rows
+    uint32_t* inc_vslot;        // [2][evnblk][2 + inc_slot] evaluation workgroups' violators of C_t
+    uint32_t* inc_wslot;        // [2][kWalkBlocks][2 + inc_wslot_n] walk workgroups' changed rows
+    uint32_t* inc_cchg;         // [2][2 + ev_cap] the commit's changed rows (a slot)
+    uint32_t* inc_dense;        // [2][nloc] every changed row but the hubs, gathered by the commit
+    uint32_t inc_slot, inc_wslot_n;   // rows per evaluation / walk slot (past it: the next sweep recounts)
+    uint32_t inc_hub_arcs;      // a changed row above this many arcs is a hub (MCMC_WIDE_INC_HUB)
+    unsigned long long inc_thresh;    // the next sweep is incremental while its changed rows' arcs stay <= this
 };
+// control words of the incremental wide sweep (SweepArgs::inc)
+constexpr uint32_t kIncMode = 0;     // the running sweep: 1 full (the tile scan recounts), 0 incremental
+constexpr uint32_t kIncOvf = 1;      // [2] a slot overflowed (by parity q): the next sweep recounts
+constexpr uint32_t kIncTch = 3;      // [2] counts that left 0, by parity of t
+constexpr uint32_t kIncTchOvf = 5;   // [2] the touched list overflowed (the flag pass visits every row)
+constexpr uint32_t kIncHubN = 7;     // [2] changed hubs, by parity q
+constexpr uint32_t kIncDenseN = 9;   // [2] rows in the dense list, by parity q
+constexpr uint32_t kIncStat = 16;    // u64 [4]: incremental sweeps, full sweeps, changed rows, their arcs
+constexpr uint32_t kIncWords = 24;
+constexpr uint32_t kIncWalkSlots = 1024;   // = kWalkBlocks (sweep_wide.h)
+
+// Row l changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1], bumped by
+// the caller's LDS counters), or the hub list. Returns the row's arcs.
+__device__ __forceinline__ uint32_t inc_list(const SweepArgs& a, uint32_t l, uint32_t t, uint32_t* slot,
+                                             uint32_t cap, uint32_t* lcount) {
+    const uint32_t q = (t + 1u) & 1u;
+    const uint32_t deg = (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+    if (deg > a.inc_hub_arcs) {
+        a.inc_hub[(size_t)q * (a.v_end - a.v_begin) + atomicAdd(&a.inc[kIncHubN + q], 1u)] = l;
+    } else {
+        const uint32_t k = atomicAdd(lcount, 1u);   // LDS
+        if (k < cap) slot[2 + k] = l;
+        else a.inc[kIncOvf + q] = 1u;
+    }
+    return deg;
+}
+
+// The commit's end of sweep t (all its threads): its own slot's header, the rows and arcs every
+// writer listed, the statistics, and the choice for sweep t + 1 -- a full recount after a slot
+// overflowed or when the changed rows carry more than inc_thresh arcs (each changed arc costs two
+// random colour reads; the tile scan streams half an entry per arc), else incremental.
+__device__ void inc_commit(const SweepArgs& a, uint32_t t, const uint32_t* cc) {
+    __shared__ unsigned long long red[2][32];
+    __shared__ unsigned long long pre[8];   // control words, loaded side by side (not one chain on thread 0)
+    __shared__ uint32_t wtot[32];
+    const uint32_t q = (t + 1u) & 1u, nloc = a.v_end - a.v_begin;
+    if (threadIdx.x < 7u) {
+        const uint32_t i = threadIdx.x;
+        pre[i] = i == 0 ? a.inc[kIncMode] : i == 1 ? a.inc[kIncOvf + q] : i == 2 ? a.inc[kIncHubN + q]
+                        : reinterpret_cast<const unsigned long long*>(a.inc + kIncStat)[i - 3u];
+    }
+    // every slot's rows gathered into one dense list (the next sweep's delta pass takes one row per
+    // wave): contiguous slot ranges per thread, their counts scanned over the workgroup
+    const uint32_t es = 2u + a.inc_slot, ws = 2u + a.inc_wslot_n, nsl = a.evnblk + kIncWalkSlots;
+    auto slot = [&](uint32_t i, uint32_t& cap) -> const uint32_t* {
+        cap = i < a.evnblk ? a.inc_slot : a.inc_wslot_n;
+        return i < a.evnblk ? a.inc_eslot + ((size_t)q * a.evnblk + i) * es
+                            : a.inc_wslot + ((size_t)q * kIncWalkSlots + (i - a.evnblk)) * ws;
+    };
+    const uint32_t per = (nsl + blockDim.x - 1u) / blockDim.x;
+    const uint32_t s0 = min(threadIdx.x * per, nsl), s1 = min(s0 + per, nsl);
+    uint32_t mine = 0;
+    unsigned long long arcs = 0;
+    for (uint32_t i = s0; i < s1; i++) {
+        uint32_t cap;
+        const uint32_t* sl = slot(i, cap);
+        mine += min(sl[0], cap);
+        arcs += sl[1];
+    }
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t inc = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    for (int o = 32; o > 0; o >>= 1) arcs += __shfl_xor(arcs, o, 64);
+    if (lane == 63u) wtot[wave] = inc;
+    if (lane == 0) red[1][wave] = arcs;
+    __syncthreads();
+    uint32_t off = inc - mine, T = 0;
+    for (uint32_t w = 0; w < nwv; w++) {
+        if (w < wave) off += wtot[w];
+        T += wtot[w];
+    }
+    uint32_t* dn = a.inc_dense + (size_t)q * nloc;
+    for (uint32_t i = s0; i < s1; i++) {
+        uint32_t cap;
+        const uint32_t* sl = slot(i, cap);
+        const uint32_t c = min(sl[0], cap);
+        for (uint32_t k = 0; k < c; k++) dn[off + k] = sl[2 + k];
+        off += c;
+    }
+    const uint32_t* cl = a.inc_cchg + (size_t)q * (2u + a.ev_cap);   // the event replay's rows after them
+    for (uint32_t k = threadIdx.x; k < cc[0]; k += blockDim.x) dn[T + k] = cl[2 + k];
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < nwv; w++) arcs += red[1][w];
+        a.inc[kIncDenseN + q] = T + cc[0];
+        const unsigned long long rows = (unsigned long long)T + cc[0] + pre[2];
+        arcs += cc[1];
+        unsigned long long* s = reinterpret_cast<unsigned long long*>(a.inc + kIncStat);
+        s[0] = pre[3] + (pre[0] ? 0ull : 1ull);
+        s[1] = pre[4] + (pre[0] ? 1ull : 0ull);
+        s[2] = pre[5] + rows;
+        s[3] = pre[6] + arcs;
+        a.inc[kIncMode] = (pre[1] || arcs > a.inc_thresh) ? 1u : 0u;
+    }
+}
 constexpr uint32_t kPairTraceMax = 256;   // pairs traced per workgroup (MCMC_PAIR_TRACE)
 constexpr uint32_t kPairTraceRec = 8;     // {start, scan end min, scan end max, eval end, barrier end, info, 0, 0}
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
@@ -215,6 +334,13 @@ __device__ __forceinline__ uint32_t minstd_pow_tab(uint64_t e) {
     for (int i = 0; e; i++, e >>= 1)
         if (e & 1) r = minstd_mulmod(r, kMinstdPow2[i]);
     return r;
+}
+// The same for an exponent every lane of the wave shares: a scalar loop (scalar table loads), where
+// a per-lane exponent is a chain of ~22 dependent vector loads and mulmods.
+__device__ __forceinline__ uint32_t minstd_pow_tab_wave(uint64_t e) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)e);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(e >> 32));
+    return minstd_pow_tab(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
@@ -302,6 +428,8 @@ template <typename CT = uint8_t>
 __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
                               uint32_t lds_cap, bool sorted = false) {
     DevState* st = a.st;
+    __shared__ uint32_t inc_cc[2];   // incremental counts: rows the event replay changed, their arcs
+    if (threadIdx.x == 0) inc_cc[0] = inc_cc[1] = 0;   // (the barriers below order it)
     MCMC_COMMIT_PHASE(a, 1);
     const CT* C = reinterpret_cast<const CT*>((t & 1) ? a.colors1 : a.colors0);
     CT* Cs = reinterpret_cast<CT*>((t & 1) ? a.colors0 : a.colors1);
@@ -392,10 +520,17 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                 a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
+            if (a.inc != nullptr && c != (uint32_t)C[v])   // (whole-graph contexts: v = l)
+                atomicAdd(&inc_cc[1], inc_list(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.ev_cap),
+                                               a.ev_cap, &inc_cc[0]));
         }
         __syncthreads();
     }
     MCMC_COMMIT_PHASE(a, 4);
+    if (a.inc != nullptr) {
+        __syncthreads();   // inc_cc complete
+        inc_commit(a, t, inc_cc);
+    }
     if (threadIdx.x == 0) {
         st->glibc_draws += E;
         st->x_t = minstd_mulmod(st->x_t, a.aN);
@@ -869,7 +1004,7 @@ __device__ __forceinline__ uint32_t evaluate_tile(const SweepArgs& a, DevState* 
     const uint32_t cv = valid ? (uint32_t)Cown[a.v_begin + l] : 0u;
     const uint32_t tab = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;
     // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139)
-    const uint32_t base = minstd_pow_tab((uint64_t)(a.v_begin + l0) + 1);
+    const uint32_t base = minstd_pow_tab_wave((uint64_t)(a.v_begin + l0) + 1);
     const uint32_t x = minstd_mulmod(minstd_mulmod(x_t, base), kMinstdLanePow[lane]);
     return evaluate_core<NW>(a, st, Cs, l0, cnt, acc, lane, ev_flag, vf, cv, tab, x);
 }
@@ -1955,7 +2090,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     // evaluation row in group g; xsg advances it by one group of this workgroup, xsk by one tile
     uint32_t xg = 0, xsg = 0, xsk = 0;
     if (!REF) {
-        xg = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + (uint64_t)g * R + 64u * wid + 1u));
+        xg = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + (uint64_t)g * R + 64u * wid + 1u));
         xsg = minstd_pow_tab((uint64_t)gridDim.x * R);
         xsk = minstd_pow_tab(64u * (uint64_t)nwaves);
     }
@@ -2513,6 +2648,10 @@ using SweepLaunch = void (*)(const SweepArgs&, dim3, dim3, size_t, hipStream_t);
 // wide sweep: grid = CUs (g.x); scan 8 x 256-thread workgroups per CU (a multiple of the 8 slabs),
 // evaluation one workgroup per 2048 vertices, walk 8 per CU
 void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
+    if (a.inc) {   // incremental counts (a full sweep: zeroed here, recounted by the tile scan; an
+                   // incremental one's flag pass runs in the tile scan's launch)
+        wide_inc_delta_kernel<<<g.x, 1024, 0, s>>>(a);
+    }
     if (a.xs_ent && a.xs_mode == 1) {
         if (!a.fp_live)
             wide_fp_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 2047u) / 2048u, 4096u)), 256, 0, s>>>(a);
@@ -2678,10 +2817,24 @@ struct mcmc_ctx {
     uint32_t* evblk = nullptr;      // per evaluation workgroup event lists
     uint32_t* evcnt = nullptr;
     uint32_t evnblk = 0;
+    uint32_t* evpow = nullptr;      // per evaluation wave: 16807^(first vertex + 1) (host-computed)
     const XSlabLayout* xs = nullptr;   // wide: XCD-slab edge layout (graph-owned; nullptr: CSR arc scan)
+    // wide: incremental violation counts (sweep_wide.h wide_inc_*; nullptr: the tile scan every sweep)
+    uint32_t* inc = nullptr;        // kIncWords control words, then counts, lists and slots (make_args)
+    unsigned long long inc_thresh = 0;
+    uint32_t inc_slot = 0, inc_wslot_n = 0, inc_hub_arcs = 256;
 };
 
 namespace {
+
+// Incremental wide sweep: lists and statistics cleared, the next sweep a full recount (after any
+// change of the colours that is not a sweep's).
+hipError_t inc_reset(mcmc_ctx* c) {
+    uint32_t h[kIncWords] = {};
+    h[kIncMode] = 1u;
+    hipError_t e = hipMemcpyAsync(c->inc, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
+    return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // h lives on this frame
+}
 
 // Host <-> device colour transfers (n colours in vertex order; partitioned replicas too).
 int upload_colors(mcmc_ctx* c, uint8_t* dst, const uint8_t* h) {
@@ -2734,6 +2887,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.maxRip = c->p.maxRip;
     a.z = c->z;
     a.aN = minstd_pow(kMinstdA, c->n);
+    a.a256 = minstd_pow(kMinstdA, 256);
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
     a.check_done = check_done;
@@ -2819,6 +2973,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.evblk = c->evblk;
         a.evcnt = c->evcnt;
         a.evnblk = c->evnblk;
+        a.evpow = c->evpow;
         a.fused = 0;
         if (c->xs) {
             a.xs_ent = c->xs->ent;
@@ -2831,6 +2986,22 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.xs_S = c->xs->S;
             a.xs_cbits = c->xs->cbits;
             a.xs_sym = c->xs->sym;
+        }
+        if (c->inc && !c->part) {
+            const size_t nloc = c->v_end - c->v_begin;
+            a.inc = c->inc;
+            a.inc_vcnt = c->inc + kIncWords;
+            a.inc_hub = a.inc_vcnt + nloc;
+            a.inc_tch = a.inc_hub + 2 * nloc;
+            a.inc_eslot = a.inc_tch + 2 * nloc;
+            a.inc_vslot = a.inc_eslot + 2 * (size_t)c->evnblk * (2 + c->inc_slot);
+            a.inc_wslot = a.inc_vslot + 2 * (size_t)c->evnblk * (2 + c->inc_slot);
+            a.inc_cchg = a.inc_wslot + 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n);
+            a.inc_dense = a.inc_cchg + 2 * (2 + (size_t)c->ev_cap);
+            a.inc_slot = c->inc_slot;
+            a.inc_wslot_n = c->inc_wslot_n;
+            a.inc_hub_arcs = c->inc_hub_arcs;
+            a.inc_thresh = c->inc_thresh;
         }
     }
     a.phase_ts = c->phase_ts;
@@ -3416,6 +3587,15 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMalloc(&c->evblk, sizeof(uint32_t) * kEvSlot * c->evnblk);
         if (ew == hipSuccess) ew = hipMalloc(&c->evcnt, sizeof(uint32_t) * c->evnblk);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->evcnt, 0, sizeof(uint32_t) * c->evnblk, c->stream);
+        {   // u_v's skip-ahead to each evaluation wave's first vertex, once (a per-lane chain of ~22
+            // table loads and mulmods in the kernel otherwise)
+            std::vector<uint32_t> pw((size_t)c->evnblk * 4);
+            for (size_t i = 0; i < pw.size(); i++)
+                pw[i] = minstd_pow(kMinstdA, (uint64_t)v_begin + 256ull * kWideEvalPer * (i / 4) + 64ull * (i % 4) + 1ull);
+            if (ew == hipSuccess) ew = hipMalloc(&c->evpow, sizeof(uint32_t) * pw.size());
+            if (ew == hipSuccess)
+                ew = hipMemcpy(c->evpow, pw.data(), sizeof(uint32_t) * pw.size(), hipMemcpyHostToDevice);
+        }
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wflag, 0, (nloc + 4u) & ~(size_t)3, c->stream);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->wcount, 0, 4 * sizeof(uint32_t), c->stream);
         if (ew == hipSuccess) {
@@ -3443,6 +3623,28 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                     if (ew == hipSuccess) ew = hipMemsetAsync(c->wfp[q], 0, (size_t)gd.n + 2048, c->stream);
                 }
             }
+        }
+        // incremental violation counts: a whole-graph context over a symmetric CSR without repeated
+        // arcs, with the LDS tile scan for its full sweeps. MCMC_WIDE_INC = 0 off, 2 every sweep after
+        // a full one incremental (tests); MCMC_WIDE_INC_DIV: full recount above m / DIV changed arcs
+        // MCMC_WIDE_INC_SLOT: changed rows per evaluation slot (walk slots: half), past which the
+        // next sweep recounts (2 on, the tests: slots hold every row, no arc limit)
+        const char* wie = getenv("MCMC_WIDE_INC");
+        const int winc = wie ? atoi(wie) : 1;
+        if (ew == hipSuccess && winc != 0 && c->xs && c->xs->mode == 1 && c->xs->simple && v_begin == 0 &&
+            v_end == gd.n) {
+            const char* sv = getenv("MCMC_WIDE_INC_SLOT");
+            c->inc_slot = winc == 2 ? 256u * kWideEvalPer : std::max<uint32_t>(1u, sv ? (uint32_t)atoi(sv) : 32u);
+            c->inc_wslot_n = winc == 2 ? std::min<uint32_t>(nloc, 1u << 16) : std::max<uint32_t>(1u, c->inc_slot / 2u);
+            const size_t words = kIncWords + 5 * (size_t)nloc + 4 * (size_t)c->evnblk * (2 + c->inc_slot) +
+                                 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n) + 2 * (2 + (size_t)c->ev_cap) +
+                                 2 * (size_t)nloc;
+            ew = hipMalloc(&c->inc, sizeof(uint32_t) * words);
+            if (ew == hipSuccess) ew = hipMemsetAsync(c->inc, 0, sizeof(uint32_t) * words, c->stream);
+            const char* dv = getenv("MCMC_WIDE_INC_DIV");
+            const uint64_t div = dv ? std::max<uint64_t>(1, strtoull(dv, nullptr, 10)) : 32;
+            c->inc_thresh = winc == 2 ? ~0ull : c->arc_count / div;
+            if (const char* hv = getenv("MCMC_WIDE_INC_HUB")) c->inc_hub_arcs = (uint32_t)atoi(hv);
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);
@@ -3554,6 +3756,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     const uint32_t n = c->n;
     const uint32_t s0 = minstd_seed_state(c->p.seed);
     if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(c->v_end - c->v_begin, 1u), c->stream));
+    if (c->inc) MCMC_HIP_TRY(inc_reset(c));
     if (C0) {
         for (uint32_t v = 0; v < n; v++)
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
@@ -3738,6 +3941,19 @@ int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]) {
         MCMC_HIP_TRY(hipMemcpy(h, c->scan_stats, sizeof(h), hipMemcpyDeviceToHost));
     }
     for (int i = 0; i < 6; i++) out[i] = h[i];
+    return MCMC_OK;
+}
+
+int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    for (int i = 0; i < 5; i++) out[i] = 0;
+    if (!c->inc || c->part) return MCMC_OK;
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long h[4];
+    MCMC_HIP_TRY(hipMemcpy(h, c->inc + kIncStat, sizeof(h), hipMemcpyDeviceToHost));
+    out[0] = 1;
+    for (int i = 0; i < 4; i++) out[1 + i] = h[i];
     return MCMC_OK;
 }
 
@@ -4076,8 +4292,10 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->evblk);
     (void)hipFree(c->ftab);
     (void)hipFree(c->evcnt);
+    (void)hipFree(c->evpow);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
+    (void)hipFree(c->inc);
     (void)hipFree(c->gmask);
     (void)hipFree(c->etab);
     (void)hipFree(c->scan_stats);

@@ -76,12 +76,155 @@ __device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
     a.wlist[idx] = a.v_begin + l;
     a.wlist[nloc + idx] = slot;
 }
-__device__ __forceinline__ void flag_violator(const SweepArgs& a, uint32_t l) {
+__device__ __forceinline__ void flag_violator(const SweepArgs& a, uint32_t l, uint32_t) {
     if (a.wflag[l]) return;
     const uint32_t bit = 1u << (8u * (l & 3u));
     if (atomicOr(reinterpret_cast<uint32_t*>(a.wflag) + (l >> 2), bit) & bit) return;
     if (a.taboo != nullptr && a.taboo[l] > 0) return;
     push_violator(a, l);
+}
+// One end of a monochromatic kept edge in a full scan: its row's same-colour count (incremental
+// contexts) and its flag.
+__device__ __forceinline__ void mono_end(const SweepArgs& a, uint32_t l, uint32_t t) {
+    if (a.inc_vcnt != nullptr) atomicAdd(&a.inc_vcnt[l], 1u);
+    flag_violator(a, l, t);
+}
+
+// ---- incremental violation counts (single context, symmetric CSR without repeated arcs) ---------
+// Most vertices keep their colour once a power-law graph with nCol = maxDeg is nearly proper (C5:
+// ~1200 of 4.2M change per sweep, mostly CDF overflows), so the violation flags of C_t follow from
+// those of C_t-1 and the rows that changed: every row keeps vcnt = its arcs to same-coloured
+// neighbours (violation_count, coloringMCMC_CPU.cpp:329-351, is vcnt > 0). Per sweep t:
+//   wide_inc_delta_kernel  each row v that changed (C_t-1 -> C_t; the writers' slots of sweep t-1,
+//                          gathered into one dense list by its commit)
+//                          moves both ends of each arc (v, w) by [C_t[v] == C_t[w]] -
+//                          [C_t-1[v] == C_t-1[w]] (an arc whose w changed too only from the smaller
+//                          end; self-arcs never move); a count leaving 0 is listed (touched). Hubs
+//                          (rows above inc_hub_arcs arcs) take a workgroup each, other rows a wave.
+//   wide_tscan_kernel      (its launch, in an incremental sweep) the violators of C_t: those of C_t-1
+//                          (the evaluation's slots) and the touched rows, where vcnt > 0
+//                          (flag_violator dedupes); and C_t+1's replica (and fingerprints) start as
+//                          C_t on the changed rows, so the writers store changes only.
+// A full sweep (the first, after a slot overflowed, or when the changed rows carry more than
+// inc_thresh arcs) zeroes the counts here and the tile scan counts every monochromatic edge at both
+// ends (mono_end). Exact, not approximate (tests/test_wide.py::test_wide_incremental_counts).
+__device__ __forceinline__ void inc_touch(const SweepArgs& a, uint32_t l, uint32_t t) {
+    const uint32_t p = t & 1u, nloc = a.v_end - a.v_begin;
+    const uint32_t idx = atomicAdd(&a.inc[kIncTch + p], 1u);
+    if (idx < nloc) a.inc_tch[(size_t)p * nloc + idx] = l;
+    else a.inc[kIncTchOvf + p] = 1u;
+}
+// Arcs k, k + step, ... < k1 of changed row v (colour cov in C_t-1, cnv in C_t): the other ends'
+// counts move; returns this thread's part of v's own move.
+__device__ __forceinline__ int inc_arcs(const SweepArgs& a, const uint16_t* __restrict__ Cp,
+                                        const uint16_t* __restrict__ Cn, uint32_t v, uint32_t cov, uint32_t cnv,
+                                        uint64_t k, uint64_t k1, uint32_t step, uint32_t t) {
+    int dv = 0;
+    for (; k < k1; k += 4ull * step) {
+        uint32_t w[4], ow[4], nw[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t kk = k + (uint64_t)j * step;
+            w[j] = kk < k1 ? a.col_idx[kk] : v;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            ow[j] = Cp[w[j]];
+            nw[j] = Cn[w[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (w[j] == v) continue;                      // a self-arc (or past the row): never moves
+            if (ow[j] != nw[j] && w[j] < v) continue;    // both ends changed: counted from row w
+            const int d = (int)(nw[j] == cnv) - (int)(ow[j] == cov);
+            if (d != 0) {
+                dv += d;
+                const uint32_t old = atomicAdd(&a.inc_vcnt[w[j]], (uint32_t)d);
+                if (d > 0 && old == 0u) inc_touch(a, w[j], t);
+            }
+        }
+    }
+    return dv;
+}
+__device__ __forceinline__ void inc_own(const SweepArgs& a, uint32_t v, int dv, uint32_t t) {
+    if (dv == 0) return;
+    const uint32_t old = atomicAdd(&a.inc_vcnt[v], (uint32_t)dv);
+    if (dv > 0 && old == 0u) inc_touch(a, v, t);
+}
+__global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    const uint32_t t = st->t, nloc = a.v_end - a.v_begin, p = t & 1u;
+    uint32_t* ctl = a.inc;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // lists sweep t appends to (their last reader: sweep t - 1)
+        const uint32_t q = p ^ 1u;
+        ctl[kIncOvf + q] = 0;
+        ctl[kIncTch + q] = 0;
+        ctl[kIncTchOvf + q] = 0;
+        ctl[kIncHubN + q] = 0;
+    }
+    if (ctl[kIncMode]) {   // full sweep: the tile scan recounts
+        for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += gridDim.x * blockDim.x)
+            a.inc_vcnt[l] = 0;
+        return;
+    }
+    const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);   // C_t
+    const uint16_t* __restrict__ Cp = reinterpret_cast<const uint16_t*>(p ? a.colors0 : a.colors1);   // C_t-1
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nh = ctl[kIncHubN + p];
+    for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {   // hubs: a workgroup each
+        const uint32_t v = a.inc_hub[(size_t)p * nloc + h];
+        int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + threadIdx.x, a.row_off[v + 1], blockDim.x, t);
+        for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+        if (lane == 0) inc_own(a, v, dv, t);
+    }
+    // other rows (the commit gathered them into one dense list): a wave each
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6, nd = ctl[kIncDenseN + p];
+    const uint32_t* dn = a.inc_dense + (size_t)p * nloc;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < nd; i += nw) {
+        const uint32_t v = dn[i];
+        int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + lane, a.row_off[v + 1], 64u, t);
+        for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+        if (lane == 0) inc_own(a, v, dv, t);
+    }
+}
+
+// An incremental sweep's flag pass (the tile scan's launch, all its threads).
+__device__ void wide_inc_flags(const SweepArgs& a, uint32_t t) {
+    const uint32_t nloc = a.v_end - a.v_begin, p = t & 1u;
+    const uint32_t* ctl = a.inc;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nthr = gridDim.x * blockDim.x;
+    {   // C_t+1's buffer (and fingerprints) = C_t on the rows that changed into C_t
+        const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);
+        uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>(p ? a.colors0 : a.colors1);
+        const uint8_t* fp = p ? a.wfp1 : a.wfp0;
+        uint8_t* fpn = p ? a.wfp0 : a.wfp1;
+        const uint32_t nh = ctl[kIncHubN + p], nd = ctl[kIncDenseN + p];
+        for (uint32_t i = tid; i < nd + nh; i += nthr) {
+            const uint32_t v = i < nd ? a.inc_dense[(size_t)p * nloc + i] : a.inc_hub[(size_t)p * nloc + (i - nd)];
+            Cs[v] = C[v];
+            if (a.fp_live) fpn[v] = fp[v];
+        }
+    }
+    if (ctl[kIncTchOvf + p]) {
+        for (uint32_t l = tid; l < nloc; l += nthr)
+            if ((int32_t)a.inc_vcnt[l] > 0) flag_violator(a, l, t);
+        return;
+    }
+    // candidates: the violators of C_t-1 (the evaluation's slots of sweep t-1) and the touched rows
+    const uint32_t vs = 2u + a.inc_slot, nv = a.evnblk * a.inc_slot, ntc = ctl[kIncTch + p];
+    for (uint32_t i = tid; i < nv + ntc; i += nthr) {
+        uint32_t l;
+        if (i < nv) {
+            const uint32_t* sl = a.inc_vslot + ((size_t)(p ^ 1u) * a.evnblk + i / a.inc_slot) * vs;
+            const uint32_t k = i % a.inc_slot;
+            if (k >= min(sl[0], a.inc_slot)) continue;
+            l = sl[2 + k];
+        } else {
+            l = a.inc_tch[(size_t)p * nloc + (i - nv)];
+        }
+        if ((int32_t)a.inc_vcnt[l] > 0) flag_violator(a, l, t);
+    }
 }
 
 __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
@@ -126,8 +269,8 @@ __global__ __launch_bounds__(256) void wide_xscan_kernel(SweepArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             if (e[i] != kXsPad && cr[i] == cc[i]) {   // rare: a monochromatic edge
-                flag_violator(a, r[i]);
-                if (a.xs_sym && j[i] - vb < nloc) flag_violator(a, j[i] - vb);
+                flag_violator(a, r[i], t);
+                if (a.xs_sym && j[i] - vb < nloc) flag_violator(a, j[i] - vb, t);
             }
         }
         if (!more) break;
@@ -186,6 +329,10 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
     __shared__ __attribute__((aligned(16))) uint8_t wins[kTscanThreads / 64][kTsWin];   // row windows, one per wave
     DevState* st = a.st;
     if (a.check_done && st->done) return;
+    if (a.inc != nullptr && a.inc[kIncMode] == 0) {   // incremental sweep: the flags from the moved counts
+        wide_inc_flags(a, st->t);
+        return;
+    }
     if (threadIdx.x == 0) ncand = 0;
     const uint32_t t = st->t;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
@@ -287,8 +434,8 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
                         } else {   // list full: settle it here
                             const uint32_t j = v0 + (e[i] & cmask);
                             if (C[(vb + r[i])] == C[j]) {
-                                flag_violator(a, r[i]);
-                                if (a.xs_sym && j - vb < nloc) flag_violator(a, j - vb);
+                                mono_end(a, r[i], t);
+                                if (a.xs_sym && j - vb < nloc) mono_end(a, j - vb, t);
                             }
                         }
                     }
@@ -321,8 +468,8 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
         for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {   // the candidates: compare colours
             const uint2 rc = cand[k];
             if (C[(vb + rc.x)] == C[rc.y]) {
-                flag_violator(a, rc.x);
-                if (a.xs_sym && rc.y - vb < nloc) flag_violator(a, rc.y - vb);
+                mono_end(a, rc.x, t);
+                if (a.xs_sym && rc.y - vb < nloc) mono_end(a, rc.y - vb, t);
             }
         }
         __syncthreads();
@@ -368,7 +515,7 @@ __global__ __launch_bounds__(256) void wide_scan_kernel(SweepArgs a) {
                 do { r++; rend = ro[r + 1] - a0; } while (rend <= k);
                 own = C[(a.v_begin + r)];
             }
-            if (nc[i] == own) flag_violator(a, r);
+            if (nc[i] == own) flag_violator(a, r, t);
         }
     }
 }
@@ -396,7 +543,8 @@ __device__ __forceinline__ void walk_gather(const SweepArgs& a, const uint16_t* 
 // All threads call it; it ends with a barrier.
 __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
                             uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* wsum,
-                            uint32_t* ev, uint32_t* nev, uint32_t cap) {
+                            uint32_t* ev, uint32_t* nev, uint32_t cap, uint32_t* islot = nullptr,
+                            uint32_t* ic = nullptr) {
     DevState* st = a.st;
     const uint32_t NWW = (a.nCol + 31u) >> 5;
     const uint32_t per = (NWW + kWideWalkThreads - 1u) / kWideWalkThreads;   // words per thread (prefix)
@@ -428,7 +576,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
     if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
         const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
         const uint32_t cv = C[v];
-        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1));
+        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)v + 1));
         const float u = minstd_canonical(x);
         uint32_t nc;
         if (Zvcomp > 0) {   // case (ii)
@@ -439,8 +587,13 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         }
         if (lane == 0) {
             const bool event = nc == a.nCol;
-            Cs[v] = (uint16_t)(event ? cv : nc);
-            if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)(event ? cv : nc);
+            const uint32_t nv = event ? cv : nc;
+            // an incremental sweep's C_t+1 buffer already holds C_t here (wide_inc_flag_kernel)
+            if (nv != cv || a.inc == nullptr || a.inc[kIncMode]) {
+                Cs[v] = (uint16_t)nv;
+                if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
+            }
+            if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list(a, l, t, islot, a.inc_wslot_n, &ic[0]));
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
             if (event) {
                 const uint32_t k = ev ? atomicAdd(nev, 1u) : cap;
@@ -460,14 +613,14 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
 // One violator's whole resample by one workgroup.
 __device__ void walk_violator(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
                               uint16_t* __restrict__ Cs, uint32_t* mask, uint32_t* pre, uint32_t* wsum, uint32_t* ev,
-                              uint32_t* nev, uint32_t cap) {
+                              uint32_t* nev, uint32_t cap, uint32_t* islot, uint32_t* ic) {
     const uint32_t NWW = (a.nCol + 31u) >> 5;
     const uint32_t l = v - a.v_begin;
     for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
     __syncthreads();
     walk_gather(a, C, mask, a.row_off[l], a.row_off[l + 1]);
     __syncthreads();
-    walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, ev, nev, cap);
+    walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, ev, nev, cap, islot, ic);
 }
 
 // The walk workgroups of the evaluation launch: tasks b, b + nb, ... (push_violator). A one-task
@@ -480,10 +633,18 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     __shared__ uint32_t pre[kWideMaskWords + 1];
     __shared__ uint32_t wsum[kWideWalkThreads / 64];
     __shared__ uint32_t sh_last;
+    __shared__ uint32_t ic[2];   // incremental counts: rows this workgroup changed, their arcs
     const uint32_t cnt = a.wcount[0];
     const uint32_t nx = a.wcount[2], ns = min(a.wcount[3], kSplitMax);
     const uint32_t T = cnt + nx;
-    if (b >= T) return;
+    // this workgroup's slot of changed rows (written every sweep, empty ones too)
+    uint32_t* islot = a.inc ? a.inc_wslot + ((size_t)((t + 1u) & 1u) * kIncWalkSlots + b) * (2u + a.inc_wslot_n)
+                            : nullptr;
+    if (b >= T) {
+        if (islot != nullptr && threadIdx.x == 0) islot[0] = islot[1] = 0;
+        return;
+    }
+    if (threadIdx.x == 0) ic[0] = ic[1] = 0;   // (read after the tasks' barriers)
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t NWW = (a.nCol + 31u) >> 5;
@@ -509,7 +670,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         }
         const uint32_t v = a.wlist[idx], slot = a.wlist[nloc + idx], l = v - a.v_begin;
         if (slot == 0xFFFFFFFFu) {
-            walk_violator(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0);
+            walk_violator(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0, islot, ic);
             continue;
         }
         const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
@@ -534,9 +695,13 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
             __threadfence();
             for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
             __syncthreads();
-            walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0);
+            walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0, islot, ic);
         }
         __syncthreads();   // sh_last and mask are reused by the next task
+    }
+    if (islot != nullptr && threadIdx.x == 0) {   // thread 0 made every entry (walk_finish's lane 0)
+        islot[0] = ic[0];
+        islot[1] = ic[1];
     }
 }
 
@@ -546,6 +711,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
 __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol, sh_nev;
     __shared__ uint32_t sh_ev[kEvSlot];   // this workgroup's overflow events (ordered at the end)
+    __shared__ uint32_t sh_ic[3];         // incremental counts: changed rows, their arcs, violators listed
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     if (blockIdx.x < kWalkBlocks) {   // the walks, beside the evaluation (dispatched first)
@@ -556,9 +722,17 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     if (threadIdx.x == 0) {
         sh_viol = 0;
         sh_nev = 0;
+        sh_ic[0] = sh_ic[1] = sh_ic[2] = 0;
     }
     __syncthreads();
     const uint32_t t = st->t, x_t = st->x_t;
+    // incremental counts: this workgroup's slots -- rows it changes (C_t+1 parity) and violators of C_t
+    uint32_t* islot = nullptr;
+    uint32_t* vslot = nullptr;
+    if (a.inc != nullptr) {
+        islot = a.inc_eslot + ((size_t)((t + 1u) & 1u) * a.evnblk + eb) * (2u + a.inc_slot);
+        vslot = a.inc_vslot + ((size_t)(t & 1u) * a.evnblk + eb) * (2u + a.inc_slot);
+    }
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t nloc = a.v_end - a.v_begin;
@@ -581,10 +755,8 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     }
     // u_v: engine draw K_t + v + 1 (bulk draw in vertex order, coloringMCMC_CPU.cpp:139); the
     // lane's draw moves by 16807^256 from one j to the next
-    const uint32_t a256 = minstd_pow_tab(256);
-    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, minstd_pow_tab((uint64_t)a.v_begin + eb * (256u * kWideEvalPer) +
-                                                                 (threadIdx.x & ~63u) + 1)),
-                               kMinstdLanePow[lane]);
+    const uint32_t a256 = a.a256;
+    uint32_t x = minstd_mulmod(minstd_mulmod(x_t, a.evpow[4u * eb + (threadIdx.x >> 6)]), kMinstdLanePow[lane]);
     uint32_t xs[kWideEvalPer];
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
@@ -596,6 +768,8 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     // u < E[nCol-1] the answer depends on u alone up to cv: F(u) = first k with E[k] > u, one load
     // of the host table ftab (indexed by x - 1, u = (x - 1) 2^-31 exactly); else the table walk.
     const bool tabled = a.eps > 0.0f;
+    // an incremental sweep stores changes only: C_t+1's buffer already holds C_t (wide_inc_flag_kernel)
+    const bool wall = a.inc == nullptr || a.inc[kIncMode] != 0u;
     uint32_t cviol = 0;
 #pragma unroll
     for (int j = 0; j < kWideEvalPer; j++) {
@@ -606,10 +780,19 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         cviol += viol[j];
         bool event = false;
         if (valid) {
-            if (viol[j]) a.wflag[l] = 0;
+            if (viol[j]) {
+                a.wflag[l] = 0;
+                if (vslot != nullptr) {   // the next sweep's flag pass starts from the violators of C_t
+                    const uint32_t k = atomicAdd(&sh_ic[2], 1u);
+                    if (k < a.inc_slot) vslot[2 + k] = l;
+                    else a.inc[kIncOvf + ((t + 1u) & 1u)] = 1u;
+                }
+            }
             if (tab[j] > 0) {   // :496-501
-                Cs[v] = (uint16_t)cv[j];
-                if (fpn) fpn[v] = (uint8_t)cv[j];
+                if (wall) {
+                    Cs[v] = (uint16_t)cv[j];
+                    if (fpn) fpn[v] = (uint8_t)cv[j];
+                }
                 a.taboo[l] = tab[j] - 1;
             } else if (viol[j]) {
                 // case (i) or (ii): a walk workgroup's (walk_tasks)
@@ -624,8 +807,12 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
                     nc = walk_own_tab(a.etab, a.nCol, cv[j], a.eps, a.hi, u);
                 }
                 event = nc == a.nCol;
-                Cs[v] = (uint16_t)(event ? cv[j] : nc);   // an event's colour is the commit's replay
-                if (fpn) fpn[v] = (uint8_t)(event ? cv[j] : nc);
+                const uint32_t nv = event ? cv[j] : nc;   // an event's colour is the commit's replay
+                if (wall || nv != cv[j]) {
+                    Cs[v] = (uint16_t)nv;
+                    if (fpn) fpn[v] = (uint8_t)nv;
+                }
+                if (islot != nullptr && nv != cv[j]) atomicAdd(&sh_ic[1], inc_list(a, l, t, islot, a.inc_slot, &sh_ic[0]));
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
             }
         }
@@ -649,7 +836,15 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         for (uint32_t k = 0; k < ne; k++) rk += sh_ev[k] < v ? 1u : 0u;
         a.evblk[(size_t)eb * kEvSlot + rk] = v;
     }
-    if (threadIdx.x == 0) a.evcnt[eb] = ne;
+    if (threadIdx.x == 0) {
+        a.evcnt[eb] = ne;
+        if (islot != nullptr) {   // slot headers, written every sweep
+            islot[0] = sh_ic[0];
+            islot[1] = sh_ic[1];
+            vslot[0] = sh_ic[2];
+            vslot[1] = 0;
+        }
+    }
     for (int off = 32; off >= 1; off >>= 1) cviol += __shfl_xor(cviol, off, 64);
     if (lane == 0 && cviol) atomicAdd(&sh_viol, cviol);
     __syncthreads();
@@ -688,6 +883,20 @@ __global__ void init_coloring_wide_kernel(uint16_t* C, uint32_t n, uint32_t x0, 
 // two arcs of a local edge exactly one survives.
 __device__ __forceinline__ bool xs_keep(uint32_t i, uint32_t j, uint32_t vb, uint32_t nloc, uint32_t sym) {
     return !sym || j - vb >= nloc || ((i + j) & 1u) == (i < j ? 1u : 0u);
+}
+
+// *bad = 1 if a local row (ascending) lists a neighbour twice: the incremental counts need every
+// edge exactly once in each end's row. One wave per row.
+__global__ __launch_bounds__(256) void xs_dupcheck_kernel(const uint64_t* __restrict__ ro,
+                                                          const uint32_t* __restrict__ col, uint32_t nloc,
+                                                          uint32_t* __restrict__ bad) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t l = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; l < nloc; l += nw) {
+        bool dup = false;
+        for (uint64_t k = ro[l] + 1u + lane; k < ro[l + 1]; k += 64) dup = dup || col[k] == col[k - 1];
+        if (__ballot(dup) && lane == 0) atomicOr(bad, 1u);
+    }
 }
 
 // cnt[l] = kept arcs of local row l. One wave per row.
@@ -958,6 +1167,15 @@ int get_xslab(mcmc_graph* gh, uint32_t vb, uint32_t ve, uint32_t mode, uint32_t 
     bool symmetric = false;   // the one-entry-per-edge layout needs every local arc's reverse
     if (int rs = csr_symmetric(gd, vb, nloc, st, &symmetric)) { cleanup(); return rs; }
     L->sym = symmetric ? 1u : 0u;
+    if (symmetric) {   // rows are sorted (above): repeated arcs sit side by side
+        xs_dupcheck_kernel<<<wblocks, 256, 0, st>>>(gd.row_off + vb, gd.col_idx, nloc, flag + 1);
+        XTRY(hipGetLastError());
+        XTRY(hipMemcpyAsync(&h[1], flag + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        XTRY(hipStreamSynchronize(st));
+        L->simple = h[1] == 0 ? 1u : 0u;
+        h[1] = 0;
+        XTRY(hipMemsetAsync(flag + 1, 0, sizeof(uint32_t), st));
+    }
     // kept arcs per row -> positions -> (slab, row) keys in CSR order -> stable sort by key
     XTRY(hipMalloc(&cnt, sizeof(uint32_t) * ((size_t)nloc + 1)));
     XTRY(hipMalloc(&pos, sizeof(uint32_t) * ((size_t)nloc + 1)));

@@ -211,9 +211,8 @@ def test_wide_forced_small_ncol(M, monkeypatch, ncol, eps, taboo):
     run_both(M, off, idx, ncol, epsilon=eps, tabooIteration=taboo, maxRip=60)
 
 
-@pytest.mark.gpu
-def test_wide_skewed_degrees(M):
-    """A hub joined to every vertex plus a sparse remainder: one long row, many empty/short ones."""
+def _hub_graph():
+    """A hub joined to 4000 vertices plus a sparse remainder: one long row, many empty/short ones."""
     rng = np.random.default_rng(5)
     n = 5000
     E = set()
@@ -231,9 +230,70 @@ def test_wide_skewed_degrees(M):
     off = np.zeros(n + 1, dtype=np.uint64)
     np.add.at(off, src + 1, 1)
     off = np.cumsum(off).astype(np.uint64)
+    return off, idx
+
+
+@pytest.mark.gpu
+def test_wide_skewed_degrees(M):
+    """A hub joined to every vertex plus a sparse remainder: one long row, many empty/short ones."""
+    off, idx = _hub_graph()
     ncol = O.max_deg(off)
     run_both(M, off, idx, ncol)
     run_both(M, off, idx, 300, maxRip=30)
+
+
+INC_CASES = {
+    # name: (graph, nCol, run kwargs, env)
+    "rmat-maxdeg": ("rmat", None, {}, {}),
+    "rmat-300": ("rmat", 300, {"maxRip": 25}, {}),
+    "hub": ("hub", 300, {"maxRip": 30}, {}),
+    "sparse-taboo": ("sparse", 1000, {"tabooIteration": 2, "maxRip": 40}, {}),
+    "sparse-eps": ("sparse", 700, {"epsilon": 1e-3, "maxRip": 40}, {}),
+    "dense-all-change": ("dense", 16, {"maxRip": 30}, {"MCMC_GATHER": "wide"}),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("case", list(INC_CASES))
+def test_wide_incremental_counts(M, monkeypatch, mode, case):
+    """The wide sweep's incremental violation counts (sweep_wide.h wide_inc_*): each sweep moves
+    every row's same-colour count by the rows that changed colour instead of rescanning every edge
+    (violation_count, coloringMCMC_CPU.cpp:329-351, is count > 0). Off (0), the default choice per
+    sweep (1) and forced after the first full sweep (2) -- including sweeps where EVERY vertex
+    changes (nCol 16: both ends of most arcs changed), hubs past kIncHub arcs (their own
+    kernel), taboo, eps 1e-3 (own-colour moves) -- give the oracle's colouring and trajectory."""
+    graph, ncol, kw, env = INC_CASES[case]
+    monkeypatch.setenv("MCMC_WIDE_INC", mode)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if graph == "rmat":
+        off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    elif graph == "hub":
+        off, idx = _hub_graph()
+    elif graph == "sparse":
+        O.srand(1)
+        off, idx = O.setup_rnd2(3000, 0.01)
+    else:
+        O.srand(1)
+        off, idx = O.setup_rnd2(2000, 0.05)
+    ncol = ncol or O.max_deg(off)
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, epsilon=kw.get("epsilon", 1e-8), maxRip=kw.get("maxRip", 250),
+                                  tabooIteration=kw.get("tabooIteration", 0))
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    st = col.run(0)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, 1, **kw)
+    assert col.info()["variant"] == "wide"
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, st.finalViol, st.glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+    s = col.wide_inc_stats()
+    assert s["enabled"] == (mode != "0")
+    if mode == "2" and st.iter > 1:
+        assert s["full_sweeps"] == 1 and s["incremental_sweeps"] >= 1, s
+    col.close()
 
 
 @pytest.mark.gpu
