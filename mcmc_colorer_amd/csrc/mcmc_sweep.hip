@@ -208,6 +208,8 @@ struct SweepArgs {
     uint32_t* inc_wslot;        // [2][kWalkBlocks][2 + inc_wslot_n] walk workgroups' changed rows
     uint32_t* inc_cchg;         // [2][2 + ev_cap] the commit's changed rows (a slot)
     uint32_t* inc_dense;        // [2][nloc] every changed row but the hubs, gathered by the commit
+    uint32_t* inc_hdr;          // [2][evnblk + kWalkBlocks][2] the slots' headers again, side by side (the
+                                //   commit reads them all: one workgroup's loads, ~64 GB/s per CU)
     uint32_t inc_slot, inc_wslot_n;   // rows per evaluation / walk slot (past it: the next sweep recounts)
     uint32_t inc_hub_arcs;      // a changed row above this many arcs is a hub (MCMC_WIDE_INC_HUB)
     unsigned long long inc_thresh;    // the next sweep is incremental while its changed rows' arcs stay <= this
@@ -265,11 +267,12 @@ __device__ void inc_commit(const SweepArgs& a, uint32_t t, const uint32_t* cc) {
     const uint32_t s0 = min(threadIdx.x * per, nsl), s1 = min(s0 + per, nsl);
     uint32_t mine = 0;
     unsigned long long arcs = 0;
+    const uint32_t* hd = a.inc_hdr + (size_t)q * nsl * 2u;
     for (uint32_t i = s0; i < s1; i++) {
         uint32_t cap;
-        const uint32_t* sl = slot(i, cap);
-        mine += min(sl[0], cap);
-        arcs += sl[1];
+        (void)slot(i, cap);
+        mine += min(hd[2u * i], cap);
+        arcs += hd[2u * i + 1u];
     }
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     uint32_t inc = mine;
@@ -644,6 +647,206 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
     }
 }
 
+// The wide sweep's commit when it is the common case -- no event on the global list (walks made
+// none), at most NT events in the evaluation workgroups' ordered lists, no error, no stop -- as
+// three dependent round trips instead of ~10. A single workgroup pulls ~64 GB/s, so what it loads
+// is kept small and side by side: (1) the state words, the glibc ring, its evaluation workgroups'
+// event counts, both parities' compact slot headers, the incremental control words; (2) the
+// events' lists, the draw coefficients of the events present, the slots' rows; (3) the event
+// colours' own loads; then the stores. Same results as commit_control + commit_accept +
+// inc_commit (the generic path below runs otherwise, nothing written before the choice). Returns
+// false to fall back.
+constexpr uint32_t kPreBlk = 2, kPreSlots = 3;
+using CT_U16 = uint16_t;
+template <int NT>
+__device__ bool wide_commit_fast(const SweepArgs& a) {
+    __shared__ uint32_t s_ev[NT];          // the events, ascending
+    __shared__ uint32_t s_raw[NT];         // their raw glibc draws
+    __shared__ uint32_t s_ring[32], s_gw[32];
+    __shared__ uint32_t s_w[NT / 64], s_w2[NT / 64];
+    __shared__ uint32_t s_hdr[8];
+    __shared__ unsigned long long s_q[8], s_arcs[NT / 64];
+    __shared__ uint32_t s_cc[3];           // the replay's changed rows: listed, their arcs, hubs
+    DevState* st = a.st;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, nwv = NT / 64u;
+    const bool inc = a.inc != nullptr;
+    const uint32_t nb = a.evnblk, nsl = inc ? nb + kIncWalkSlots : 0u;
+    if (nb > NT * kPreBlk || nsl > NT * kPreSlots) return false;
+    // ---- (1) every independent load: state words, the glibc ring, draw tid's 31 coefficients,
+    // this thread's evaluation workgroups' event counts, both parities' slot headers ----
+    uint32_t hv = 0;
+    unsigned long long hq = 0;
+    if (tid < 6u)
+        hv = tid == 0 ? st->done : tid == 1 ? st->t : tid == 2 ? st->err : tid == 3 ? st->ev_count
+           : tid == 4 ? st->glibc_head : st->x_t;
+    if (tid < 2u) hq = tid == 0 ? st->viol : st->glibc_draws;
+    const uint32_t ring = tid < 31u ? st->glibc_ring[tid] : 0u;
+    const uint32_t b0 = min(tid * kPreBlk, nb), b1 = min(b0 + kPreBlk, nb);
+    uint32_t bc[kPreBlk];
+#pragma unroll
+    for (uint32_t j = 0; j < kPreBlk; j++) bc[j] = b0 + j < b1 ? a.evcnt[b0 + j] : 0u;
+    const uint32_t s0 = min(tid * kPreSlots, nsl), s1 = min(s0 + kPreSlots, nsl);
+    uint32_t sc[2][kPreSlots], sa[2][kPreSlots];
+#pragma unroll
+    for (uint32_t p = 0; p < 2; p++)
+#pragma unroll
+        for (uint32_t j = 0; j < kPreSlots; j++) {
+            const uint32_t i = s0 + j;
+            sc[p][j] = i < s1 ? min(a.inc_hdr[((size_t)p * nsl + i) * 2u], i < nb ? a.inc_slot : a.inc_wslot_n) : 0u;
+            sa[p][j] = i < s1 ? a.inc_hdr[((size_t)p * nsl + i) * 2u + 1u] : 0u;
+        }
+    uint32_t cw[5] = {0, 0, 0, 0, 0};   // mode, ovf[0..1], hubN[0..1]
+    if (inc && tid == 0) {
+        cw[0] = a.inc[kIncMode];
+        cw[1] = a.inc[kIncOvf];
+        cw[2] = a.inc[kIncOvf + 1];
+        cw[3] = a.inc[kIncHubN];
+        cw[4] = a.inc[kIncHubN + 1];
+    }
+    unsigned long long stq = 0;
+    if (inc && tid < 4u) stq = reinterpret_cast<const unsigned long long*>(a.inc + kIncStat)[tid];
+    if (tid < 8u) {
+        s_hdr[tid] = hv;
+        s_q[tid] = hq;
+    }
+    if (tid < 32u) s_ring[tid] = ring;
+    if (tid == 0) s_cc[0] = s_cc[1] = s_cc[2] = 0;
+    // ---- (2) orders: the events (per-workgroup counts) and the changed rows (slot counts) ----
+    uint32_t me = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPreBlk; j++) me += bc[j];
+    uint32_t ie = me;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(ie, o, 64);
+        if (lane >= (uint32_t)o) ie += y;
+    }
+    if (lane == 63u) s_w[wave] = ie;
+    __syncthreads();
+    const uint32_t done = s_hdr[0], t = s_hdr[1], err = s_hdr[2], Eg = s_hdr[3], head = s_hdr[4], x_t = s_hdr[5];
+    const unsigned long long viol = s_q[0], draws0 = s_q[1];
+    if (done) return true;
+    uint32_t off = ie - me, E = 0;
+    for (uint32_t w = 0; w < nwv; w++) {
+        if (w < wave) off += s_w[w];
+        E += s_w[w];
+    }
+    const bool stop = t == a.maxRip + 1 || (!a.bench && viol <= a.z);
+    if (Eg != 0 || err != 0 || E > NT || E > a.ev_cap || stop) return false;   // the generic path
+    uint32_t tab[31];   // draw tid's coefficients (tid < E): r = sum_i T[i][tid] w[i] (commit_accept)
+#pragma unroll
+    for (int i = 0; i < 31; i++) tab[i] = tid < E ? kGlibcTab[i * kGlibcTabK + tid] : 0u;
+    const uint32_t q = (t + 1u) & 1u;
+    uint32_t sm = 0;
+    unsigned long long arcs = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPreSlots; j++) {
+        sm += q ? sc[1][j] : sc[0][j];
+        arcs += q ? sa[1][j] : sa[0][j];
+    }
+    uint32_t is = sm;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(is, o, 64);
+        if (lane >= (uint32_t)o) is += y;
+    }
+    for (int o = 32; o > 0; o >>= 1) arcs += __shfl_xor(arcs, o, 64);
+    if (lane == 63u) s_w2[wave] = is;
+    if (lane == 0) s_arcs[wave] = arcs;
+#pragma unroll
+    for (uint32_t j = 0; j < kPreBlk; j++) {   // this thread's workgroups' events, in order
+        const uint32_t b = b0 + j;
+        if (b >= b1) break;
+        for (uint32_t k = 0; k < bc[j]; k++) s_ev[off + k] = a.evblk[(size_t)b * kEvSlot + k];
+        off += bc[j];
+    }
+    if (tid == 0 && t < a.traj_cap) a.traj[t] = viol;
+    if (tid < 31u) s_gw[tid] = s_ring[(head + tid) % 31u];
+    __syncthreads();
+    uint32_t soff = is - sm, T = 0;
+    for (uint32_t w = 0; w < nwv; w++) {
+        if (w < wave) soff += s_w2[w];
+        T += s_w2[w];
+    }
+    const uint32_t nloc = a.v_end - a.v_begin;
+    uint32_t* dn = inc ? a.inc_dense + (size_t)q * nloc : nullptr;
+    // ---- (3) the events' glibc draws and colours; the slots' rows into the dense list ----
+    const CT_U16* C = reinterpret_cast<const CT_U16*>((t & 1) ? a.colors1 : a.colors0);
+    CT_U16* Cs = reinterpret_cast<CT_U16*>((t & 1) ? a.colors0 : a.colors1);
+    uint32_t v = 0, c = 0, oc = 0;
+    uint64_t r0 = 0, r1 = 0;
+    if (tid < E) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int i = 0; i < 31; i++) acc += tab[i] * s_gw[i];
+        s_raw[tid] = acc;
+        v = s_ev[tid];
+        c = (acc >> 1) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+        oc = C[v];
+        if (inc) {
+            r0 = a.row_off[v - a.v_begin];
+            r1 = a.row_off[v - a.v_begin + 1];
+        }
+    }
+    if (inc) {
+        const uint32_t es = 2u + a.inc_slot, ws = 2u + a.inc_wslot_n;
+#pragma unroll
+        for (uint32_t j = 0; j < kPreSlots; j++) {
+            const uint32_t i = s0 + j;
+            if (i >= s1) break;
+            const uint32_t n = q ? sc[1][j] : sc[0][j];
+            const uint32_t* sl = i < nb ? a.inc_eslot + ((size_t)q * nb + i) * es
+                                        : a.inc_wslot + ((size_t)q * kIncWalkSlots + (i - nb)) * ws;
+            for (uint32_t k = 0; k < n; k++) dn[soff + k] = sl[2 + k];
+            soff += n;
+        }
+    }
+    __syncthreads();   // s_raw complete
+    uint32_t nwin = 0;
+    if (tid < 31u) nwin = (E < 31u && tid < 31u - E) ? s_gw[E + tid] : s_raw[E + tid - 31u];
+    if (tid < E) {
+        Cs[v] = (CT_U16)c;
+        if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
+        if (a.taboo != nullptr) a.taboo[v - a.v_begin] = (c == oc) ? a.tabooIteration : 0u;
+        if (inc && c != oc) {   // the replay's changed rows go straight after the slots' in the dense list
+            const uint32_t l = v - a.v_begin, deg = (uint32_t)(r1 - r0);
+            if (deg > a.inc_hub_arcs) {
+                a.inc_hub[(size_t)q * nloc + atomicAdd(&a.inc[kIncHubN + q], 1u)] = l;
+                atomicAdd(&s_cc[2], 1u);
+            } else {
+                dn[T + atomicAdd(&s_cc[0], 1u)] = l;
+            }
+            atomicAdd(&s_cc[1], deg);
+        }
+    }
+    if (tid < 31u) st->glibc_ring[tid] = nwin;
+    if (tid == 0) {
+        st->glibc_head = 0;
+        st->glibc_draws = draws0 + E;
+        st->x_t = minstd_mulmod(x_t, a.aN);
+        st->t = t + 1;
+        st->viol = 0;
+        st->ev_count = 0;
+        st->arrive = 0;
+        st->arrive_viol = 0;
+    }
+    if (!inc) return true;
+    // ---- (4) the next sweep's mode and the statistics ----
+    if (tid < 4u) s_q[tid] = stq;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long ar = s_cc[1];
+        for (uint32_t w = 0; w < nwv; w++) ar += s_arcs[w];
+        a.inc[kIncDenseN + q] = T + s_cc[0];
+        const unsigned long long rows = (unsigned long long)T + s_cc[0] + s_cc[2] + (q ? cw[4] : cw[3]);
+        unsigned long long* sst = reinterpret_cast<unsigned long long*>(a.inc + kIncStat);
+        sst[0] = s_q[0] + (cw[0] ? 0ull : 1ull);
+        sst[1] = s_q[1] + (cw[0] ? 1ull : 0ull);
+        sst[2] = s_q[2] + rows;
+        sst[3] = s_q[3] + ar;
+        a.inc[kIncMode] = ((q ? cw[2] : cw[1]) || ar > a.inc_thresh) ? 1u : 0u;
+    }
+    return true;
+}
+
 // Stand-alone commit (the wide sweep; MCMC_FUSED_COMMIT=0 A/B builds): same control, own launch.
 // NT threads: the wide sweep's hundreds of events per sweep rank-sort faster on 1024.
 template <typename CT, int NT = kCommitThreads>
@@ -654,6 +857,9 @@ __global__ __launch_bounds__(NT) void commit_kernel(SweepArgs a) {
     DevState* st = a.st;
     MCMC_COMMIT_PHASE(a, 0);
     if (a.wcount && threadIdx.x < 4) a.wcount[threadIdx.x] = 0;   // the walk list, for the next sweep
+    if constexpr (sizeof(CT) == 2 && NT == 1024) {
+        if (a.evcnt != nullptr && !a.phase_ts && wide_commit_fast<NT>(a)) return;
+    }
     if (threadIdx.x == 0) {
         sh_done = st->done;
         sh_t = st->t;
@@ -2998,6 +3204,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.inc_wslot = a.inc_vslot + 2 * (size_t)c->evnblk * (2 + c->inc_slot);
             a.inc_cchg = a.inc_wslot + 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n);
             a.inc_dense = a.inc_cchg + 2 * (2 + (size_t)c->ev_cap);
+            a.inc_hdr = a.inc_dense + 2 * nloc;
             a.inc_slot = c->inc_slot;
             a.inc_wslot_n = c->inc_wslot_n;
             a.inc_hub_arcs = c->inc_hub_arcs;
@@ -3638,7 +3845,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             c->inc_wslot_n = winc == 2 ? std::min<uint32_t>(nloc, 1u << 16) : std::max<uint32_t>(1u, c->inc_slot / 2u);
             const size_t words = kIncWords + 5 * (size_t)nloc + 4 * (size_t)c->evnblk * (2 + c->inc_slot) +
                                  2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n) + 2 * (2 + (size_t)c->ev_cap) +
-                                 2 * (size_t)nloc;
+                                 2 * (size_t)nloc + 4 * ((size_t)c->evnblk + kIncWalkSlots);
             ew = hipMalloc(&c->inc, sizeof(uint32_t) * words);
             if (ew == hipSuccess) ew = hipMemsetAsync(c->inc, 0, sizeof(uint32_t) * words, c->stream);
             const char* dv = getenv("MCMC_WIDE_INC_DIV");

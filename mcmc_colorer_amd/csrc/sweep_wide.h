@@ -57,10 +57,8 @@ constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (n
 // kSplitMax global masks last, takes a slot and nt - 1 more tasks (count + xbase[slot] ...), its
 // arcs dealt out split_arcs per task. wcount: [0] violators, [2..3] one 64-bit word (extra tasks,
 // slots taken) -- zeroed by the commit (the sweep's last kernel) for the next sweep.
-__device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
+__device__ __forceinline__ void push_violator_at(const SweepArgs& a, uint32_t l, uint32_t idx, uint64_t deg) {
     const uint32_t nloc = a.v_end - a.v_begin;
-    const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
-    const uint32_t idx = atomicAdd(&a.wcount[0], 1u);
     uint32_t slot = 0xFFFFFFFFu;
     if (deg > a.split_arcs) {
         const uint32_t nx = (uint32_t)((deg + a.split_arcs - 1) / a.split_arcs) - 1u;
@@ -76,12 +74,47 @@ __device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
     a.wlist[idx] = a.v_begin + l;
     a.wlist[nloc + idx] = slot;
 }
+__device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
+    push_violator_at(a, l, atomicAdd(&a.wcount[0], 1u), a.row_off[l + 1] - a.row_off[l]);
+}
 __device__ __forceinline__ void flag_violator(const SweepArgs& a, uint32_t l, uint32_t) {
     if (a.wflag[l]) return;
     const uint32_t bit = 1u << (8u * (l & 3u));
     if (atomicOr(reinterpret_cast<uint32_t*>(a.wflag) + (l >> 2), bit) & bit) return;
     if (a.taboo != nullptr && a.taboo[l] > 0) return;
     push_violator(a, l);
+}
+// flag_violator for up to two rows per lane of a wave (l0 where want0, l1 where want1; all lanes
+// call it): the flag atomics and the rows' offsets are issued side by side, and the walk list's slots
+// are taken by ONE counter atomic per wave -- a device-scope atomic on one word serialises at ~90 per
+// us, and a chain of dependent round trips per flagged row made a sweep with 11 000 violators' scan
+// ~60 us slower than a converged one.
+__device__ __forceinline__ void flag_violators_wave(const SweepArgs& a, uint32_t l0, bool want0, uint32_t l1 = 0,
+                                                    bool want1 = false) {
+    if (!__ballot(want0 || want1)) return;
+    bool first0 = false, first1 = false;
+    uint64_t d0 = 0, d1 = 0;
+    if (want0) {
+        const uint32_t bit = 1u << (8u * (l0 & 3u));
+        first0 = (atomicOr(reinterpret_cast<uint32_t*>(a.wflag) + (l0 >> 2), bit) & bit) == 0u;
+        d0 = a.row_off[l0 + 1] - a.row_off[l0];
+    }
+    if (want1) {
+        const uint32_t bit = 1u << (8u * (l1 & 3u));
+        first1 = (atomicOr(reinterpret_cast<uint32_t*>(a.wflag) + (l1 >> 2), bit) & bit) == 0u;
+        d1 = a.row_off[l1 + 1] - a.row_off[l1];
+    }
+    const bool push0 = first0 && !(a.taboo != nullptr && a.taboo[l0] > 0);
+    const bool push1 = first1 && !(a.taboo != nullptr && a.taboo[l1] > 0);
+    const uint64_t m0 = __ballot(push0), m1 = __ballot(push1);
+    if ((m0 | m1) == 0) return;
+    const int lane = (int)(threadIdx.x & 63u), lead = __ffsll((long long)(m0 | m1)) - 1;
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&a.wcount[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
+    base = __shfl(base, lead, 64);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if (push0) push_violator_at(a, l0, base + (uint32_t)__popcll(m0 & below), d0);
+    if (push1) push_violator_at(a, l1, base + (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & below), d1);
 }
 // One end of a monochromatic kept edge in a full scan: its row's same-colour count (incremental
 // contexts) and its flag.
@@ -151,6 +184,8 @@ __device__ __forceinline__ void inc_own(const SweepArgs& a, uint32_t v, int dv, 
     const uint32_t old = atomicAdd(&a.inc_vcnt[v], (uint32_t)dv);
     if (dv > 0 && old == 0u) inc_touch(a, v, t);
 }
+constexpr uint32_t kIncHubLds = 1024;   // hubs whose tasks a workgroup scans in LDS (more: a workgroup each)
+constexpr uint32_t kIncHubTask = 4096;  // arcs per hub task (4 per thread of a 1024-thread workgroup)
 __global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
     DevState* st = a.st;
     if (a.check_done && st->done) return;
@@ -170,13 +205,54 @@ __global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
     }
     const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);   // C_t
     const uint16_t* __restrict__ Cp = reinterpret_cast<const uint16_t*>(p ? a.colors0 : a.colors1);   // C_t-1
-    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t nh = ctl[kIncHubN + p];
-    for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {   // hubs: a workgroup each
-        const uint32_t v = a.inc_hub[(size_t)p * nloc + h];
-        int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + threadIdx.x, a.row_off[v + 1], blockDim.x, t);
-        for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
-        if (lane == 0) inc_own(a, v, dv, t);
+    if (nh > 0 && nh <= kIncHubLds) {
+        // hubs cut into tasks of kIncHubTask arcs over the grid (one hub of C5's 29 438 arcs is 8
+        // tasks, not one workgroup's 29 dependent steps): every workgroup scans the hubs' task counts
+        __shared__ uint32_t s_pre[kIncHubLds], s_v[kIncHubLds], s_w[16];
+        uint32_t nt = 0, hv = 0;
+        if (threadIdx.x < nh) {
+            hv = a.inc_hub[(size_t)p * nloc + threadIdx.x];
+            nt = (uint32_t)((a.row_off[hv + 1] - a.row_off[hv] + kIncHubTask - 1) / kIncHubTask);
+        }
+        uint32_t in = nt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(in, o, 64);
+            if (lane >= (uint32_t)o) in += y;
+        }
+        if (lane == 63u) s_w[wave] = in;
+        __syncthreads();
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64u; k++) {
+            if (k < wave) in += s_w[k];
+            tot += s_w[k];
+        }
+        if (threadIdx.x < nh) {
+            s_pre[threadIdx.x] = in;   // inclusive: tasks of hubs 0..threadIdx.x
+            s_v[threadIdx.x] = hv;
+        }
+        __syncthreads();
+        for (uint32_t task = blockIdx.x; task < tot; task += gridDim.x) {
+            uint32_t lo = 0, hi = nh - 1u;   // the first hub whose inclusive count passes task
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[mid] > task) hi = mid; else lo = mid + 1u;
+            }
+            const uint32_t v = s_v[lo], c = task - (lo ? s_pre[lo - 1u] : 0u);
+            const uint64_t rb = a.row_off[v] + (uint64_t)c * kIncHubTask;
+            const uint64_t re = min<uint64_t>(a.row_off[v + 1], rb + kIncHubTask);
+            int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], rb + threadIdx.x, re, blockDim.x, t);
+            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+            if (lane == 0) inc_own(a, v, dv, t);
+        }
+    } else {
+        for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {   // many hubs: a workgroup each
+            const uint32_t v = a.inc_hub[(size_t)p * nloc + h];
+            int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + threadIdx.x, a.row_off[v + 1], blockDim.x, t);
+            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+            if (lane == 0) inc_own(a, v, dv, t);
+        }
     }
     // other rows (the commit gathered them into one dense list): a wave each
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6, nd = ctl[kIncDenseN + p];
@@ -206,24 +282,32 @@ __device__ void wide_inc_flags(const SweepArgs& a, uint32_t t) {
             if (a.fp_live) fpn[v] = fp[v];
         }
     }
+    const uint32_t lane = threadIdx.x & 63u, tw = tid & ~63u;   // wave-uniform loops (flag_violators_wave)
     if (ctl[kIncTchOvf + p]) {
-        for (uint32_t l = tid; l < nloc; l += nthr)
-            if ((int32_t)a.inc_vcnt[l] > 0) flag_violator(a, l, t);
+        for (uint32_t l0 = tw; l0 < nloc; l0 += nthr) {
+            const uint32_t l = l0 + lane;
+            flag_violators_wave(a, l < nloc ? l : 0u, l < nloc && (int32_t)a.inc_vcnt[l] > 0);
+        }
         return;
     }
     // candidates: the violators of C_t-1 (the evaluation's slots of sweep t-1) and the touched rows
     const uint32_t vs = 2u + a.inc_slot, nv = a.evnblk * a.inc_slot, ntc = ctl[kIncTch + p];
-    for (uint32_t i = tid; i < nv + ntc; i += nthr) {
-        uint32_t l;
+    for (uint32_t i0 = tw; i0 < nv + ntc; i0 += nthr) {
+        const uint32_t i = i0 + lane;
+        uint32_t l = 0;
+        bool cand = false;
         if (i < nv) {
             const uint32_t* sl = a.inc_vslot + ((size_t)(p ^ 1u) * a.evnblk + i / a.inc_slot) * vs;
             const uint32_t k = i % a.inc_slot;
-            if (k >= min(sl[0], a.inc_slot)) continue;
-            l = sl[2 + k];
-        } else {
+            if (k < min(sl[0], a.inc_slot)) {
+                l = sl[2 + k];
+                cand = true;
+            }
+        } else if (i < nv + ntc) {
             l = a.inc_tch[(size_t)p * nloc + (i - nv)];
+            cand = true;
         }
-        if ((int32_t)a.inc_vcnt[l] > 0) flag_violator(a, l, t);
+        flag_violators_wave(a, l, cand && (int32_t)a.inc_vcnt[l] > 0);
     }
 }
 
@@ -465,12 +549,20 @@ __global__ __launch_bounds__(kTscanThreads, 4) void wide_tscan_kernel(SweepArgs 
         }
         __syncthreads();
         const uint32_t nc = min(ncand, kTsCand);
-        for (uint32_t k = threadIdx.x; k < nc; k += blockDim.x) {   // the candidates: compare colours
-            const uint2 rc = cand[k];
-            if (C[(vb + rc.x)] == C[rc.y]) {
-                mono_end(a, rc.x, t);
-                if (a.xs_sym && rc.y - vb < nloc) mono_end(a, rc.y - vb, t);
+        for (uint32_t k0 = threadIdx.x & ~63u; k0 < nc; k0 += blockDim.x) {   // the candidates: compare colours
+            const uint32_t k = k0 + lane;
+            uint2 rc = make_uint2(0u, 0u);
+            bool mono = false;
+            if (k < nc) {
+                rc = cand[k];
+                mono = C[(vb + rc.x)] == C[rc.y];
             }
+            const bool other = mono && a.xs_sym && rc.y - vb < nloc;
+            if (a.inc_vcnt != nullptr) {
+                if (mono) atomicAdd(&a.inc_vcnt[rc.x], 1u);
+                if (other) atomicAdd(&a.inc_vcnt[rc.y - vb], 1u);
+            }
+            flag_violators_wave(a, rc.x, mono, other ? rc.y - vb : 0u, other);
         }
         __syncthreads();
         if (threadIdx.x == 0) ncand = 0;
@@ -641,7 +733,11 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     uint32_t* islot = a.inc ? a.inc_wslot + ((size_t)((t + 1u) & 1u) * kIncWalkSlots + b) * (2u + a.inc_wslot_n)
                             : nullptr;
     if (b >= T) {
-        if (islot != nullptr && threadIdx.x == 0) islot[0] = islot[1] = 0;
+        if (islot != nullptr && threadIdx.x == 0) {
+            islot[0] = islot[1] = 0;
+            uint32_t* hd = a.inc_hdr + ((size_t)((t + 1u) & 1u) * (a.evnblk + kIncWalkSlots) + a.evnblk + b) * 2u;
+            hd[0] = hd[1] = 0;
+        }
         return;
     }
     if (threadIdx.x == 0) ic[0] = ic[1] = 0;   // (read after the tasks' barriers)
@@ -702,6 +798,9 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     if (islot != nullptr && threadIdx.x == 0) {   // thread 0 made every entry (walk_finish's lane 0)
         islot[0] = ic[0];
         islot[1] = ic[1];
+        uint32_t* hd = a.inc_hdr + ((size_t)((t + 1u) & 1u) * (a.evnblk + kIncWalkSlots) + a.evnblk + b) * 2u;
+        hd[0] = ic[0];
+        hd[1] = ic[1];
     }
 }
 
@@ -841,6 +940,9 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         if (islot != nullptr) {   // slot headers, written every sweep
             islot[0] = sh_ic[0];
             islot[1] = sh_ic[1];
+            uint32_t* hd = a.inc_hdr + ((size_t)((t + 1u) & 1u) * (a.evnblk + kIncWalkSlots) + eb) * 2u;
+            hd[0] = sh_ic[0];
+            hd[1] = sh_ic[1];
             vslot[0] = sh_ic[2];
             vslot[1] = 0;
         }

@@ -211,10 +211,9 @@ def test_wide_forced_small_ncol(M, monkeypatch, ncol, eps, taboo):
     run_both(M, off, idx, ncol, epsilon=eps, tabooIteration=taboo, maxRip=60)
 
 
-def _hub_graph():
-    """A hub joined to 4000 vertices plus a sparse remainder: one long row, many empty/short ones."""
+def _hub_graph(n=5000):
+    """A hub joined to n - 1000 vertices plus a sparse remainder: one long row, many empty/short ones."""
     rng = np.random.default_rng(5)
-    n = 5000
     E = set()
     for v in range(1, n):
         E.add((0, v))
@@ -222,7 +221,7 @@ def _hub_graph():
         a, b = rng.integers(1, n, 2)
         if a != b:
             E.add((min(a, b), max(a, b)))
-    for v in range(4000, n):   # isolated tail: drop the hub arcs too
+    for v in range(n - 1000, n):   # isolated tail: drop the hub arcs too
         E.discard((0, v))
     arcs = sorted([(a, b) for a, b in E] + [(b, a) for a, b in E])
     src = np.array([a for a, _ in arcs], dtype=np.int64)
@@ -247,6 +246,7 @@ INC_CASES = {
     "rmat-maxdeg": ("rmat", None, {}, {}),
     "rmat-300": ("rmat", 300, {"maxRip": 25}, {}),
     "hub": ("hub", 300, {"maxRip": 30}, {}),
+    "big-hub": ("bighub", 300, {"maxRip": 30}, {}),   # a 10 999-arc hub: three delta tasks (kIncHubTask)
     "sparse-taboo": ("sparse", 1000, {"tabooIteration": 2, "maxRip": 40}, {}),
     "sparse-eps": ("sparse", 700, {"epsilon": 1e-3, "maxRip": 40}, {}),
     "dense-all-change": ("dense", 16, {"maxRip": 30}, {"MCMC_GATHER": "wide"}),
@@ -271,6 +271,8 @@ def test_wide_incremental_counts(M, monkeypatch, mode, case):
         off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
     elif graph == "hub":
         off, idx = _hub_graph()
+    elif graph == "bighub":
+        off, idx = _hub_graph(12000)
     elif graph == "sparse":
         O.srand(1)
         off, idx = O.setup_rnd2(3000, 0.01)
