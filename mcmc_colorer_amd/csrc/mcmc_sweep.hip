@@ -225,12 +225,11 @@ constexpr uint32_t kIncStat = 16;    // u64 [4]: incremental sweeps, full sweeps
 constexpr uint32_t kIncWords = 24;
 constexpr uint32_t kIncWalkSlots = 1024;   // = kWalkBlocks (sweep_wide.h)
 
-// Row l changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1], bumped by
-// the caller's LDS counters), or the hub list. Returns the row's arcs.
-__device__ __forceinline__ uint32_t inc_list(const SweepArgs& a, uint32_t l, uint32_t t, uint32_t* slot,
-                                             uint32_t cap, uint32_t* lcount) {
+// Row l (deg arcs) changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1],
+// bumped by the caller's LDS counters), or the hub list. Returns deg.
+__device__ __forceinline__ uint32_t inc_list_deg(const SweepArgs& a, uint32_t l, uint32_t t, uint32_t* slot,
+                                                 uint32_t cap, uint32_t* lcount, uint32_t deg) {
     const uint32_t q = (t + 1u) & 1u;
-    const uint32_t deg = (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
     if (deg > a.inc_hub_arcs) {
         a.inc_hub[(size_t)q * (a.v_end - a.v_begin) + atomicAdd(&a.inc[kIncHubN + q], 1u)] = l;
     } else {
@@ -239,6 +238,10 @@ __device__ __forceinline__ uint32_t inc_list(const SweepArgs& a, uint32_t l, uin
         else a.inc[kIncOvf + q] = 1u;
     }
     return deg;
+}
+__device__ __forceinline__ uint32_t inc_list(const SweepArgs& a, uint32_t l, uint32_t t, uint32_t* slot,
+                                             uint32_t cap, uint32_t* lcount) {
+    return inc_list_deg(a, l, t, slot, cap, lcount, (uint32_t)(a.row_off[l + 1] - a.row_off[l]));
 }
 
 // The commit's end of sweep t (all its threads): its own slot's header, the rows and arcs every

@@ -47,6 +47,7 @@ constexpr uint32_t kSplitArcs = 2048;     // arcs per task of a split walk (Swee
 #define MCMC_WALK_BLOCKS 1024   // 4 per CU: the violator-heavy C5 sweep 0.44 -> 0.32 ms (256 / 512 / 1024 measured), none idle when converged
 #endif
 constexpr uint32_t kWalkBlocks = MCMC_WALK_BLOCKS;   // walk workgroups beside the evaluation
+static_assert(kWalkBlocks == kIncWalkSlots, "one incremental-count slot per walk workgroup");
 constexpr uint32_t kSplitMax = 64;        // violators with a global occupancy mask (split walks)
 constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
 
@@ -629,14 +630,18 @@ __device__ __forceinline__ void walk_gather(const SweepArgs& a, const uint16_t* 
     }
 }
 
+// A workgroup barrier for LDS hand-offs only: the walks' global loads and stores stay in flight
+// across it (__syncthreads waits for every outstanding one: with the loaded latency of a sweep full of
+// random gathers, each such wait costs microseconds).
+__device__ __forceinline__ void walk_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // The resample of violator v (fill_p case (ii) / (i)) from its occupancy mask in LDS, by a whole
-// 256-thread workgroup: word prefix counts, then one wave walks them. `ev` (LDS list + count,
-// capacity cap): where an overflow event goes; past cap, or with ev == nullptr, the global list.
-// All threads call it; it ends with a barrier.
-__device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
+// 256-thread workgroup: word prefix counts, then one wave walks them. cv = C_t[v] and x = u_v's
+// minstd state come in (loaded beside the task's first loads); deg = v's arcs. Overflow events go
+// to the global list. All threads call it; it ends with an LDS barrier.
+__device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t cv, uint32_t x, uint32_t deg,
                             uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* wsum,
-                            uint32_t* ev, uint32_t* nev, uint32_t cap, uint32_t* islot = nullptr,
-                            uint32_t* ic = nullptr) {
+                            uint32_t* islot, uint32_t* ic) {
     DevState* st = a.st;
     const uint32_t NWW = (a.nCol + 31u) >> 5;
     const uint32_t per = (NWW + kWideWalkThreads - 1u) / kWideWalkThreads;   // words per thread (prefix)
@@ -652,7 +657,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         if (lane >= (uint32_t)o) inc += y;
     }
     if (lane == 63u) wsum[wave] = inc;
-    __syncthreads();
+    walk_sync();
     uint32_t run = inc - s;
     for (uint32_t k = 0; k < wave; k++) run += wsum[k];
     for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
@@ -664,11 +669,9 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         for (uint32_t k = 0; k < kWideWalkThreads / 64; k++) T += wsum[k];
         pre[NWW] = T;
     }
-    __syncthreads();
+    walk_sync();
     if (wave == 0) {   // the walk: one wave, all lanes in step (walk_mask_pre ballots)
         const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
-        const uint32_t cv = C[v];
-        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)v + 1));
         const float u = minstd_canonical(x);
         uint32_t nc;
         if (Zvcomp > 0) {   // case (ii)
@@ -680,46 +683,30 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         if (lane == 0) {
             const bool event = nc == a.nCol;
             const uint32_t nv = event ? cv : nc;
-            // an incremental sweep's C_t+1 buffer already holds C_t here (wide_inc_flag_kernel)
+            // an incremental sweep's C_t+1 buffer already holds C_t here (wide_inc_flags)
             if (nv != cv || a.inc == nullptr || a.inc[kIncMode]) {
                 Cs[v] = (uint16_t)nv;
                 if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
             }
-            if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list(a, l, t, islot, a.inc_wslot_n, &ic[0]));
+            if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
             if (event) {
-                const uint32_t k = ev ? atomicAdd(nev, 1u) : cap;
-                if (k < cap) {
-                    ev[k] = v;
-                } else {
-                    const uint32_t idx = atomicAdd(&st->ev_count, 1u);
-                    if (idx < a.ev_cap) a.events[idx] = v;
-                    else atomicOr(&st->err, 1u);
-                }
+                const uint32_t idx = atomicAdd(&st->ev_count, 1u);
+                if (idx < a.ev_cap) a.events[idx] = v;
+                else atomicOr(&st->err, 1u);
             }
         }
     }
-    __syncthreads();
-}
-
-// One violator's whole resample by one workgroup.
-__device__ void walk_violator(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t x_t, const uint16_t* __restrict__ C,
-                              uint16_t* __restrict__ Cs, uint32_t* mask, uint32_t* pre, uint32_t* wsum, uint32_t* ev,
-                              uint32_t* nev, uint32_t cap, uint32_t* islot, uint32_t* ic) {
-    const uint32_t NWW = (a.nCol + 31u) >> 5;
-    const uint32_t l = v - a.v_begin;
-    for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
-    __syncthreads();
-    walk_gather(a, C, mask, a.row_off[l], a.row_off[l + 1]);
-    __syncthreads();
-    walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, ev, nev, cap, islot, ic);
+    walk_sync();
 }
 
 // The walk workgroups of the evaluation launch: tasks b, b + nb, ... (push_violator). A one-task
 // violator: its whole occupancy mask and walk here. A split violator (a hub, whose gathers would
 // otherwise be one workgroup's serial latency chain): each task ORs its part of the occupancy into
 // the slot's global mask, and the workgroup finishing the last task takes the mask back
-// (atomicExch: read and clear for the next sweep) and walks.
+// (atomicExch: read and clear for the next sweep) and walks. Software-pipelined: the next task's list
+// entry is loaded beside this task's row offsets, own colour and first gathers, and LDS hand-offs
+// use walk_sync, so a task costs its offsets, ids and colours round trips (~3), not ~7.
 __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t t, uint32_t x_t) {
     __shared__ uint32_t mask[kWideMaskWords];
     __shared__ uint32_t pre[kWideMaskWords + 1];
@@ -740,7 +727,9 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         }
         return;
     }
-    if (threadIdx.x == 0) ic[0] = ic[1] = 0;   // (read after the tasks' barriers)
+    if (threadIdx.x == 0) ic[0] = ic[1] = 0;   // (only thread 0 uses them)
+    const unsigned long long ts0 = a.phase_ts ? wall_clock64() : 0ull;   // diagnostics (MCMC_PHASE_DUMP)
+    uint32_t ntask = 0, nsplit = 0;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t NWW = (a.nCol + 31u) >> 5;
@@ -748,52 +737,83 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     const uint32_t* sidx = a.gdone + kSplitMax;
     const uint32_t* xbase = a.gdone + 2 * kSplitMax;
     const uint32_t SA = a.split_arcs;
-    for (uint32_t task = b; task < T; task += nb) {
-        uint32_t idx, c = 0;
+    // task -> (list index, chunk); false past the last live split slot
+    auto decode = [&](uint32_t task, uint32_t& idx, uint32_t& c) -> bool {
+        c = 0;
         if (task < cnt) {
             idx = task;
-        } else {   // extra task j: the slot with the last xbase <= j
-            const uint32_t j = task - cnt;
-            if (ns == 0) break;
-            uint32_t lo = 0, hi = ns;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (xbase[mid] <= j) lo = mid;
-                else hi = mid;
-            }
-            idx = sidx[lo];
-            c = j - xbase[lo] + 1u;
+            return true;
         }
-        const uint32_t v = a.wlist[idx], slot = a.wlist[nloc + idx], l = v - a.v_begin;
-        if (slot == 0xFFFFFFFFu) {
-            walk_violator(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0, islot, ic);
-            continue;
+        const uint32_t j = task - cnt;   // extra task j: the slot with the last xbase <= j
+        if (ns == 0) return false;
+        uint32_t lo = 0, hi = ns;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (xbase[mid] <= j) lo = mid;
+            else hi = mid;
         }
+        idx = sidx[lo];
+        c = j - xbase[lo] + 1u;
+        return true;
+    };
+    uint32_t idx = 0, c = 0;
+    bool live = decode(b, idx, c);
+    uint32_t v = live ? a.wlist[idx] : 0u, slot = live ? a.wlist[nloc + idx] : 0u;
+    for (uint32_t task = b; live && task < T; task += nb) {
+        const uint32_t l = v - a.v_begin;
+        // this task's offsets, own colour and u_v; the next task's list entry (side by side)
         const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
-        const uint32_t nt = (uint32_t)((re - rb + SA - 1) / SA);
-        if (c >= nt) continue;   // an extra task of a slotless split violator
-        uint32_t* gm = a.gmask + (size_t)slot * kWideMaskWords;
-        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
-        __syncthreads();
-        walk_gather(a, C, mask, rb + (uint64_t)c * SA, min<uint64_t>(re, rb + (uint64_t)(c + 1) * SA));
-        __syncthreads();
-        for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x)
-            if (mask[w]) atomicOr(&gm[w], mask[w]);
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t done = atomicAdd(&a.gdone[slot], 1u) + 1u;
-            sh_last = done == nt;
-            if (done == nt) a.gdone[slot] = 0;   // every task of this sweep has counted
+        const uint32_t cv = C[v];
+        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)v + 1));
+        uint32_t nidx = 0, nc = 0;
+        const bool nlive = task + nb < T && decode(task + nb, nidx, nc);
+        const uint32_t nv = nlive ? a.wlist[nidx] : 0u, nslot = nlive ? a.wlist[nloc + nidx] : 0u;
+        ntask++;
+        if (slot == 0xFFFFFFFFu) {   // one task: the whole row
+            for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
+            walk_sync();
+            walk_gather(a, C, mask, rb, re);
+            walk_sync();
+            walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
+        } else {
+            const uint32_t ntk = (uint32_t)((re - rb + SA - 1) / SA);
+            nsplit++;
+            if (c < ntk) {   // (else: an extra task of a slotless split violator)
+                uint32_t* gm = a.gmask + (size_t)slot * kWideMaskWords;
+                for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
+                walk_sync();
+                walk_gather(a, C, mask, rb + (uint64_t)c * SA, min<uint64_t>(re, rb + (uint64_t)(c + 1) * SA));
+                walk_sync();
+                for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x)
+                    if (mask[w]) atomicOr(&gm[w], mask[w]);
+                __threadfence();
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    const uint32_t done = atomicAdd(&a.gdone[slot], 1u) + 1u;
+                    sh_last = done == ntk;
+                    if (done == ntk) a.gdone[slot] = 0;   // every task of this sweep has counted
+                }
+                __syncthreads();
+                if (sh_last) {
+                    __threadfence();
+                    for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
+                    walk_sync();
+                    walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
+                }
+                walk_sync();   // sh_last and mask are reused by the next task
+            }
         }
-        __syncthreads();
-        if (sh_last) {
-            __threadfence();
-            for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
-            __syncthreads();
-            walk_finish(a, v, t, x_t, C, Cs, mask, pre, wsum, nullptr, nullptr, 0, islot, ic);
-        }
-        __syncthreads();   // sh_last and mask are reused by the next task
+        live = nlive;
+        idx = nidx;
+        c = nc;
+        v = nv;
+        slot = nslot;
+    }
+    if (a.phase_ts && threadIdx.x == 0) {   // walk workgroup b: start, end, tasks, split tasks
+        a.phase_ts[b * 8u + 0] = ts0;
+        a.phase_ts[b * 8u + 1] = wall_clock64();
+        a.phase_ts[b * 8u + 2] = ntask;
+        a.phase_ts[b * 8u + 3] = nsplit;
     }
     if (islot != nullptr && threadIdx.x == 0) {   // thread 0 made every entry (walk_finish's lane 0)
         islot[0] = ic[0];

@@ -1,0 +1,44 @@
+"""Per-workgroup walk timings of the violator-heavy C5 sweep (nCol = maxDeg / 4, sweep 0 from C_0):
+MCMC_PHASE_DUMP stamps of the wide evaluation launch's walk workgroups (start, end, tasks, split tasks)."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    out = sys.argv[1]
+    os.environ["MCMC_PHASE_DUMP"] = out
+    import torch
+
+    torch.cuda.init()
+    import mcmc_colorer_amd.colorer as M
+    from mcmc_colorer_amd._lib import check, lib
+
+    g = M.Graph.rmat(22, 10, 0.5, 0.2, 0.2, 1)
+    nc = max(257, g.getMaxNodeDeg() // 4)
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=nc, maxRip=0x7FFFFFF0))
+    col.init(0)
+    tot, ker = ctypes.c_double(), ctypes.c_double()
+    check(lib().mcmc_bench_sweeps(col._ctx, 1, ctypes.byref(tot), ctypes.byref(ker)))
+    print(f"sweep 0: {ker.value * 1e3:.1f} us (phase stamps on)")
+    t = np.fromfile(out, dtype=np.uint64).reshape(-1, 8).astype(np.int64)[:1024]
+    live = t[t[:, 0] > 0]
+    d = (live[:, 1] - live[:, 0]) / 100.0
+    print(f"walk workgroups with tasks: {len(live)}; duration us: min {d.min():.1f} med {np.median(d):.1f} "
+          f"p90 {np.percentile(d, 90):.1f} max {d.max():.1f}; tasks per wg med {np.median(live[:, 2]):.0f} max {live[:, 2].max()}; "
+          f"split tasks total {live[:, 3].sum()}")
+    st = (live[:, 0] - live[:, 0].min()) / 100.0
+    print(f"start spread: max {st.max():.1f} us")
+    i = np.argsort(-d)[:8]
+    for k in i:
+        print(f"  wg {k}: {d[k]:.1f} us, tasks {live[k, 2]}, split {live[k, 3]}, start +{st[k]:.1f}")
+    col.close()
+
+
+if __name__ == "__main__":
+    main()
