@@ -170,6 +170,8 @@ struct SweepArgs {
     uint32_t* evcnt;            // wide: their number per workgroup [nblk] (written every sweep)
     uint32_t evnblk;            // wide: evaluation workgroups
     const uint32_t* evpow;      // wide: [evnblk][4] 16807^(v + 1) of each evaluation wave's first vertex
+    const uint32_t* gpow;       // tiled: [ngroups][16] 16807^(v_begin + g R + 64 w + 1) (u_v of wave w's first row)
+    uint32_t apow_grid, apow_tile;   // tiled: 16807^(gridDim R), 16807^(64 * 16)
     uint32_t a256;              // 16807^256 mod (2^31 - 1)
     // wide: XCD-slab edge layout of the violation scan (sweep_wide.h, get_xslab); xs_ent == nullptr
     // -> the CSR arc scan
@@ -1348,8 +1350,12 @@ struct TailShared {
     uint32_t qn[2];       // tiled tail queue: entries of the two queues
 };
 
+// t0 / err0 (when t0 != ~0u): the sweep's t and the error word as every workgroup read them at its
+// start; the error word changes during a sweep only where a workgroup appended overflow events, so
+// a sweep without events commits with no state load after the arrival.
 __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, TailShared& sh, uint32_t wave_viol,
-                                           uint32_t wave_ev, int lane, uint32_t* lds, uint32_t cap) {
+                                           uint32_t wave_ev, int lane, uint32_t* lds, uint32_t cap,
+                                           uint32_t t0 = ~0u, uint32_t err0 = 0u) {
     if (lane == 0) {
         if (wave_viol) atomicAdd(&sh.wg_viol, wave_viol);
         if (wave_ev) sh.wg_ev = 1u;
@@ -1382,11 +1388,12 @@ __device__ __forceinline__ void sweep_tail(const SweepArgs& a, DevState* st, Tai
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 sh.E = __hip_atomic_load(&st->ev_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sh.err = __hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 sh.E = 0;
+                sh.err = t0 != ~0u ? err0 : __hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            sh.t = st->t;
-            sh.err = __hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh.t = t0 != ~0u ? t0 : st->t;
         }
     }
     __syncthreads();
@@ -2243,11 +2250,20 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
     __shared__ TailShared sh;
     DevState* __restrict__ st = a.st;
+    // loads that depend on the launch alone go out beside the state words: the first pair's
+    // first-row bounds and (u_v) this wave's first-row power
+    const uint32_t wid0 = threadIdx.x >> 6;
+    const uint32_t gclamp = min(blockIdx.x, a.ngroups ? a.ngroups - 1u : 0u);
+    uint32_t fpos, fend, fpads;
+    tile_first_row(a, gclamp, 0, a.v_end - a.v_begin, wid0, blockDim.x >> 6, (threadIdx.x & 63u) >> a.sub_log2,
+                   fpos, fend, fpads);
+    const uint32_t gp = (!REF && a.gpow != nullptr && blockIdx.x < a.ngroups) ? a.gpow[(size_t)blockIdx.x * 16u + wid0] : 0u;
     if (a.check_done && st->done) return;
     MCMC_PHASE(a, 0);
     if (threadIdx.x == 0) { sh.wg_viol = 0; sh.wg_ev = 0; sh.viol = 0; }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
+    const uint32_t err0 = st->err;
     uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * (a.v_end - a.v_begin) : nullptr;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
@@ -2298,12 +2314,15 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     // u_v (evaluation): xg = x_t 16807^(v_begin + g R + 64 wid + 1), the draw of this wave's first
     // evaluation row in group g; xsg advances it by one group of this workgroup, xsk by one tile
     uint32_t xg = 0, xsg = 0, xsk = 0;
-    if (!REF) {
+    if (!REF && a.gpow != nullptr && nwaves == 16u) {   // host-computed (create_impl)
+        xg = minstd_mulmod(x_t, gp);
+        xsg = a.apow_grid;
+        xsk = a.apow_tile;
+    } else if (!REF) {
         xg = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + (uint64_t)g * R + 64u * wid + 1u));
         xsg = minstd_pow_tab((uint64_t)gridDim.x * R);
         xsk = minstd_pow_tab(64u * (uint64_t)nwaves);
     }
-    const uint32_t gclamp = min(g, a.ngroups ? a.ngroups - 1u : 0u);
     for (uint32_t i = threadIdx.x; i < R * NW; i += blockDim.x) smask[i] = 0;
     if (threadIdx.x == 0) {
         sh.cursor[0] = nwaves * nsub;
@@ -2341,9 +2360,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         if (RS) tile_dma_slice(a, C, 1, lds0 + SB, wid, nwaves, lane);   // block 1's slice, resident too
         if (REF && !RES) tile_dma_own(a, C, g, lds_addr(own_base), wid, nwaves, lane);
     }
-    // the first pair's first quads (bounds from the global table), then the resident replica
-    uint32_t fpos, fend, fpads;
-    tile_first_row(a, gclamp, 0, nloc, wid, nwaves, sub, fpos, fend, fpads);
+    // the first pair's first quads (bounds loaded at the top), then the resident replica
     fpos += 8u * li;
     __amdgpu_buffer_rsrc_t gr = tile_group_rsrc(a, gclamp);
     const uint16_t* __restrict__ gcol = a.tcol + a.gbase[gclamp];
@@ -2788,7 +2805,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
         sweep_tail_ref(a, st, sh, (unsigned long long)x, lane);
     } else {
-        sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap);
+        sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(lds_raw), a.lds_sort_cap, t, err0);
     }
     MCMC_PHASE(a, 4);
 }
@@ -3027,6 +3044,8 @@ struct mcmc_ctx {
     uint32_t* evcnt = nullptr;
     uint32_t evnblk = 0;
     uint32_t* evpow = nullptr;      // per evaluation wave: 16807^(first vertex + 1) (host-computed)
+    uint32_t* gpow = nullptr;       // tiled: per (group, wave) the same (host-computed)
+    uint32_t apow_grid = 0, apow_tile = 0;
     const XSlabLayout* xs = nullptr;   // wide: XCD-slab edge layout (graph-owned; nullptr: CSR arc scan)
     // wide: incremental violation counts (sweep_wide.h wide_inc_*; nullptr: the tile scan every sweep)
     uint32_t* inc = nullptr;        // kIncWords control words, then counts, lists and slots (make_args)
@@ -3160,6 +3179,9 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.sub_log2 = c->sub_log2;
         a.slice_bytes = c->slice_bytes;
         a.seg_buf_bytes = (tseg_stride(c->tl->grp_rows) * 4u + 1023u) & ~1023u;
+        a.gpow = c->gpow;
+        a.apow_grid = c->apow_grid;
+        a.apow_tile = c->apow_tile;
     }
     if (c->wide) {
         a.arc_begin = c->arc_begin;
@@ -3628,6 +3650,20 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         int rs = get_tiled_layout(const_cast<mcmc_graph*>(g), v_begin, v_end, R, c->block_log2, c->stream, &c->tl);
         if (rs) { mcmc_destroy(c); return rs; }
         R = c->tl->grp_rows;   // a generated graph's layout brings its own group size
+        if (!ref && c->block.x == 1024) {   // u_v's skip-ahead per (group, wave) and per step, once
+            std::vector<uint32_t> pw((size_t)c->tl->ngroups * 16u);
+            for (size_t i = 0; i < pw.size(); i++)
+                pw[i] = minstd_pow(kMinstdA, (uint64_t)v_begin + (uint64_t)(i / 16) * R + 64ull * (i % 16) + 1ull);
+            c->apow_grid = minstd_pow(kMinstdA, (uint64_t)c->grid.x * R);
+            c->apow_tile = minstd_pow(kMinstdA, 64ull * 16ull);
+            hipError_t ep = pw.empty() ? hipSuccess : hipMalloc(&c->gpow, sizeof(uint32_t) * pw.size());
+            if (ep == hipSuccess && !pw.empty())
+                ep = hipMemcpy(c->gpow, pw.data(), sizeof(uint32_t) * pw.size(), hipMemcpyHostToDevice);
+            if (ep != hipSuccess) {
+                mcmc_destroy(c);
+                return fail(MCMC_E_HIP, std::string("group powers: ") + hipGetErrorString(ep));
+            }
+        }
         if (R > rmax) {
             mcmc_destroy(c);
             return fail(MCMC_E_ARG, "generated layout's group rows exceed this nCol's LDS budget (streaming: nCol > 64)");
@@ -4503,6 +4539,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->ftab);
     (void)hipFree(c->evcnt);
     (void)hipFree(c->evpow);
+    (void)hipFree(c->gpow);
     (void)hipFree(c->wlist);
     (void)hipFree(c->wcount);
     (void)hipFree(c->inc);
