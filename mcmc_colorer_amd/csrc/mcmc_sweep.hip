@@ -225,7 +225,10 @@ constexpr uint32_t kIncHubN = 7;     // [2] changed hubs, by parity q
 constexpr uint32_t kIncDenseN = 9;   // [2] rows in the dense list, by parity q
 constexpr uint32_t kIncStat = 16;    // u64 [4]: incremental sweeps, full sweeps, changed rows, their arcs
 constexpr uint32_t kIncWords = 24;
-constexpr uint32_t kIncWalkSlots = 1024;   // = kWalkBlocks (sweep_wide.h)
+#ifndef MCMC_WALK_BLOCKS
+#define MCMC_WALK_BLOCKS 1024   // walk workgroups of the wide evaluation launch (sweep_wide.h kWalkBlocks)
+#endif
+constexpr uint32_t kIncWalkSlots = MCMC_WALK_BLOCKS;   // one changed-row slot per walk workgroup
 
 // Row l (deg arcs) changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1],
 // bumped by the caller's LDS counters), or the hub list. Returns deg.
@@ -2885,7 +2888,7 @@ void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
     }
     else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
-    wide_eval_kernel<<<a.evnblk + kWalkBlocks, 256, 0, s>>>(a);
+    wide_eval_kernel<<<a.evnblk + kWalkBlocks, 256, wide_walk_lds(a.nCol), s>>>(a);
 }
 // REF wide (ref_wide.h): grid = 8 blocks per CU (g.x = CUs) for the list kernels; masks of nCol bits
 // per violator in LDS (at most 32 KiB per 256-thread block)

@@ -708,8 +708,12 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
 // entry is loaded beside this task's row offsets, own colour and first gathers, and LDS hand-offs
 // use walk_sync, so a task costs its offsets, ids and colours round trips (~3), not ~7.
 __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t t, uint32_t x_t) {
-    __shared__ uint32_t mask[kWideMaskWords];
-    __shared__ uint32_t pre[kWideMaskWords + 1];
+    // the occupancy mask and its word prefix counts: dynamic LDS sized for nCol (wide_walk_lds), so
+    // the evaluation launch's workgroups are not all sized for 65 536 colours
+    extern __shared__ __attribute__((aligned(16))) uint32_t wlds[];
+    const uint32_t nww = (a.nCol + 31u) >> 5;
+    uint32_t* mask = wlds;
+    uint32_t* pre = wlds + ((nww + 3u) & ~3u);
     __shared__ uint32_t wsum[kWideWalkThreads / 64];
     __shared__ uint32_t sh_last;
     __shared__ uint32_t ic[2];   // incremental counts: rows this workgroup changed, their arcs
@@ -822,6 +826,12 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         hd[0] = ic[0];
         hd[1] = ic[1];
     }
+}
+
+// Dynamic LDS of the evaluation launch: a walk's mask (nCol bits) and prefix counts.
+inline size_t wide_walk_lds(uint32_t nCol) {
+    const size_t nww = (nCol + 31u) >> 5;
+    return 4u * (((nww + 3u) & ~(size_t)3) + nww + 1u);
 }
 
 // Grid: kWalkBlocks walk workgroups (walk_tasks; first, so that they start at once), then evnblk =
