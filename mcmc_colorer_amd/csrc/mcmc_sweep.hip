@@ -154,6 +154,7 @@ struct SweepArgs {
     uint32_t* gmask;            // wide: [kSplitMax][kWideMaskWords] occupancy of split walks (zero between sweeps)
     uint32_t* gdone;            // wide: [3][kSplitMax] tasks counted per split walk (zero between sweeps), list index, xbase
     uint32_t split_arcs;        // wide: arcs per task of a split walk
+    uint32_t walk_light;        // wide: a violator of at most this many arcs is walked by one wave
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
     // tiled sweep: stop scanning a row once its occupancy mask holds every colour (count_free_colors
     // cannot change any more: the sweep's results are unchanged); 0 = scan every arc (A/B runs)
@@ -655,8 +656,8 @@ __device__ void commit_control_ref(const SweepArgs& a, uint32_t t, unsigned long
     }
 }
 
-// The wide sweep's commit when it is the common case -- no event on the global list (walks made
-// none), at most NT events in the evaluation workgroups' ordered lists, no error, no stop -- as
+// The wide sweep's commit when it is the common case -- at most NT events (the evaluation
+// workgroups' ordered lists, plus the walks' global list sorted in LDS), no error, no stop -- as
 // three dependent round trips instead of ~10. A single workgroup pulls ~64 GB/s, so what it loads
 // is kept small and side by side: (1) the state words, the glibc ring, its evaluation workgroups'
 // event counts, both parities' compact slot headers, the incremental control words; (2) the
@@ -739,7 +740,9 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
         E += s_w[w];
     }
     const bool stop = t == a.maxRip + 1 || (!a.bench && viol <= a.z);
-    if (Eg != 0 || err != 0 || E > NT || E > a.ev_cap || stop) return false;   // the generic path
+    const uint32_t Eb = E;   // the evaluation workgroups' events; the walks' (unsorted) follow them
+    E += Eg;
+    if (err != 0 || E > NT || E > a.ev_cap || stop) return false;   // the generic path
     uint32_t tab[31];   // draw tid's coefficients (tid < E): r = sum_i T[i][tid] w[i] (commit_accept)
 #pragma unroll
     for (int i = 0; i < 31; i++) tab[i] = tid < E ? kGlibcTab[i * kGlibcTabK + tid] : 0u;
@@ -766,9 +769,17 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
         for (uint32_t k = 0; k < bc[j]; k++) s_ev[off + k] = a.evblk[(size_t)b * kEvSlot + k];
         off += bc[j];
     }
+    if (tid < Eg) s_ev[Eb + tid] = a.events[tid];
     if (tid == 0 && t < a.traj_cap) a.traj[t] = viol;
     if (tid < 31u) s_gw[tid] = s_ring[(head + tid) % 31u];
     __syncthreads();
+    if (Eg != 0) {   // walk events: the whole list into ascending order (distinct vertices; LDS bitonic)
+        uint32_t P = 1;
+        while (P < E) P <<= 1;
+        for (uint32_t k = E + tid; k < P; k += NT) s_ev[k] = 0xFFFFFFFFu;
+        __syncthreads();
+        bitonic_sort_block(s_ev, P);
+    }
     uint32_t soff = is - sm, T = 0;
     for (uint32_t w = 0; w < nwv; w++) {
         if (w < wave) soff += s_w2[w];
@@ -3039,6 +3050,7 @@ struct mcmc_ctx {
     uint32_t* wcount = nullptr;
     uint32_t* gmask = nullptr;      // split walks: masks, then kSplitMax task counters
     uint32_t split_arcs = kSplitArcs;   // MCMC_SPLIT_ARCS (tests)
+    uint32_t walk_light = kWalkLight;   // MCMC_WALK_LIGHT (0: every walk by a whole workgroup)
     float* etab = nullptr;
     float emax = 0.0f;
     uint16_t* ftab = nullptr;       // F(u) table of the evaluation (ftab_n entries)
@@ -3200,6 +3212,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.gmask = c->gmask;
         a.gdone = c->gmask ? c->gmask + (size_t)kSplitMax * kWideMaskWords : nullptr;
         a.split_arcs = c->split_arcs;
+        a.walk_light = c->walk_light;
         a.etab = c->etab;
         a.emax = c->emax;
         a.ftab = c->ftab;
@@ -3810,6 +3823,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMalloc(&c->gmask, gmb);
         if (ew == hipSuccess) ew = hipMemsetAsync(c->gmask, 0, gmb, c->stream);
         if (const char* e = getenv("MCMC_SPLIT_ARCS")) c->split_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(e, nullptr, 10));
+        if (const char* e = getenv("MCMC_WALK_LIGHT")) c->walk_light = (uint32_t)strtoul(e, nullptr, 10);
         std::vector<float> et((size_t)p->nCol + 1);
         eps_table(p->epsilon, p->nCol, et.data());
         c->emax = et[p->nCol - 1];

@@ -49,15 +49,23 @@ constexpr uint32_t kSplitArcs = 2048;     // arcs per task of a split walk (Swee
 constexpr uint32_t kWalkBlocks = MCMC_WALK_BLOCKS;   // walk workgroups beside the evaluation
 static_assert(kWalkBlocks == kIncWalkSlots, "one incremental-count slot per walk workgroup");
 constexpr uint32_t kSplitMax = 64;        // violators with a global occupancy mask (split walks)
+constexpr uint32_t kWalkLight = 512;      // light walks: one wave each (SweepArgs::walk_light)
+constexpr uint32_t kWalkLdsWords = 4096;  // walk workgroup LDS budget for the light walks' mask sets (16 KiB)
 constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
 
 // Violators. The scans flag vertex l (byte wflag[l]; one atomic per flag decides the first) and
 // list it for a walk unless it is taboo'd (the evaluation keeps those). The walks (fill_p cases
-// (i)/(ii)) run as extra workgroups of the evaluation launch, beside the evaluation proper: task k <
-// count walks violator k (from chunk 0 of its arcs); a violator above split_arcs arcs, while
-// kSplitMax global masks last, takes a slot and nt - 1 more tasks (count + xbase[slot] ...), its
-// arcs dealt out split_arcs per task. wcount: [0] violators, [2..3] one 64-bit word (extra tasks,
-// slots taken) -- zeroed by the commit (the sweep's last kernel) for the next sweep.
+// (i)/(ii)) run as extra workgroups of the evaluation launch, beside the evaluation proper. A light
+// violator (at most walk_light arcs) goes to the front of wlist (wcount[0]) and is walked by ONE
+// wave; a heavy one to the back (wcount[1]: index nloc - 1 - k) and is walked by a whole workgroup:
+// heavy task k < wcount[1] walks heavy violator k (from chunk 0 of its arcs); a violator above
+// split_arcs arcs, while kSplitMax global masks last, takes a slot and nt - 1 more tasks
+// (wcount[1] + xbase[slot] ...), its arcs dealt out split_arcs per task. wcount: [0] light, [1]
+// heavy violators, [2..3] one 64-bit word (extra tasks, slots taken) -- zeroed by the commit (the
+// sweep's last kernel) for the next sweep.
+__device__ __forceinline__ bool walk_heavy(const SweepArgs& a, uint64_t deg) {
+    return deg > a.walk_light || deg > a.split_arcs;
+}
 __device__ __forceinline__ void push_violator_at(const SweepArgs& a, uint32_t l, uint32_t idx, uint64_t deg) {
     const uint32_t nloc = a.v_end - a.v_begin;
     uint32_t slot = 0xFFFFFFFFu;
@@ -76,7 +84,9 @@ __device__ __forceinline__ void push_violator_at(const SweepArgs& a, uint32_t l,
     a.wlist[nloc + idx] = slot;
 }
 __device__ __forceinline__ void push_violator(const SweepArgs& a, uint32_t l) {
-    push_violator_at(a, l, atomicAdd(&a.wcount[0], 1u), a.row_off[l + 1] - a.row_off[l]);
+    const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
+    if (walk_heavy(a, deg)) push_violator_at(a, l, a.v_end - a.v_begin - 1u - atomicAdd(&a.wcount[1], 1u), deg);
+    else push_violator_at(a, l, atomicAdd(&a.wcount[0], 1u), deg);
 }
 __device__ __forceinline__ void flag_violator(const SweepArgs& a, uint32_t l, uint32_t) {
     if (a.wflag[l]) return;
@@ -107,15 +117,32 @@ __device__ __forceinline__ void flag_violators_wave(const SweepArgs& a, uint32_t
     }
     const bool push0 = first0 && !(a.taboo != nullptr && a.taboo[l0] > 0);
     const bool push1 = first1 && !(a.taboo != nullptr && a.taboo[l1] > 0);
-    const uint64_t m0 = __ballot(push0), m1 = __ballot(push1);
-    if ((m0 | m1) == 0) return;
-    const int lane = (int)(threadIdx.x & 63u), lead = __ffsll((long long)(m0 | m1)) - 1;
-    uint32_t base = 0;
-    if (lane == lead) base = atomicAdd(&a.wcount[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
-    base = __shfl(base, lead, 64);
+    const bool h0 = push0 && walk_heavy(a, d0), h1 = push1 && walk_heavy(a, d1);
+    const uint64_t m0 = __ballot(push0 && !h0), m1 = __ballot(push1 && !h1);   // light
+    const uint64_t g0 = __ballot(h0), g1 = __ballot(h1);                       // heavy
+    if ((m0 | m1 | g0 | g1) == 0) return;
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t base = 0, hbase = 0;
+    if (m0 | m1) {
+        const int lead = __ffsll((long long)(m0 | m1)) - 1;
+        if (lane == lead) base = atomicAdd(&a.wcount[0], (uint32_t)(__popcll(m0) + __popcll(m1)));
+        base = __shfl(base, lead, 64);
+    }
+    if (g0 | g1) {
+        const int lead = __ffsll((long long)(g0 | g1)) - 1;
+        if (lane == lead) hbase = atomicAdd(&a.wcount[1], (uint32_t)(__popcll(g0) + __popcll(g1)));
+        hbase = __shfl(hbase, lead, 64);
+    }
+    const uint32_t top = a.v_end - a.v_begin - 1u;   // heavy violator k sits at top - k
     const uint64_t below = (1ull << lane) - 1ull;
-    if (push0) push_violator_at(a, l0, base + (uint32_t)__popcll(m0 & below), d0);
-    if (push1) push_violator_at(a, l1, base + (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & below), d1);
+    if (push0)
+        push_violator_at(a, l0, h0 ? top - (hbase + (uint32_t)__popcll(g0 & below)) : base + (uint32_t)__popcll(m0 & below),
+                         d0);
+    if (push1)
+        push_violator_at(a, l1,
+                         h1 ? top - (hbase + (uint32_t)__popcll(g0) + (uint32_t)__popcll(g1 & below))
+                            : base + (uint32_t)__popcll(m0) + (uint32_t)__popcll(m1 & below),
+                         d1);
 }
 // One end of a monochromatic kept edge in a full scan: its row's same-colour count (incremental
 // contexts) and its flag.
@@ -700,7 +727,89 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
     walk_sync();
 }
 
-// The walk workgroups of the evaluation launch: tasks b, b + nb, ... (push_violator). A one-task
+// One wave's LDS hand-off: DS operations of a wave complete in order, so its lanes see each other's
+// writes once they have completed (and the compiler may not move LDS accesses across it).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// walk_gather for one wave: arcs [k0, k1) OR-ed into the wave's own LDS mask, 8 gathers per lane in flight.
+__device__ __forceinline__ void walk_gather_wave(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t* mask,
+                                                 uint64_t k0, uint64_t k1, uint32_t lane) {
+    for (uint64_t k = k0 + lane; k < k1; k += 8u * 64u) {
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t kk = k + (uint64_t)j * 64u;
+            c[j] = kk < k1 ? (uint32_t)C[a.col_idx[kk]] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
+    }
+}
+
+// walk_finish for one wave and its own mask set (a light walk): the word prefix counts by the
+// wave's 64 lanes, then the same walk and stores. All 64 lanes call it.
+__device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t cv, uint32_t x, uint32_t deg,
+                                 uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* islot,
+                                 uint32_t* ic, uint32_t lane) {
+    DevState* st = a.st;
+    const uint32_t NWW = (a.nCol + 31u) >> 5;
+    const uint32_t per = (NWW + 63u) >> 6;
+    const uint32_t l = v - a.v_begin;
+    const uint32_t w0 = lane * per;
+    uint32_t s = 0;
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) s += __popc(mask[w]);
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    uint32_t run = inc - s;
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
+        pre[w] = run;
+        run += __popc(mask[w]);
+    }
+    if (lane == 63u) pre[NWW] = inc;
+    wave_lds_sync();
+    const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
+    const float u = minstd_canonical(x);
+    uint32_t nc;
+    if (Zvcomp > 0) {   // case (ii)
+        const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
+        nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
+    } else {            // case (i)
+        nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+    }
+    if (lane == 0) {
+        const bool event = nc == a.nCol;
+        const uint32_t nv = event ? cv : nc;
+        if (nv != cv || a.inc == nullptr || a.inc[kIncMode]) {
+            Cs[v] = (uint16_t)nv;
+            if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
+        }
+        if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
+        if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+        if (event) {
+            const uint32_t idx = atomicAdd(&st->ev_count, 1u);
+            if (idx < a.ev_cap) a.events[idx] = v;
+            else atomicOr(&st->err, 1u);
+        }
+    }
+    wave_lds_sync();
+}
+
+// Light-walk mask sets: words of one (mask + prefix counts), and how many fit the LDS budget (the
+// worker waves of a walk workgroup, at most its 4).
+__host__ __device__ inline uint32_t walk_set_words(uint32_t nCol) {
+    const uint32_t nww = (nCol + 31u) >> 5;
+    return ((nww + 3u) & ~3u) + ((nww + 4u) & ~3u);
+}
+__host__ __device__ inline uint32_t walk_waves(uint32_t nCol) {
+    const uint32_t g = kWalkLdsWords / walk_set_words(nCol);
+    return g < 1u ? 1u : (g > 4u ? 4u : g);
+}
+
+// The walk workgroups of the evaluation launch. Heavy tasks first, b, b + nb, ... (push_violator). A one-task
 // violator: its whole occupancy mask and walk here. A split violator (a hub, whose gathers would
 // otherwise be one workgroup's serial latency chain): each task ORs its part of the occupancy into
 // the slot's global mask, and the workgroup finishing the last task takes the mask back
@@ -717,13 +826,13 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     __shared__ uint32_t wsum[kWideWalkThreads / 64];
     __shared__ uint32_t sh_last;
     __shared__ uint32_t ic[2];   // incremental counts: rows this workgroup changed, their arcs
-    const uint32_t cnt = a.wcount[0];
+    const uint32_t cnt = a.wcount[0], nh = a.wcount[1];   // light, heavy violators
     const uint32_t nx = a.wcount[2], ns = min(a.wcount[3], kSplitMax);
-    const uint32_t T = cnt + nx;
+    const uint32_t T = nh + nx;   // heavy tasks
     // this workgroup's slot of changed rows (written every sweep, empty ones too)
     uint32_t* islot = a.inc ? a.inc_wslot + ((size_t)((t + 1u) & 1u) * kIncWalkSlots + b) * (2u + a.inc_wslot_n)
                             : nullptr;
-    if (b >= T) {
+    if (b >= T && b >= cnt) {
         if (islot != nullptr && threadIdx.x == 0) {
             islot[0] = islot[1] = 0;
             uint32_t* hd = a.inc_hdr + ((size_t)((t + 1u) & 1u) * (a.evnblk + kIncWalkSlots) + a.evnblk + b) * 2u;
@@ -731,7 +840,9 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         }
         return;
     }
-    if (threadIdx.x == 0) ic[0] = ic[1] = 0;   // (only thread 0 uses them)
+    __shared__ uint32_t sh_nt[2];   // diagnostics: tasks, split tasks
+    if (threadIdx.x == 0) ic[0] = ic[1] = sh_nt[0] = sh_nt[1] = 0;   // (lane 0 of each wave uses them)
+    walk_sync();
     const unsigned long long ts0 = a.phase_ts ? wall_clock64() : 0ull;   // diagnostics (MCMC_PHASE_DUMP)
     uint32_t ntask = 0, nsplit = 0;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
@@ -744,11 +855,11 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     // task -> (list index, chunk); false past the last live split slot
     auto decode = [&](uint32_t task, uint32_t& idx, uint32_t& c) -> bool {
         c = 0;
-        if (task < cnt) {
-            idx = task;
+        if (task < nh) {
+            idx = nloc - 1u - task;
             return true;
         }
-        const uint32_t j = task - cnt;   // extra task j: the slot with the last xbase <= j
+        const uint32_t j = task - nh;   // extra task j: the slot with the last xbase <= j
         if (ns == 0) return false;
         uint32_t lo = 0, hi = ns;
         while (hi - lo > 1) {
@@ -761,7 +872,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         return true;
     };
     uint32_t idx = 0, c = 0;
-    bool live = decode(b, idx, c);
+    bool live = b < T && decode(b, idx, c);
     uint32_t v = live ? a.wlist[idx] : 0u, slot = live ? a.wlist[nloc + idx] : 0u;
     for (uint32_t task = b; live && task < T; task += nb) {
         const uint32_t l = v - a.v_begin;
@@ -813,13 +924,43 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         v = nv;
         slot = nslot;
     }
+    // light tasks: one wave each, worker b + nb w (w < the waves whose mask sets fit), own mask set
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u, G = walk_waves(a.nCol);
+    uint32_t nlight = 0;
+    if (wave < G) {
+        uint32_t* wm = wlds + wave * walk_set_words(a.nCol);
+        uint32_t* wp = wm + ((NWW + 3u) & ~3u);
+        const uint32_t stride = nb * G;
+        uint32_t k = b + nb * wave;
+        uint32_t lv = k < cnt ? a.wlist[k] : 0u;
+        for (; k < cnt; k += stride) {
+            const uint32_t l = lv - a.v_begin;
+            // this task's offsets, own colour and u_v; the next task's list entry (side by side)
+            const uint64_t rb = a.row_off[l], re = a.row_off[l + 1];
+            const uint32_t cv = C[lv];
+            const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)lv + 1));
+            const uint32_t nv = k + stride < cnt ? a.wlist[k + stride] : 0u;
+            for (uint32_t w = lane; w < NWW; w += 64u) wm[w] = 0;
+            wave_lds_sync();
+            walk_gather_wave(a, C, wm, rb, re, lane);
+            wave_lds_sync();
+            walk_finish_wave(a, lv, t, cv, x, (uint32_t)(re - rb), Cs, wm, wp, islot, ic, lane);
+            nlight++;
+            lv = nv;
+        }
+    }
+    if (a.phase_ts && lane == 0) {
+        atomicAdd(&sh_nt[0], nlight + (wave == 0 ? ntask : 0u));   // heavy tasks: counted by every wave
+        if (wave == 0) atomicAdd(&sh_nt[1], nsplit);
+    }
+    __syncthreads();   // every wave's entries and counts are in
     if (a.phase_ts && threadIdx.x == 0) {   // walk workgroup b: start, end, tasks, split tasks
         a.phase_ts[b * 8u + 0] = ts0;
         a.phase_ts[b * 8u + 1] = wall_clock64();
-        a.phase_ts[b * 8u + 2] = ntask;
-        a.phase_ts[b * 8u + 3] = nsplit;
+        a.phase_ts[b * 8u + 2] = sh_nt[0];
+        a.phase_ts[b * 8u + 3] = sh_nt[1];
     }
-    if (islot != nullptr && threadIdx.x == 0) {   // thread 0 made every entry (walk_finish's lane 0)
+    if (islot != nullptr && threadIdx.x == 0) {   // lane 0 of the walking wave made every entry
         islot[0] = ic[0];
         islot[1] = ic[1];
         uint32_t* hd = a.inc_hdr + ((size_t)((t + 1u) & 1u) * (a.evnblk + kIncWalkSlots) + a.evnblk + b) * 2u;
@@ -828,11 +969,9 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
     }
 }
 
-// Dynamic LDS of the evaluation launch: a walk's mask (nCol bits) and prefix counts.
-inline size_t wide_walk_lds(uint32_t nCol) {
-    const size_t nww = (nCol + 31u) >> 5;
-    return 4u * (((nww + 3u) & ~(size_t)3) + nww + 1u);
-}
+// Dynamic LDS of the evaluation launch: walk_waves mask sets, a walk's mask (nCol bits) and prefix
+// counts each (a heavy walk uses the first).
+inline size_t wide_walk_lds(uint32_t nCol) { return 4u * (size_t)walk_waves(nCol) * walk_set_words(nCol); }
 
 // Grid: kWalkBlocks walk workgroups (walk_tasks; first, so that they start at once), then evnblk =
 // ceil(nloc / (256 * kWideEvalPer)) evaluation workgroups of 256; lane `tid` of evaluation

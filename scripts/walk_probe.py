@@ -23,6 +23,18 @@ def main():
     nc = max(257, g.getMaxNodeDeg() // 4)
     col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=nc, maxRip=0x7FFFFFF0))
     col.init(0)
+    # C_0's violators and their degrees (host count over the downloaded CSR)
+    S = g.getStruct()
+    C0 = col.coloring().astype(np.int64)
+    deg = np.diff(S.cumulDegs.astype(np.int64))
+    src = np.repeat(np.arange(g.nNodes), deg)
+    bad = np.zeros(g.nNodes, dtype=bool)
+    bad[src[C0[src] == C0[S.neighs.astype(np.int64)]]] = True
+    vd = deg[bad]
+    light = int(os.environ.get("MCMC_WALK_LIGHT", "512"))
+    print(f"violators {bad.sum()}: degree med {np.median(vd):.0f} p90 {np.percentile(vd, 90):.0f} max {vd.max()}; "
+          f"light (<= {light}) {(vd <= light).sum()} ({vd[vd <= light].sum()} arcs), heavy {(vd > light).sum()} "
+          f"({vd[vd > light].sum()} arcs), > 2048: {(vd > 2048).sum()}", flush=True)
     tot, ker = ctypes.c_double(), ctypes.c_double()
     check(lib().mcmc_bench_sweeps(col._ctx, 1, ctypes.byref(tot), ctypes.byref(ker)))
     print(f"sweep 0: {ker.value * 1e3:.1f} us (phase stamps on)")
