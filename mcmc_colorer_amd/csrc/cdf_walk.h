@@ -113,6 +113,47 @@ MCMC_HD bool binade_inc(float x, uint32_t E, uint32_t& d) {
     return true;
 }
 
+// binade_inc with ties kept: x / U = d + tie / 2 (tie: the fraction is exactly 1/2, and the sum
+// k + x / U rounds to the even neighbour). False only when x / U >= 2^8.
+MCMC_HD bool binade_inc_t(float x, uint32_t E, uint32_t& d, uint32_t& tie) {
+    const uint32_t bx = f32_bits(x);
+    const uint32_t ex = bx >> 23, mx = (bx & 0x7FFFFFu) | 0x800000u;
+    tie = 0;
+    if (ex >= E) {
+        if (ex - E > 7u) return false;
+        d = mx << (ex - E);
+        return true;
+    }
+    const uint32_t sh = E - ex;
+    if (sh > 25u) { d = 0; return true; }
+    const uint32_t rem = mx & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+    tie = rem == half ? 1u : 0u;
+    d = (mx >> sh) + (rem > half ? 1u : 0u);
+    return true;
+}
+
+// One 32-colour word of a binade with a tying addend, as a function of the parity of the mantissa
+// integer k on entry: a step adds d, plus 1 when the addend ties and k + d is odd (round half to
+// even), so the word's total increment and k's parity on exit depend on the entry parity only.
+// Colours [b0, nb) of `word`; a[p], q[p]: increment and exit parity for entry parity p.
+MCMC_HD void tie_word(uint32_t word, uint32_t b0, uint32_t nb, uint32_t dE, uint32_t tE, uint32_t dP, uint32_t tP,
+                      uint32_t (&a)[2], uint32_t (&q)[2]) {
+    uint32_t a0 = 0, a1 = 0, p0 = 0, p1 = 1;
+    for (uint32_t b = b0; b < nb; b++) {
+        const bool occ = (word >> b) & 1u;
+        const uint32_t d = occ ? dE : dP, t = occ ? tE : tP;
+        const uint32_t i0 = d + (t & ((p0 + d) & 1u)), i1 = d + (t & ((p1 + d) & 1u));
+        a0 += i0;
+        a1 += i1;
+        p0 = (p0 + i0) & 1u;
+        p1 = (p1 + i1) & 1u;
+    }
+    a[0] = a0;
+    a[1] = a1;
+    q[0] = p0;
+    q[1] = p1;
+}
+
 // Case (ii) (:414-420): p[c] = eps where colour c is occupied (bit set in `mask`, nCol bits,
 // 32 per word), pf where it is free. Per 32-colour word: inside one binade the sum is order-free
 // (k += popc * dE + (32 - popc) * dP) as long as neither addend ties, the word's end stays in the
@@ -212,7 +253,82 @@ MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32
     while (c < nCol) {
         const uint32_t bc = f32_bits(cdf);
         const uint32_t E = bc >> 23;
-        uint32_t dE = 0, dP = 0;
+        uint32_t dE = 0, dP = 0, tE = 0, tP = 0;
+        if (E != 0u && binade_inc_t(eps, E, dE, tE) && binade_inc_t(pf, E, dP, tP) && (tE | tP) != 0u) {
+            // a tie binade with mixed words: each word is a function of k's parity on entry
+            // (tie_word); 64 words at a time, the functions composed by a wave scan, the first word
+            // whose end passes T found by a ballot, then that word colour by colour (a violator's
+            // mask with runs of a few colours crossed such a binade run by run: ~250 us per walk)
+            const uint32_t k0 = (bc & 0x7FFFFFu) | 0x800000u;
+            const uint32_t T = ((bu >> 23) == E) ? ((bu & 0x7FFFFFu) | 0x800000u) : 0xFFFFFFu;
+            const uint32_t w0 = c >> 5;
+            uint32_t k = k0, wf = NWW, ks = 0;
+            for (uint32_t wb = w0; wb < NWW && wf == NWW; wb += 64u) {
+#ifdef __HIP_DEVICE_COMPILE__
+                const uint32_t lane = __lane_id(), w = wb + lane;
+                uint32_t fa[2] = {0u, 0u}, fq[2] = {0u, 1u};   // identity past the last word
+                if (w < NWW)
+                    tie_word(mask[w], w == w0 ? (c & 31u) : 0u, nCol - 32u * w < 32u ? nCol - 32u * w : 32u, dE, tE,
+                             dP, tP, fa, fq);
+                for (int o = 1; o < 64; o <<= 1) {   // inclusive scan: the words before, then this one
+                    const uint32_t pa0 = __shfl_up(fa[0], o, 64), pa1 = __shfl_up(fa[1], o, 64);
+                    const uint32_t pq0 = __shfl_up(fq[0], o, 64), pq1 = __shfl_up(fq[1], o, 64);
+                    if (lane >= (uint32_t)o) {
+                        const uint32_t na0 = pa0 + fa[pq0], na1 = pa1 + fa[pq1];
+                        const uint32_t nq0 = fq[pq0], nq1 = fq[pq1];
+                        fa[0] = na0;
+                        fa[1] = na1;
+                        fq[0] = nq0;
+                        fq[1] = nq1;
+                    }
+                }
+                const uint32_t kend = k + fa[k & 1u];
+                const unsigned long long hb = __ballot(w < NWW && kend > T);
+                const uint32_t kprev = __shfl_up(kend, 1, 64);
+                if (hb) {
+                    const uint32_t f = (uint32_t)(__ffsll(hb) - 1);
+                    wf = wb + f;
+                    ks = f == 0u ? k : __shfl(kprev, f, 64);
+                } else {
+                    k = __shfl(kend, 63, 64);
+                }
+#else
+                for (uint32_t w = wb; w < wb + 64u && w < NWW; w++) {
+                    uint32_t fa[2], fq[2];
+                    tie_word(mask[w], w == w0 ? (c & 31u) : 0u, nCol - 32u * w < 32u ? nCol - 32u * w : 32u, dE, tE, dP,
+                             tP, fa, fq);
+                    const uint32_t kend = k + fa[k & 1u];
+                    if (kend > T) {
+                        wf = w;
+                        ks = k;
+                        break;
+                    }
+                    k = kend;
+                }
+#endif
+            }
+            if (wf == NWW) return nCol;   // the rest of the walk stays in the binade at or below u
+            const uint32_t word = mask[wf];
+            const uint32_t nb = nCol - 32u * wf < 32u ? nCol - 32u * wf : 32u;
+            uint32_t kk = ks, y = nCol, kb = ks;
+            bool occ = false;
+            for (uint32_t b = wf == w0 ? (c & 31u) : 0u; b < nb; b++) {
+                occ = (word >> b) & 1u;
+                const uint32_t d = occ ? dE : dP, t = occ ? tE : tP;
+                kb = kk;
+                kk += d + (t & ((kk + d) & 1u));
+                if (kk > T) {
+                    y = 32u * wf + b;
+                    break;
+                }
+            }
+            if (T < 0xFFFFFFu) return y;   // u is in this binade: the sum passes it at y
+            cdf = f32_from((E << 23) | (kb & 0x7FFFFFu));   // the sum leaves the binade at y: one fp32 step
+            cdf += occ ? eps : pf;
+            if (cdf > u) return y;
+            c = y + 1u;
+            continue;
+        }
         if (E == 0u || !binade_inc(eps, E, dE) || !binade_inc(pf, E, dP)) {
             // cdf = 0 or a tying increment: the run of equal addends from c (colours of one kind,
             // across words) by cdf_run, exact step by step where the rounding depends on the sum's

@@ -3614,8 +3614,8 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         chk(hipMemsetAsync(c->pair_trace, 0, sizeof(unsigned long long) * words, c->stream));
     }
     if (getenv("MCMC_PHASE_DUMP")) {
-        chk(hipMalloc(&c->phase_ts, sizeof(unsigned long long) * 8u * 4096u));
-        chk(hipMemsetAsync(c->phase_ts, 0, sizeof(unsigned long long) * 8u * 4096u, c->stream));
+        chk(hipMalloc(&c->phase_ts, sizeof(unsigned long long) * kPhaseWords));
+        chk(hipMemsetAsync(c->phase_ts, 0, sizeof(unsigned long long) * kPhaseWords, c->stream));
     }
     if (e != hipSuccess) {
         mcmc_destroy(c);
@@ -4434,7 +4434,7 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
         }
     }
     if (c->phase_ts) {   // diagnostics: the last sweep's per-workgroup phase timestamps (+ commit stamps)
-        std::vector<unsigned long long> h_ts((size_t)8 * 4096u);
+        std::vector<unsigned long long> h_ts(kPhaseWords);
         MCMC_HIP_TRY(hipMemcpy(h_ts.data(), c->phase_ts, h_ts.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("MCMC_PHASE_DUMP"), "wb")) {
             fwrite(h_ts.data(), sizeof(unsigned long long), h_ts.size(), f);

@@ -51,6 +51,9 @@ static_assert(kWalkBlocks == kIncWalkSlots, "one incremental-count slot per walk
 constexpr uint32_t kSplitMax = 64;        // violators with a global occupancy mask (split walks)
 constexpr uint32_t kWalkLight = 512;      // light walks: one wave each (SweepArgs::walk_light)
 constexpr uint32_t kWalkLdsWords = 4096;  // walk workgroup LDS budget for the light walks' mask sets (16 KiB)
+// MCMC_PHASE_DUMP buffer: 8 words per workgroup (4096), then 2 per walk task (walk_task_stamp)
+constexpr uint32_t kPhaseTaskBase = 8u * 4096u, kPhaseTaskMax = 32768u;
+constexpr size_t kPhaseWords = kPhaseTaskBase + 2u * kPhaseTaskMax;
 constexpr uint32_t kXsPad = 0xFFFFFFFFu;  // padding entry of the slab layout (never a valid entry)
 
 // Violators. The scans flag vertex l (byte wflag[l]; one atomic per flag decides the first) and
@@ -798,6 +801,16 @@ __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uin
     wave_lds_sync();
 }
 
+// Diagnostics (MCMC_PHASE_DUMP): walk task k's gather and walk durations (wall-clock ticks, packed
+// 32 | 32) and its arcs | kind << 32 (0 light, 1 heavy whole row, 2 split chunk, 3 split chunk + walk).
+__device__ __forceinline__ void walk_task_stamp(const SweepArgs& a, uint32_t k, unsigned long long t0,
+                                                unsigned long long t1, uint64_t deg, uint32_t kind) {
+    if (k >= kPhaseTaskMax) return;
+    const unsigned long long t2 = wall_clock64();
+    a.phase_ts[kPhaseTaskBase + 2u * k] = (t1 - t0) | ((t2 - t1) << 32);
+    a.phase_ts[kPhaseTaskBase + 2u * k + 1] = deg | ((unsigned long long)kind << 32);
+}
+
 // Light-walk mask sets: words of one (mask + prefix counts), and how many fit the LDS budget (the
 // worker waves of a walk workgroup, at most its 4).
 __host__ __device__ inline uint32_t walk_set_words(uint32_t nCol) {
@@ -884,12 +897,15 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
         const bool nlive = task + nb < T && decode(task + nb, nidx, nc);
         const uint32_t nv = nlive ? a.wlist[nidx] : 0u, nslot = nlive ? a.wlist[nloc + nidx] : 0u;
         ntask++;
+        const unsigned long long tt0 = a.phase_ts ? wall_clock64() : 0ull;
         if (slot == 0xFFFFFFFFu) {   // one task: the whole row
             for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = 0;
             walk_sync();
             walk_gather(a, C, mask, rb, re);
             walk_sync();
+            const unsigned long long tt1 = a.phase_ts ? wall_clock64() : 0ull;
             walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
+            if (a.phase_ts && threadIdx.x == 0) walk_task_stamp(a, cnt + task, tt0, tt1, re - rb, 1u);
         } else {
             const uint32_t ntk = (uint32_t)((re - rb + SA - 1) / SA);
             nsplit++;
@@ -909,12 +925,14 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
                     if (done == ntk) a.gdone[slot] = 0;   // every task of this sweep has counted
                 }
                 __syncthreads();
+                const unsigned long long tt1 = a.phase_ts ? wall_clock64() : 0ull;
                 if (sh_last) {
                     __threadfence();
                     for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
                     walk_sync();
                     walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
                 }
+                if (a.phase_ts && threadIdx.x == 0) walk_task_stamp(a, cnt + task, tt0, tt1, re - rb, sh_last ? 3u : 2u);
                 walk_sync();   // sh_last and mask are reused by the next task
             }
         }
@@ -940,11 +958,14 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
             const uint32_t cv = C[lv];
             const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)lv + 1));
             const uint32_t nv = k + stride < cnt ? a.wlist[k + stride] : 0u;
+            const unsigned long long tt0 = a.phase_ts ? wall_clock64() : 0ull;
             for (uint32_t w = lane; w < NWW; w += 64u) wm[w] = 0;
             wave_lds_sync();
             walk_gather_wave(a, C, wm, rb, re, lane);
             wave_lds_sync();
+            const unsigned long long tt1 = a.phase_ts ? wall_clock64() : 0ull;
             walk_finish_wave(a, lv, t, cv, x, (uint32_t)(re - rb), Cs, wm, wp, islot, ic, lane);
+            if (a.phase_ts && lane == 0) walk_task_stamp(a, k, tt0, tt1, re - rb, 0u);
             nlight++;
             lv = nv;
         }

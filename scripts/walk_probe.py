@@ -49,6 +49,22 @@ def main():
     i = np.argsort(-d)[:8]
     for k in i:
         print(f"  wg {k}: {d[k]:.1f} us, tasks {live[k, 2]}, split {live[k, 3]}, start +{st[k]:.1f}")
+    # per-task stamps (walk_task_stamp): gather | walk ticks (10 ns), arcs | kind
+    rec = np.fromfile(out, dtype=np.uint64)[8 * 4096:].reshape(-1, 2)
+    rec = rec[rec[:, 1] > 0]
+    gat = (rec[:, 0] & 0xFFFFFFFF).astype(np.int64) / 100.0
+    wlk = (rec[:, 0] >> np.uint64(32)).astype(np.int64) / 100.0
+    dg = (rec[:, 1] & 0xFFFFFFFF).astype(np.int64)
+    kind = (rec[:, 1] >> np.uint64(32)).astype(np.int64)
+    for k, name in enumerate(["light (wave)", "heavy row (workgroup)", "split chunk", "split chunk + walk"]):
+        m = kind == k
+        if m.any():
+            print(f"{name:22s} n {m.sum():5d}  gather us med {np.median(gat[m]):6.1f} p90 {np.percentile(gat[m], 90):6.1f} "
+                  f"max {gat[m].max():6.1f} | walk us med {np.median(wlk[m]):6.1f} p90 {np.percentile(wlk[m], 90):6.1f} "
+                  f"max {wlk[m].max():6.1f} | arcs med {np.median(dg[m]):.0f} max {dg[m].max()}")
+    top = np.argsort(-(gat + wlk))[:6]
+    for i in top:
+        print(f"  slow task: kind {kind[i]} arcs {dg[i]} gather {gat[i]:.1f} walk {wlk[i]:.1f} us")
     col.close()
 
 

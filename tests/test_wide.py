@@ -125,6 +125,44 @@ def test_cdf_walk_tie_binades_long_runs():
     assert not mism, mism[:5]
 
 
+def _tie_binades(pf):
+    """Binades E (biased exponents above pf's, up to 1.0's) where adding pf ties (x / ulp = d + 1/2)."""
+    b = int(np.frombuffer(np.float32(pf).tobytes(), dtype=np.uint32)[0])
+    ex, mx = b >> 23, (b & 0x7FFFFF) | 0x800000
+    return [E for E in range(ex + 1, 127) if E - ex <= 25 and (mx & ((1 << (E - ex)) - 1)) == 1 << (E - ex - 1)]
+
+
+def test_cdf_walk_tie_binades_mixed_masks():
+    """A violator's mask with short runs (random occupancy 5-60 %) whose pf ties in a wide binade:
+    walk_mask_pre's word-function path (each word a function of the mantissa's parity, composed 64
+    words at a time) against the literal float32 walk, u inside, below and above the tie binade."""
+    rng = np.random.default_rng(9090)
+    mism, cases = [], 0
+    for it in range(4000):
+        if cases >= 40:
+            break
+        ncol = int(rng.integers(1500, 20000))
+        dens = float(rng.uniform(0.05, 0.6))
+        bits = rng.random(ncol) < dens
+        pop = int(bits.sum())
+        eps = [1e-8, 3e-7, 2.0 ** -30 * 3][it % 3]
+        pf = np.float32((np.float32(1.0) - np.float32(eps) * np.float32(pop)) / np.float32(ncol - pop))
+        ties = [E for E in _tie_binades(pf) if E >= 120]
+        if not ties:
+            continue
+        cases += 1
+        E = ties[-1]
+        lo = np.float32(2.0 ** (E - 127))
+        for u in (np.float32(lo * np.float32(1.5)), np.float32(lo * np.float32(1.999)), np.float32(lo * np.float32(0.75)),
+                  np.float32(1.0) - np.float32(2.0 ** -24), canon(int(rng.integers(1, 2**31 - 1)))):
+            u = np.float32(min(u, np.float32(np.nextafter(np.float32(1), np.float32(0)))))
+            a, b = lib_walk(bits, ncol, 0, eps, pf, u), naive_walk(bits, ncol, eps, pf, u)
+            if a != b:
+                mism.append((ncol, pop, eps, float(pf), float(u), a, b))
+    assert cases >= 20
+    assert not mism, mism[:5]
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU parity
 
