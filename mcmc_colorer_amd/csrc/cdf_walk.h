@@ -244,7 +244,7 @@ MCMC_HD uint32_t mask_run_len(const uint32_t* mask, uint32_t nCol, uint32_t c, u
 // continues in the next binade. Binades whose increments tie (or cdf = 0) step one colour at a
 // time. Cost: O(binades + nCol / 2048) wave steps instead of O(nCol / 32) serial ones.
 MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32_t nCol, float eps, float pf,
-                               float u) {
+                               float u, bool tie_scan = true) {
     if (!pos_normal(eps) || !pos_normal(pf)) return walk_mask(mask, nCol, eps, pf, u);
     const uint32_t NWW = (nCol + 31u) >> 5;
     const uint32_t bu = f32_bits(u);
@@ -254,7 +254,7 @@ MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32
         const uint32_t bc = f32_bits(cdf);
         const uint32_t E = bc >> 23;
         uint32_t dE = 0, dP = 0, tE = 0, tP = 0;
-        if (E != 0u && binade_inc_t(eps, E, dE, tE) && binade_inc_t(pf, E, dP, tP) && (tE | tP) != 0u) {
+        if (tie_scan && E != 0u && binade_inc_t(eps, E, dE, tE) && binade_inc_t(pf, E, dP, tP) && (tE | tP) != 0u) {
             // a tie binade with mixed words: each word is a function of k's parity on entry
             // (tie_word); 64 words at a time, the functions composed by a wave scan, the first word
             // whose end passes T found by a ballot, then that word colour by colour (a violator's

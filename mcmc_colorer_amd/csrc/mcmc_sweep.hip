@@ -155,6 +155,7 @@ struct SweepArgs {
     uint32_t* gdone;            // wide: [3][kSplitMax] tasks counted per split walk (zero between sweeps), list index, xbase
     uint32_t split_arcs;        // wide: arcs per task of a split walk
     uint32_t walk_light;        // wide: a violator of at most this many arcs is walked by one wave
+    uint32_t walk_tie;          // wide: tie binades by word functions (walk_mask_pre tie_scan; MCMC_WALK_TIE=1)
     int bench;                  // throughput mode (mcmc_bench_*): no convergence stop
     // tiled sweep: stop scanning a row once its occupancy mask holds every colour (count_free_colors
     // cannot change any more: the sweep's results are unchanged); 0 = scan every arc (A/B runs)
@@ -3051,6 +3052,7 @@ struct mcmc_ctx {
     uint32_t* gmask = nullptr;      // split walks: masks, then kSplitMax task counters
     uint32_t split_arcs = kSplitArcs;   // MCMC_SPLIT_ARCS (tests)
     uint32_t walk_light = kWalkLight;   // MCMC_WALK_LIGHT (0: every walk by a whole workgroup)
+    uint32_t walk_tie = 0;              // MCMC_WALK_TIE (device tie-binade scan; off until measured on the GPU)
     float* etab = nullptr;
     float emax = 0.0f;
     uint16_t* ftab = nullptr;       // F(u) table of the evaluation (ftab_n entries)
@@ -3213,6 +3215,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.gdone = c->gmask ? c->gmask + (size_t)kSplitMax * kWideMaskWords : nullptr;
         a.split_arcs = c->split_arcs;
         a.walk_light = c->walk_light;
+        a.walk_tie = c->walk_tie;
         a.etab = c->etab;
         a.emax = c->emax;
         a.ftab = c->ftab;
@@ -3824,6 +3827,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         if (ew == hipSuccess) ew = hipMemsetAsync(c->gmask, 0, gmb, c->stream);
         if (const char* e = getenv("MCMC_SPLIT_ARCS")) c->split_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(e, nullptr, 10));
         if (const char* e = getenv("MCMC_WALK_LIGHT")) c->walk_light = (uint32_t)strtoul(e, nullptr, 10);
+        if (const char* e = getenv("MCMC_WALK_TIE")) c->walk_tie = (uint32_t)strtoul(e, nullptr, 10);
         std::vector<float> et((size_t)p->nCol + 1);
         eps_table(p->epsilon, p->nCol, et.data());
         c->emax = et[p->nCol - 1];

@@ -706,7 +706,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
         uint32_t nc;
         if (Zvcomp > 0) {   // case (ii)
             const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
-            nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
+            nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u, a.walk_tie != 0u);
         } else {            // case (i)
             nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
         }
@@ -779,7 +779,7 @@ __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uin
     uint32_t nc;
     if (Zvcomp > 0) {   // case (ii)
         const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
-        nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u);
+        nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u, a.walk_tie != 0u);
     } else {            // case (i)
         nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
     }
