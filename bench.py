@@ -220,6 +220,70 @@ def refstruct_full_occupancy(dev: int, ncol: int, seed: int, value: float, sweep
     return r
 
 
+def rank_share(a, dev: int = 0) -> dict:
+    """One rank's share of configs[3] on one GPU: rows [0, n/K) of the C3 graph (every rank of the
+    equal-rows plan holds as many rows and, G(n, p) being uniform, as many arcs), generated alone
+    (Graph.er_fast(rows=...)), timed two ways:
+      plain: a context over those rows, the one-GPU step (the sweep commits in its last workgroup),
+             K steps as one hipGraph -- what the rank's sweep itself costs;
+      rank:  a world-K partitioned context of rank 0 through the native driver (mcmc_part_bench_rank):
+             sweep with the delta packing and footer, the part_commit launch, batches and polling,
+             with the exchange left out -- everything of a world-K step but the RCCL transfers.
+    The strong-scaling budget is the one-GPU C3 step / 6 (north_star: >= 6x at 8 GPUs)."""
+    import mcmc_colorer_amd.colorer as M
+    from mcmc_colorer_amd._lib import MCMCRunStats, check, lib, u32ptr
+    from mcmc_colorer_amd.distributed import plan_rows
+
+    n, p, K = 10_000_000, 0.001, a.rank_share
+    bounds = plan_rows(n, K)
+    b1 = int(bounds[1])
+    t0 = time.perf_counter()
+    g = M.Graph.er_fast(n, p, 1, device=dev, rows=(0, b1))
+    gen = time.perf_counter() - t0
+    params = M.ColoringMCMCParams(nCol=32, maxRip=0x7FFFFFF0)
+    tot, ker = ctypes.c_double(), ctypes.c_double()
+    col = M.ColoringMCMC(g, M.GPURand(n, a.seed, M.GlibcRand(1)), params, v_begin=0, v_end=b1)
+    col.init(0)
+    if a.warmup:
+        check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
+    check(lib().mcmc_bench_prepare(col._ctx, a.steps))
+    t1 = time.perf_counter()
+    check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
+    plain_wall = time.perf_counter() - t1
+    info = col.info()
+    col.close()
+    prm = params.to_c(a.seed)
+    ctx = ctypes.c_void_p()
+    check(lib().mcmc_part_create(g.handle, ctypes.byref(prm), K, 0, u32ptr(bounds), None, ctypes.byref(ctx)))
+    check(lib().mcmc_set_glibc_window(ctx, u32ptr(M.GlibcRand(1).window)))
+    check(lib().mcmc_init_coloring(ctx, None))
+    check(lib().mcmc_set_bench_mode(ctx, 1))
+    st = MCMCRunStats()
+    if a.warmup:
+        check(lib().mcmc_part_bench_rank(ctx, a.warmup, ctypes.byref(st)))
+    t1 = time.perf_counter()
+    check(lib().mcmc_part_bench_rank(ctx, a.steps, ctypes.byref(st)))
+    rank_wall = time.perf_counter() - t1
+    rank_dev = st.loopMs / a.steps
+    xs = [ctypes.c_uint64() for _ in range(4)]
+    check(lib().mcmc_part_exchange_stats(ctx, *[ctypes.byref(x) for x in xs]))
+    lib().mcmc_destroy(ctx)
+    full_ms = 0.8955   # BENCH_r03.json (driver): the one-GPU C3 step
+    return {
+        "metric": "ms per step of one rank's share of configs[3]",
+        "rank_share": K, "rows": b1, "arcs": g.nEdges, "graph_gen_s": round(gen, 2),
+        "steps": a.steps, "warmup": a.warmup,
+        "plain": {"ms_per_step": plain_wall * 1e3 / a.steps, "device_ms_per_step": ker.value,
+                  "what": "context over rows [0, n/K), one-GPU fused step, hipGraph of the K steps"},
+        "rank": {"ms_per_step": rank_wall * 1e3 / a.steps, "device_ms_per_step": rank_dev,
+                 "delta_steps": xs[0].value, "full_steps": xs[1].value, "overflows": xs[2].value,
+                 "what": "world-K rank 0 through mcmc_part_bench_rank: sweep + delta packing + part_commit "
+                         "launch + driver batches/polls, exchange left out (RCCL over xGMI unmeasured)"},
+        "budget_ms": full_ms / 6.0, "one_gpu_c3_ms": full_ms,
+        "layout": info,
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,7 +311,13 @@ def main() -> int:
     ap.add_argument("--variant", default=None,
                     help="sweep kernel: lds | tiled | blocked | global[:block_log2[:lanes_log2[:group_rows"
                          "[:stream]]]] (empty field / default: the library's choice)")
+    ap.add_argument("--rank-share", type=int, default=0,
+                    help="K > 1: time one rank's share of configs[3] (rows [0, n/K) of the C3 graph) on this GPU, "
+                         "as a plain sweep and as a world-K rank with the exchange left out (rank_share)")
     a = ap.parse_args()
+    if a.rank_share > 1:
+        print(json.dumps(rank_share(a)), flush=True)
+        return 0
     if a.variant:
         for key, v in zip(("MCMC_GATHER", "MCMC_BLOCK_LOG2", "MCMC_SUB_LOG2", "MCMC_GROUP_ROWS",
                            "MCMC_TILE_STREAM"), a.variant.split(":")):

@@ -324,6 +324,11 @@ int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, 
  * stats: k entries (identical loop fields on every rank; loopMs = device time on ctxs[0]'s stream).
  * Colourings and trajectories then come from mcmc_get_coloring / mcmc_get_trajectory of any rank. */
 int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_stats* stats /* k */);
+/* Measurement only: `steps` steps of ONE rank of a loopback partition (comm NULL) through the same
+ * driver as mcmc_part_run -- sweep, delta packing, commit launch, batches and polling -- with the
+ * exchange left out (the peers' footers and delta slots stay empty). What one GPU can time of a
+ * world-N step; the colouring it leaves is not the partitioned run's. */
+int mcmc_part_bench_rank(mcmc_ctx* c, uint32_t steps, mcmc_run_stats* stats);
 
 /* ---- other colorers -------------------------------------------------
  * The reference's parallel greedy first-fit colorer (ColoringGreedyFF::run,

@@ -83,6 +83,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_comm_destroy": (None, [c_void_p]),
     "mcmc_part_create": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, _u32p, c_void_p, POINTER(c_void_p)]),
     "mcmc_part_run": (c_int, [POINTER(c_void_p), c_uint32, c_uint32, c_void_p]),
+    "mcmc_part_bench_rank": (c_int, [c_void_p, c_uint32, c_void_p]),
     "mcmc_xorwow_state": (c_int, [c_uint64, c_uint64, c_int, _u32p]),
     "mcmc_gpurand_create": (c_int, [c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "mcmc_gpurand_states": (c_int, [c_void_p, _u32p]),

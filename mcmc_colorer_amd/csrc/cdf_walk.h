@@ -254,7 +254,11 @@ MCMC_HD uint32_t walk_mask_pre(const uint32_t* mask, const uint32_t* pre, uint32
         const uint32_t bc = f32_bits(cdf);
         const uint32_t E = bc >> 23;
         uint32_t dE = 0, dP = 0, tE = 0, tP = 0;
-        if (tie_scan && E != 0u && binade_inc_t(eps, E, dE, tE) && binade_inc_t(pf, E, dP, tP) && (tE | tP) != 0u) {
+        // (increments below 2^20: 64 words x 32 colours of them, ties included, stay below 2^32 in the
+        // uint32 word functions and their scan; a larger increment leaves the binade within 16
+        // steps, so the run-by-run path below is as short)
+        if (tie_scan && E != 0u && binade_inc_t(eps, E, dE, tE) && binade_inc_t(pf, E, dP, tP) && (tE | tP) != 0u &&
+            (dE | dP) < (1u << 20)) {
             // a tie binade with mixed words: each word is a function of k's parity on entry
             // (tie_word); 64 words at a time, the functions composed by a wave scan, the first word
             // whose end passes T found by a ballot, then that word colour by colour (a violator's

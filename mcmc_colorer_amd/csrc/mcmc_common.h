@@ -181,7 +181,7 @@ struct PartRes {
 };
 int part_resources(mcmc_ctx* c, PartRes** out);
 int part_run_begin(mcmc_ctx* c);   // a run's start: this rank's delta slots empty, no tail-cut result, stats zero
-void part_add_xstats(mcmc_ctx* c, uint64_t delta_steps, uint64_t full_steps, uint64_t ovf, uint64_t bytes);
+void part_add_xstats(mcmc_ctx* c, int64_t delta_steps, int64_t full_steps, int64_t ovf, int64_t bytes);
 // Partitioned tail cut (mcmc_sweep.hip): state and colorIdx at loop exit (global Cviol, the final t,
 // the final colouring's buffer); one rank's repair of its flagged rows; its recount (device sum
 // word); the result for the run summary.

@@ -3471,6 +3471,12 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     const GraphDev& gd = g->g;
     if (p->nCol == 0) return fail(MCMC_E_ARG, "nCol must be >= 1");
     if (v_begin > v_end || v_end > gd.n) return fail(MCMC_E_ARG, "bad vertex range");
+    // The tail queue packs a row's taboo counter in 24 bits (own colour | counter << 8). A counter
+    // past the loop's last sweep never expires within the loop, so a larger tabooIteration is
+    // clamped to maxRip + 2 (the same run); with a loop that long it is refused.
+    constexpr uint32_t kTabooMax = (1u << 24) - 1u;
+    if (p->tabooIteration > kTabooMax && (uint64_t)p->maxRip + 2u > kTabooMax)
+        return fail(MCMC_E_ARG, "tabooIteration >= 2^24 needs maxRip + 2 < 2^24 (24-bit taboo counters)");
     // nCol > 256: the wide sweep (uint16 replicas, sweep_wide.h); MCMC_GATHER=wide forces it
     const char* gv = getenv("MCMC_GATHER");
     const std::string gsel = gv ? gv : "";
@@ -3499,6 +3505,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     mcmc_ctx* c = new mcmc_ctx();
     c->g = &gd;
     c->p = *p;
+    if (c->p.tabooIteration > kTabooMax) c->p.tabooIteration = p->maxRip + 2u;
     c->n = gd.n;
     c->v_begin = v_begin;
     c->v_end = v_end;
@@ -4713,7 +4720,7 @@ int part_resources(mcmc_ctx* c, PartRes** out) {
     return MCMC_OK;
 }
 
-void part_add_xstats(mcmc_ctx* c, uint64_t delta_steps, uint64_t full_steps, uint64_t ovf, uint64_t bytes) {
+void part_add_xstats(mcmc_ctx* c, int64_t delta_steps, int64_t full_steps, int64_t ovf, int64_t bytes) {
     c->xs_delta += delta_steps;
     c->xs_full += full_steps;
     c->xs_ovf += ovf;

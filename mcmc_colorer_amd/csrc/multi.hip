@@ -77,6 +77,7 @@ struct Driver {
     std::vector<PartDesc> d;
     std::vector<hipEvent_t> ev;   // loopback: per rank, its copies of the step are enqueued
     bool rccl = false;
+    bool stub = false;            // mcmc_part_bench_rank: one rank's steps with the exchange left out
     uint32_t world = 1;
     int mode = 0;
     bool delta_ok = false;        // every local context can run delta-mode steps
@@ -99,7 +100,9 @@ struct Driver {
             if (rccl && (d[i].comm->world != world || d[i].comm->rank != d[i].rank || d[i].comm->device != d[i].device))
                 return fail(MCMC_E_ARG, "communicator does not match the context's rank/device");
         }
-        if (!rccl) {
+        if (stub) {
+            if (k != 1 || rccl) return fail(MCMC_E_ARG, "rank bench: one loopback context");
+        } else if (!rccl) {
             if (k != world) return fail(MCMC_E_ARG, "loopback transport: all ranks must be passed");
             for (uint32_t i = 0; i < k; i++)
                 if (d[i].rank != i) return fail(MCMC_E_ARG, "loopback transport: contexts in rank order");
@@ -125,6 +128,7 @@ struct Driver {
 
     // Step t's exchange. delta: footers + delta slots; else footers + the row ranges.
     int exchange(uint32_t t, bool delta) {
+        if (stub) return MCMC_OK;   // peers' footers and slots stay empty: no Cviol, events or changes
         const uint32_t nb = (t + 1) & 1u;
         if (rccl) {
             if (world == 1) return MCMC_OK;   // nothing leaves the rank
@@ -461,9 +465,13 @@ int mcmc_part_create(const mcmc_graph* g, const mcmc_params* p, uint32_t world, 
     return MCMC_OK;
 }
 
-int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_stats* stats) {
+}  // extern "C"
+
+namespace {
+int part_run_impl(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_stats* stats, bool stub) {
     if (!ctxs || k == 0) return fail(MCMC_E_ARG, "no contexts");
     Driver D;
+    D.stub = stub;
     if (int rc = D.setup(ctxs, k)) return rc;
     const uint32_t limit = max_sweeps ? max_sweeps : D.d[0].maxRip + 2;   // + the final count pass (sweeps)
     struct Ev { hipEvent_t e; };   // the context's cached events (part_resources)
@@ -515,6 +523,12 @@ int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
             int32_t dn2 = 0;
             uint32_t err2 = 0;
             if (int rc = mcmc_part_state(D.ctx[0], &dn2, &td, &err2)) return rc;
+            // the steps enqueued behind the paused sweep were no-ops on the device: uncount them
+            for (uint32_t s = td + 1; s < t; s++) {
+                const bool dl = s - t_begin < was_delta.size() && was_delta[s - t_begin];
+                for (size_t i = 0; i < D.d.size(); i++)
+                    part_add_xstats(D.ctx[i], dl ? -1 : 0, dl ? 0 : -1, 0, -(int64_t)D.step_bytes(D.d[i], dl));
+            }
             if (int rc = D.resume(td, err2, td - t_begin < was_delta.size() && was_delta[td - t_begin])) return rc;
             if (err2 & 4u) full_left = kFullAfterOverflow;
             t = td + 1;
@@ -545,6 +559,18 @@ int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
         if (stats) stats[i] = s;
     }
     return MCMC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mcmc_part_run(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_stats* stats) {
+    return part_run_impl(ctxs, k, max_sweeps, stats, false);
+}
+
+int mcmc_part_bench_rank(mcmc_ctx* c, uint32_t steps, mcmc_run_stats* stats) {
+    if (!c || steps == 0) return fail(MCMC_E_ARG, "a context and steps > 0");
+    return part_run_impl(&c, 1, steps, stats, true);
 }
 
 }  // extern "C"

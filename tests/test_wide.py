@@ -163,6 +163,40 @@ def test_cdf_walk_tie_binades_mixed_masks():
     assert not mism, mism[:5]
 
 
+def test_cdf_walk_tie_binade_large_free_increment():
+    """eps ties in the binade of 2 eps (odd mantissa) while pf / eps is 32-512: there a free colour
+    moves the mantissa integer by up to 2^31 units, so a 32-colour word's increment does not fit 32
+    bits. Masks enter that binade through occupied colours and then mix free ones; every
+    case against the literal float32 walk."""
+    rng = np.random.default_rng(5151)
+    mism, cases = [], 0
+    for it in range(300):
+        eps = np.float32(rng.uniform(2e-6, 5e-5))
+        b = int(np.frombuffer(eps.tobytes(), dtype=np.uint32)[0]) | 1   # odd mantissa: ties at 2 eps
+        eps = np.frombuffer(np.uint32(b).tobytes(), dtype=np.float32)[0]
+        ratio = float(rng.uniform(32, 512))
+        nfree = max(2, int(1.0 / (float(eps) * ratio)))
+        ncol = nfree + int(rng.integers(nfree // 4 + 1, 2 * nfree + 2))
+        bits = np.ones(ncol, dtype=bool)
+        free = rng.choice(np.arange(2, ncol), size=nfree, replace=False)
+        bits[free] = False
+        bits[:2] = True                                   # cdf = 2 eps: the tie binade
+        bits[2:2 + int(rng.integers(2, 30))] = False      # then a run of free colours in that word
+        pop = int(bits.sum())
+        pf = np.float32((np.float32(1.0) - eps * np.float32(pop)) / np.float32(ncol - pop))
+        if not (32 <= pf / eps <= 512):
+            continue
+        cases += 1
+        for u in (canon(int(rng.integers(1, 2**31 - 1))), np.float32(pf * np.float32(rng.uniform(1, 20))),
+                  np.float32(1.0) - np.float32(2.0 ** -24), np.float32(eps * np.float32(rng.uniform(2, 40)))):
+            u = np.float32(min(u, np.float32(np.nextafter(np.float32(1), np.float32(0)))))
+            a, b2 = lib_walk(bits, ncol, 0, eps, pf, u), naive_walk(bits, ncol, eps, pf, u)
+            if a != b2:
+                mism.append((ncol, pop, float(eps), float(pf), float(u), a, b2))
+    assert cases >= 50
+    assert not mism, mism[:5]
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU parity
 
