@@ -56,7 +56,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-KERNELS = {"lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
+KERNELS = {"dense": "dc_update_kernel+dc_eval_kernel (one sweep)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
            "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)",
            "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
@@ -422,12 +422,14 @@ def main() -> int:
             check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
         check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
         inc0 = None if ref else col.wide_inc_stats()
+        dn0 = None if ref else col.dense_stats()
         t0 = time.perf_counter()
         check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
         wall = time.perf_counter() - t0
         kernel_ms = ker.value
         info = col.info()
         inc1 = None if ref else col.wide_inc_stats()
+        dn1 = None if ref else col.dense_stats()
     else:
         import torch
 
@@ -468,6 +470,64 @@ def main() -> int:
     variant = info["variant"]
     scan = None
     b_alg = b_fmt
+    if dist is not None:
+        dn0 = dn1 = None
+        if not ref:
+            out8 = (ctypes.c_uint64 * 8)()
+            check(lib().mcmc_get_dense_stats(drv._ctx, out8))
+            dn1 = {"enabled": bool(out8[0])}
+    dense_on = bool(dn1 and dn1["enabled"])
+    if dense_on:
+        variant = "dense"
+        if dist is not None:   # this rank's evaluation bytes: its rows' dense masks, own colours, writes
+            nwd = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
+            b_alg = int(bounds[rank + 1] - bounds[rank]) * (4 * nwd + 2)
+    dense = None
+    if dense_on and dist is None:
+        # the dense-count sweep (csrc/dense_counts.h): per sweep every row's dense mask (NW words) and
+        # own colour read, its new colour written; per vertex of the dense range that changed colour
+        # its local arcs (id + two count atomics); rows that scanned past the range (ids + colour
+        # gathers, an upper bound: their whole rows outside it); a rebuild reads every row's arcs
+        # into the range
+        d = {k: dn1[k] - dn0[k] for k in ("incremental_sweeps", "rebuilds", "moved_vertices", "open_rows")}
+        S = max(1, d["incremental_sweeps"] + d["rebuilds"])
+        nw = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
+        deg = m / max(1, n)
+        span = dn1["s1"] - dn1["s0"]
+        per_row = 4 * nw + 2
+        b_eval = n * per_row
+        b_upd = d["moved_vertices"] * deg * 10.0
+        b_open = d["open_rows"] * deg * (1.0 - span / max(1, n)) * 3.0
+        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 3.0 + n * a.ncol * 4.0 + n * nw * 4.0)
+        b_alg = b_eval + (b_upd + b_open + b_rebuild) / S
+        dense = dict(d, sweeps_counted=S, dense_range=[dn1["s0"], dn1["s1"]],
+                     moved_vertices_per_sweep=d["moved_vertices"] / S, open_rows_per_sweep=d["open_rows"] / S,
+                     rebuild_threshold=dn1["rebuild_threshold"], bytes_per_sweep=b_alg,
+                     bytes={"evaluation": b_eval, "updates": b_upd / S, "open_rows": b_open / S,
+                            "rebuilds": b_rebuild / S},
+                     note="dense-count sweep: every row keeps the counts of its neighbours' colours over a fixed "
+                          "dense column range, moved each sweep by the vertices there that changed colour; a row "
+                          "whose dense mask holds every colour is evaluated without a scan, the rest scan their "
+                          "other column blocks. Bit-identical to the scan sweeps (tests/test_dense.py).")
+        if not a.no_full_scan:
+            # the same graph through the tiled scan sweep (MCMC_DENSE=0, the r03 early-exit kernel) and
+            # the full scan (MCMC_FULL_SCAN=1): every sweep scans the layout
+            for label, env in (("scan_sweep", "MCMC_DENSE"), ("full_scan", "MCMC_FULL_SCAN")):
+                os.environ[env] = "0" if env == "MCMC_DENSE" else "1"
+                cf = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1)), params)
+                cf.init(0)
+                tot2, ker2 = ctypes.c_double(), ctypes.c_double()
+                check(lib().mcmc_bench_sweeps(cf._ctx, 3, ctypes.byref(tot2), ctypes.byref(ker2)))
+                k = max(3, min(a.steps, 10))
+                check(lib().mcmc_bench_sweeps(cf._ctx, k, ctypes.byref(tot2), ctypes.byref(ker2)))
+                os.environ.pop(env)
+                fi = cf.info()
+                dense[label] = {"ms_per_sweep": ker2.value, "value": g.nNodes / (ker2.value * 1e-3), "sweeps": k,
+                                "layout_bytes": fi["sweep_bytes"],
+                                "layout_frac_if_full": fi["sweep_bytes"] / (ker2.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                "what": ("the tiled early-exit scan (MCMC_DENSE=0)" if env == "MCMC_DENSE" else
+                                         "every arc scanned (MCMC_FULL_SCAN=1)")}
+                cf.close()
     if not ref and variant == "tiled":
         # The tiled sweep stops scanning a row once its occupancy mask holds every colour (the
         # result cannot change; MCMC_FULL_SCAN=1 scans every arc): the bytes one launch moves are
@@ -583,6 +643,8 @@ def main() -> int:
         out["convergence"] = conv
     if wide_inc is not None:
         out["wide_inc"] = wide_inc
+    if dense is not None:
+        out["dense"] = dense
     if dist is None and a.config == "c5" and not a.no_convergence:
         # the wide sweep WITH violators in every timed sweep (nCol = maxDeg / 4 does not converge):
         # the reference loop capped at 20 sweeps, device time per sweep and the per-sweep Cviol

@@ -31,6 +31,8 @@ struct GraphDev {
     uint32_t maxDeg = 0, minDeg = 0;
     bool sorted = false;           // every neighbour list ascending
     int sym = -1;                  // whole CSR symmetric: 1 yes, 0 no, -1 not checked (csr_symmetric)
+    int simple_sym = -1;           // every arc's reverse present and no arc repeated: 1 yes (the counter-based
+                                   // G(n, p) by construction, or checked), 0 no, -1 not known
     uint64_t* row_off = nullptr;   // [n+1]
     uint32_t* col_idx = nullptr;   // [m]
 };

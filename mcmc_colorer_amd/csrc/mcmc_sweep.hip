@@ -217,6 +217,14 @@ struct SweepArgs {
     uint32_t inc_slot, inc_wslot_n;   // rows per evaluation / walk slot (past it: the next sweep recounts)
     uint32_t inc_hub_arcs;      // a changed row above this many arcs is a hub (MCMC_WIDE_INC_HUB)
     unsigned long long inc_thresh;    // the next sweep is incremental while its changed rows' arcs stay <= this
+    // dense-count sweep (dense_counts.h; tiled contexts): per local row the counts of the colours of
+    // its neighbours in the dense column range [dc_s0, dc_s1) and their occupancy bits
+    uint32_t* dc_ctl;           // kDcWords control words (nullptr: the tiled scan sweeps)
+    uint32_t* dc_cnt;           // [nloc][dc_cw] uint32 counts
+    uint32_t* dc_mask;          // [nloc][NW] occupancy of the counts
+    uint32_t* dc_list;          // [2][dc_cap] vertices of S whose colour changed, by parity (t + 1) & 1
+    uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max;
+    uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
 constexpr uint32_t kIncMode = 0;     // the running sweep: 1 full (the tile scan recounts), 0 incremental
@@ -231,6 +239,39 @@ constexpr uint32_t kIncWords = 24;
 #define MCMC_WALK_BLOCKS 1024   // walk workgroups of the wide evaluation launch (sweep_wide.h kWalkBlocks)
 #endif
 constexpr uint32_t kIncWalkSlots = MCMC_WALK_BLOCKS;   // one changed-row slot per walk workgroup
+
+// control words of the dense-count sweep (SweepArgs::dc_ctl; dense_counts.h)
+constexpr uint32_t kDcMode = 0;    // the running sweep's update: 1 rebuild every count, 0 incremental
+constexpr uint32_t kDcLen = 1;     // [2] vertices of S listed for the next sweep's update, by parity (t + 1) & 1
+constexpr uint32_t kDcOvf = 3;     // [2] that list overflowed: the next sweep rebuilds
+constexpr uint32_t kDcOpen = 5;    // rows of the running sweep whose dense mask was not full
+constexpr uint32_t kDcStat = 8;    // u64 [4]: incremental sweeps, rebuilds, listed vertices, open rows
+constexpr uint32_t kDcWords = 16;
+constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: the commit's sort buffer
+
+
+// The commit's bookkeeping of sweep t (thread 0, after the event replay listed its vertices of S):
+// statistics, list t & 1 (read by this sweep's update) emptied for sweep t + 1's writers, and the
+// mode of sweep t + 1's update -- a rebuild when list (t + 1) & 1 overflowed or holds more
+// vertices than an incremental update pays for (dc_max).
+__device__ void dc_commit(const SweepArgs& a, uint32_t t) {
+    uint32_t* k = a.dc_ctl;
+    const uint32_t q = (t + 1u) & 1u, p = t & 1u;
+    const uint32_t len = __hip_atomic_load(&k[kDcLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ovf = __hip_atomic_load(&k[kDcOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t open = __hip_atomic_load(&k[kDcOpen], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t mode = k[kDcMode];
+    unsigned long long* s = reinterpret_cast<unsigned long long*>(k + kDcStat);
+    s[0] += mode ? 0ull : 1ull;
+    s[1] += mode ? 1ull : 0ull;
+    s[2] += min(len, a.dc_cap);
+    s[3] += open;
+    k[kDcOpen] = 0;
+    k[kDcLen + p] = 0;
+    k[kDcOvf + p] = 0;
+    k[kDcMode] = (ovf || len > a.dc_max) ? 1u : 0u;
+}
+
 
 // Row l (deg arcs) changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1],
 // bumped by the caller's LDS counters), or the hub list. Returns deg.
@@ -536,10 +577,20 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             if (a.inc != nullptr && c != (uint32_t)C[v])   // (whole-graph contexts: v = l)
                 atomicAdd(&inc_cc[1], inc_list(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.ev_cap),
                                                a.ev_cap, &inc_cc[0]));
+            if (a.dc_list != nullptr && c != (uint32_t)C[v] && v - a.dc_s0 < a.dc_s1 - a.dc_s0) {
+                const uint32_t q = (t + 1u) & 1u;   // dense-count sweep: the next update moves v
+                const uint32_t idx = atomicAdd(&a.dc_ctl[kDcLen + q], 1u);
+                if (idx < a.dc_cap) a.dc_list[(size_t)q * a.dc_cap + idx] = v;
+                else a.dc_ctl[kDcOvf + q] = 1u;
+            }
         }
         __syncthreads();
     }
     MCMC_COMMIT_PHASE(a, 4);
+    if (a.dc_ctl != nullptr) {
+        __syncthreads();   // the replay's list appends are in
+        if (threadIdx.x == 0) dc_commit(a, t);
+    }
     if (a.inc != nullptr) {
         __syncthreads();   // inc_cc complete
         inc_commit(a, t, inc_cc);
@@ -1190,6 +1241,24 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
                 dl[kDeltaHead + 2u * idx] = v;
                 dl[kDeltaHead + 2u * idx + 1u] = newc;
             }
+        }
+    }
+    // dense-count sweep: the vertices of S whose colour changes (events aside: the commit's replay
+    // lists those), for the next sweep's update of the counts
+    if (a.dc_list != nullptr) {
+        const bool dchg = valid && tab == 0 && !event && newc != cv && v - a.dc_s0 < a.dc_s1 - a.dc_s0;
+        const uint64_t db = __ballot(dchg);
+        if (db) {
+            const uint32_t q = (Cs == a.colors1) ? 1u : 0u;   // (t + 1) & 1
+            uint32_t based = 0;
+            if (lane == 0) based = atomicAdd(&a.dc_ctl[kDcLen + q], (uint32_t)__popcll(db));
+            based = __shfl(based, 0, 64);
+            const uint32_t idx = based + (uint32_t)__popcll(db & ((1ull << lane) - 1ull));
+            if (dchg) {
+                if (idx < a.dc_cap) a.dc_list[(size_t)q * a.dc_cap + idx] = v;
+                else a.dc_ctl[kDcOvf + q] = 1u;
+            }
+            ev_flag = 1u;   // the commit reads the list's length: this workgroup releases (sweep_tail)
         }
     }
 
@@ -2825,6 +2894,8 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     MCMC_PHASE(a, 4);
 }
 
+#include "dense_counts.h"
+
 // Layout construction lives in tiled_layout.hip.
 __global__ void segment_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
                                uint32_t nloc, uint32_t nb, uint32_t block_log2, uint32_t* __restrict__ seg);
@@ -3068,6 +3139,12 @@ struct mcmc_ctx {
     uint32_t* inc = nullptr;        // kIncWords control words, then counts, lists and slots (make_args)
     unsigned long long inc_thresh = 0;
     uint32_t inc_slot = 0, inc_wslot_n = 0, inc_hub_arcs = 256;
+    // dense-count sweep (dense_counts.h; MCMC_DENSE=0: the tiled scan sweep)
+    bool dc = false;
+    uint32_t* dc_ctl = nullptr;     // kDcWords control words, then the lists (one allocation)
+    uint32_t* dc_cnt = nullptr;
+    uint32_t* dc_mask = nullptr;
+    uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1;
 };
 
 namespace {
@@ -3078,6 +3155,15 @@ hipError_t inc_reset(mcmc_ctx* c) {
     uint32_t h[kIncWords] = {};
     h[kIncMode] = 1u;
     hipError_t e = hipMemcpyAsync(c->inc, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
+    return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // h lives on this frame
+}
+
+// Dense-count sweep: lists and statistics cleared, the next sweep's update a rebuild (after any
+// change of the colours that is not a sweep's).
+hipError_t dc_reset(mcmc_ctx* c) {
+    uint32_t h[kDcWords] = {};
+    h[kDcMode] = 1u;
+    hipError_t e = hipMemcpyAsync(c->dc_ctl, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
     return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // h lives on this frame
 }
 
@@ -3254,6 +3340,19 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.inc_hub_arcs = c->inc_hub_arcs;
             a.inc_thresh = c->inc_thresh;
         }
+    }
+    if (c->dc) {
+        a.dc_ctl = c->dc_ctl;
+        a.dc_list = c->dc_ctl + kDcWords;
+        a.dc_cnt = c->dc_cnt;
+        a.dc_mask = c->dc_mask;
+        a.dc_s0 = c->dc_s0;
+        a.dc_s1 = c->dc_s1;
+        a.dc_cw = c->p.nCol;
+        a.dc_cap = c->dc_cap;
+        a.dc_max = c->dc_max;
+        a.dc_apow = c->dc_apow;
+        a.lds_sort_cap = kDcEvalLds / 4u;
     }
     a.phase_ts = c->phase_ts;
     a.pair_trace = c->pair_trace;
@@ -3435,6 +3534,81 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
         (*passes)++;
     }
     *finalViol = cviol;
+    return MCMC_OK;
+}
+
+// Every local arc's reverse present and no local row listing a neighbour twice: then, for u and w
+// both local, w's row holds u exactly as often as u's row holds w (the dense counts' update reads
+// u's row for the rows holding u). Generated G(n, p) graphs are so by construction.
+int local_simple_symmetric(mcmc_ctx* c, bool* ok) {
+    GraphDev& gd = const_cast<GraphDev&>(*c->g);
+    const uint32_t nloc = c->v_end - c->v_begin;
+    const bool whole = c->v_begin == 0 && c->v_end == gd.n;
+    *ok = false;
+    if (gd.simple_sym == 1 || (whole && gd.simple_sym == 0)) {
+        *ok = gd.simple_sym == 1;
+        return MCMC_OK;
+    }
+    if (!gd.row_off || !gd.sorted) return MCMC_OK;   // (tiled layouts of CSR graphs sort the rows)
+    bool sym = false;
+    if (int rc = csr_symmetric(gd, c->v_begin, nloc, c->stream, &sym)) return rc;
+    if (sym && nloc) {
+        uint32_t* bad = nullptr;
+        uint32_t h = 0;
+        MCMC_HIP_TRY(hipMalloc(&bad, sizeof(uint32_t)));
+        hipError_t e = hipMemsetAsync(bad, 0, sizeof(uint32_t), c->stream);
+        if (e == hipSuccess) {
+            xs_dupcheck_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 3u) / 4u, 65535u)), 256, 0, c->stream>>>(
+                gd.row_off + c->v_begin, gd.col_idx, nloc, bad);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&h, bad, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(bad);
+        if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("duplicate-arc check: ") + hipGetErrorString(e));
+        sym = h == 0;
+    }
+    if (whole) gd.simple_sym = sym ? 1 : 0;
+    *ok = sym;
+    return MCMC_OK;
+}
+
+// The dense-count sweep of a tiled context (dense_counts.h), when the graph allows it and
+// MCMC_DENSE is not 0: S = the first |S| local rows, |S| such that a row's expected neighbours in
+// S number nCol (ln nCol + 10) (MCMC_DENSE_ROWS overrides |S|); counts, masks and lists allocated.
+int setup_dense(mcmc_ctx* c, uint32_t nloc) {
+    const char* de = getenv("MCMC_DENSE");
+    if ((de && atoi(de) == 0) || nloc == 0 || c->p.nCol > 256 || !c->tl) return MCMC_OK;
+    bool ok = false;
+    if (int rc = local_simple_symmetric(c, &ok)) return rc;
+    if (!ok) return MCMC_OK;
+    const uint32_t nCol = c->p.nCol;
+    const double dbar = (double)c->tl->arcs / (double)nloc;
+    const double target = (double)nCol * (std::log((double)nCol) + 10.0);
+    uint64_t S = dbar > 0.0 ? (uint64_t)std::ceil(target * (double)c->n / dbar) : nloc;
+    if (const char* dr = getenv("MCMC_DENSE_ROWS")) S = (uint64_t)std::max(1, atoi(dr));
+    S = std::max<uint64_t>(1, std::min<uint64_t>(S, nloc));
+    const size_t cnt_bytes = (size_t)nloc * nCol * sizeof(uint32_t);
+    if (cnt_bytes > (64ull << 30)) return MCMC_OK;   // counts beyond 64 GiB: the scan sweep
+    c->dc_s0 = c->v_begin;
+    c->dc_s1 = c->v_begin + (uint32_t)S;
+    c->dc_cap = (uint32_t)S;
+    c->dc_max = std::max<uint32_t>(64u, (uint32_t)(S / 8u));
+    c->dc_apow = minstd_pow(kMinstdA, 64ull * c->grid.x * (c->block.x / 64u));
+    hipError_t e = hipMalloc(&c->dc_ctl, sizeof(uint32_t) * (kDcWords + 2ull * S));
+    if (e == hipSuccess) e = hipMalloc(&c->dc_cnt, std::max<size_t>(cnt_bytes, 4));
+    if (e == hipSuccess) e = hipMalloc(&c->dc_mask, sizeof(uint32_t) * (size_t)nloc * c->nw);
+    if (e != hipSuccess) {
+        (void)hipFree(c->dc_ctl);
+        (void)hipFree(c->dc_cnt);
+        (void)hipFree(c->dc_mask);
+        c->dc_ctl = c->dc_cnt = c->dc_mask = nullptr;
+        if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return MCMC_OK; }   // the scan sweep then
+        return fail(MCMC_E_HIP, std::string("dense counts: ") + hipGetErrorString(e));
+    }
+    c->dc = true;
+    e = dc_reset(c);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("dense counts: ") + hipGetErrorString(e));
     return MCMC_OK;
 }
 
@@ -3744,11 +3918,16 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 c->lds += ob;
             }
         }
+        // the dense-count sweep (dense_counts.h) where it applies; MCMC_DENSE=0 keeps the scan
+        if (!ref && c->early) {
+            int rd = setup_dense(c, nloc);
+            if (rd) { mcmc_destroy(c); return rd; }
+        }
         // the tail queue (streaming early exit with more blocks than the dense ones): every
         // workgroup's queues hold all rows of its groups
         const char* tqe = getenv("MCMC_TQ_DENSE");
         const uint32_t tqd = tqe ? (uint32_t)std::max(0, atoi(tqe)) : 2u;
-        if (!ref && c->early && !resident && tqd > 0 && tqd < c->nblocks && c->tl->ngroups > 0) {
+        if (!ref && c->early && !c->dc && !resident && tqd > 0 && tqd < c->nblocks && c->tl->ngroups > 0) {
             const uint32_t gpw = (c->tl->ngroups + c->grid.x - 1) / c->grid.x;
             c->tq_cap = gpw * R;
             const size_t ents = (size_t)c->grid.x * 2u * c->tq_cap;
@@ -3775,6 +3954,13 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 ea = wi == 0 ? allow_lds_tiled<1, false, true>(c->lds) : wi == 1 ? allow_lds_tiled<2, false, true>(c->lds)
                    : wi == 2 ? allow_lds_tiled<4, false, true>(c->lds) : allow_lds_tiled<8, false, true>(c->lds);
             }
+        } else if (c->dc) {   // the dense-count sweep (update + evaluation launches)
+            static const SweepLaunch tab[4] = {launch_dc<1>, launch_dc<2>, launch_dc<4>, launch_dc<8>};
+            c->sweep = tab[wi];
+            c->sweep_diag = nullptr;
+            c->lds = kDcEvalLds;
+            ea = wi == 0 ? allow_lds_dc<1>(c->lds) : wi == 1 ? allow_lds_dc<2>(c->lds)
+               : wi == 2 ? allow_lds_dc<4>(c->lds) : allow_lds_dc<8>(c->lds);
         } else if (c->early) {   // the early-exit instantiations
             if (resident) {
                 static const SweepLaunch tab[4] = {launch_tiled<1, true, false, true>, launch_tiled<2, true, false, true>,
@@ -4031,6 +4217,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     const uint32_t s0 = minstd_seed_state(c->p.seed);
     if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(c->v_end - c->v_begin, 1u), c->stream));
     if (c->inc) MCMC_HIP_TRY(inc_reset(c));
+    if (c->dc) MCMC_HIP_TRY(dc_reset(c));
     if (C0) {
         for (uint32_t v = 0; v < n; v++)
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
@@ -4228,6 +4415,26 @@ int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
     MCMC_HIP_TRY(hipMemcpy(h, c->inc + kIncStat, sizeof(h), hipMemcpyDeviceToHost));
     out[0] = 1;
     for (int i = 0; i < 4; i++) out[1 + i] = h[i];
+    return MCMC_OK;
+}
+
+int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[8]) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    for (int i = 0; i < 8; i++) out[i] = 0;
+    if (!c->dc) return MCMC_OK;
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    uint32_t h[kDcWords];
+    MCMC_HIP_TRY(hipMemcpyAsync(h, c->dc_ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(h + kDcStat);
+    out[0] = 1;
+    out[1] = c->dc_s0;
+    out[2] = c->dc_s1;
+    out[3] = s[0];
+    out[4] = s[1];
+    out[5] = s[2];
+    out[6] = s[3];
+    out[7] = c->dc_max;
     return MCMC_OK;
 }
 
@@ -4574,6 +4781,9 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->gmask);
     (void)hipFree(c->etab);
     (void)hipFree(c->scan_stats);
+    (void)hipFree(c->dc_ctl);
+    (void)hipFree(c->dc_cnt);
+    (void)hipFree(c->dc_mask);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
@@ -4910,6 +5120,7 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t*
     c->world = world;
     c->rank = rank;
     c->part = true;
+    if (c->dc && c->stream) MCMC_HIP_TRY(dc_reset(c));   // new replicas: the counts are rebuilt
     // the caller's stream as given: 0 is the legacy null stream (torch's default current stream)
     // the context's uploads so far ran on its own (non-blocking) stream: finish them before the
     // caller's stream takes over, or the first sweep could overtake them

@@ -1,0 +1,155 @@
+"""The dense-count sweep (mcmc_colorer_amd/csrc/dense_counts.h) against the oracle.
+
+Each tiled context keeps, per row, the counts of the colours of its neighbours in a dense column
+range S of its own rows, moved every sweep by the vertices of S that changed colour (or rebuilt);
+a row whose dense mask is full is evaluated without scanning, the others scan their remaining
+column blocks first. Bar: bit-exact -- colouring, per-sweep Cviol trajectory, iteration count and
+glibc draws equal the oracle's restatement of ColoringMCMC_CPU::run (coloringMCMC_CPU.cpp:115-270).
+MCMC_DENSE_ROWS shrinks S so that most rows scan past it and the update lists overflow (the
+rebuild path); MCMC_DENSE=0 is the tiled scan sweep.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_ref as O
+from test_gpu_parity import assert_same, circulant, gpu_run, oracle_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def M(hip_lib):
+    import mcmc_colorer_amd.colorer as M
+
+    return M
+
+
+def dense_stats(col):
+    from mcmc_colorer_amd._lib import check, lib, u64ptr
+
+    out = np.zeros(8, dtype=np.uint64)
+    check(lib().mcmc_get_dense_stats(col._ctx, u64ptr(out)))
+    return {"on": int(out[0]), "s0": int(out[1]), "s1": int(out[2]), "incremental": int(out[3]),
+            "rebuilds": int(out[4]), "listed": int(out[5]), "open": int(out[6]), "max": int(out[7])}
+
+
+CASES = [
+    # n, p, nCol, seed, eps, taboo, maxRip, |S| (None: the library's choice)
+    (3000, 0.02, 16, 31, 1e-8, 0, 60, None),
+    (3000, 0.02, 16, 31, 1e-8, 0, 60, 40),
+    (2000, 0.05, 100, 32, 1e-8, 2, 20, 300),
+    (1500, 0.3, 5, 33, 3.3e6, 1, 15, 200),
+    (2500, 0.1, 200, 34, 1e-8, 0, 10, 1000),
+    (4000, 0.05, 32, 35, 1e-3, 0, 30, 2000),
+    (4000, 0.05, 32, 36, 1e-3, 3, 30, None),
+    (900, 0.08, 33, 3, 1e-8, 4, 40, 100),
+    (1200, 0.05, 64, 4, 1e-8, 1, 40, 64),
+    (3000, 0.01, 9, 10, 1e-8, 0, 250, 500),
+    (64, 0.5, 2, 11, 1e-8, 0, 50, None),
+    (1, 0.5, 1, 12, 1e-8, 0, 5, None),
+]
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,eps,taboo,maxrip,srows", CASES)
+def test_dense_matches_oracle(M, monkeypatch, n, p, ncol, seed, eps, taboo, maxrip, srows):
+    if srows is not None:
+        monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, tabooIteration=taboo, maxRip=maxrip)
+    col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip, taboo=taboo)
+    assert_same(col, st, r)
+    ds = dense_stats(col)
+    assert ds["on"] == 1 and ds["s0"] == 0 and ds["s1"] == (min(srows, n) if srows else ds["s1"])
+    assert ds["rebuilds"] >= 1   # the first sweep builds the counts
+    if st.sweepsRun > 3 and eps <= 1e-8:
+        assert ds["incremental"] >= 1
+    if srows is not None and srows < n // 4 and n > 1000:
+        assert ds["open"] > 0    # rows whose neighbours in S miss a colour scanned the other blocks
+
+
+def test_dense_list_overflow_rebuilds(M, monkeypatch):
+    """eps = 3.3e6 changes most colours every sweep: with |S| = 600 (rebuild threshold 75 listed
+    vertices) the update lists outgrow the threshold and the counts are rebuilt, still exact."""
+    monkeypatch.setenv("MCMC_DENSE_ROWS", "600")
+    off, idx, nc, r = oracle_case(1500, 0.3, 7, 9, epsilon=3.3e6, tabooIteration=0, maxRip=25)
+    col, st, _ = gpu_run(M, off, idx, nc, 9, 1500 * 1501 // 2, eps=3.3e6, maxRip=25)
+    assert_same(col, st, r)
+    ds = dense_stats(col)
+    assert ds["max"] == 75 and ds["rebuilds"] > 1
+
+
+def test_dense_off_is_the_scan_sweep(M, monkeypatch):
+    monkeypatch.setenv("MCMC_DENSE", "0")
+    off, idx, nc, r = oracle_case(3000, 0.02, 16, 31, epsilon=1e-8, maxRip=60)
+    col, st, _ = gpu_run(M, off, idx, nc, 31, 3000 * 3001 // 2, maxRip=60)
+    assert_same(col, st, r)
+    assert dense_stats(col)["on"] == 0
+
+
+def test_dense_needs_simple_symmetric_graph(M):
+    """A directed ring (v -> v+1..v+4 only) and a CSR with a repeated arc: the counts could not be
+    moved through the changed vertices' own rows, so the context keeps the scan sweep (exact)."""
+    n, K = 3000, 4
+    idx = ((np.arange(n)[:, None] + np.arange(1, K + 1)[None, :]) % n).astype(np.uint32)
+    idx.sort(axis=1)
+    off = np.arange(0, n * K + 1, K, dtype=np.uint64)
+    O.srand(1)
+    r = O.mcmc_run(off, idx.ravel(), 3, 5, maxRip=20)
+    col, st, _ = gpu_run(M, off, idx.ravel(), 3, 5, 0, maxRip=20)
+    assert_same(col, st, r)
+    assert dense_stats(col)["on"] == 0
+    off2, idx2 = circulant(2000, 3)
+    rows = np.split(idx2, off2[1:-1].astype(np.int64))
+    rows[5] = np.sort(np.append(rows[5], rows[5][0]))
+    idx3 = np.concatenate(rows).astype(np.uint32)
+    off3 = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.uint64)
+    O.srand(1)
+    r = O.mcmc_run(off3, idx3, 4, 6, maxRip=20)
+    col, st, _ = gpu_run(M, off3, idx3, 4, 6, 0, maxRip=20)
+    assert_same(col, st, r)
+    assert dense_stats(col)["on"] == 0
+
+
+@pytest.mark.parametrize("eps,srows", [(1e-8, None), (1e-3, None), (1e-8, 3000)])
+def test_dense_generated_graph_matches_oracle(M, monkeypatch, eps, srows):
+    """The counter-based G(n, p) (no CSR: rows come from the tiled layout), n = 150000, mean degree
+    450, 32 colours: 8 sweeps equal to the oracle on the same graph."""
+    if srows:
+        monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
+    n, p, seed = 150000, 0.003, 8
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 32, seed, epsilon=eps, maxRip=7, nthreads=8)
+    g = M.Graph.er_fast(n, p, seed)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=32, epsilon=eps, maxRip=7))
+    st = col.run(0)
+    assert_same(col, st, r)
+    ds = dense_stats(col)
+    assert ds["on"] == 1 and ds["incremental"] >= 6
+    if srows:
+        assert ds["open"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dense_partitioned_loopback(M, monkeypatch, world):
+    """Every rank keeps the counts of its own rows over a range of its own rows (|S| = 150 each:
+    most rows scan past it); the native loopback driver's run equals the oracle's."""
+    from mcmc_colorer_amd.distributed import LoopbackPartition, plan_rows
+
+    monkeypatch.setenv("MCMC_DENSE_ROWS", "150")
+    off, idx, nc, r = oracle_case(3000, 0.02, 16, 41, epsilon=1e-3, maxRip=30)
+    g = M.Graph.from_csr(off, idx)
+    lp = LoopbackPartition(g, M.ColoringMCMCParams(nCol=nc, epsilon=1e-3, maxRip=30), 41, plan_rows(3000, world))
+    st = lp.run(M.GlibcRand(1, 3000 * 3001 // 2))
+    for k in range(world):
+        assert lp.coloring(k).tolist() == r.colors.tolist(), k
+        assert lp.trajectory(k).tolist() == r.traj.tolist(), k
+        assert (st[k].iter, st[k].finalViol, st[k].glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+    from mcmc_colorer_amd._lib import check, lib, u64ptr
+
+    out = np.zeros(8, dtype=np.uint64)
+    check(lib().mcmc_get_dense_stats(lp._ctx[world - 1], u64ptr(out)))
+    b = plan_rows(3000, world)
+    assert out[0] == 1 and out[1] == b[world - 1] and out[2] == b[world - 1] + 150 and out[3] > 0
+    lp.close()
