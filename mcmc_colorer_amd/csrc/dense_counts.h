@@ -162,9 +162,12 @@ __device__ __noinline__ void dc_open_scan(const SweepArgs& a, const uint8_t* __r
     }
 }
 
-// Sweep t's evaluation: persistent, one 1024-thread workgroup per CU, wave w of the grid takes the
-// 64-row tiles w, w + (all waves), ...; lane per row. u_v of row l is x_t 16807^(v_begin + l + 1):
-// the wave's running power advances by 16807^(64 x all waves) per tile (a.dc_apow).
+// Sweep t's evaluation: persistent, one 1024-thread workgroup per CU; wave w of the grid takes the
+// 64-row tiles w, w + W, w + 2 W, ... (W = all waves), kDcTiles of them per step with every load
+// issued before the first evaluation (each tile alone is one dependent HBM round trip); lane per
+// row. u_v of row l is x_t 16807^(v_begin + l + 1): 16807^(64 W) (a.dc_apow) steps a tile's power to
+// the next tile of the wave.
+constexpr int kDcTiles = 4;
 template <int NW>
 __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     extern __shared__ uint4 dc_lds[];
@@ -202,26 +205,41 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     const uint32_t ntiles = (nloc + 63u) >> 6;
     uint32_t wave_viol = 0, wave_ev = 0, wave_open = 0;
     const uint32_t lpow = kMinstdLanePow[lane];
+    uint32_t apk[kDcTiles];   // 16807^(64 W k)
+    apk[0] = 1u;
+#pragma unroll
+    for (int k = 1; k < kDcTiles; k++) apk[k] = minstd_mulmod(apk[k - 1], a.dc_apow);
+    const uint32_t astep = minstd_mulmod(apk[kDcTiles - 1], a.dc_apow);
     uint32_t xb = gw < ntiles ? minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + 64ull * gw + 1ull)) : 0u;
-    for (uint32_t tau = gw; tau < ntiles; tau += GW) {
-        const uint32_t l = 64u * tau + (uint32_t)lane;
-        const bool valid = l < nloc;
-        uint32_t acc[NW];
+    for (uint32_t tau0 = gw; tau0 < ntiles; tau0 += kDcTiles * GW) {
+        uint32_t acc[kDcTiles][NW], cv[kDcTiles], tab[kDcTiles];
 #pragma unroll
-        for (int i = 0; i < NW; i++) acc[i] = valid ? a.dc_mask[(size_t)l * NW + i] : 0u;
-        const uint32_t cv = valid ? (uint32_t)C[a.v_begin + l] : 0u;
-        const uint32_t tab = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;
-        bool full = true;
+        for (int k = 0; k < kDcTiles; k++) {
+            const uint32_t l = 64u * (tau0 + k * GW) + (uint32_t)lane;
+            const bool valid = l < nloc;
 #pragma unroll
-        for (int i = 0; i < NW; i++) full = full && ((acc[i] & fullw[i]) == fullw[i]);
-        const bool open = valid && !full;
-        const uint64_t ob = __ballot(open);
-        if (ob) {
-            wave_open += (uint32_t)__popcll(ob);
-            dc_open_scan<NW>(a, C, l, open, acc, fullw, lane);
+            for (int i = 0; i < NW; i++) acc[k][i] = valid ? a.dc_mask[(size_t)l * NW + i] : 0u;
+            cv[k] = valid ? (uint32_t)C[a.v_begin + l] : 0u;
+            tab[k] = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;
         }
-        wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, acc, lane, wave_ev, vf, cv, tab, minstd_mulmod(xb, lpow), ew);
-        xb = minstd_mulmod(xb, a.dc_apow);
+#pragma unroll
+        for (int k = 0; k < kDcTiles; k++) {
+            const uint32_t l = 64u * (tau0 + k * GW) + (uint32_t)lane;
+            const bool valid = l < nloc;
+            if (!__ballot(valid)) break;   // this wave's tiles end here (uniform)
+            bool full = true;
+#pragma unroll
+            for (int i = 0; i < NW; i++) full = full && ((acc[k][i] & fullw[i]) == fullw[i]);
+            const bool open = valid && !full;
+            const uint64_t ob = __ballot(open);
+            if (ob) {
+                wave_open += (uint32_t)__popcll(ob);
+                dc_open_scan<NW>(a, C, l, open, acc[k], fullw, lane);
+            }
+            wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, acc[k], lane, wave_ev, vf, cv[k], tab[k],
+                                           minstd_mulmod(minstd_mulmod(xb, apk[k]), lpow), ew);
+        }
+        xb = minstd_mulmod(xb, astep);
     }
     if (wave_open) {   // statistics; the commit reads the word (this workgroup releases)
         if (lane == 0) atomicAdd(&a.dc_ctl[kDcOpen], wave_open);

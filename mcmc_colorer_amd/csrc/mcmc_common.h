@@ -33,6 +33,7 @@ struct GraphDev {
     int sym = -1;                  // whole CSR symmetric: 1 yes, 0 no, -1 not checked (csr_symmetric)
     int simple_sym = -1;           // every arc's reverse present and no arc repeated: 1 yes (the counter-based
                                    // G(n, p) by construction, or checked), 0 no, -1 not known
+    bool partial_rows = false;     // generated for a row range only: rows outside it hold no arcs
     uint64_t* row_off = nullptr;   // [n+1]
     uint32_t* col_idx = nullptr;   // [m]
 };

@@ -69,6 +69,8 @@ struct DevState {
 
 struct SweepArgs {
     const uint64_t* row_off;    // local rows: row_off[v - v_begin], length (v_end - v_begin) + 1
+    const uint64_t* row_off_g;  // the whole graph's offsets (row_off_g[v], any v): the wide sweep's
+                                // partitioned incremental counts read other ranks' rows
     const uint32_t* col_idx;    // global vertex ids
     uint8_t* colors0;           // full-length colour replicas (C_t lives in colors[t & 1])
     uint8_t* colors1;
@@ -160,7 +162,6 @@ struct SweepArgs {
     // tiled sweep: stop scanning a row once its occupancy mask holds every colour (count_free_colors
     // cannot change any more: the sweep's results are unchanged); 0 = scan every arc (A/B runs)
     int early;
-    uint32_t dbg_max_pairs;     // diagnostics only (MCMC_DEBUG_MAX_PAIRS): cut every group after k pairs (wrong results)
     uint32_t drain_rows;        // tiled early exit: a group with at most this many rows left drains them (<= 256)
     // tiled early exit: a group's next pair (its next block) is staged at the END of the current
     // pair's scan, and only while some row is still open (rows expected to fill inside a block: C2)
@@ -205,13 +206,16 @@ struct SweepArgs {
     // (vslot[p][eb], p = t & 1): the next sweep's flag pass starts from them.
     uint32_t* inc;              // [kIncWords] control words
     uint32_t* inc_vcnt;         // [nloc] same-colour arcs of every row in C_t
-    uint32_t* inc_hub;          // [2][nloc] changed rows above inc_hub_arcs arcs
+    uint32_t* inc_hub;          // [2][inc_lcap] changed rows above inc_hub_arcs arcs (global ids)
     uint32_t* inc_tch;          // [2][nloc] rows whose count left 0 in sweep t's delta pass
     uint32_t* inc_eslot;        // [2][evnblk][2 + inc_slot] evaluation workgroups' changed rows
     uint32_t* inc_vslot;        // [2][evnblk][2 + inc_slot] evaluation workgroups' violators of C_t
     uint32_t* inc_wslot;        // [2][kWalkBlocks][2 + inc_wslot_n] walk workgroups' changed rows
-    uint32_t* inc_cchg;         // [2][2 + ev_cap] the commit's changed rows (a slot)
-    uint32_t* inc_dense;        // [2][nloc] every changed row but the hubs, gathered by the commit
+    uint32_t* inc_cchg;         // [2][2 + inc_ccap] the commit's changed rows (a slot; global ids)
+    uint32_t* inc_dense;        // [2][inc_lcap] every changed row but the hubs (global ids), gathered by
+                                //   the commit: this rank's, the event replay's, other ranks' (delta mode)
+    uint32_t inc_lcap;          // entries of those lists: n (changed rows of a sweep are distinct vertices)
+    uint32_t inc_ccap;          // entries of the commit's slot inc_cchg (the replayed events of every rank: n)
     uint32_t* inc_hdr;          // [2][evnblk + kWalkBlocks][2] the slots' headers again, side by side (the
                                 //   commit reads them all: one workgroup's loads, ~64 GB/s per CU)
     uint32_t inc_slot, inc_wslot_n;   // rows per evaluation / walk slot (past it: the next sweep recounts)
@@ -279,7 +283,7 @@ __device__ __forceinline__ uint32_t inc_list_deg(const SweepArgs& a, uint32_t l,
                                                  uint32_t cap, uint32_t* lcount, uint32_t deg) {
     const uint32_t q = (t + 1u) & 1u;
     if (deg > a.inc_hub_arcs) {
-        a.inc_hub[(size_t)q * (a.v_end - a.v_begin) + atomicAdd(&a.inc[kIncHubN + q], 1u)] = l;
+        a.inc_hub[(size_t)q * a.inc_lcap + atomicAdd(&a.inc[kIncHubN + q], 1u)] = a.v_begin + l;
     } else {
         const uint32_t k = atomicAdd(lcount, 1u);   // LDS
         if (k < cap) slot[2 + k] = l;
@@ -291,6 +295,24 @@ __device__ __forceinline__ uint32_t inc_list(const SweepArgs& a, uint32_t l, uin
                                              uint32_t cap, uint32_t* lcount) {
     return inc_list_deg(a, l, t, slot, cap, lcount, (uint32_t)(a.row_off[l + 1] - a.row_off[l]));
 }
+// The same for vertex v by its global id (the event replay: any rank's vertex). Slot entries of this
+// kind hold global ids (the commit's own slot, inc_cchg).
+__device__ __forceinline__ uint32_t inc_list_global(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t* slot,
+                                                    uint32_t cap, uint32_t* lcount) {
+    const uint32_t q = (t + 1u) & 1u, deg = (uint32_t)(a.row_off_g[v + 1] - a.row_off_g[v]);
+    if (deg > a.inc_hub_arcs) {
+        a.inc_hub[(size_t)q * a.inc_lcap + atomicAdd(&a.inc[kIncHubN + q], 1u)] = v;
+    } else {
+        const uint32_t k = atomicAdd(lcount, 1u);   // LDS
+        if (k < cap) slot[2 + k] = v;
+        else a.inc[kIncOvf + q] = 1u;
+    }
+    return deg;
+}
+
+constexpr uint32_t kDeltaWords = 4096;  // MCMC delta slot per rank: head + (v, c) pairs (16 KiB)
+constexpr uint32_t kDeltaHead = 2;
+constexpr uint32_t kDeltaPairs = (kDeltaWords - kDeltaHead) / 2;
 
 // The commit's end of sweep t (all its threads): its own slot's header, the rows and arcs every
 // writer listed, the statistics, and the choice for sweep t + 1 -- a full recount after a slot
@@ -300,7 +322,7 @@ __device__ void inc_commit(const SweepArgs& a, uint32_t t, const uint32_t* cc) {
     __shared__ unsigned long long red[2][32];
     __shared__ unsigned long long pre[8];   // control words, loaded side by side (not one chain on thread 0)
     __shared__ uint32_t wtot[32];
-    const uint32_t q = (t + 1u) & 1u, nloc = a.v_end - a.v_begin;
+    const uint32_t q = (t + 1u) & 1u;
     if (threadIdx.x < 7u) {
         const uint32_t i = threadIdx.x;
         pre[i] = i == 0 ? a.inc[kIncMode] : i == 1 ? a.inc[kIncOvf + q] : i == 2 ? a.inc[kIncHubN + q]
@@ -340,19 +362,46 @@ __device__ void inc_commit(const SweepArgs& a, uint32_t t, const uint32_t* cc) {
         if (w < wave) off += wtot[w];
         T += wtot[w];
     }
-    uint32_t* dn = a.inc_dense + (size_t)q * nloc;
+    uint32_t* dn = a.inc_dense + (size_t)q * a.inc_lcap;
     for (uint32_t i = s0; i < s1; i++) {
         uint32_t cap;
         const uint32_t* sl = slot(i, cap);
         const uint32_t c = min(sl[0], cap);
-        for (uint32_t k = 0; k < c; k++) dn[off + k] = sl[2 + k];
+        for (uint32_t k = 0; k < c; k++) dn[off + k] = a.v_begin + sl[2 + k];   // (slots: local rows)
         off += c;
     }
-    const uint32_t* cl = a.inc_cchg + (size_t)q * (2u + a.ev_cap);   // the event replay's rows after them
+    const uint32_t* cl = a.inc_cchg + (size_t)q * (2u + a.inc_ccap);   // the event replay's rows after them
     for (uint32_t k = threadIdx.x; k < cc[0]; k += blockDim.x) dn[T + k] = cl[2 + k];
+    // a partitioned delta-mode commit: the other ranks' changed vertices (their delta slots) after
+    // those -- their rows' arcs into this rank's rows move its counts, and the next sweep copies
+    // their colours into its output buffer (part_commit_kernel wrote them into C_t+1's only)
+    __shared__ uint32_t s_rem;
+    __shared__ unsigned long long s_rarcs;
+    if (threadIdx.x == 0) {
+        s_rem = 0;
+        s_rarcs = 0;
+    }
+    __syncthreads();
+    if (a.world > 1 && a.part_delta > 0) {
+        const uint32_t* dall = (t & 1) ? a.dall0 : a.dall1;   // sweep t's slots (next-colour parity)
+        for (uint32_t r = 0; r < a.world; r++) {
+            if (r == a.rank) continue;
+            const uint32_t* d = dall + (size_t)r * kDeltaWords;
+            const uint32_t nr = min(d[0], kDeltaPairs);
+            for (uint32_t i = threadIdx.x; i < nr; i += blockDim.x) {
+                const uint32_t v = d[kDeltaHead + 2u * i];
+                const uint32_t deg = (uint32_t)(a.row_off_g[v + 1] - a.row_off_g[v]);
+                if (deg > a.inc_hub_arcs) a.inc_hub[(size_t)q * a.inc_lcap + atomicAdd(&a.inc[kIncHubN + q], 1u)] = v;
+                else dn[T + cc[0] + atomicAdd(&s_rem, 1u)] = v;
+                atomicAdd(&s_rarcs, (unsigned long long)deg);
+            }
+        }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         for (uint32_t w = 1; w < nwv; w++) arcs += red[1][w];
-        a.inc[kIncDenseN + q] = T + cc[0];
+        arcs += s_rarcs;
+        a.inc[kIncDenseN + q] = T + cc[0] + s_rem;
         const unsigned long long rows = (unsigned long long)T + cc[0] + pre[2];
         arcs += cc[1];
         unsigned long long* s = reinterpret_cast<unsigned long long*>(a.inc + kIncStat);
@@ -360,15 +409,14 @@ __device__ void inc_commit(const SweepArgs& a, uint32_t t, const uint32_t* cc) {
         s[1] = pre[4] + (pre[0] ? 1ull : 0ull);
         s[2] = pre[5] + rows;
         s[3] = pre[6] + arcs;
-        a.inc[kIncMode] = (pre[1] || arcs > a.inc_thresh) ? 1u : 0u;
+        // a full-mode exchange tells no rank which of the others' vertices changed: a recount
+        const bool blind = a.world > 1 && a.part_delta <= 0;
+        a.inc[kIncMode] = (pre[1] || arcs > a.inc_thresh || blind) ? 1u : 0u;
     }
 }
 constexpr uint32_t kPairTraceMax = 256;   // pairs traced per workgroup (MCMC_PAIR_TRACE)
 constexpr uint32_t kPairTraceRec = 8;     // {start, scan end min, scan end max, eval end, barrier end, info, 0, 0}
 constexpr uint32_t kHistWords = 260;   // colours 0..255 (a colour may equal nCol <= 255)
-constexpr uint32_t kDeltaWords = 4096;  // MCMC delta slot per rank: head + (v, c) pairs (16 KiB)
-constexpr uint32_t kDeltaHead = 2;
-constexpr uint32_t kDeltaPairs = (kDeltaWords - kDeltaHead) / 2;
 
 // Phase timestamps of the last sweep, 8 slots per workgroup (wall_clock64, 100 MHz): 0 start,
 // 1 first scan begins, 2 scans done, 3 evaluation done, 4 tail done (last workgroup: commit done).
@@ -570,13 +618,14 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
             Cs[v] = (CT)c;
             // delta mode: both replicas carry C_t+1 on the remote rows (part_commit_kernel)
-            if (a.part_delta > 0 && (v < a.v_begin || v >= a.v_end)) const_cast<CT*>(C)[v] = (CT)c;
+            // (the wide sweep's incremental counts need C_t there: its next sweep copies the change)
+            if (a.part_delta > 0 && a.inc == nullptr && (v < a.v_begin || v >= a.v_end)) const_cast<CT*>(C)[v] = (CT)c;
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
                 a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
-            if (a.inc != nullptr && c != (uint32_t)C[v])   // (whole-graph contexts: v = l)
-                atomicAdd(&inc_cc[1], inc_list(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.ev_cap),
-                                               a.ev_cap, &inc_cc[0]));
+            if (a.inc != nullptr && c != (uint32_t)C[v])   // (any rank's vertex: global ids)
+                atomicAdd(&inc_cc[1], inc_list_global(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.inc_ccap),
+                                                      a.inc_ccap, &inc_cc[0]));
             if (a.dc_list != nullptr && c != (uint32_t)C[v] && v - a.dc_s0 < a.dc_s1 - a.dc_s0) {
                 const uint32_t q = (t + 1u) & 1u;   // dense-count sweep: the next update moves v
                 const uint32_t idx = atomicAdd(&a.dc_ctl[kDcLen + q], 1u);
@@ -837,8 +886,8 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
         if (w < wave) soff += s_w2[w];
         T += s_w2[w];
     }
-    const uint32_t nloc = a.v_end - a.v_begin;
-    uint32_t* dn = inc ? a.inc_dense + (size_t)q * nloc : nullptr;
+
+    uint32_t* dn = inc ? a.inc_dense + (size_t)q * a.inc_lcap : nullptr;
     // ---- (3) the events' glibc draws and colours; the slots' rows into the dense list ----
     const CT_U16* C = reinterpret_cast<const CT_U16*>((t & 1) ? a.colors1 : a.colors0);
     CT_U16* Cs = reinterpret_cast<CT_U16*>((t & 1) ? a.colors0 : a.colors1);
@@ -866,7 +915,7 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
             const uint32_t n = q ? sc[1][j] : sc[0][j];
             const uint32_t* sl = i < nb ? a.inc_eslot + ((size_t)q * nb + i) * es
                                         : a.inc_wslot + ((size_t)q * kIncWalkSlots + (i - nb)) * ws;
-            for (uint32_t k = 0; k < n; k++) dn[soff + k] = sl[2 + k];
+            for (uint32_t k = 0; k < n; k++) dn[soff + k] = a.v_begin + sl[2 + k];
             soff += n;
         }
     }
@@ -878,12 +927,12 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
         if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
         if (a.taboo != nullptr) a.taboo[v - a.v_begin] = (c == oc) ? a.tabooIteration : 0u;
         if (inc && c != oc) {   // the replay's changed rows go straight after the slots' in the dense list
-            const uint32_t l = v - a.v_begin, deg = (uint32_t)(r1 - r0);
+            const uint32_t deg = (uint32_t)(r1 - r0);
             if (deg > a.inc_hub_arcs) {
-                a.inc_hub[(size_t)q * nloc + atomicAdd(&a.inc[kIncHubN + q], 1u)] = l;
+                a.inc_hub[(size_t)q * a.inc_lcap + atomicAdd(&a.inc[kIncHubN + q], 1u)] = v;
                 atomicAdd(&s_cc[2], 1u);
             } else {
-                dn[T + atomicAdd(&s_cc[0], 1u)] = l;
+                dn[T + atomicAdd(&s_cc[0], 1u)] = v;
             }
             atomicAdd(&s_cc[1], deg);
         }
@@ -1091,7 +1140,7 @@ __global__ __launch_bounds__(kCommitThreads) void part_commit_kernel(SweepArgs a
                     const uint32_t v = d[2u * i];
                     const CT c = (CT)d[2u * i + 1u];
                     B[v] = c;
-                    A[v] = c;
+                    if (a.inc == nullptr) A[v] = c;   // (incremental counts: the next sweep copies it)
                 }
             }
         }
@@ -2328,7 +2377,7 @@ __device__ __forceinline__ void tile_tail(const SweepArgs& a, DevState* __restri
 // same-colour arcs (own colours from the replica, or streamed per group into LDS), the evaluation
 // is evaluate_ref_tile, the arrival carries the count (sweep_tail_ref).
 // DG: the diagnostics instantiation (scan_stats counters, MCMC_PHASE_DUMP cycle accounting,
-// MCMC_DEBUG_MAX_PAIRS), kept out of the timed kernels' registers.
+// kept out of the timed kernels' registers.
 template <int NW, bool RES, bool REF, bool EX, bool DG = false>
 __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
     extern __shared__ uint4 lds_raw[];
@@ -2521,7 +2570,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
         }
         const uint32_t kslot = kpair % 3u;
         // the group's last pair: its last block, every row already full, or the drain
-        const bool last = (b + 1 == nb) || allfull || drain || split || (DG && a.dbg_max_pairs && b + 1 >= a.dbg_max_pairs);
+        const bool last = (b + 1 == nb) || allfull || drain || split;
         // the next pair's row cursor (its first nwaves * nsub rows are assigned statically)
         if (threadIdx.x == 0) sh.cursor[buf ^ 1u] = nwaves * nsub;
         // the next pair: its table (and slice) by DMA into the other buffers, its first-row bounds
@@ -3200,6 +3249,7 @@ int download_state(mcmc_ctx* c, DevState* h) {
 SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     SweepArgs a{};
     a.row_off = c->g->row_off ? c->g->row_off + c->v_begin : nullptr;
+    a.row_off_g = c->g->row_off;
     a.col_idx = c->g->col_idx;
     a.colors0 = c->colors[0];
     a.colors1 = c->colors[1];
@@ -3234,7 +3284,6 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.ewalk_off = c->ewalk_off;
     a.drain_rows = c->drain_rows;
     a.late_stage = c->late_stage;
-    if (const char* dm = getenv("MCMC_DEBUG_MAX_PAIRS")) a.dbg_max_pairs = (uint32_t)atoi(dm);
     a.scan_stats = c->scan_stats_on ? c->scan_stats : nullptr;
     a.fused = c->part ? 2 : (check_done ? c->fused : 0);
     a.seg = c->seg;
@@ -3323,18 +3372,20 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.xs_cbits = c->xs->cbits;
             a.xs_sym = c->xs->sym;
         }
-        if (c->inc && !c->part) {
-            const size_t nloc = c->v_end - c->v_begin;
+        if (c->inc) {   // (layout: inc_words)
+            const size_t nloc = c->v_end - c->v_begin, L = c->n;
             a.inc = c->inc;
             a.inc_vcnt = c->inc + kIncWords;
             a.inc_hub = a.inc_vcnt + nloc;
-            a.inc_tch = a.inc_hub + 2 * nloc;
+            a.inc_tch = a.inc_hub + 2 * L;
             a.inc_eslot = a.inc_tch + 2 * nloc;
             a.inc_vslot = a.inc_eslot + 2 * (size_t)c->evnblk * (2 + c->inc_slot);
             a.inc_wslot = a.inc_vslot + 2 * (size_t)c->evnblk * (2 + c->inc_slot);
             a.inc_cchg = a.inc_wslot + 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n);
-            a.inc_dense = a.inc_cchg + 2 * (2 + (size_t)c->ev_cap);
-            a.inc_hdr = a.inc_dense + 2 * nloc;
+            a.inc_dense = a.inc_cchg + 2 * (2 + L);
+            a.inc_hdr = a.inc_dense + 2 * L;
+            a.inc_lcap = (uint32_t)L;
+            a.inc_ccap = (uint32_t)L;
             a.inc_slot = c->inc_slot;
             a.inc_wslot_n = c->inc_wslot_n;
             a.inc_hub_arcs = c->inc_hub_arcs;
@@ -3389,7 +3440,7 @@ int ensure_constants() {
 
 // The sweep launch for these arguments: the diagnostics instantiation when they ask for it.
 void launch_tiled_or_diag(mcmc_ctx* c, const SweepArgs& a) {
-    const bool diag = a.scan_stats || a.phase_ts || a.dbg_max_pairs || a.pair_trace;
+    const bool diag = a.scan_stats || a.phase_ts || a.pair_trace;
     (diag && c->sweep_diag ? c->sweep_diag : c->sweep)(a, c->grid, c->block, c->lds, c->stream);
 }
 
@@ -3537,13 +3588,13 @@ int run_tailcut(mcmc_ctx* c, const DevState& h, uint64_t* finalViol, uint32_t* p
     return MCMC_OK;
 }
 
-// Every local arc's reverse present and no local row listing a neighbour twice: then, for u and w
-// both local, w's row holds u exactly as often as u's row holds w (the dense counts' update reads
-// u's row for the rows holding u). Generated G(n, p) graphs are so by construction.
-int local_simple_symmetric(mcmc_ctx* c, bool* ok) {
-    GraphDev& gd = const_cast<GraphDev&>(*c->g);
-    const uint32_t nloc = c->v_end - c->v_begin;
-    const bool whole = c->v_begin == 0 && c->v_end == gd.n;
+// Every arc of rows [vb, ve) into that range has its reverse and no row of it lists a neighbour
+// twice: then, for u and w both in the range, w's row holds u exactly as often as u's row holds w
+// (the dense counts' update reads u's row for the rows holding u; the wide sweep's partitioned
+// incremental counts ask it of the whole graph). Generated G(n, p) graphs are so by construction.
+int simple_symmetric(GraphDev& gd, uint32_t vb, uint32_t ve, hipStream_t stream, bool* ok) {
+    const uint32_t nloc = ve - vb;
+    const bool whole = vb == 0 && ve == gd.n;
     *ok = false;
     if (gd.simple_sym == 1 || (whole && gd.simple_sym == 0)) {
         *ok = gd.simple_sym == 1;
@@ -3551,19 +3602,19 @@ int local_simple_symmetric(mcmc_ctx* c, bool* ok) {
     }
     if (!gd.row_off || !gd.sorted) return MCMC_OK;   // (tiled layouts of CSR graphs sort the rows)
     bool sym = false;
-    if (int rc = csr_symmetric(gd, c->v_begin, nloc, c->stream, &sym)) return rc;
+    if (int rc = csr_symmetric(gd, vb, nloc, stream, &sym)) return rc;
     if (sym && nloc) {
         uint32_t* bad = nullptr;
         uint32_t h = 0;
         MCMC_HIP_TRY(hipMalloc(&bad, sizeof(uint32_t)));
-        hipError_t e = hipMemsetAsync(bad, 0, sizeof(uint32_t), c->stream);
+        hipError_t e = hipMemsetAsync(bad, 0, sizeof(uint32_t), stream);
         if (e == hipSuccess) {
-            xs_dupcheck_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 3u) / 4u, 65535u)), 256, 0, c->stream>>>(
-                gd.row_off + c->v_begin, gd.col_idx, nloc, bad);
+            xs_dupcheck_kernel<<<std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 3u) / 4u, 65535u)), 256, 0, stream>>>(
+                gd.row_off + vb, gd.col_idx, nloc, bad);
             e = hipGetLastError();
         }
-        if (e == hipSuccess) e = hipMemcpyAsync(&h, bad, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&h, bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
         (void)hipFree(bad);
         if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("duplicate-arc check: ") + hipGetErrorString(e));
         sym = h == 0;
@@ -3580,7 +3631,7 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     const char* de = getenv("MCMC_DENSE");
     if ((de && atoi(de) == 0) || nloc == 0 || c->p.nCol > 256 || !c->tl) return MCMC_OK;
     bool ok = false;
-    if (int rc = local_simple_symmetric(c, &ok)) return rc;
+    if (int rc = simple_symmetric(const_cast<GraphDev&>(*c->g), c->v_begin, c->v_end, c->stream, &ok)) return rc;
     if (!ok) return MCMC_OK;
     const uint32_t nCol = c->p.nCol;
     const double dbar = (double)c->tl->arcs / (double)nloc;
@@ -4091,14 +4142,28 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         // next sweep recounts (2 on, the tests: slots hold every row, no arc limit)
         const char* wie = getenv("MCMC_WIDE_INC");
         const int winc = wie ? atoi(wie) : 1;
-        if (ew == hipSuccess && winc != 0 && c->xs && c->xs->mode == 1 && c->xs->simple && v_begin == 0 &&
-            v_end == gd.n) {
+        // A row range (a rank of a partitioned run) keeps them too when the graph holds every row's
+        // arcs and is simple and symmetric as a whole: other ranks' changed vertices move this rank's
+        // counts through their own rows (sweep_wide.h wide_inc_delta_kernel).
+        bool inc_ok = ew == hipSuccess && winc != 0 && c->xs && c->xs->mode == 1 && c->xs->simple;
+        if (inc_ok && !(v_begin == 0 && v_end == gd.n)) {
+            bool whole_ss = false;
+            if (!gd.partial_rows) {
+                int rs = simple_symmetric(const_cast<GraphDev&>(gd), 0, gd.n, c->stream, &whole_ss);
+                if (rs) { mcmc_destroy(c); return rs; }
+            }
+            inc_ok = whole_ss;
+        }
+        if (inc_ok) {
             const char* sv = getenv("MCMC_WIDE_INC_SLOT");
             c->inc_slot = winc == 2 ? 256u * kWideEvalPer : std::max<uint32_t>(1u, sv ? (uint32_t)atoi(sv) : 32u);
             c->inc_wslot_n = winc == 2 ? std::min<uint32_t>(nloc, 1u << 16) : std::max<uint32_t>(1u, c->inc_slot / 2u);
-            const size_t words = kIncWords + 5 * (size_t)nloc + 4 * (size_t)c->evnblk * (2 + c->inc_slot) +
-                                 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n) + 2 * (2 + (size_t)c->ev_cap) +
-                                 2 * (size_t)nloc + 4 * ((size_t)c->evnblk + kIncWalkSlots);
+            // layout (make_args): counts [nloc], hub lists [2][n], touched [2][nloc], the evaluation's
+            // and walks' slots, the commit's slots [2][2 + n], dense lists [2][n], slot headers
+            const size_t L = gd.n;
+            const size_t words = kIncWords + 3 * (size_t)nloc + 2 * L + 4 * (size_t)c->evnblk * (2 + c->inc_slot) +
+                                 2 * (size_t)kIncWalkSlots * (2 + c->inc_wslot_n) + 2 * (2 + L) +
+                                 2 * L + 4 * ((size_t)c->evnblk + kIncWalkSlots);
             ew = hipMalloc(&c->inc, sizeof(uint32_t) * words);
             if (ew == hipSuccess) ew = hipMemsetAsync(c->inc, 0, sizeof(uint32_t) * words, c->stream);
             const char* dv = getenv("MCMC_WIDE_INC_DIV");
@@ -4408,7 +4473,7 @@ int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]) {
 int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
     if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
     for (int i = 0; i < 5; i++) out[i] = 0;
-    if (!c->inc || c->part) return MCMC_OK;
+    if (!c->inc) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned long long h[4];
@@ -4857,7 +4922,7 @@ int part_set_delta(mcmc_ctx* c, uint32_t* d0, uint32_t* d1) {
     return MCMC_OK;
 }
 
-bool part_delta_ok(const mcmc_ctx* c) { return c && c->part && c->dlt[0] && !c->wide; }
+bool part_delta_ok(const mcmc_ctx* c) { return c && c->part && c->dlt[0]; }
 
 // A partition of one rank (world 1) steps exactly like a whole-graph context: the sweep commits in
 // its last workgroup (no footer, no exchange, no commit launch). Not for the reference-semantics mode.

@@ -203,17 +203,21 @@ __device__ __forceinline__ int inc_arcs(const SweepArgs& a, const uint16_t* __re
             const int d = (int)(nw[j] == cnv) - (int)(ow[j] == cov);
             if (d != 0) {
                 dv += d;
-                const uint32_t old = atomicAdd(&a.inc_vcnt[w[j]], (uint32_t)d);
-                if (d > 0 && old == 0u) inc_touch(a, w[j], t);
+                const uint32_t lw = w[j] - a.v_begin;   // counts of this context's rows only
+                if (lw < a.v_end - a.v_begin) {
+                    const uint32_t old = atomicAdd(&a.inc_vcnt[lw], (uint32_t)d);
+                    if (d > 0 && old == 0u) inc_touch(a, lw, t);
+                }
             }
         }
     }
     return dv;
 }
 __device__ __forceinline__ void inc_own(const SweepArgs& a, uint32_t v, int dv, uint32_t t) {
-    if (dv == 0) return;
-    const uint32_t old = atomicAdd(&a.inc_vcnt[v], (uint32_t)dv);
-    if (dv > 0 && old == 0u) inc_touch(a, v, t);
+    const uint32_t l = v - a.v_begin;
+    if (dv == 0 || l >= a.v_end - a.v_begin) return;   // another rank's row: its counts live there
+    const uint32_t old = atomicAdd(&a.inc_vcnt[l], (uint32_t)dv);
+    if (dv > 0 && old == 0u) inc_touch(a, l, t);
 }
 constexpr uint32_t kIncHubLds = 1024;   // hubs whose tasks a workgroup scans in LDS (more: a workgroup each)
 constexpr uint32_t kIncHubTask = 4096;  // arcs per hub task (4 per thread of a 1024-thread workgroup)
@@ -229,13 +233,21 @@ __global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
         ctl[kIncTchOvf + q] = 0;
         ctl[kIncHubN + q] = 0;
     }
+    const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);   // C_t
+    const uint16_t* __restrict__ Cp = reinterpret_cast<const uint16_t*>(p ? a.colors0 : a.colors1);   // C_t-1
     if (ctl[kIncMode]) {   // full sweep: the tile scan recounts
         for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += gridDim.x * blockDim.x)
             a.inc_vcnt[l] = 0;
+        // other ranks' vertices that changed into C_t (a delta-mode commit wrote them into C_t's buffer
+        // only): C_t+1's buffer takes them before this sweep's commit adds the next changes
+        uint16_t* __restrict__ Cs = const_cast<uint16_t*>(Cp);
+        const uint32_t nd = ctl[kIncDenseN + p], nh = ctl[kIncHubN + p];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd + nh; i += gridDim.x * blockDim.x) {
+            const uint32_t v = i < nd ? a.inc_dense[(size_t)p * a.inc_lcap + i] : a.inc_hub[(size_t)p * a.inc_lcap + (i - nd)];
+            if (v - a.v_begin >= nloc) Cs[v] = Cn[v];
+        }
         return;
     }
-    const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);   // C_t
-    const uint16_t* __restrict__ Cp = reinterpret_cast<const uint16_t*>(p ? a.colors0 : a.colors1);   // C_t-1
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t nh = ctl[kIncHubN + p];
     if (nh > 0 && nh <= kIncHubLds) {
@@ -244,8 +256,8 @@ __global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
         __shared__ uint32_t s_pre[kIncHubLds], s_v[kIncHubLds], s_w[16];
         uint32_t nt = 0, hv = 0;
         if (threadIdx.x < nh) {
-            hv = a.inc_hub[(size_t)p * nloc + threadIdx.x];
-            nt = (uint32_t)((a.row_off[hv + 1] - a.row_off[hv] + kIncHubTask - 1) / kIncHubTask);
+            hv = a.inc_hub[(size_t)p * a.inc_lcap + threadIdx.x];
+            nt = (uint32_t)((a.row_off_g[hv + 1] - a.row_off_g[hv] + kIncHubTask - 1) / kIncHubTask);
         }
         uint32_t in = nt;
         for (int o = 1; o < 64; o <<= 1) {
@@ -271,26 +283,26 @@ __global__ __launch_bounds__(1024) void wide_inc_delta_kernel(SweepArgs a) {
                 if (s_pre[mid] > task) hi = mid; else lo = mid + 1u;
             }
             const uint32_t v = s_v[lo], c = task - (lo ? s_pre[lo - 1u] : 0u);
-            const uint64_t rb = a.row_off[v] + (uint64_t)c * kIncHubTask;
-            const uint64_t re = min<uint64_t>(a.row_off[v + 1], rb + kIncHubTask);
+            const uint64_t rb = a.row_off_g[v] + (uint64_t)c * kIncHubTask;
+            const uint64_t re = min<uint64_t>(a.row_off_g[v + 1], rb + kIncHubTask);
             int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], rb + threadIdx.x, re, blockDim.x, t);
             for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
             if (lane == 0) inc_own(a, v, dv, t);
         }
     } else {
         for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {   // many hubs: a workgroup each
-            const uint32_t v = a.inc_hub[(size_t)p * nloc + h];
-            int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + threadIdx.x, a.row_off[v + 1], blockDim.x, t);
+            const uint32_t v = a.inc_hub[(size_t)p * a.inc_lcap + h];
+            int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off_g[v] + threadIdx.x, a.row_off_g[v + 1], blockDim.x, t);
             for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
             if (lane == 0) inc_own(a, v, dv, t);
         }
     }
     // other rows (the commit gathered them into one dense list): a wave each
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6, nd = ctl[kIncDenseN + p];
-    const uint32_t* dn = a.inc_dense + (size_t)p * nloc;
+    const uint32_t* dn = a.inc_dense + (size_t)p * a.inc_lcap;
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < nd; i += nw) {
         const uint32_t v = dn[i];
-        int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off[v] + lane, a.row_off[v + 1], 64u, t);
+        int dv = inc_arcs(a, Cp, Cn, v, Cp[v], Cn[v], a.row_off_g[v] + lane, a.row_off_g[v + 1], 64u, t);
         for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
         if (lane == 0) inc_own(a, v, dv, t);
     }
@@ -308,7 +320,7 @@ __device__ void wide_inc_flags(const SweepArgs& a, uint32_t t) {
         uint8_t* fpn = p ? a.wfp0 : a.wfp1;
         const uint32_t nh = ctl[kIncHubN + p], nd = ctl[kIncDenseN + p];
         for (uint32_t i = tid; i < nd + nh; i += nthr) {
-            const uint32_t v = i < nd ? a.inc_dense[(size_t)p * nloc + i] : a.inc_hub[(size_t)p * nloc + (i - nd)];
+            const uint32_t v = i < nd ? a.inc_dense[(size_t)p * a.inc_lcap + i] : a.inc_hub[(size_t)p * a.inc_lcap + (i - nd)];
             Cs[v] = C[v];
             if (a.fp_live) fpn[v] = fp[v];
         }
@@ -665,6 +677,17 @@ __device__ __forceinline__ void walk_gather(const SweepArgs& a, const uint16_t* 
 // random gathers, each such wait costs microseconds).
 __device__ __forceinline__ void walk_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Partitioned delta exchange (a.dcap > 0): this rank's vertex v takes colour c in sweep t (overflow
+// events aside: every rank replays those), into its delta slot of the next-colour parity. One lane.
+__device__ __forceinline__ void wide_delta_one(const SweepArgs& a, uint32_t t, uint32_t v, uint32_t c) {
+    uint32_t* dl = (t & 1) ? a.dlt0 : a.dlt1;
+    const uint32_t idx = atomicAdd(dl, 1u);
+    if (idx < a.dcap) {
+        dl[kDeltaHead + 2u * idx] = v;
+        dl[kDeltaHead + 2u * idx + 1u] = c;
+    }
+}
+
 // The resample of violator v (fill_p case (ii) / (i)) from its occupancy mask in LDS, by a whole
 // 256-thread workgroup: word prefix counts, then one wave walks them. cv = C_t[v] and x = u_v's
 // minstd state come in (loaded beside the task's first loads); deg = v's arcs. Overflow events go
@@ -719,6 +742,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
                 if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
             }
             if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
+            if (a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
             if (event) {
                 const uint32_t idx = atomicAdd(&st->ev_count, 1u);
@@ -791,6 +815,7 @@ __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uin
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
         }
         if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
+        if (a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
         if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
         if (event) {
             const uint32_t idx = atomicAdd(&st->ev_count, 1u);
@@ -1068,6 +1093,8 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
         const float u = minstd_canonical(xs[j]);
         cviol += viol[j];
         bool event = false;
+        bool dch = false;   // a case (iii) change of colour (the delta slot's)
+        uint32_t dnv = 0;
         if (valid) {
             if (viol[j]) {
                 a.wflag[l] = 0;
@@ -1103,6 +1130,23 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
                 }
                 if (islot != nullptr && nv != cv[j]) atomicAdd(&sh_ic[1], inc_list(a, l, t, islot, a.inc_slot, &sh_ic[0]));
                 if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv[j]) ? a.tabooIteration : 0u;
+                dch = nv != cv[j];
+                dnv = nv;
+            }
+        }
+        if (a.dcap) {   // partitioned delta exchange: one slot atomic per wave
+            const uint64_t db = __ballot(dch);
+            if (db) {
+                uint32_t* dl = (t & 1) ? a.dlt0 : a.dlt1;
+                const int lead = __ffsll((long long)db) - 1;
+                uint32_t base = 0;
+                if (lane == lead) base = atomicAdd(dl, (uint32_t)__popcll(db));
+                base = __shfl(base, lead, 64);
+                const uint32_t idx = base + (uint32_t)__popcll(db & ((1ull << lane) - 1ull));
+                if (dch && idx < a.dcap) {
+                    dl[kDeltaHead + 2u * idx] = v;
+                    dl[kDeltaHead + 2u * idx + 1u] = dnv;
+                }
             }
         }
         if (event) {   // into this workgroup's LDS list; past kEvSlot, the global list

@@ -432,6 +432,7 @@ static int er_fast_range(uint32_t n, double prob, uint64_t seed, uint32_t vb, ui
     g->g.n = n;
     g->g.sorted = false;
     g->g.simple_sym = 1;   // one draw per unordered pair, both arcs, no loops (tests/test_er_generator.py)
+    g->g.partial_rows = vb != 0 || ve != n;
     std::unique_ptr<TiledLayout> L(new_layout(n, vb, ve, R, er::kBlockLog2));
     const uint32_t nb = L->nblocks;
     ErArgs e{};

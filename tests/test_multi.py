@@ -147,11 +147,24 @@ def test_native_loopback_wide(M, world):
 
     off, idx = NP.rmat(11, 8, 0.5, 0.2, 0.2, 3)
     ncol = int(np.diff(off.astype(np.int64)).max())
-    O.srand(1)
-    r = O.mcmc_run(off, idx, ncol, 1, maxRip=6)
-    lp, st, _ = loopback(M, off, idx, ncol, 1, plan_csr(off, world), 0, maxRip=6)
-    assert_native(lp, st, r, world)
-    lp.close()
+    for nc, mr in ((ncol, 6), (max(257, ncol // 4), 12)):
+        O.srand(1)
+        r = O.mcmc_run(off, idx, nc, 1, maxRip=mr)
+        lp, st, _ = loopback(M, off, idx, nc, 1, plan_csr(off, world), 0, maxRip=mr)
+        assert_native(lp, st, r, world)
+        # the delta exchange (changed vertices only) and the incremental violation counts, per rank
+        import ctypes
+
+        from mcmc_colorer_amd._lib import check, lib
+
+        for k in range(world):
+            xs = [ctypes.c_uint64() for _ in range(4)]
+            check(lib().mcmc_part_exchange_stats(lp._ctx[k], *[ctypes.byref(x) for x in xs]))
+            assert xs[0].value > 0, (k, [x.value for x in xs])
+            inc = (ctypes.c_uint64 * 5)()
+            check(lib().mcmc_get_wide_inc_stats(lp._ctx[k], inc))
+            assert inc[0] == 1 and inc[1] > 0, (k, list(inc))
+        lp.close()
 
 
 @pytest.mark.gpu
