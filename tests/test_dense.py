@@ -61,7 +61,8 @@ def test_dense_matches_oracle(M, monkeypatch, n, p, ncol, seed, eps, taboo, maxr
     assert_same(col, st, r)
     ds = dense_stats(col)
     assert ds["on"] == 1 and ds["s0"] == 0 and ds["s1"] == (min(srows, n) if srows else ds["s1"])
-    assert ds["rebuilds"] >= 1   # the first sweep builds the counts
+    if st.iter >= 1:
+        assert ds["rebuilds"] >= 1   # the first accepted sweep built the counts
     if st.sweepsRun > 3 and eps <= 1e-8:
         assert ds["incremental"] >= 1
     if srows is not None and srows < n // 4 and n > 1000:
