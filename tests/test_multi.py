@@ -163,7 +163,9 @@ def test_native_loopback_wide(M, world):
             assert xs[0].value > 0, (k, [x.value for x in xs])
             inc = (ctypes.c_uint64 * 5)()
             check(lib().mcmc_get_wide_inc_stats(lp._ctx[k], inc))
-            assert inc[0] == 1 and inc[1] > 0, (k, list(inc))
+            assert inc[0] == 1, (k, list(inc))
+            if nc < ncol:   # (nCol = maxDeg converges after a full sweep or two)
+                assert inc[1] > 0, (k, list(inc))
         lp.close()
 
 
