@@ -30,6 +30,23 @@ def _torch_first():
             torch.cuda.init()
 
 
+_GPU_SESSION = []
+
+
+def pytest_collection_modifyitems(config, items):
+    if any(item.get_closest_marker("gpu") for item in items):
+        _GPU_SESSION.append(1)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_first_in_gpu_sessions():
+    """A session that runs GPU tests initialises torch before any test (CPU ones included, e.g. the
+    host CDF-walk hooks) loads the product library."""
+    if _GPU_SESSION:
+        _torch_first()
+    yield
+
+
 @pytest.fixture(autouse=True)
 def _torch_before_library(request):
     if request.node.get_closest_marker("gpu"):
