@@ -124,25 +124,38 @@ __global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
 
 // Rows of this wave whose dense mask is not full (`open`): each in turn, the whole wave scans its
 // segments in the column blocks not inside S (colours of C_t from the replica), OR-ing into its
-// mask until it is full or the blocks run out; lane j's acc then holds row j's full mask.
+// mask until it is full or the blocks run out; lane j's mask comes back full. Out of line (rare:
+// C3 ~0.005 % of rows) and with everything passed by value -- a reference to the kernel's
+// SweepArgs would copy the whole struct to scratch in every lane.
 template <int NW>
-__device__ __noinline__ void dc_open_scan(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t l, bool open,
-                                          uint32_t (&acc)[NW], const uint32_t (&fullw)[NW], int lane) {
+struct DcMask {
+    uint32_t w[NW];
+};
+struct DcScan {
+    const uint32_t* tseg;
+    const uint64_t* gbase;
+    const uint16_t* tcol;
+    uint32_t R, nb, bl, s0, s1;
+};
+template <int NW>
+__device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restrict__ C, uint32_t l, bool open,
+                                                DcMask<NW> acc, DcMask<NW> fullw, int lane) {
     uint64_t pend = __ballot(open);
-    const uint32_t bl = a.block_log2;
     while (pend) {
         const int j = __ffsll((long long)pend) - 1;
         pend &= pend - 1ull;
         const uint32_t lj = __shfl(l, j, 64);
+        const uint32_t g = lj / d.R, r = lj - g * d.R;
+        const uint16_t* __restrict__ gc = d.tcol + d.gbase[g];
         uint32_t cur[NW];
 #pragma unroll
-        for (int i = 0; i < NW; i++) cur[i] = __shfl(acc[i], j, 64);
-        for (uint32_t b = 0; b < a.nblocks; b++) {
-            const uint32_t lo = b << bl;
-            if (lo >= a.dc_s0 && lo + (1u << bl) <= a.dc_s1) continue;   // inside S: in the counts
-            uint32_t s0, s1;
-            const uint16_t* gc;
-            dc_segment(a, lj, b, s0, s1, gc);
+        for (int i = 0; i < NW; i++) cur[i] = __shfl(acc.w[i], j, 64);
+        for (uint32_t b = 0; b < d.nb; b++) {
+            const uint32_t lo = b << d.bl;
+            if (lo >= d.s0 && lo + (1u << d.bl) <= d.s1) continue;   // inside S: in the counts
+            const uint32_t* ts = d.tseg + ((size_t)g * d.nb + b) * tseg_stride(d.R);
+            const uint32_t raw = ts[r];
+            const uint32_t s0 = raw & kTsegPos, s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
             uint32_t m[NW];
 #pragma unroll
             for (int i = 0; i < NW; i++) m[i] = 0;
@@ -151,15 +164,16 @@ __device__ __noinline__ void dc_open_scan(const SweepArgs& a, const uint8_t* __r
 #pragma unroll
             for (int i = 0; i < NW; i++) {
                 cur[i] |= wave_or_uniform(m[i]);
-                full = full && ((cur[i] & fullw[i]) == fullw[i]);
+                full = full && ((cur[i] & fullw.w[i]) == fullw.w[i]);
             }
             if (full) break;
         }
         if (lane == j) {
 #pragma unroll
-            for (int i = 0; i < NW; i++) acc[i] = cur[i];
+            for (int i = 0; i < NW; i++) acc.w[i] = cur[i];
         }
     }
+    return acc;
 }
 
 // Sweep t's evaluation: persistent, one 1024-thread workgroup per CU; wave w of the grid takes the
@@ -234,7 +248,16 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
             const uint64_t ob = __ballot(open);
             if (ob) {
                 wave_open += (uint32_t)__popcll(ob);
-                dc_open_scan<NW>(a, C, l, open, acc[k], fullw, lane);
+                DcMask<NW> m, fw;
+#pragma unroll
+                for (int i = 0; i < NW; i++) {
+                    m.w[i] = acc[k][i];
+                    fw.w[i] = fullw[i];
+                }
+                const DcScan ds{a.tseg, a.gbase, a.tcol, a.grp_rows, a.nblocks, a.block_log2, a.dc_s0, a.dc_s1};
+                m = dc_open_scan<NW>(ds, C, l, open, m, fw, lane);
+#pragma unroll
+                for (int i = 0; i < NW; i++) acc[k][i] = m.w[i];
             }
             wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, acc[k], lane, wave_ev, vf, cv[k], tab[k],
                                            minstd_mulmod(minstd_mulmod(xb, apk[k]), lpow), ew);
