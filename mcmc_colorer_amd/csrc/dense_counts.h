@@ -19,7 +19,7 @@
 //                     so the tiled layout lists them. The first sweep after a colouring is set, or
 //                     one after more changes than pay, rebuilds every count from the layout.
 //   dc_eval_kernel    lane per row: a full dense mask is the row's mask and the row is evaluated at
-//                     once (evaluate_lane); a row whose dense mask is not full first scans its other
+//                     once; a row whose dense mask is not full first scans its other
 //                     column blocks (the wave together, colours from the replica, stopping once the
 //                     mask is full). evaluate_lane lists the vertices of S that change colour for
 //                     the next update; the last workgroup commits (sweep_tail), and the commit's
@@ -177,9 +177,11 @@ __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restr
 }
 
 // Sweep t's evaluation: persistent, one 1024-thread workgroup per CU; wave w of the grid takes the
-// 64-row tiles w, w + W, w + 2 W, ... (W = all waves), kDcTiles of them per step with every load
-// issued before the first evaluation (each tile alone is one dependent HBM round trip); lane per
-// row. u_v of row l is x_t 16807^(v_begin + l + 1): 16807^(64 W) (a.dc_apow) steps a tile's power to
+// 64-row tiles w, w + W, w + 2 W, ... (W = all waves), kDcTiles of them per step, the next step's
+// loads in flight while this step is evaluated; lane per row. A full mask holds the row's own colour
+// and no free colour -- fill_p's case (i) -- so with the closed-form walk (SweepArgs::ewalk) a row
+// keeps its colour exactly when u in [E[cv], S[cv]) (evaluate_lane's shortcut); a tile whose valid
+// rows all do is written directly (C_t+1 = C_t, Cviol, taboo reset), any other takes evaluate_lane. u_v of row l is x_t 16807^(v_begin + l + 1): 16807^(64 W) (a.dc_apow) steps a tile's power to
 // the next tile of the wave.
 constexpr int kDcTiles = 4;
 template <int NW>
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint32_t nwaves = blockDim.x >> 6;
-    const uint32_t gw = blockIdx.x * nwaves + (threadIdx.x >> 6), GW = gridDim.x * nwaves;
+    const uint32_t gw = blockIdx.x * nwaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = gridDim.x * nwaves;
     const uint32_t ntiles = (nloc + 63u) >> 6;
     uint32_t wave_viol = 0, wave_ev = 0, wave_open = 0;
     const uint32_t lpow = kMinstdLanePow[lane];
@@ -225,45 +227,94 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     for (int k = 1; k < kDcTiles; k++) apk[k] = minstd_mulmod(apk[k - 1], a.dc_apow);
     const uint32_t astep = minstd_mulmod(apk[kDcTiles - 1], a.dc_apow);
     uint32_t xb = gw < ntiles ? minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + 64ull * gw + 1ull)) : 0u;
-    for (uint32_t tau0 = gw; tau0 < ntiles; tau0 += kDcTiles * GW) {
-        uint32_t acc[kDcTiles][NW], cv[kDcTiles], tab[kDcTiles];
-#pragma unroll
-        for (int k = 0; k < kDcTiles; k++) {
-            const uint32_t l = 64u * (tau0 + k * GW) + (uint32_t)lane;
-            const bool valid = l < nloc;
-#pragma unroll
-            for (int i = 0; i < NW; i++) acc[k][i] = valid ? a.dc_mask[(size_t)l * NW + i] : 0u;
-            cv[k] = valid ? (uint32_t)C[a.v_begin + l] : 0u;
-            tab[k] = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kDcTiles; k++) {
-            const uint32_t l = 64u * (tau0 + k * GW) + (uint32_t)lane;
-            const bool valid = l < nloc;
-            if (!__ballot(valid)) break;   // this wave's tiles end here (uniform)
-            bool full = true;
-#pragma unroll
-            for (int i = 0; i < NW; i++) full = full && ((acc[k][i] & fullw[i]) == fullw[i]);
-            const bool open = valid && !full;
-            const uint64_t ob = __ballot(open);
-            if (ob) {
-                wave_open += (uint32_t)__popcll(ob);
-                DcMask<NW> m, fw;
-#pragma unroll
-                for (int i = 0; i < NW; i++) {
-                    m.w[i] = acc[k][i];
-                    fw.w[i] = fullw[i];
-                }
-                const DcScan ds{a.tseg, a.gbase, a.tcol, a.grp_rows, a.nblocks, a.block_log2, a.dc_s0, a.dc_s1};
-                m = dc_open_scan<NW>(ds, C, l, open, m, fw, lane);
-#pragma unroll
-                for (int i = 0; i < NW; i++) acc[k][i] = m.w[i];
-            }
-            wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, acc[k], lane, wave_ev, vf, cv[k], tab[k],
-                                           minstd_mulmod(minstd_mulmod(xb, apk[k]), lpow), ew);
-        }
-        xb = minstd_mulmod(xb, astep);
+    xb = __builtin_amdgcn_readfirstlane(xb);   // wave-uniform: the tile powers run on the scalar unit
+    // Steps over ping-pong register sets: step s + 1's loads are in flight while step s is evaluated.
+    // The step's open rows are scanned BEFORE the next loads are issued, and evaluation has no early
+    // exit (a tile past the wave's end evaluates nothing): hipcc's wait counting drains every load
+    // after an out-of-line call or on a path that skips a set's uses, so neither may sit between a
+    // set's loads and their use. Loads past the end read nothing (exec-masked).
+#define DC_LOAD(ACC, CV, TAB, T0)                                                                   \
+    _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                          \
+        const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                                  \
+        const bool valid = (T0) < ntiles && l < nloc;                                               \
+        _Pragma("unroll") for (int i = 0; i < NW; i++) ACC[k][i] = valid ? a.dc_mask[(size_t)l * NW + i] : 0u; \
+        CV[k] = valid ? (uint32_t)C[a.v_begin + l] : 0u;                                            \
+        TAB[k] = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;                                   \
     }
+#define DC_OPEN(ACC, T0)                                                                            \
+    {                                                                                               \
+        bool anyo = false;                                                                          \
+        _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                      \
+            const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                              \
+            bool full = true;                                                                       \
+            _Pragma("unroll") for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]); \
+            anyo = anyo || (l < nloc && !full);                                                     \
+        }                                                                                           \
+        if (__ballot(anyo)) {                                                                       \
+            for (int k = 0; k < kDcTiles; k++) {                                                    \
+                const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                          \
+                bool full = true;                                                                   \
+                for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]);   \
+                const bool open = l < nloc && !full;                                                \
+                const uint64_t ob = __ballot(open);                                                 \
+                if (!ob) continue;                                                                  \
+                wave_open += (uint32_t)__popcll(ob);                                                \
+                DcMask<NW> m, fw;                                                                   \
+                for (int i = 0; i < NW; i++) {                                                      \
+                    m.w[i] = ACC[k][i];                                                             \
+                    fw.w[i] = fullw[i];                                                             \
+                }                                                                                   \
+                const DcScan ds{a.tseg, a.gbase, a.tcol, a.grp_rows, a.nblocks, a.block_log2, a.dc_s0, a.dc_s1}; \
+                m = dc_open_scan<NW>(ds, C, l, open, m, fw, lane);                                  \
+                for (int i = 0; i < NW; i++) ACC[k][i] = m.w[i];                                    \
+            }                                                                                       \
+        }                                                                                           \
+    }
+#define DC_EVAL(ACC, CV, TAB, T0)                                                                   \
+    _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                          \
+        const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                                  \
+        const bool valid = l < nloc;                                                                \
+        const uint32_t x = minstd_mulmod(minstd_mulmod(xb, apk[k]), lpow);                          \
+        bool keep = false;                                                                          \
+        if (ew != nullptr) {                                                                        \
+            bool full = true;                                                                       \
+            _Pragma("unroll") for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]); \
+            const float u = minstd_canonical(x);                                                    \
+            const float2 es = ew[CV[k]];                                                            \
+            keep = full && TAB[k] == 0u && u >= es.x && es.y > u;                                   \
+        }                                                                                           \
+        const uint64_t vb = __ballot(valid);                                                        \
+        if (!__ballot(valid && !keep)) {                                                            \
+            if (valid) {                                                                            \
+                Cs[a.v_begin + l] = (uint8_t)CV[k];                                                 \
+                if (vf != nullptr) vf[l] = 1u;                                                      \
+                if (a.taboo != nullptr) a.taboo[l] = a.tabooIteration;                              \
+            }                                                                                       \
+            wave_viol += (uint32_t)__popcll(vb);                                                    \
+        } else {                                                                                    \
+            wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, ACC[k], lane, wave_ev, vf, CV[k], TAB[k], x, ew); \
+        }                                                                                           \
+    }                                                                                               \
+    xb = minstd_mulmod(xb, astep);
+    uint32_t accA[kDcTiles][NW], cvA[kDcTiles], tabA[kDcTiles];
+    uint32_t accB[kDcTiles][NW], cvB[kDcTiles], tabB[kDcTiles];
+    uint32_t tau0 = gw;
+    const uint32_t stride = kDcTiles * GW;
+    DC_LOAD(accA, cvA, tabA, tau0)
+    while (tau0 < ntiles) {
+        DC_OPEN(accA, tau0)
+        DC_LOAD(accB, cvB, tabB, tau0 + stride)
+        DC_EVAL(accA, cvA, tabA, tau0)
+        tau0 += stride;
+        if (tau0 >= ntiles) break;
+        DC_OPEN(accB, tau0)
+        DC_LOAD(accA, cvA, tabA, tau0 + stride)
+        DC_EVAL(accB, cvB, tabB, tau0)
+        tau0 += stride;
+    }
+#undef DC_LOAD
+#undef DC_OPEN
+#undef DC_EVAL
     if (wave_open) {   // statistics; the commit reads the word (this workgroup releases)
         if (lane == 0) atomicAdd(&a.dc_ctl[kDcOpen], wave_open);
         wave_ev = 1u;
