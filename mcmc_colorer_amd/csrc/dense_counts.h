@@ -11,19 +11,24 @@
 // nCol (ln nCol + 10) (a row misses a colour there with probability ~nCol e^-(ln nCol + 10)), and
 // keeps per local row w
 //     cnt[w][c] = #{u in S : (w, u) an arc, C_t[u] = c}    (uint32)
-// and the occupancy bits of those counts (dense mask). A sweep is then two launches:
-//   dc_update_kernel  moves the counts by the vertices of S whose colour the previous sweep changed
+// and the occupancy bits of those counts (dense mask), plus one "open" bit per row and mask word
+// (that word of the dense mask is not full). A sweep is then two launches:
+//   dc_update_kernel  brings the buffer the sweep writes (it holds C_t-1) to C_t on the local rows
+//                     (the previous sweep's restore list of changed rows, or a full copy), then
+//                     moves the counts by the vertices of S whose colour the previous sweep changed
 //                     (u's old colour -1, new colour +1 in every row holding u; a count crossing 0
-//                     flips its mask bit). For a simple symmetric graph the rows holding u are u's
-//                     own neighbours, and row u is a local row (S lies inside the context's rows),
-//                     so the tiled layout lists them. The first sweep after a colouring is set, or
-//                     one after more changes than pay, rebuilds every count from the layout.
-//   dc_eval_kernel    lane per row: a full dense mask is the row's mask and the row is evaluated at
-//                     once; a row whose dense mask is not full first scans its other
-//                     column blocks (the wave together, colours from the replica, stopping once the
-//                     mask is full). evaluate_lane lists the vertices of S that change colour for
-//                     the next update; the last workgroup commits (sweep_tail), and the commit's
-//                     glibc replay lists the overflow events of S (commit_accept, dc_commit).
+//                     flips its mask bit and, when the word's fullness changed, its open bit). For a
+//                     simple symmetric graph the rows holding u are u's own neighbours, and row u is
+//                     a local row (S lies inside the context's rows), so the tiled layout lists
+//                     them. The first sweep after a colouring is set, or one after more changes than
+//                     pay, rebuilds every count from the layout.
+//   dc_eval_kernel    lane per row, reading the row's colour and its tile's open words: a row that
+//                     is not open has the full mask and is evaluated at once; an open row first
+//                     scans its other column blocks (the wave together, colours from the replica,
+//                     stopping once the mask is full). Only rows that change colour are written
+//                     (both lists take them); the last workgroup commits (sweep_tail), and the
+//                     commit's glibc replay lists the overflow events (commit_accept,
+//                     dc_list_change, dc_commit).
 // Exact, not approximate: the counts are integers and the mask is the set the full scan ORs
 // together (tests/test_dense.py: every variant against the early-exit scan and the oracle).
 // Reference counterpart: the per-sweep neighbour scans of ColoringMCMC_CPU::run (:136-270).
@@ -41,21 +46,38 @@ __device__ __forceinline__ void dc_segment(const SweepArgs& a, uint32_t l, uint3
     gc = a.tcol + a.gbase[g];
 }
 
-// Vertex u of S moved from colour ca to cb: row lw's counts and dense mask.
+// Word i of a full mask (colours [32 i, 32 i + 32) below nCol).
+__device__ __forceinline__ uint32_t dc_fullw(uint32_t nCol, uint32_t i) {
+    const uint32_t lo = 32u * i;
+    return nCol >= lo + 32u ? ~0u : (nCol > lo ? (1u << (nCol - lo)) - 1u : 0u);
+}
+
+// Row lw's count of colour c crossed zero: flip its mask bit, and its open bit when that changed
+// whether mask word c / 32 is full. Flips of one word are ordered by its atomics, so the open bit
+// ends as (word not full) whatever the interleaving.
+template <int NW>
+__device__ __forceinline__ void dc_flip(const SweepArgs& a, uint32_t lw, uint32_t c) {
+    const uint32_t i = c >> 5, bit = 1u << (c & 31u), fw = dc_fullw(a.nCol, i);
+    const uint32_t o = atomicXor(&a.dc_mask[(size_t)lw * NW + i], bit);
+    if (((o & fw) == fw) != (((o ^ bit) & fw) == fw))
+        atomicXor(&a.dc_open[(size_t)(lw >> 6) * NW + i], 1ull << (lw & 63u));
+}
+
+// Vertex u of S moved from colour ca to cb: row lw's counts, dense mask and open bits.
 template <int NW>
 __device__ __forceinline__ void dc_move(const SweepArgs& a, uint32_t lw, uint32_t ca, uint32_t cb) {
     uint32_t* cw = a.dc_cnt + (size_t)lw * a.dc_cw;
-    uint32_t* mw = a.dc_mask + (size_t)lw * NW;
     const uint32_t oa = atomicSub(&cw[ca], 1u);   // >= 1: u itself holds colour ca
     const uint32_t ob = atomicAdd(&cw[cb], 1u);
-    // a count crossing zero flips its bit; crossings of one count alternate in the order of its
-    // atomics, so the flips leave the bit = (count > 0) whatever the interleaving
-    if (oa == 1u) atomicXor(&mw[ca >> 5], 1u << (ca & 31u));
-    if (ob == 0u) atomicXor(&mw[cb >> 5], 1u << (cb & 31u));
+    if (oa == 1u) dc_flip<NW>(a, lw, ca);
+    if (ob == 0u) dc_flip<NW>(a, lw, cb);
 }
 
-// Sweep t's update of the dense counts (all waves; grid-stride). Rebuild: a wave per local row,
-// its segments in the blocks overlapping S, colours of C_t counted in an LDS histogram. Incremental:
+// Sweep t's update (all waves; grid-stride). First the buffer sweep t writes (it holds C_t-1) is
+// brought to C_t on the local rows: the vertices on the restore list are copied, or every local row
+// when that list overflowed or the counts are rebuilt -- the evaluation then writes only the rows
+// that change. Then the counts. Rebuild: a wave per local row, its segments in the blocks
+// overlapping S, colours of C_t counted in an LDS histogram, mask and open bits written. Incremental:
 // a wave per (listed vertex u, column block b of the local rows): u's neighbours in block b.
 template <int NW>
 __global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
@@ -67,7 +89,28 @@ __global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
     const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwv = (gridDim.x * blockDim.x) >> 6;
     const uint32_t bl = a.block_log2;
-    if (a.dc_ctl[kDcMode]) {
+    const uint32_t p = t & 1u;
+    const uint32_t mode = a.dc_ctl[kDcMode];
+    uint8_t* __restrict__ Y = (t & 1) ? a.colors0 : a.colors1;   // C_t-1, becomes C_t+1
+    {
+        const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+        if (mode || a.dc_ctl[kDcChgOvf + p]) {
+            const size_t b0 = a.v_begin, b1 = a.v_end;
+            const size_t q0 = (b0 + 15) & ~(size_t)15, q1 = (b1 & ~(size_t)15) > q0 ? (b1 & ~(size_t)15) : q0;
+            for (size_t i = q0 + 16 * tid; i < q1; i += 16 * nth)
+                *reinterpret_cast<uint4*>(Y + i) = *reinterpret_cast<const uint4*>(C + i);
+            for (size_t i = b0 + tid; i < (q0 < b1 ? q0 : b1); i += nth) Y[i] = C[i];
+            for (size_t i = (q1 > b0 ? q1 : b0) + tid; i < b1; i += nth) Y[i] = C[i];
+        } else {
+            const uint32_t m = min(a.dc_ctl[kDcChgLen + p], a.dc_chg_cap);
+            const uint32_t* __restrict__ R = a.dc_chg + (size_t)p * a.dc_chg_cap;
+            for (size_t i = tid; i < m; i += nth) {
+                const uint32_t u = R[i];
+                Y[u] = C[u];
+            }
+        }
+    }
+    if (mode) {
         uint32_t* h = hist[threadIdx.x >> 6];
         const uint32_t b0 = a.dc_s0 >> bl, b1 = (a.dc_s1 - 1u) >> bl, sw = a.dc_s1 - a.dc_s0;
         for (uint32_t l = wave; l < nloc; l += nwv) {
@@ -87,30 +130,33 @@ __global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
             uint32_t* cr = a.dc_cnt + (size_t)l * a.dc_cw;
             for (uint32_t i = lane; i < a.dc_cw; i += 64u) cr[i] = h[i];
             uint32_t* mk = a.dc_mask + (size_t)l * NW;
+            unsigned long long* ow = a.dc_open + (size_t)(l >> 6) * NW;
+            const unsigned long long obit = 1ull << (l & 63u);
             for (uint32_t c0 = 0; c0 < 32u * NW; c0 += 64u) {
                 const uint32_t c = c0 + lane;
                 const uint64_t bm = __ballot(c < a.nCol && h[c] != 0u);
                 if (lane == 0) {
-                    mk[c0 >> 5] = (uint32_t)bm;
-                    if ((c0 >> 5) + 1u < (uint32_t)NW) mk[(c0 >> 5) + 1u] = (uint32_t)(bm >> 32);
+                    for (uint32_t i = c0 >> 5; i < min((c0 >> 5) + 2u, (uint32_t)NW); i++) {
+                        const uint32_t m = (uint32_t)(bm >> (32u * (i - (c0 >> 5)))), fw = dc_fullw(a.nCol, i);
+                        mk[i] = m;
+                        if ((m & fw) != fw) atomicOr(&ow[i], obit);
+                        else atomicAnd(&ow[i], ~obit);
+                    }
                 }
             }
             dc_lds_wait();   // every lane's reads of h are done before the next row clears it
         }
         return;
     }
-    const uint32_t p = t & 1u;
     const uint32_t len = min(a.dc_ctl[kDcLen + p], a.dc_cap);
     if (len == 0) return;
-    const uint8_t* __restrict__ P = (t & 1) ? a.colors0 : a.colors1;   // C_t-1 (sweep t overwrites it later)
-    const uint32_t* __restrict__ L = a.dc_list + (size_t)p * a.dc_cap;
+    const uint32_t* __restrict__ L = a.dc_list + 2u * (size_t)p * a.dc_cap;   // (u, ca << 16 | cb)
     const uint32_t bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
     const uint64_t tasks = (uint64_t)len * nbl;
     for (uint64_t task = wave; task < tasks; task += nwv) {
         const uint32_t i = (uint32_t)(task / nbl), b = bl0 + (uint32_t)(task - (uint64_t)i * nbl);
-        const uint32_t u = L[i];
-        const uint32_t ca = P[u], cb = C[u];
-        if (ca == cb) continue;
+        const uint32_t u = L[2u * i], ab = L[2u * i + 1u];
+        const uint32_t ca = ab >> 16, cb = ab & 0xFFFFu;
         uint32_t s0, s1;
         const uint16_t* gc;
         dc_segment(a, u - a.v_begin, b, s0, s1, gc);
@@ -127,6 +173,13 @@ __global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
 // mask until it is full or the blocks run out; lane j's mask comes back full. Out of line (rare:
 // C3 ~0.005 % of rows) and with everything passed by value -- a reference to the kernel's
 // SweepArgs would copy the whole struct to scratch in every lane.
+// Lane j's 64-bit value (wave-uniform result).
+__device__ __forceinline__ unsigned long long dc_lane64(unsigned long long x, int j) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), j);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 template <int NW>
 struct DcMask {
     uint32_t w[NW];
@@ -176,14 +229,18 @@ __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restr
     return acc;
 }
 
-// Sweep t's evaluation: persistent, one 1024-thread workgroup per CU; wave w of the grid takes the
-// 64-row tiles w, w + W, w + 2 W, ... (W = all waves), kDcTiles of them per step, the next step's
-// loads in flight while this step is evaluated; lane per row. A full mask holds the row's own colour
-// and no free colour -- fill_p's case (i) -- so with the closed-form walk (SweepArgs::ewalk) a row
-// keeps its colour exactly when u in [E[cv], S[cv]) (evaluate_lane's shortcut); a tile whose valid
-// rows all do is written directly (C_t+1 = C_t, Cviol, taboo reset), any other takes evaluate_lane. u_v of row l is x_t 16807^(v_begin + l + 1): 16807^(64 W) (a.dc_apow) steps a tile's power to
-// the next tile of the wave.
-constexpr int kDcTiles = 4;
+// Sweep t's evaluation: persistent, one 1024-thread workgroup per CU. Lane j of a wave holds 16
+// consecutive rows (kDcLaneRows), so a wave step covers a span of 1024 rows: one 16-byte colour
+// load and one open word per lane. Wave w of the grid takes spans w, w + W, w + 2 W, ... (W = all
+// waves), the next span's loads in flight while this one is evaluated. A row that is not open has
+// the full mask: it holds its own colour and no free colour -- fill_p's case (i) -- so with the
+// closed-form walk (SweepArgs::ewalk) it keeps its colour exactly when u in [E[cv], S[cv])
+// (evaluate_lane's shortcut). Kept rows are only counted (Cviol; the update already holds C_t in
+// the buffer written); any other row -- open, taboo, changing, or the walk's rare cases -- goes
+// through evaluate_lane, one row position j of the lanes at a time, open rows first completing
+// their mask (dc_open_scan). u_v of row l is x_t 16807^(v_begin + l + 1).
+constexpr uint32_t kDcLaneRows = 16;
+constexpr uint32_t kDcSpan = 64u * kDcLaneRows;
 template <int NW>
 __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     extern __shared__ uint4 dc_lds[];
@@ -210,111 +267,123 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     }
     uint32_t fullw[NW];
 #pragma unroll
-    for (int i = 0; i < NW; i++) {
-        const uint32_t lo = 32u * i;
-        fullw[i] = a.nCol >= lo + 32u ? ~0u : (a.nCol > lo ? (1u << (a.nCol - lo)) - 1u : 0u);
-    }
+    for (int i = 0; i < NW; i++) fullw[i] = dc_fullw(a.nCol, (uint32_t)i);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint32_t nwaves = blockDim.x >> 6;
     const uint32_t gw = blockIdx.x * nwaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = gridDim.x * nwaves;
-    const uint32_t ntiles = (nloc + 63u) >> 6;
-    uint32_t wave_viol = 0, wave_ev = 0, wave_open = 0;
-    const uint32_t lpow = kMinstdLanePow[lane];
-    uint32_t apk[kDcTiles];   // 16807^(64 W k)
-    apk[0] = 1u;
+    const uint32_t nspan = (nloc + kDcSpan - 1u) / kDcSpan;
+    const bool al16 = (a.v_begin & 15u) == 0u;   // 16-byte colour loads (else byte loads)
+    uint32_t wave_viol = 0, wave_ev = 0, wave_open = 0, kept = 0;
+    // 16807^16 (a row block of a lane), 16807^(16 lane), 16807^(1024 W) (a wave's next span)
+    uint32_t a16 = kMinstdA;
 #pragma unroll
-    for (int k = 1; k < kDcTiles; k++) apk[k] = minstd_mulmod(apk[k - 1], a.dc_apow);
-    const uint32_t astep = minstd_mulmod(apk[kDcTiles - 1], a.dc_apow);
-    uint32_t xb = gw < ntiles ? minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + 64ull * gw + 1ull)) : 0u;
-    xb = __builtin_amdgcn_readfirstlane(xb);   // wave-uniform: the tile powers run on the scalar unit
-    // Steps over ping-pong register sets: step s + 1's loads are in flight while step s is evaluated.
-    // The step's open rows are scanned BEFORE the next loads are issued, and evaluation has no early
-    // exit (a tile past the wave's end evaluates nothing): hipcc's wait counting drains every load
-    // after an out-of-line call or on a path that skips a set's uses, so neither may sit between a
-    // set's loads and their use. Loads past the end read nothing (exec-masked).
-#define DC_LOAD(ACC, CV, TAB, T0)                                                                   \
-    _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                          \
-        const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                                  \
-        const bool valid = (T0) < ntiles && l < nloc;                                               \
-        _Pragma("unroll") for (int i = 0; i < NW; i++) ACC[k][i] = valid ? a.dc_mask[(size_t)l * NW + i] : 0u; \
-        CV[k] = valid ? (uint32_t)C[a.v_begin + l] : 0u;                                            \
-        TAB[k] = (a.taboo != nullptr && valid) ? a.taboo[l] : 0u;                                   \
-    }
-#define DC_OPEN(ACC, T0)                                                                            \
+    for (int i = 0; i < 4; i++) a16 = minstd_mulmod(a16, a16);
+    uint32_t lp16 = 1u;
+    for (uint32_t e = (uint32_t)lane, b = a16; e; e >>= 1, b = minstd_mulmod(b, b))
+        if (e & 1u) lp16 = minstd_mulmod(lp16, b);
+    uint32_t aspan = a.dc_apow;   // 16807^(64 W)
+#pragma unroll
+    for (int i = 0; i < 4; i++) aspan = minstd_mulmod(aspan, aspan);
+    uint32_t xs = gw < nspan ? minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + (uint64_t)kDcSpan * gw + 1ull)) : 0u;
+    xs = __builtin_amdgcn_readfirstlane(xs);   // wave-uniform: the span powers run on the scalar unit
+    // lane's rows of span S: l0 = S kDcSpan + 16 lane; colours as four words, open bits as 16 bits
+#define DC_LOAD(CW, OPW, S)                                                                         \
     {                                                                                               \
-        bool anyo = false;                                                                          \
-        _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                      \
-            const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                              \
-            bool full = true;                                                                       \
-            _Pragma("unroll") for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]); \
-            anyo = anyo || (l < nloc && !full);                                                     \
+        const uint32_t l0 = (S) * kDcSpan + kDcLaneRows * (uint32_t)lane;                           \
+        const bool in = (S) < nspan && l0 < nloc;                                                   \
+        const uint32_t nv = in ? min(kDcLaneRows, nloc - l0) : 0u;                                  \
+        if (al16 && nv == kDcLaneRows) {                                                            \
+            const uint4 q = *reinterpret_cast<const uint4*>(C + a.v_begin + l0);                    \
+            CW[0] = q.x; CW[1] = q.y; CW[2] = q.z; CW[3] = q.w;                                     \
+        } else {                                                                                    \
+            CW[0] = CW[1] = CW[2] = CW[3] = 0u;                                                     \
+            for (uint32_t j = 0; j < nv; j++) CW[j >> 2] |= (uint32_t)C[a.v_begin + l0 + j] << (8u * (j & 3u)); \
         }                                                                                           \
-        if (__ballot(anyo)) {                                                                       \
-            for (int k = 0; k < kDcTiles; k++) {                                                    \
-                const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                          \
-                bool full = true;                                                                   \
-                for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]);   \
-                const bool open = l < nloc && !full;                                                \
-                const uint64_t ob = __ballot(open);                                                 \
-                if (!ob) continue;                                                                  \
-                wave_open += (uint32_t)__popcll(ob);                                                \
+        unsigned long long o = 0;                                                                   \
+        if (in) {                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < NW; i++) o |= a.dc_open[(size_t)(l0 >> 6) * NW + i]; \
+        }                                                                                           \
+        OPW = (uint32_t)(o >> (l0 & 63u)) & 0xFFFFu;                                                \
+    }
+#define DC_EVAL(CW, OPW, S)                                                                         \
+    {                                                                                               \
+        const uint32_t l0 = (S) * kDcSpan + kDcLaneRows * (uint32_t)lane;                           \
+        const uint32_t nv = l0 < nloc ? min(kDcLaneRows, nloc - l0) : 0u;                           \
+        const uint32_t vmask = (1u << nv) - 1u;                                                     \
+        uint32_t tabw[kDcLaneRows];                                                                 \
+        if (a.taboo != nullptr) {                                                                   \
+            _Pragma("unroll") for (uint32_t j = 0; j < kDcLaneRows; j++)                            \
+                tabw[j] = j < nv ? a.taboo[l0 + j] : 0u;                                            \
+        }                                                                                           \
+        const uint32_t xl = minstd_mulmod(xs, lp16);                                                \
+        uint32_t keepm = 0;                                                                         \
+        if (ew != nullptr) {                                                                        \
+            uint32_t x = xl;                                                                        \
+            _Pragma("unroll") for (uint32_t j = 0; j < kDcLaneRows; j++) {                          \
+                if (j) x = minstd_mulmod(x, kMinstdA);                                              \
+                const uint32_t cv = (CW[j >> 2] >> (8u * (j & 3u))) & 0xFFu;                        \
+                const float u = minstd_canonical(x);                                                \
+                const float2 es = ew[cv];                                                           \
+                bool k = u >= es.x && es.y > u;                                                     \
+                if (a.taboo != nullptr) k = k && tabw[j] == 0u;                                     \
+                keepm |= (k ? 1u : 0u) << j;                                                        \
+            }                                                                                       \
+            keepm &= vmask & ~(OPW);                                                                \
+            kept += (uint32_t)__popc(keepm);                                                        \
+            if (keepm != 0u && (vf != nullptr || a.taboo != nullptr)) {                             \
+                for (uint32_t j = 0; j < kDcLaneRows; j++) {                                        \
+                    if (!((keepm >> j) & 1u)) continue;                                             \
+                    if (vf != nullptr) vf[l0 + j] = 1u;                                             \
+                    if (a.taboo != nullptr) a.taboo[l0 + j] = a.tabooIteration;                     \
+                }                                                                                   \
+            }                                                                                       \
+        }                                                                                           \
+        const uint32_t need = vmask & ~keepm;                                                       \
+        if (__ballot(need != 0u)) {                                                                 \
+            for (uint32_t j = 0; j < kDcLaneRows; j++) {                                            \
+                const bool nd = ((need >> j) & 1u) != 0u;                                           \
+                if (!__ballot(nd)) continue;                                                        \
+                const uint32_t l = l0 + j;                                                          \
+                const uint32_t cv = nd ? (uint32_t)C[a.v_begin + l] : 0u;                           \
+                const uint32_t tab = (nd && a.taboo != nullptr) ? a.taboo[l] : 0u;                  \
+                const bool opn = nd && ((OPW >> j) & 1u) != 0u;                                     \
                 DcMask<NW> m, fw;                                                                   \
-                for (int i = 0; i < NW; i++) {                                                      \
-                    m.w[i] = ACC[k][i];                                                             \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) {                                    \
+                    m.w[i] = opn ? a.dc_mask[(size_t)l * NW + i] : fullw[i];                        \
                     fw.w[i] = fullw[i];                                                             \
                 }                                                                                   \
-                const DcScan ds{a.tseg, a.gbase, a.tcol, a.grp_rows, a.nblocks, a.block_log2, a.dc_s0, a.dc_s1}; \
-                m = dc_open_scan<NW>(ds, C, l, open, m, fw, lane);                                  \
-                for (int i = 0; i < NW; i++) ACC[k][i] = m.w[i];                                    \
+                const uint64_t ob = __ballot(opn);                                                  \
+                if (ob) {                                                                           \
+                    wave_open += (uint32_t)__popcll(ob);                                            \
+                    const DcScan ds{a.tseg, a.gbase, a.tcol, a.grp_rows, a.nblocks, a.block_log2, a.dc_s0, a.dc_s1}; \
+                    m = dc_open_scan<NW>(ds, C, l, opn, m, fw, lane);                               \
+                }                                                                                   \
+                uint32_t acc[NW];                                                                   \
+                _Pragma("unroll") for (int i = 0; i < NW; i++) acc[i] = m.w[i];                     \
+                wave_viol += evaluate_lane<NW>(a, st, Cs, nd, l, acc, lane, wave_ev, vf, cv, tab,   \
+                                               minstd_mulmod(xl, kMinstdLanePow[j]), ew);           \
             }                                                                                       \
         }                                                                                           \
+        xs = minstd_mulmod(xs, aspan);                                                              \
     }
-#define DC_EVAL(ACC, CV, TAB, T0)                                                                   \
-    _Pragma("unroll") for (int k = 0; k < kDcTiles; k++) {                                          \
-        const uint32_t l = 64u * ((T0) + k * GW) + (uint32_t)lane;                                  \
-        const bool valid = l < nloc;                                                                \
-        const uint32_t x = minstd_mulmod(minstd_mulmod(xb, apk[k]), lpow);                          \
-        bool keep = false;                                                                          \
-        if (ew != nullptr) {                                                                        \
-            bool full = true;                                                                       \
-            _Pragma("unroll") for (int i = 0; i < NW; i++) full = full && ((ACC[k][i] & fullw[i]) == fullw[i]); \
-            const float u = minstd_canonical(x);                                                    \
-            const float2 es = ew[CV[k]];                                                            \
-            keep = full && TAB[k] == 0u && u >= es.x && es.y > u;                                   \
-        }                                                                                           \
-        const uint64_t vb = __ballot(valid);                                                        \
-        if (!__ballot(valid && !keep)) {                                                            \
-            if (valid) {                                                                            \
-                Cs[a.v_begin + l] = (uint8_t)CV[k];                                                 \
-                if (vf != nullptr) vf[l] = 1u;                                                      \
-                if (a.taboo != nullptr) a.taboo[l] = a.tabooIteration;                              \
-            }                                                                                       \
-            wave_viol += (uint32_t)__popcll(vb);                                                    \
-        } else {                                                                                    \
-            wave_viol += evaluate_lane<NW>(a, st, Cs, valid, l, ACC[k], lane, wave_ev, vf, CV[k], TAB[k], x, ew); \
-        }                                                                                           \
-    }                                                                                               \
-    xb = minstd_mulmod(xb, astep);
-    uint32_t accA[kDcTiles][NW], cvA[kDcTiles], tabA[kDcTiles];
-    uint32_t accB[kDcTiles][NW], cvB[kDcTiles], tabB[kDcTiles];
-    uint32_t tau0 = gw;
-    const uint32_t stride = kDcTiles * GW;
-    DC_LOAD(accA, cvA, tabA, tau0)
-    while (tau0 < ntiles) {
-        DC_OPEN(accA, tau0)
-        DC_LOAD(accB, cvB, tabB, tau0 + stride)
-        DC_EVAL(accA, cvA, tabA, tau0)
-        tau0 += stride;
-        if (tau0 >= ntiles) break;
-        DC_OPEN(accB, tau0)
-        DC_LOAD(accA, cvA, tabA, tau0 + stride)
-        DC_EVAL(accB, cvB, tabB, tau0)
-        tau0 += stride;
+    uint32_t cA[4], cB[4], oA, oB;
+    uint32_t sp = gw;
+    DC_LOAD(cA, oA, sp)
+    while (sp < nspan) {
+        DC_LOAD(cB, oB, sp + GW)
+        DC_EVAL(cA, oA, sp)
+        sp += GW;
+        if (sp >= nspan) break;
+        DC_LOAD(cA, oA, sp + GW)
+        DC_EVAL(cB, oB, sp)
+        sp += GW;
     }
 #undef DC_LOAD
-#undef DC_OPEN
 #undef DC_EVAL
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kept += __shfl_xor(kept, o, 64);
+    wave_viol += kept;   // every kept row is a violator: its own colour is in the full mask
     if (wave_open) {   // statistics; the commit reads the word (this workgroup releases)
         if (lane == 0) atomicAdd(&a.dc_ctl[kDcOpen], wave_open);
         wave_ev = 1u;

@@ -226,8 +226,11 @@ struct SweepArgs {
     uint32_t* dc_ctl;           // kDcWords control words (nullptr: the tiled scan sweeps)
     uint32_t* dc_cnt;           // [nloc][dc_cw] uint32 counts
     uint32_t* dc_mask;          // [nloc][NW] occupancy of the counts
-    uint32_t* dc_list;          // [2][dc_cap] vertices of S whose colour changed, by parity (t + 1) & 1
-    uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max;
+    uint32_t* dc_list;          // [2][dc_cap] (v, old colour << 16 | new colour): the vertices of S
+                                //   whose colour changed, by parity (t + 1) & 1
+    uint32_t* dc_chg;           // [2][dc_chg_cap] every local vertex whose colour changed (restore list)
+    unsigned long long* dc_open;   // [ntiles][NW] bit j of word (tile, i): row 64 tile + j's mask word i not full
+    uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max, dc_chg_cap;
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -250,7 +253,9 @@ constexpr uint32_t kDcLen = 1;     // [2] vertices of S listed for the next swee
 constexpr uint32_t kDcOvf = 3;     // [2] that list overflowed: the next sweep rebuilds
 constexpr uint32_t kDcOpen = 5;    // rows of the running sweep whose dense mask was not full
 constexpr uint32_t kDcStat = 8;    // u64 [4]: incremental sweeps, rebuilds, listed vertices, open rows
-constexpr uint32_t kDcWords = 16;
+constexpr uint32_t kDcChgLen = 16; // [2] local vertices on the restore list, by parity (t + 1) & 1
+constexpr uint32_t kDcChgOvf = 18; // [2] that list overflowed: the next update copies every local row
+constexpr uint32_t kDcWords = 24;
 constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: the commit's sort buffer
 
 
@@ -273,9 +278,31 @@ __device__ void dc_commit(const SweepArgs& a, uint32_t t) {
     k[kDcOpen] = 0;
     k[kDcLen + p] = 0;
     k[kDcOvf + p] = 0;
+    k[kDcChgLen + p] = 0;
+    k[kDcChgOvf + p] = 0;
     k[kDcMode] = (ovf || len > a.dc_max) ? 1u : 0u;
 }
 
+// Vertex v changed colour (ca -> cb) in the sweep whose lists have parity q, one thread: onto the
+// restore list when local (the next update copies it into the buffer that sweep overwrites), and
+// onto the count list when in S.
+__device__ __forceinline__ void dc_list_change(const SweepArgs& a, uint32_t q, uint32_t v, uint32_t ca, uint32_t cb) {
+    if (v - a.v_begin < a.v_end - a.v_begin) {
+        const uint32_t j = atomicAdd(&a.dc_ctl[kDcChgLen + q], 1u);
+        if (j < a.dc_chg_cap) a.dc_chg[(size_t)q * a.dc_chg_cap + j] = v;
+        else a.dc_ctl[kDcChgOvf + q] = 1u;
+    }
+    if (v - a.dc_s0 < a.dc_s1 - a.dc_s0) {
+        const uint32_t j = atomicAdd(&a.dc_ctl[kDcLen + q], 1u);
+        if (j < a.dc_cap) {
+            uint32_t* e = a.dc_list + 2u * ((size_t)q * a.dc_cap + j);
+            e[0] = v;
+            e[1] = (ca << 16) | cb;
+        } else {
+            a.dc_ctl[kDcOvf + q] = 1u;
+        }
+    }
+}
 
 // Row l (deg arcs) changes colour in sweep t: into slot `slot` (count in slot[0], arcs in slot[1],
 // bumped by the caller's LDS counters), or the hub list. Returns deg.
@@ -626,12 +653,8 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             if (a.inc != nullptr && c != (uint32_t)C[v])   // (any rank's vertex: global ids)
                 atomicAdd(&inc_cc[1], inc_list_global(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.inc_ccap),
                                                       a.inc_ccap, &inc_cc[0]));
-            if (a.dc_list != nullptr && c != (uint32_t)C[v] && v - a.dc_s0 < a.dc_s1 - a.dc_s0) {
-                const uint32_t q = (t + 1u) & 1u;   // dense-count sweep: the next update moves v
-                const uint32_t idx = atomicAdd(&a.dc_ctl[kDcLen + q], 1u);
-                if (idx < a.dc_cap) a.dc_list[(size_t)q * a.dc_cap + idx] = v;
-                else a.dc_ctl[kDcOvf + q] = 1u;
-            }
+            if (a.dc_list != nullptr && c != (uint32_t)C[v])   // dense-count sweep: the next update's lists
+                dc_list_change(a, (t + 1u) & 1u, v, (uint32_t)C[v], c);
         }
         __syncthreads();
     }
@@ -1292,22 +1315,39 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
             }
         }
     }
-    // dense-count sweep: the vertices of S whose colour changes (events aside: the commit's replay
-    // lists those), for the next sweep's update of the counts
+    // dense-count sweep: the vertices whose colour changes (events aside: the commit's replay lists
+    // those) -- every one on the restore list, those of S on the count list (pairs with both colours)
     if (a.dc_list != nullptr) {
-        const bool dchg = valid && tab == 0 && !event && newc != cv && v - a.dc_s0 < a.dc_s1 - a.dc_s0;
+        const bool dchg = valid && tab == 0 && !event && newc != cv;
         const uint64_t db = __ballot(dchg);
         if (db) {
             const uint32_t q = (Cs == a.colors1) ? 1u : 0u;   // (t + 1) & 1
-            uint32_t based = 0;
-            if (lane == 0) based = atomicAdd(&a.dc_ctl[kDcLen + q], (uint32_t)__popcll(db));
-            based = __shfl(based, 0, 64);
-            const uint32_t idx = based + (uint32_t)__popcll(db & ((1ull << lane) - 1ull));
-            if (dchg) {
-                if (idx < a.dc_cap) a.dc_list[(size_t)q * a.dc_cap + idx] = v;
-                else a.dc_ctl[kDcOvf + q] = 1u;
+            const bool ins = dchg && v - a.dc_s0 < a.dc_s1 - a.dc_s0;
+            const uint64_t sb = __ballot(ins);
+            uint32_t bc = 0, bs = 0;
+            if (lane == 0) {
+                bc = atomicAdd(&a.dc_ctl[kDcChgLen + q], (uint32_t)__popcll(db));
+                if (sb) bs = atomicAdd(&a.dc_ctl[kDcLen + q], (uint32_t)__popcll(sb));
             }
-            ev_flag = 1u;   // the commit reads the list's length: this workgroup releases (sweep_tail)
+            bc = __shfl(bc, 0, 64);
+            bs = __shfl(bs, 0, 64);
+            const uint64_t below = (1ull << lane) - 1ull;
+            if (dchg) {
+                const uint32_t j = bc + (uint32_t)__popcll(db & below);
+                if (j < a.dc_chg_cap) a.dc_chg[(size_t)q * a.dc_chg_cap + j] = v;
+                else a.dc_ctl[kDcChgOvf + q] = 1u;
+            }
+            if (ins) {
+                const uint32_t j = bs + (uint32_t)__popcll(sb & below);
+                if (j < a.dc_cap) {
+                    uint32_t* e = a.dc_list + 2u * ((size_t)q * a.dc_cap + j);
+                    e[0] = v;
+                    e[1] = (cv << 16) | newc;
+                } else {
+                    a.dc_ctl[kDcOvf + q] = 1u;
+                }
+            }
+            ev_flag = 1u;   // the commit reads the lists' lengths: this workgroup releases (sweep_tail)
         }
     }
 
@@ -3193,7 +3233,8 @@ struct mcmc_ctx {
     uint32_t* dc_ctl = nullptr;     // kDcWords control words, then the lists (one allocation)
     uint32_t* dc_cnt = nullptr;
     uint32_t* dc_mask = nullptr;
-    uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1;
+    unsigned long long* dc_open = nullptr;
+    uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1, dc_chg_cap = 0;
 };
 
 namespace {
@@ -3395,6 +3436,9 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     if (c->dc) {
         a.dc_ctl = c->dc_ctl;
         a.dc_list = c->dc_ctl + kDcWords;
+        a.dc_chg = a.dc_list + 4ull * c->dc_cap;
+        a.dc_chg_cap = c->dc_chg_cap;
+        a.dc_open = c->dc_open;
         a.dc_cnt = c->dc_cnt;
         a.dc_mask = c->dc_mask;
         a.dc_s0 = c->dc_s0;
@@ -3646,14 +3690,20 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     c->dc_cap = (uint32_t)S;
     c->dc_max = std::max<uint32_t>(64u, (uint32_t)(S / 8u));
     c->dc_apow = minstd_pow(kMinstdA, 64ull * c->grid.x * (c->block.x / 64u));
-    hipError_t e = hipMalloc(&c->dc_ctl, sizeof(uint32_t) * (kDcWords + 2ull * S));
+    c->dc_chg_cap = std::max<uint32_t>(4096u, nloc / 32u);   // past it: a full copy of the local rows
+    const size_t open_bytes = sizeof(unsigned long long) * (((size_t)nloc + 63u) / 64u) * c->nw;
+    hipError_t e = hipMalloc(&c->dc_ctl, sizeof(uint32_t) * (kDcWords + 4ull * S + 2ull * c->dc_chg_cap));
     if (e == hipSuccess) e = hipMalloc(&c->dc_cnt, std::max<size_t>(cnt_bytes, 4));
     if (e == hipSuccess) e = hipMalloc(&c->dc_mask, sizeof(uint32_t) * (size_t)nloc * c->nw);
+    if (e == hipSuccess) e = hipMalloc(&c->dc_open, open_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(c->dc_open, 0, open_bytes, c->stream);   // rows past nloc: never open
     if (e != hipSuccess) {
         (void)hipFree(c->dc_ctl);
         (void)hipFree(c->dc_cnt);
         (void)hipFree(c->dc_mask);
+        (void)hipFree(c->dc_open);
         c->dc_ctl = c->dc_cnt = c->dc_mask = nullptr;
+        c->dc_open = nullptr;
         if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); return MCMC_OK; }   // the scan sweep then
         return fail(MCMC_E_HIP, std::string("dense counts: ") + hipGetErrorString(e));
     }
@@ -4395,6 +4445,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     if (h.done && c->tailcut_max) {
         rc = run_tailcut(c, h, &s.finalViol, &s.tailcutPasses);
         if (rc) return rc;
+        if (c->dc) MCMC_HIP_TRY(dc_reset(c));   // the passes changed colours outside a sweep
     }
     c->last = s;
     // keep the host copy of the glibc window in step with the device stream
@@ -4849,6 +4900,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dc_ctl);
     (void)hipFree(c->dc_cnt);
     (void)hipFree(c->dc_mask);
+    (void)hipFree(c->dc_open);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
