@@ -12,17 +12,17 @@
 // keeps per local row w
 //     cnt[w][c] = #{u in S : (w, u) an arc, C_t[u] = c}    (uint32)
 // and the occupancy bits of those counts (dense mask), plus one "open" bit per row and mask word
-// (that word of the dense mask is not full). A sweep is then two launches:
-//   dc_update_kernel  brings the buffer the sweep writes (it holds C_t-1) to C_t on the local rows
-//                     (the previous sweep's restore list of changed rows, or a full copy), then
-//                     moves the counts by the vertices of S whose colour the previous sweep changed
-//                     (u's old colour -1, new colour +1 in every row holding u; a count crossing 0
-//                     flips its mask bit and, when the word's fullness changed, its open bit). For a
-//                     simple symmetric graph the rows holding u are u's own neighbours, and row u is
-//                     a local row (S lies inside the context's rows), so the tiled layout lists
-//                     them. The first sweep after a colouring is set, or one after more changes than
-//                     pay, rebuilds every count from the layout.
-//   dc_eval_kernel    lane per row, reading the row's colour and its tile's open words: a row that
+// (that word of the dense mask is not full). A sweep is one launch, dc_eval_kernel, in two phases:
+//   update            (dc_update_tasks) brings the buffer the sweep writes (it holds C_t-1) to C_t
+//                     on the local rows (the previous sweep's restore list of changed rows, or a
+//                     full copy), then moves the counts by the vertices of S whose colour the
+//                     previous sweep changed (u's old colour -1, new colour +1 in every row holding
+//                     u; a count crossing 0 flips its mask bit and, when the word's fullness
+//                     changed, its open bit). For a simple symmetric graph the rows holding u are
+//                     u's own neighbours, and row u is a local row (S lies inside the context's
+//                     rows), so the tiled layout lists them. The first sweep after a colouring is
+//                     set, or one after more changes than pay, rebuilds every count from the layout.
+//   evaluation        lane per row, reading the row's colour and its tile's open words: a row that
 //                     is not open has the full mask and is evaluated at once; an open row first
 //                     scans its other column blocks (the wave together, colours from the replica,
 //                     stopping once the mask is full). Only rows that change colour are written
@@ -73,99 +73,135 @@ __device__ __forceinline__ void dc_move(const SweepArgs& a, uint32_t lw, uint32_
     if (ob == 0u) dc_flip<NW>(a, lw, cb);
 }
 
-// Sweep t's update (all waves; grid-stride). First the buffer sweep t writes (it holds C_t-1) is
-// brought to C_t on the local rows: the vertices on the restore list are copied, or every local row
-// when that list overflowed or the counts are rebuilt -- the evaluation then writes only the rows
-// that change. Then the counts. Rebuild: a wave per local row, its segments in the blocks
-// overlapping S, colours of C_t counted in an LDS histogram, mask and open bits written. Incremental:
-// a wave per (listed vertex u, column block b of the local rows): u's neighbours in block b.
+// Sweep t's update, at the start of the evaluation launch (every workgroup of it). First the
+// buffer sweep t writes (it holds C_t-1) is brought to C_t on the local rows: the vertices on the
+// restore list are copied, or every local row when that list overflowed or the counts are rebuilt
+// -- the evaluation then writes only the rows that change. Then the counts. Rebuild: a wave per
+// local row, its segments in the blocks overlapping S, colours of C_t counted in an LDS histogram,
+// mask and open bits written. Incremental: a wave per (listed vertex u, column block b of the local
+// rows): u's neighbours in block b. The work is cut into tasks that the workgroups claim from a
+// counter (kDcTask); each adds its completed tasks to kDcDone once (a release) and every workgroup
+// waits for all of them (an acquire) before evaluating. A waiting workgroup only waits for tasks a
+// running workgroup has claimed, so the grid need not be co-resident; with nothing to update (the
+// usual converged sweep) no counter is touched.
+constexpr uint32_t kDcCopyRows = 16384;   // copy task: 1024 threads x 16 B
+constexpr uint32_t kDcRebuildRows = 64;   // rebuild task: 4 rows per wave
+// The control words the update reads (loaded by thread 0 at the launch's start, both parities).
+struct DcCtl {
+    uint32_t mode, ovf[2], chg[2], len[2];
+};
+__device__ __forceinline__ void dc_ctl_load(const SweepArgs& a, DcCtl& w) {
+    w.mode = a.dc_ctl[kDcMode];
+    for (int q = 0; q < 2; q++) {
+        w.ovf[q] = a.dc_ctl[kDcChgOvf + q];
+        w.chg[q] = a.dc_ctl[kDcChgLen + q];
+        w.len[q] = a.dc_ctl[kDcLen + q];
+    }
+}
 template <int NW>
-__global__ __launch_bounds__(256) void dc_update_kernel(SweepArgs a) {
-    __shared__ uint32_t hist[4][256];
-    const DevState* st = a.st;
-    if (st->done) return;
-    const uint32_t t = st->t;
-    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;   // C_t
-    const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwv = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t bl = a.block_log2;
+__device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, const DcCtl& w) {
+    __shared__ uint32_t sh_k;
     const uint32_t p = t & 1u;
-    const uint32_t mode = a.dc_ctl[kDcMode];
-    uint8_t* __restrict__ Y = (t & 1) ? a.colors0 : a.colors1;   // C_t-1, becomes C_t+1
-    {
-        const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
-        if (mode || a.dc_ctl[kDcChgOvf + p]) {
-            const size_t b0 = a.v_begin, b1 = a.v_end;
+    const uint32_t mode = w.mode, copy = mode | w.ovf[p];
+    const uint32_t m = min(w.chg[p], a.dc_chg_cap), len = min(w.len[p], a.dc_cap);
+    const uint32_t nloc = a.v_end - a.v_begin, bl = a.block_log2;
+    const uint32_t bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
+    const uint32_t nmov_w = mode ? 0u : len * nbl;   // len <= |S| / 8 + 1 when incremental: no overflow
+    const uint32_t n1 = copy ? (nloc + kDcCopyRows - 1u) / kDcCopyRows : (m + 1023u) / 1024u;
+    const uint32_t n2 = mode ? (nloc + kDcRebuildRows - 1u) / kDcRebuildRows : (nmov_w + 15u) / 16u;
+    const uint32_t T = n1 + n2;
+    if (T == 0u) return;
+    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;   // C_t
+    uint8_t* __restrict__ Y = (t & 1) ? a.colors0 : a.colors1;         // C_t-1, becomes C_t+1
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t* h = lds + 256u * wv;
+    uint32_t mine = 0;
+    for (;;) {
+        if (threadIdx.x == 0) sh_k = atomicAdd(&a.dc_ctl[kDcTask], 1u);
+        __syncthreads();
+        const uint32_t k = sh_k;
+        __syncthreads();   // every thread has read sh_k before thread 0 claims again
+        if (k >= T) break;
+        mine++;
+        if (k < n1 && copy) {
+            const size_t b0 = (size_t)a.v_begin + (size_t)k * kDcCopyRows, b1 = min((size_t)a.v_end, b0 + kDcCopyRows);
             const size_t q0 = (b0 + 15) & ~(size_t)15, q1 = (b1 & ~(size_t)15) > q0 ? (b1 & ~(size_t)15) : q0;
-            for (size_t i = q0 + 16 * tid; i < q1; i += 16 * nth)
+            for (size_t i = q0 + 16u * threadIdx.x; i < q1; i += 16u * blockDim.x)
                 *reinterpret_cast<uint4*>(Y + i) = *reinterpret_cast<const uint4*>(C + i);
-            for (size_t i = b0 + tid; i < (q0 < b1 ? q0 : b1); i += nth) Y[i] = C[i];
-            for (size_t i = (q1 > b0 ? q1 : b0) + tid; i < b1; i += nth) Y[i] = C[i];
-        } else {
-            const uint32_t m = min(a.dc_ctl[kDcChgLen + p], a.dc_chg_cap);
-            const uint32_t* __restrict__ R = a.dc_chg + (size_t)p * a.dc_chg_cap;
-            for (size_t i = tid; i < m; i += nth) {
-                const uint32_t u = R[i];
+            for (size_t i = b0 + threadIdx.x; i < (q0 < b1 ? q0 : b1); i += blockDim.x) Y[i] = C[i];
+            for (size_t i = (q1 > b0 ? q1 : b0) + threadIdx.x; i < b1; i += blockDim.x) Y[i] = C[i];
+        } else if (k < n1) {
+            const uint32_t i = k * 1024u + threadIdx.x;
+            if (i < m) {
+                const uint32_t u = a.dc_chg[(size_t)p * a.dc_chg_cap + i];
                 Y[u] = C[u];
             }
-        }
-    }
-    if (mode) {
-        uint32_t* h = hist[threadIdx.x >> 6];
-        const uint32_t b0 = a.dc_s0 >> bl, b1 = (a.dc_s1 - 1u) >> bl, sw = a.dc_s1 - a.dc_s0;
-        for (uint32_t l = wave; l < nloc; l += nwv) {
-            for (uint32_t i = lane; i < a.dc_cw; i += 64u) h[i] = 0;
-            dc_lds_wait();
-            for (uint32_t b = b0; b <= b1; b++) {
-                uint32_t s0, s1;
-                const uint16_t* gc;
-                dc_segment(a, l, b, s0, s1, gc);
-                const uint32_t base = b << bl;
-                for (uint32_t k = s0 + lane; k < s1; k += 64u) {
-                    const uint32_t u = base | (uint32_t)gc[k];
-                    if (u - a.dc_s0 < sw) atomicAdd(&h[C[u]], 1u);
-                }
-            }
-            dc_lds_wait();
-            uint32_t* cr = a.dc_cnt + (size_t)l * a.dc_cw;
-            for (uint32_t i = lane; i < a.dc_cw; i += 64u) cr[i] = h[i];
-            uint32_t* mk = a.dc_mask + (size_t)l * NW;
-            unsigned long long* ow = a.dc_open + (size_t)(l >> 6) * NW;
-            const unsigned long long obit = 1ull << (l & 63u);
-            for (uint32_t c0 = 0; c0 < 32u * NW; c0 += 64u) {
-                const uint32_t c = c0 + lane;
-                const uint64_t bm = __ballot(c < a.nCol && h[c] != 0u);
-                if (lane == 0) {
-                    for (uint32_t i = c0 >> 5; i < min((c0 >> 5) + 2u, (uint32_t)NW); i++) {
-                        const uint32_t m = (uint32_t)(bm >> (32u * (i - (c0 >> 5)))), fw = dc_fullw(a.nCol, i);
-                        mk[i] = m;
-                        if ((m & fw) != fw) atomicOr(&ow[i], obit);
-                        else atomicAnd(&ow[i], ~obit);
+        } else if (mode) {
+            const uint32_t b0 = a.dc_s0 >> bl, b1 = (a.dc_s1 - 1u) >> bl, sw = a.dc_s1 - a.dc_s0;
+            const uint32_t r0 = (k - n1) * kDcRebuildRows;
+            for (uint32_t l = r0 + wv; l < min(r0 + kDcRebuildRows, nloc); l += blockDim.x >> 6) {
+                for (uint32_t i = lane; i < a.dc_cw; i += 64u) h[i] = 0;
+                dc_lds_wait();
+                for (uint32_t b = b0; b <= b1; b++) {
+                    uint32_t s0, s1;
+                    const uint16_t* gc;
+                    dc_segment(a, l, b, s0, s1, gc);
+                    const uint32_t base = b << bl;
+                    for (uint32_t q = s0 + lane; q < s1; q += 64u) {
+                        const uint32_t u = base | (uint32_t)gc[q];
+                        if (u - a.dc_s0 < sw) atomicAdd(&h[C[u]], 1u);
                     }
                 }
+                dc_lds_wait();
+                uint32_t* cr = a.dc_cnt + (size_t)l * a.dc_cw;
+                for (uint32_t i = lane; i < a.dc_cw; i += 64u) cr[i] = h[i];
+                uint32_t* mk = a.dc_mask + (size_t)l * NW;
+                unsigned long long* ow = a.dc_open + (size_t)(l >> 6) * NW;
+                const unsigned long long obit = 1ull << (l & 63u);
+                for (uint32_t c0 = 0; c0 < 32u * NW; c0 += 64u) {
+                    const uint32_t c = c0 + lane;
+                    const uint64_t bm = __ballot(c < a.nCol && h[c] != 0u);
+                    if (lane == 0) {
+                        for (uint32_t i = c0 >> 5; i < min((c0 >> 5) + 2u, (uint32_t)NW); i++) {
+                            const uint32_t mw = (uint32_t)(bm >> (32u * (i - (c0 >> 5)))), fw = dc_fullw(a.nCol, i);
+                            mk[i] = mw;
+                            if ((mw & fw) != fw) atomicOr(&ow[i], obit);
+                            else atomicAnd(&ow[i], ~obit);
+                        }
+                    }
+                }
+                dc_lds_wait();   // every lane's reads of h are done before the next row clears it
             }
-            dc_lds_wait();   // every lane's reads of h are done before the next row clears it
+        } else {
+            const uint32_t task = (k - n1) * 16u + wv;
+            if (task < nmov_w) {
+                const uint32_t i = task / nbl, b = bl0 + (task - i * nbl);
+                const uint32_t* e = a.dc_list + 2u * ((size_t)p * a.dc_cap + i);   // (u, ca << 16 | cb)
+                const uint32_t u = e[0], ab = e[1];
+                const uint32_t ca = ab >> 16, cb = ab & 0xFFFFu;
+                uint32_t s0, s1;
+                const uint16_t* gc;
+                dc_segment(a, u - a.v_begin, b, s0, s1, gc);
+                const uint32_t base = b << bl;
+                for (uint32_t q = s0 + lane; q < s1; q += 64u) {
+                    const uint32_t lw = (base | (uint32_t)gc[q]) - a.v_begin;
+                    if (lw < nloc) dc_move<NW>(a, lw, ca, cb);
+                }
+            }
         }
-        return;
+        __syncthreads();   // the task's stores are complete before the next claim / the release
     }
-    const uint32_t len = min(a.dc_ctl[kDcLen + p], a.dc_cap);
-    if (len == 0) return;
-    const uint32_t* __restrict__ L = a.dc_list + 2u * (size_t)p * a.dc_cap;   // (u, ca << 16 | cb)
-    const uint32_t bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
-    const uint64_t tasks = (uint64_t)len * nbl;
-    for (uint64_t task = wave; task < tasks; task += nwv) {
-        const uint32_t i = (uint32_t)(task / nbl), b = bl0 + (uint32_t)(task - (uint64_t)i * nbl);
-        const uint32_t u = L[2u * i], ab = L[2u * i + 1u];
-        const uint32_t ca = ab >> 16, cb = ab & 0xFFFFu;
-        uint32_t s0, s1;
-        const uint16_t* gc;
-        dc_segment(a, u - a.v_begin, b, s0, s1, gc);
-        const uint32_t base = b << bl;
-        for (uint32_t k = s0 + lane; k < s1; k += 64u) {
-            const uint32_t lw = (base | (uint32_t)gc[k]) - a.v_begin;
-            if (lw < nloc) dc_move<NW>(a, lw, ca, cb);
+    if (threadIdx.x == 0) {
+        if (mine) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            atomicAdd(&a.dc_ctl[kDcDone], mine);
         }
+        while (__hip_atomic_load(&a.dc_ctl[kDcDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < T)
+            __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
+    __syncthreads();
 }
 
 // Rows of this wave whose dense mask is not full (`open`): each in turn, the whole wave scans its
@@ -246,12 +282,14 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     extern __shared__ uint4 dc_lds[];
     __shared__ TailShared sh;
     __shared__ float2 ewl[256];
+    __shared__ DcCtl sh_ctl;
     DevState* __restrict__ st = a.st;
     if (a.check_done && st->done) return;
     if (threadIdx.x == 0) {
         sh.wg_viol = 0;
         sh.wg_ev = 0;
         sh.viol = 0;
+        dc_ctl_load(a, sh_ctl);
     }
     const uint32_t t = st->t;
     const uint32_t x_t = st->x_t;
@@ -269,6 +307,7 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
 #pragma unroll
     for (int i = 0; i < NW; i++) fullw[i] = dc_fullw(a.nCol, (uint32_t)i);
     __syncthreads();
+    dc_update_tasks<NW>(a, t, reinterpret_cast<uint32_t*>(dc_lds), sh_ctl);
     const int lane = threadIdx.x & 63;
     const uint32_t nwaves = blockDim.x >> 6;
     const uint32_t gw = blockIdx.x * nwaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = gridDim.x * nwaves;
@@ -394,7 +433,6 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
 
 template <int NW>
 void launch_dc(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
-    dc_update_kernel<NW><<<g.x * 8u, 256, 0, s>>>(a);
     dc_eval_kernel<NW><<<g, b, lds, s>>>(a);
 }
 template <int NW>

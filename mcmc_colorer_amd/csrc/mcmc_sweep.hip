@@ -255,6 +255,9 @@ constexpr uint32_t kDcOpen = 5;    // rows of the running sweep whose dense mask
 constexpr uint32_t kDcStat = 8;    // u64 [4]: incremental sweeps, rebuilds, listed vertices, open rows
 constexpr uint32_t kDcChgLen = 16; // [2] local vertices on the restore list, by parity (t + 1) & 1
 constexpr uint32_t kDcChgOvf = 18; // [2] that list overflowed: the next update copies every local row
+constexpr uint32_t kDcCommitRestore = 8192;   // restore lists up to this long: applied by the commit
+constexpr uint32_t kDcTask = 20;   // the running sweep's update tasks claimed (dense_counts.h dc_update_tasks)
+constexpr uint32_t kDcDone = 21;   // and completed
 constexpr uint32_t kDcWords = 24;
 constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: the commit's sort buffer
 
@@ -280,6 +283,8 @@ __device__ void dc_commit(const SweepArgs& a, uint32_t t) {
     k[kDcOvf + p] = 0;
     k[kDcChgLen + p] = 0;
     k[kDcChgOvf + p] = 0;
+    k[kDcTask] = 0;
+    k[kDcDone] = 0;
     k[kDcMode] = (ovf || len > a.dc_max) ? 1u : 0u;
 }
 
@@ -661,6 +666,20 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
     MCMC_COMMIT_PHASE(a, 4);
     if (a.dc_ctl != nullptr) {
         __syncthreads();   // the replay's list appends are in
+        // a short restore list is applied here, C_t+1 into the C_t buffer (the one sweep t + 1
+        // writes), so that sweep's update has nothing to do when no vertex of S moved
+        const uint32_t q = (t + 1u) & 1u;
+        const uint32_t m = __hip_atomic_load(&a.dc_ctl[kDcChgLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ovf = __hip_atomic_load(&a.dc_ctl[kDcChgOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (m != 0u && ovf == 0u && m <= kDcCommitRestore) {
+            CT* B = const_cast<CT*>(C);
+            for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+                const uint32_t u = a.dc_chg[(size_t)q * a.dc_chg_cap + i];
+                B[u] = Cs[u];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) a.dc_ctl[kDcChgLen + q] = 0;
+        }
         if (threadIdx.x == 0) dc_commit(a, t);
     }
     if (a.inc != nullptr) {
