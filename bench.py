@@ -56,7 +56,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-KERNELS = {"dense": "dc_update_kernel+dc_eval_kernel (one sweep)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
+KERNELS = {"dense": "dc_eval_kernel (one sweep: update + evaluation + commit)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
            "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)",
            "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
@@ -473,42 +473,46 @@ def main() -> int:
     if dist is not None:
         dn0 = dn1 = None
         if not ref:
-            out8 = (ctypes.c_uint64 * 8)()
+            out8 = (ctypes.c_uint64 * 10)()
             check(lib().mcmc_get_dense_stats(drv._ctx, out8))
             dn1 = {"enabled": bool(out8[0])}
     dense_on = bool(dn1 and dn1["enabled"])
     if dense_on:
         variant = "dense"
-        if dist is not None:   # this rank's evaluation bytes: its rows' dense masks, own colours, writes
+        if dist is not None:   # this rank's evaluation bytes: its rows' colours and open words
             nwd = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
-            b_alg = int(bounds[rank + 1] - bounds[rank]) * (4 * nwd + 2)
+            b_alg = int(bounds[rank + 1] - bounds[rank]) * (1 + nwd / 8)
     dense = None
     if dense_on and dist is None:
-        # the dense-count sweep (csrc/dense_counts.h): per sweep every row's dense mask (NW words) and
-        # own colour read, its new colour written; per vertex of the dense range that changed colour
-        # its local arcs (id + two count atomics); rows that scanned past the range (ids + colour
-        # gathers, an upper bound: their whole rows outside it); a rebuild reads every row's arcs
-        # into the range
-        d = {k: dn1[k] - dn0[k] for k in ("incremental_sweeps", "rebuilds", "moved_vertices", "open_rows")}
+        # the dense-count sweep (csrc/dense_counts.h): per sweep every row's own colour and its open
+        # bits (NW bits) read; per row that changed colour its new colour written, and the restore
+        # (read + write) into the next sweep's buffer; per vertex of the dense range that changed
+        # colour its local arcs (id + two count atomics); rows that scanned past the range (their
+        # dense mask, ids + colour gathers, an upper bound: their whole rows outside it); a rebuild
+        # reads every row's arcs into the range and copies the local colours
+        d = {k: dn1[k] - dn0[k] for k in ("incremental_sweeps", "rebuilds", "moved_vertices", "open_rows",
+                                          "changed_rows", "copy_sweeps")}
         S = max(1, d["incremental_sweeps"] + d["rebuilds"])
         nw = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
         deg = m / max(1, n)
         span = dn1["s1"] - dn1["s0"]
-        per_row = 4 * nw + 2
-        b_eval = n * per_row
+        b_eval = n * (1.0 + nw / 8.0)
+        b_chg = d["changed_rows"] * 3.0 + d["copy_sweeps"] * 2.0 * n
         b_upd = d["moved_vertices"] * deg * 10.0
-        b_open = d["open_rows"] * deg * (1.0 - span / max(1, n)) * 3.0
-        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 3.0 + n * a.ncol * 4.0 + n * nw * 4.0)
-        b_alg = b_eval + (b_upd + b_open + b_rebuild) / S
+        b_open = d["open_rows"] * (4.0 * nw + deg * (1.0 - span / max(1, n)) * 3.0)
+        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 3.0 + n * a.ncol * 4.0 + n * nw * 4.0 + 2.0 * n)
+        b_alg = b_eval + (b_chg + b_upd + b_open + b_rebuild) / S
         dense = dict(d, sweeps_counted=S, dense_range=[dn1["s0"], dn1["s1"]],
                      moved_vertices_per_sweep=d["moved_vertices"] / S, open_rows_per_sweep=d["open_rows"] / S,
                      rebuild_threshold=dn1["rebuild_threshold"], bytes_per_sweep=b_alg,
-                     bytes={"evaluation": b_eval, "updates": b_upd / S, "open_rows": b_open / S,
-                            "rebuilds": b_rebuild / S},
+                     changed_rows_per_sweep=d["changed_rows"] / S,
+                     bytes={"evaluation": b_eval, "changed_rows": b_chg / S, "updates": b_upd / S,
+                            "open_rows": b_open / S, "rebuilds": b_rebuild / S},
                      note="dense-count sweep: every row keeps the counts of its neighbours' colours over a fixed "
                           "dense column range, moved each sweep by the vertices there that changed colour; a row "
-                          "whose dense mask holds every colour is evaluated without a scan, the rest scan their "
-                          "other column blocks. Bit-identical to the scan sweeps (tests/test_dense.py).")
+                          "whose dense mask holds every colour (open bit clear) is evaluated from its own colour "
+                          "alone, the rest scan their other column blocks; only rows that change colour are "
+                          "written. One launch per sweep. Bit-identical to the scan sweeps (tests/test_dense.py).")
         if not a.no_full_scan:
             # the same graph through the tiled scan sweep (MCMC_DENSE=0, the r03 early-exit kernel) and
             # the full scan (MCMC_FULL_SCAN=1): every sweep scans the layout

@@ -172,8 +172,9 @@ int mcmc_set_bench_mode(mcmc_ctx* c, int on);
 /* The dense-count sweep of a tiled context (csrc/dense_counts.h; on unless MCMC_DENSE=0 or the graph
  * is not simple and symmetric): out = {on, dense range begin, end, incremental sweeps, count
  * rebuilds, vertices of the range moved by updates, rows that scanned beyond the range, the update
- * list's rebuild threshold}; all 0 when off. */
-int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[8]);
+ * list's rebuild threshold, local rows that changed colour (the restore lists; a list past its
+ * capacity counts as its capacity), sweeps whose restore list overflowed}; all 0 when off. */
+int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[10]);
 /* Diagnostics of the tiled sweep's scan (no reference counterpart): with stats on, every sweep adds
  * the 16-byte id quads it loaded and the (group, column block) pairs it staged (table + colour
  * slice); mcmc_set_scan_stats(c, 1) also zeroes them. The sweep stops scanning a row once its

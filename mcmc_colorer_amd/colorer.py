@@ -309,12 +309,12 @@ class ColoringMCMC:
         """The dense-count sweep since the colouring was initialised (mcmc_get_dense_stats; csrc/
         dense_counts.h): whether the context runs it, its dense column range, sweeps whose update moved
         the counts by the changed vertices, count rebuilds, vertices moved, rows that scanned past the
-        range, and the update list's rebuild threshold."""
-        out = (ctypes.c_uint64 * 8)()
+        range, the update list's rebuild threshold, rows that changed colour and restore-list overflows."""
+        out = (ctypes.c_uint64 * 10)()
         check(lib().mcmc_get_dense_stats(self._ctx, out))
         return {"enabled": bool(out[0]), "s0": int(out[1]), "s1": int(out[2]), "incremental_sweeps": int(out[3]),
                 "rebuilds": int(out[4]), "moved_vertices": int(out[5]), "open_rows": int(out[6]),
-                "rebuild_threshold": int(out[7])}
+                "rebuild_threshold": int(out[7]), "changed_rows": int(out[8]), "copy_sweeps": int(out[9])}
 
     def save(self, iteration: int) -> None:
         d = self.directory

@@ -231,6 +231,7 @@ struct SweepArgs {
     uint32_t* dc_chg;           // [2][dc_chg_cap] every local vertex whose colour changed (restore list)
     unsigned long long* dc_open;   // [ntiles][NW] bit j of word (tile, i): row 64 tile + j's mask word i not full
     uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max, dc_chg_cap;
+    uint32_t dc_commit_restore;  // restore lists up to this long are applied by the commit
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -256,8 +257,10 @@ constexpr uint32_t kDcStat = 8;    // u64 [4]: incremental sweeps, rebuilds, lis
 constexpr uint32_t kDcChgLen = 16; // [2] local vertices on the restore list, by parity (t + 1) & 1
 constexpr uint32_t kDcChgOvf = 18; // [2] that list overflowed: the next update copies every local row
 constexpr uint32_t kDcCommitRestore = 8192;   // restore lists up to this long: applied by the commit
+                                               // (at most half the list's capacity)
 constexpr uint32_t kDcTask = 20;   // the running sweep's update tasks claimed (dense_counts.h dc_update_tasks)
 constexpr uint32_t kDcDone = 21;   // and completed
+constexpr uint32_t kDcStat2 = 22;  // u32 [2]: rows on the restore lists (saturating), restore-list overflows
 constexpr uint32_t kDcWords = 24;
 constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: the commit's sort buffer
 
@@ -671,7 +674,12 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         const uint32_t q = (t + 1u) & 1u;
         const uint32_t m = __hip_atomic_load(&a.dc_ctl[kDcChgLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t ovf = __hip_atomic_load(&a.dc_ctl[kDcChgOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (m != 0u && ovf == 0u && m <= kDcCommitRestore) {
+        if (threadIdx.x == 0) {
+            const uint32_t r = a.dc_ctl[kDcStat2] + min(m, a.dc_chg_cap);
+            a.dc_ctl[kDcStat2] = r < a.dc_ctl[kDcStat2] ? ~0u : r;
+            a.dc_ctl[kDcStat2 + 1] += ovf ? 1u : 0u;
+        }
+        if (m != 0u && ovf == 0u && m <= a.dc_commit_restore) {
             CT* B = const_cast<CT*>(C);
             for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
                 const uint32_t u = a.dc_chg[(size_t)q * a.dc_chg_cap + i];
@@ -3457,6 +3465,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.dc_list = c->dc_ctl + kDcWords;
         a.dc_chg = a.dc_list + 4ull * c->dc_cap;
         a.dc_chg_cap = c->dc_chg_cap;
+        a.dc_commit_restore = std::min<uint32_t>(kDcCommitRestore, c->dc_chg_cap / 2u);
         a.dc_open = c->dc_open;
         a.dc_cnt = c->dc_cnt;
         a.dc_mask = c->dc_mask;
@@ -3710,6 +3719,7 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     c->dc_max = std::max<uint32_t>(64u, (uint32_t)(S / 8u));
     c->dc_apow = minstd_pow(kMinstdA, 64ull * c->grid.x * (c->block.x / 64u));
     c->dc_chg_cap = std::max<uint32_t>(4096u, nloc / 32u);   // past it: a full copy of the local rows
+    if (const char* cc = getenv("MCMC_DENSE_CHG_CAP")) c->dc_chg_cap = (uint32_t)std::max(2, atoi(cc));   // tests
     const size_t open_bytes = sizeof(unsigned long long) * (((size_t)nloc + 63u) / 64u) * c->nw;
     hipError_t e = hipMalloc(&c->dc_ctl, sizeof(uint32_t) * (kDcWords + 4ull * S + 2ull * c->dc_chg_cap));
     if (e == hipSuccess) e = hipMalloc(&c->dc_cnt, std::max<size_t>(cnt_bytes, 4));
@@ -4553,9 +4563,9 @@ int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
     return MCMC_OK;
 }
 
-int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[8]) {
+int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[10]) {
     if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
-    for (int i = 0; i < 8; i++) out[i] = 0;
+    for (int i = 0; i < 10; i++) out[i] = 0;
     if (!c->dc) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     uint32_t h[kDcWords];
@@ -4570,6 +4580,8 @@ int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[8]) {
     out[5] = s[2];
     out[6] = s[3];
     out[7] = c->dc_max;
+    out[8] = h[kDcStat2];
+    out[9] = h[kDcStat2 + 1];
     return MCMC_OK;
 }
 

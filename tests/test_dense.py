@@ -29,10 +29,11 @@ def M(hip_lib):
 def dense_stats(col):
     from mcmc_colorer_amd._lib import check, lib, u64ptr
 
-    out = np.zeros(8, dtype=np.uint64)
+    out = np.zeros(10, dtype=np.uint64)
     check(lib().mcmc_get_dense_stats(col._ctx, u64ptr(out)))
     return {"on": int(out[0]), "s0": int(out[1]), "s1": int(out[2]), "incremental": int(out[3]),
-            "rebuilds": int(out[4]), "listed": int(out[5]), "open": int(out[6]), "max": int(out[7])}
+            "rebuilds": int(out[4]), "listed": int(out[5]), "open": int(out[6]), "max": int(out[7]),
+            "changed": int(out[8]), "copies": int(out[9])}
 
 
 CASES = [
@@ -78,6 +79,21 @@ def test_dense_list_overflow_rebuilds(M, monkeypatch):
     assert_same(col, st, r)
     ds = dense_stats(col)
     assert ds["max"] == 75 and ds["rebuilds"] > 1
+
+
+@pytest.mark.parametrize("eps,cap", [(1e-3, 64), (1e-3, 8), (3.3e6, 64), (1e-8, 2)])
+def test_dense_restore_lists(M, monkeypatch, eps, cap):
+    """The evaluation writes only rows that change colour; the next sweep's buffer gets them back
+    from the restore list -- applied by the commit (lists up to cap / 2), by the next launch's
+    update tasks (longer ones), or by a full copy once the list overflows (MCMC_DENSE_CHG_CAP)."""
+    monkeypatch.setenv("MCMC_DENSE_CHG_CAP", str(cap))
+    off, idx, nc, r = oracle_case(3000, 0.02, 16, 37, epsilon=eps, tabooIteration=1, maxRip=40)
+    col, st, _ = gpu_run(M, off, idx, nc, 37, 3000 * 3001 // 2, eps=eps, maxRip=40, taboo=1)
+    assert_same(col, st, r)
+    ds = dense_stats(col)
+    assert ds["on"] == 1 and ds["changed"] > 0
+    if eps > 1.0:
+        assert ds["copies"] > 0   # most colours change every sweep: the lists overflow
 
 
 def test_dense_off_is_the_scan_sweep(M, monkeypatch):
@@ -149,7 +165,7 @@ def test_dense_partitioned_loopback(M, monkeypatch, world):
         assert (st[k].iter, st[k].finalViol, st[k].glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
     from mcmc_colorer_amd._lib import check, lib, u64ptr
 
-    out = np.zeros(8, dtype=np.uint64)
+    out = np.zeros(10, dtype=np.uint64)
     check(lib().mcmc_get_dense_stats(lp._ctx[world - 1], u64ptr(out)))
     b = plan_rows(3000, world)
     assert out[0] == 1 and out[1] == b[world - 1] and out[2] == b[world - 1] + 150 and out[3] > 0
