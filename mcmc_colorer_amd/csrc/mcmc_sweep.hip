@@ -3698,7 +3698,7 @@ int simple_symmetric(GraphDev& gd, uint32_t vb, uint32_t ve, hipStream_t stream,
 
 // The dense-count sweep of a tiled context (dense_counts.h), when the graph allows it and
 // MCMC_DENSE is not 0: S = the first |S| local rows, |S| such that a row's expected neighbours in
-// S number nCol (ln nCol + 10) (MCMC_DENSE_ROWS overrides |S|); counts, masks and lists allocated.
+// S number nCol (ln nCol + K), K below (MCMC_DENSE_ROWS overrides |S|); counts, masks and lists allocated.
 int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     const char* de = getenv("MCMC_DENSE");
     if ((de && atoi(de) == 0) || nloc == 0 || c->p.nCol > 256 || !c->tl) return MCMC_OK;
@@ -3707,7 +3707,13 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     if (!ok) return MCMC_OK;
     const uint32_t nCol = c->p.nCol;
     const double dbar = (double)c->tl->arcs / (double)nloc;
-    const double target = (double)nCol * (std::log((double)nCol) + 10.0);
+    // K = 10: a row misses a colour in S with probability ~e^-10. Each sweep with an open row pays
+    // a chain of dependent loads (~6 us) in the wave holding it, while every unit of K costs the
+    // rebuild nloc nCol more counted arcs (~2.3 ms at C3, ~12 us at C2): small contexts take
+    // K = ln(nloc) + 3 (an open row in ~5 % of sweeps), large ones keep 10.
+    double K = 10.0;
+    if ((double)nloc * nCol <= 2e7) K = std::max(K, std::log((double)nloc) + 3.0);
+    const double target = (double)nCol * (std::log((double)nCol) + K);
     uint64_t S = dbar > 0.0 ? (uint64_t)std::ceil(target * (double)c->n / dbar) : nloc;
     if (const char* dr = getenv("MCMC_DENSE_ROWS")) S = (uint64_t)std::max(1, atoi(dr));
     S = std::max<uint64_t>(1, std::min<uint64_t>(S, nloc));
