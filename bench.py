@@ -449,6 +449,11 @@ def main() -> int:
         barrier()
         wall = time.perf_counter() - t0
         kernel_ms = st.loopMs / a.steps   # device time of one whole step on this rank's stream
+        xs = [ctypes.c_uint64() for _ in range(4)]
+        check(lib().mcmc_part_exchange_stats(drv._ctx, *[ctypes.byref(x) for x in xs]))
+        exchange = {"delta_steps": xs[0].value, "full_steps": xs[1].value, "overflows": xs[2].value,
+                    "bytes_sent": xs[3].value, "bytes_sent_per_step": xs[3].value / max(1, a.steps),
+                    "what": "this rank's timed steps (mcmc_part_exchange_stats); world 1 sends nothing"}
         info = drv.info()
         info["bounds"] = [int(x) for x in bounds]
         w = torch.tensor([wall], dtype=torch.float64)
@@ -649,6 +654,8 @@ def main() -> int:
         out["wide_inc"] = wide_inc
     if dense is not None:
         out["dense"] = dense
+    if dist is not None:
+        out["exchange"] = exchange
     if dist is None and a.config == "c5" and not a.no_convergence:
         # the wide sweep WITH violators in every timed sweep (nCol = maxDeg / 4 does not converge):
         # the reference loop capped at 20 sweeps, device time per sweep and the per-sweep Cviol

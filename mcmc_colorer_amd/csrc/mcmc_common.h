@@ -172,6 +172,9 @@ int part_set_delta(mcmc_ctx* c, uint32_t* d0, uint32_t* d1);
 bool part_delta_ok(const mcmc_ctx* c);
 const void* part_state_ptr(const mcmc_ctx* c);   // device state: {t, done, x_t, err} in its first 16 bytes
 int part_sweep(mcmc_ctx* c, bool delta);
+// A world-1 partition's `steps` full-mode steps as one cached hipGraph launch (the one-GPU fused
+// step each); returns 1 (nothing launched) when the context is not such a partition.
+int part_solo_batch(mcmc_ctx* c, uint32_t steps);
 int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride);
 int part_sync_remote(mcmc_ctx* c);
 // Per-context driver resources, created on first use and kept until mcmc_destroy (a run then pays no

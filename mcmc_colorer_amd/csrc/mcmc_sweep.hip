@@ -5043,6 +5043,29 @@ int part_sweep(mcmc_ctx* c, bool delta) {
     return MCMC_OK;
 }
 
+int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
+    if (!c || !c->part || !part_solo(c) || !c->initialized || steps == 0) return 1;
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    c->ran = true;
+    const uint32_t key = 0x80000000u | steps;   // (c->batch: the one-GPU run's batches are plain counts)
+    if (!(c->batch_exec && c->batch == key)) {
+        if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
+        SweepArgs a = make_args(c, 1);
+        a.dcap = 0u;
+        a.fused = c->wide ? 0 : 1;   // as part_sweep's world-1 step
+        hipGraph_t graph;
+        MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        for (uint32_t i = 0; i < steps; i++) launch_pair(c, a);
+        MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
+        hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+        c->batch = key;
+    }
+    MCMC_HIP_TRY(hipGraphLaunch(c->batch_exec, c->stream));
+    return MCMC_OK;
+}
+
 int part_commit(mcmc_ctx* c, int mode, const uint32_t* spill, uint32_t stride) {
     if (!c || !c->part) return fail(MCMC_E_STATE, "mcmc_part_attach first");
     if (part_solo(c)) return MCMC_OK;   // world 1: the sweep committed (part_sweep)

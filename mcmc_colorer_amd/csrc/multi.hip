@@ -490,6 +490,20 @@ int part_run_impl(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
     uint32_t full_left = 0;                // steps to run in full mode after a delta overflow
     std::vector<uint8_t> was_delta;        // mode of every enqueued step (index t - t_begin)
     auto enqueue = [&](uint32_t steps) -> int {
+        if (D.d.size() == 1 && D.world == 1 && !D.stub && !(D.delta_ok && full_left == 0)) {
+            // world 1 in full mode: the steps are the one-GPU fused step, one cached graph per batch
+            const int rc = part_solo_batch(D.ctx[0], steps);
+            if (rc == MCMC_OK) {
+                for (uint32_t s = 0; s < steps; s++, t++) {
+                    if (full_left) full_left--;
+                    was_delta.push_back(0);
+                    part_add_xstats(D.ctx[0], 0, 1, 0, 0);
+                }
+                D.synced = false;
+                return MCMC_OK;
+            }
+            if (rc != 1) return rc;
+        }
         for (uint32_t s = 0; s < steps; s++, t++) {
             const bool delta = D.delta_ok && full_left == 0;
             if (full_left) full_left--;
