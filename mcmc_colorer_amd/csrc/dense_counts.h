@@ -229,6 +229,11 @@ struct DcScan {
 template <int NW>
 __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restrict__ C, uint32_t l, bool open,
                                                 DcMask<NW> acc, DcMask<NW> fullw, int lane) {
+    // kDcScanBlocks column blocks per round, 16 lanes each (segment start/end, then up to 8 ids per
+    // lane in flight, then their colours): one chain of three dependent loads covers the blocks a
+    // missing colour is almost always found in, instead of one chain per block
+    constexpr uint32_t kDcScanBlocks = 4;
+    const uint32_t grp = (uint32_t)lane >> 4, gl = (uint32_t)lane & 15u;
     uint64_t pend = __ballot(open);
     while (pend) {
         const int j = __ffsll((long long)pend) - 1;
@@ -239,16 +244,28 @@ __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restr
         uint32_t cur[NW];
 #pragma unroll
         for (int i = 0; i < NW; i++) cur[i] = __shfl(acc.w[i], j, 64);
-        for (uint32_t b = 0; b < d.nb; b++) {
-            const uint32_t lo = b << d.bl;
-            if (lo >= d.s0 && lo + (1u << d.bl) <= d.s1) continue;   // inside S: in the counts
-            const uint32_t* ts = d.tseg + ((size_t)g * d.nb + b) * tseg_stride(d.R);
-            const uint32_t raw = ts[r];
-            const uint32_t s0 = raw & kTsegPos, s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
+        for (uint32_t b0 = 0; b0 < d.nb; b0 += kDcScanBlocks) {
+            const uint32_t b = b0 + grp, lo = b << d.bl;
+            const bool act = b < d.nb && !(lo >= d.s0 && lo + (1u << d.bl) <= d.s1);   // inside S: counted
+            if (!__ballot(act)) continue;
+            uint32_t s0 = 0, s1 = 0;
+            if (act) {
+                const uint32_t* ts = d.tseg + ((size_t)g * d.nb + b) * tseg_stride(d.R);
+                const uint32_t raw = ts[r];
+                s0 = raw & kTsegPos;
+                s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
+            }
             uint32_t m[NW];
 #pragma unroll
             for (int i = 0; i < NW; i++) m[i] = 0;
-            for (uint32_t k = s0 + (uint32_t)lane; k < s1; k += 64u) set_color_bit<NW>(m, C[lo | (uint32_t)gc[k]]);
+            for (uint32_t k = s0 + gl; __ballot(k < s1); k += 128u) {
+                uint32_t id[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) id[q] = k + 16u * q < s1 ? (uint32_t)gc[k + 16u * q] : 0xFFFFFFFFu;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (id[q] != 0xFFFFFFFFu) set_color_bit<NW>(m, C[lo | id[q]]);
+            }
             bool full = true;
 #pragma unroll
             for (int i = 0; i < NW; i++) {
@@ -275,6 +292,50 @@ __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restr
 // the buffer written); any other row -- open, taboo, changing, or the walk's rare cases -- goes
 // through evaluate_lane, one row position j of the lanes at a time, open rows first completing
 // their mask (dc_open_scan). u_v of row l is x_t 16807^(v_begin + l + 1).
+// The workgroup's staged appends (DcStage, evaluate_lane) into the global lists, all threads: a
+// stage that never filled is copied behind one reservation per list; one that overflowed (its
+// holes are ~0u) entry by entry. Returns whether anything was appended (the workgroup releases).
+__device__ bool dc_stage_flush(const SweepArgs& a, DevState* st, DcStage& stg, uint32_t t) {
+    __shared__ uint32_t base[3];
+    const uint32_t q = (t + 1u) & 1u;
+    const uint32_t caps[3] = {kDcStageChg, kDcStageS, kDcStageEv};
+    const uint32_t n0 = stg.n[0], n1 = stg.n[1], n2 = stg.n[2];
+    if ((n0 | n1 | n2) == 0u) return false;
+    if (threadIdx.x == 0) {
+        base[0] = (n0 && n0 <= caps[0]) ? atomicAdd(&a.dc_ctl[kDcChgLen + q], n0) : 0u;
+        base[1] = (n1 && n1 <= caps[1]) ? atomicAdd(&a.dc_ctl[kDcLen + q], n1) : 0u;
+        base[2] = (n2 && n2 <= caps[2]) ? atomicAdd(&st->ev_count, n2) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < min(n0, caps[0]); i += blockDim.x) {
+        const uint32_t v = stg.chg[i];
+        if (v == ~0u) continue;
+        const uint32_t j = n0 <= caps[0] ? base[0] + i : atomicAdd(&a.dc_ctl[kDcChgLen + q], 1u);
+        if (j < a.dc_chg_cap) a.dc_chg[(size_t)q * a.dc_chg_cap + j] = v;
+        else a.dc_ctl[kDcChgOvf + q] = 1u;
+    }
+    for (uint32_t i = threadIdx.x; i < min(n1, caps[1]); i += blockDim.x) {
+        const uint32_t v = stg.s[2u * i];
+        if (v == ~0u) continue;
+        const uint32_t j = n1 <= caps[1] ? base[1] + i : atomicAdd(&a.dc_ctl[kDcLen + q], 1u);
+        if (j < a.dc_cap) {
+            uint32_t* e = a.dc_list + 2u * ((size_t)q * a.dc_cap + j);
+            e[0] = v;
+            e[1] = stg.s[2u * i + 1u];
+        } else {
+            a.dc_ctl[kDcOvf + q] = 1u;
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < min(n2, caps[2]); i += blockDim.x) {
+        const uint32_t v = stg.ev[i];
+        if (v == ~0u) continue;
+        const uint32_t j = n2 <= caps[2] ? base[2] + i : atomicAdd(&st->ev_count, 1u);
+        if (j < a.ev_cap) a.events[j] = v;
+        else atomicOr(&st->err, 1u);
+    }
+    return true;
+}
+
 constexpr uint32_t kDcLaneRows = 16;
 constexpr uint32_t kDcSpan = 64u * kDcLaneRows;
 template <int NW>
@@ -284,16 +345,17 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     __shared__ float2 ewl[256];
     __shared__ DcCtl sh_ctl;
     DevState* __restrict__ st = a.st;
-    if (a.check_done && st->done) return;
+    const uint4 s4 = *reinterpret_cast<const uint4*>(st);   // {t, done, x_t, err}: one load
+    if (a.check_done && s4.y) return;
     if (threadIdx.x == 0) {
         sh.wg_viol = 0;
         sh.wg_ev = 0;
         sh.viol = 0;
         dc_ctl_load(a, sh_ctl);
     }
-    const uint32_t t = st->t;
-    const uint32_t x_t = st->x_t;
-    const uint32_t err0 = st->err;
+    const uint32_t t = s4.x;
+    const uint32_t x_t = s4.z;
+    const uint32_t err0 = s4.w;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     const uint32_t nloc = a.v_end - a.v_begin;
@@ -308,6 +370,19 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     for (int i = 0; i < NW; i++) fullw[i] = dc_fullw(a.nCol, (uint32_t)i);
     __syncthreads();
     dc_update_tasks<NW>(a, t, reinterpret_cast<uint32_t*>(dc_lds), sh_ctl);
+    // the list appends' stage (dc_lds is free between the update's histograms and the commit)
+    __shared__ DcStage stg;
+    {
+        uint32_t* w = reinterpret_cast<uint32_t*>(dc_lds);
+        for (uint32_t i = threadIdx.x; i < kDcStageChg + 2u * kDcStageS + kDcStageEv; i += blockDim.x) w[i] = ~0u;
+        if (threadIdx.x == 0) {
+            stg.n[0] = stg.n[1] = stg.n[2] = 0;
+            stg.chg = w;
+            stg.s = w + kDcStageChg;
+            stg.ev = w + kDcStageChg + 2u * kDcStageS;
+        }
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const uint32_t nwaves = blockDim.x >> 6;
     const uint32_t gw = blockIdx.x * nwaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), GW = gridDim.x * nwaves;
@@ -401,7 +476,7 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
                 uint32_t acc[NW];                                                                   \
                 _Pragma("unroll") for (int i = 0; i < NW; i++) acc[i] = m.w[i];                     \
                 wave_viol += evaluate_lane<NW>(a, st, Cs, nd, l, acc, lane, wave_ev, vf, cv, tab,   \
-                                               minstd_mulmod(xl, kMinstdLanePow[j]), ew);           \
+                                               minstd_mulmod(xl, kMinstdLanePow[j]), ew, &stg);     \
             }                                                                                       \
         }                                                                                           \
         xs = minstd_mulmod(xs, aspan);                                                              \
@@ -427,7 +502,9 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
         if (lane == 0) atomicAdd(&a.dc_ctl[kDcOpen], wave_open);
         wave_ev = 1u;
     }
-    __syncthreads();   // ewl's last readers are done before the commit may reuse LDS (it uses dc_lds)
+    __syncthreads();   // every wave's stage entries are in
+    if (dc_stage_flush(a, st, stg, t)) wave_ev = 1u;
+    __syncthreads();   // ewl's and the stage's last readers are done before the commit may reuse LDS
     sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(dc_lds), a.lds_sort_cap, t, err0);
 }
 

@@ -269,18 +269,29 @@ constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: 
 // statistics, list t & 1 (read by this sweep's update) emptied for sweep t + 1's writers, and the
 // mode of sweep t + 1's update -- a rebuild when list (t + 1) & 1 overflowed or holds more
 // vertices than an incremental update pays for (dc_max).
-__device__ void dc_commit(const SweepArgs& a, uint32_t t) {
+// The dense sweep's control words the commit reads (thread 0, loaded together).
+struct DcCommitWords {
+    uint32_t chg, chg_ovf, len, ovf, open, mode;
+};
+__device__ __forceinline__ DcCommitWords dc_commit_load(const SweepArgs& a, uint32_t q) {
+    const uint32_t* k = a.dc_ctl;
+    DcCommitWords w;
+    w.chg = __hip_atomic_load(&k[kDcChgLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w.chg_ovf = __hip_atomic_load(&k[kDcChgOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w.len = __hip_atomic_load(&k[kDcLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w.ovf = __hip_atomic_load(&k[kDcOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w.open = __hip_atomic_load(&k[kDcOpen], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w.mode = k[kDcMode];
+    return w;
+}
+__device__ void dc_commit(const SweepArgs& a, uint32_t t, const DcCommitWords& w) {
     uint32_t* k = a.dc_ctl;
-    const uint32_t q = (t + 1u) & 1u, p = t & 1u;
-    const uint32_t len = __hip_atomic_load(&k[kDcLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t ovf = __hip_atomic_load(&k[kDcOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t open = __hip_atomic_load(&k[kDcOpen], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t mode = k[kDcMode];
+    const uint32_t p = t & 1u;
     unsigned long long* s = reinterpret_cast<unsigned long long*>(k + kDcStat);
-    s[0] += mode ? 0ull : 1ull;
-    s[1] += mode ? 1ull : 0ull;
-    s[2] += min(len, a.dc_cap);
-    s[3] += open;
+    s[0] += w.mode ? 0ull : 1ull;
+    s[1] += w.mode ? 1ull : 0ull;
+    s[2] += min(w.len, a.dc_cap);
+    s[3] += w.open;
     k[kDcOpen] = 0;
     k[kDcLen + p] = 0;
     k[kDcOvf + p] = 0;
@@ -288,14 +299,15 @@ __device__ void dc_commit(const SweepArgs& a, uint32_t t) {
     k[kDcChgOvf + p] = 0;
     k[kDcTask] = 0;
     k[kDcDone] = 0;
-    k[kDcMode] = (ovf || len > a.dc_max) ? 1u : 0u;
+    k[kDcMode] = (w.ovf || w.len > a.dc_max) ? 1u : 0u;
 }
 
 // Vertex v changed colour (ca -> cb) in the sweep whose lists have parity q, one thread: onto the
 // restore list when local (the next update copies it into the buffer that sweep overwrites), and
 // onto the count list when in S.
-__device__ __forceinline__ void dc_list_change(const SweepArgs& a, uint32_t q, uint32_t v, uint32_t ca, uint32_t cb) {
-    if (v - a.v_begin < a.v_end - a.v_begin) {
+__device__ __forceinline__ void dc_list_change(const SweepArgs& a, uint32_t q, uint32_t v, uint32_t ca, uint32_t cb,
+                                               bool restore = true) {
+    if (restore && v - a.v_begin < a.v_end - a.v_begin) {
         const uint32_t j = atomicAdd(&a.dc_ctl[kDcChgLen + q], 1u);
         if (j < a.dc_chg_cap) a.dc_chg[(size_t)q * a.dc_chg_cap + j] = v;
         else a.dc_ctl[kDcChgOvf + q] = 1u;
@@ -651,18 +663,24 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         for (uint32_t i = threadIdx.x; i < E; i += blockDim.x) {
             const uint32_t v = s[i];
             const uint32_t c = draws[i] % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+            const uint32_t old = (uint32_t)C[v];
             Cs[v] = (CT)c;
             // delta mode: both replicas carry C_t+1 on the remote rows (part_commit_kernel)
             // (the wide sweep's incremental counts need C_t there: its next sweep copies the change)
             if (a.part_delta > 0 && a.inc == nullptr && (v < a.v_begin || v >= a.v_end)) const_cast<CT*>(C)[v] = (CT)c;
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)c;
             if (a.taboo != nullptr && v >= a.v_begin && v < a.v_end)
-                a.taboo[v - a.v_begin] = (c == (uint32_t)C[v]) ? a.tabooIteration : 0u;
-            if (a.inc != nullptr && c != (uint32_t)C[v])   // (any rank's vertex: global ids)
+                a.taboo[v - a.v_begin] = (c == old) ? a.tabooIteration : 0u;
+            if (a.inc != nullptr && c != old)   // (any rank's vertex: global ids)
                 atomicAdd(&inc_cc[1], inc_list_global(a, v, t, a.inc_cchg + (size_t)((t + 1u) & 1u) * (2u + a.inc_ccap),
                                                       a.inc_ccap, &inc_cc[0]));
-            if (a.dc_list != nullptr && c != (uint32_t)C[v])   // dense-count sweep: the next update's lists
-                dc_list_change(a, (t + 1u) & 1u, v, (uint32_t)C[v], c);
+            if (a.dc_list != nullptr && c != old) {
+                // dense-count sweep: the count list when v is in S; a local v's new colour also
+                // goes into the C_t buffer now (nothing reads C_t after the evaluation), so the
+                // next sweep needs no restore of it
+                dc_list_change(a, (t + 1u) & 1u, v, old, c, false);
+                if (v - a.v_begin < a.v_end - a.v_begin) const_cast<CT*>(C)[v] = (CT)c;
+            }
         }
         __syncthreads();
     }
@@ -672,8 +690,10 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
         // a short restore list is applied here, C_t+1 into the C_t buffer (the one sweep t + 1
         // writes), so that sweep's update has nothing to do when no vertex of S moved
         const uint32_t q = (t + 1u) & 1u;
-        const uint32_t m = __hip_atomic_load(&a.dc_ctl[kDcChgLen + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t ovf = __hip_atomic_load(&a.dc_ctl[kDcChgOvf + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __shared__ DcCommitWords dcw;
+        if (threadIdx.x == 0) dcw = dc_commit_load(a, q);
+        __syncthreads();
+        const uint32_t m = dcw.chg, ovf = dcw.chg_ovf;
         if (threadIdx.x == 0) {
             const uint32_t r = a.dc_ctl[kDcStat2] + min(m, a.dc_chg_cap);
             a.dc_ctl[kDcStat2] = r < a.dc_ctl[kDcStat2] ? ~0u : r;
@@ -688,7 +708,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
             __syncthreads();
             if (threadIdx.x == 0) a.dc_ctl[kDcChgLen + q] = 0;
         }
-        if (threadIdx.x == 0) dc_commit(a, t);
+        if (threadIdx.x == 0) dc_commit(a, t, dcw);
     }
     if (a.inc != nullptr) {
         __syncthreads();   // inc_cc complete
@@ -1258,12 +1278,33 @@ __global__ __launch_bounds__(kCommitThreads) void wide_footer_kernel(SweepArgs a
 // eps leaves S unchanged (checked on the host for every colour), so once u >= E[cv] the walk's answer
 // is cv when S > u, else a CDF overflow; below E[cv] (probability ~E[cv], < 3e-6 at eps 1e-8) the
 // step-by-step walk runs. Bit-identical to the loop.
+// The dense sweep's per-workgroup staging of evaluate_lane's list appends (restore list, count
+// list, overflow events) in LDS: a wave that appends pays an LDS atomic instead of a global round
+// trip; the workgroup flushes once at its end (dc_stage_flush). Full stages fall back to the
+// global appends.
+constexpr uint32_t kDcStageChg = 4096, kDcStageS = 2048, kDcStageEv = 1024;
+struct DcStage {
+    uint32_t n[3];      // entries staged: restore list, count list (pairs), events
+    uint32_t* chg;      // [kDcStageChg]
+    uint32_t* s;        // [2 kDcStageS]
+    uint32_t* ev;       // [kDcStageEv]
+};
+// lane 0 reserves `cnt` entries of stage list i (cap entries); returns the base or ~0u when full
+__device__ __forceinline__ uint32_t dc_stage_reserve(uint32_t* n, uint32_t cnt, uint32_t cap, int lane) {
+    uint32_t b = 0;
+    if (lane == 0) {
+        b = atomicAdd(n, cnt);
+        if (b + cnt > cap) b = ~0u;
+    }
+    return __shfl(b, 0, 64);
+}
+
 template <int NW>
 __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* __restrict__ st,
                                                   uint8_t* __restrict__ Cs, bool valid, uint32_t l,
                                                   const uint32_t (&acc)[NW], int lane, uint32_t& ev_flag,
                                                   uint8_t* __restrict__ vf, uint32_t cv, uint32_t tab, uint32_t x,
-                                                  const float2* ew = nullptr) {
+                                                  const float2* ew = nullptr, DcStage* stg = nullptr) {
     const uint32_t v = a.v_begin + l;
     uint32_t pop = 0;
 #pragma unroll
@@ -1347,10 +1388,28 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
     if (a.dc_list != nullptr) {
         const bool dchg = valid && tab == 0 && !event && newc != cv;
         const uint64_t db = __ballot(dchg);
-        if (db) {
+        const bool ins0 = dchg && v - a.dc_s0 < a.dc_s1 - a.dc_s0;
+        const uint64_t sb0 = __ballot(ins0);
+        bool staged = false;
+        if (db && stg != nullptr) {
+            const uint64_t below = (1ull << lane) - 1ull;
+            const uint32_t bc = dc_stage_reserve(&stg->n[0], (uint32_t)__popcll(db), kDcStageChg, lane);
+            const uint32_t bs = sb0 ? dc_stage_reserve(&stg->n[1], (uint32_t)__popcll(sb0), kDcStageS, lane) : 0u;
+            if (bc != ~0u && bs != ~0u) {
+                if (dchg) stg->chg[bc + (uint32_t)__popcll(db & below)] = v;
+                if (ins0) {
+                    const uint32_t j = bs + (uint32_t)__popcll(sb0 & below);
+                    stg->s[2u * j] = v;
+                    stg->s[2u * j + 1u] = (cv << 16) | newc;
+                }
+                staged = true;
+            }   // else a full stage: this wave's entries go global; what it reserved stays ~0u
+                // (the stage is pre-filled), a hole the flush skips
+        }
+        if (db && !staged) {
             const uint32_t q = (Cs == a.colors1) ? 1u : 0u;   // (t + 1) & 1
-            const bool ins = dchg && v - a.dc_s0 < a.dc_s1 - a.dc_s0;
-            const uint64_t sb = __ballot(ins);
+            const bool ins = ins0;
+            const uint64_t sb = sb0;
             uint32_t bc = 0, bs = 0;
             if (lane == 0) {
                 bc = atomicAdd(&a.dc_ctl[kDcChgLen + q], (uint32_t)__popcll(db));
@@ -1379,7 +1438,14 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
     }
 
     const uint32_t nviol = (uint32_t)__popcll(__ballot(viol));
-    const uint64_t eb = __ballot(event);
+    uint64_t eb = __ballot(event);
+    if (eb && stg != nullptr) {
+        const uint32_t be = dc_stage_reserve(&stg->n[2], (uint32_t)__popcll(eb), kDcStageEv, lane);
+        if (be != ~0u) {
+            if (event) stg->ev[be + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull))] = v;
+            eb = 0;
+        }
+    }
     if (eb) {
         ev_flag = 1u;
         uint32_t basei = 0;
