@@ -142,14 +142,24 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
             for (uint32_t l = r0 + wv; l < min(r0 + kDcRebuildRows, nloc); l += blockDim.x >> 6) {
                 for (uint32_t i = lane; i < a.dc_cw; i += 64u) h[i] = 0;
                 dc_lds_wait();
-                for (uint32_t b = b0; b <= b1; b++) {
-                    uint32_t s0, s1;
-                    const uint16_t* gc;
-                    dc_segment(a, l, b, s0, s1, gc);
+                // 8 column blocks per round, 8 lanes each, 8 ids per lane in flight: one chain of
+                // three dependent loads (segment bounds, ids, colours) per 8 blocks, not per block
+                const uint32_t grp = lane >> 3, gl = lane & 7u;
+                for (uint32_t bb = b0; bb <= b1; bb += 8u) {
+                    const uint32_t b = bb + grp;
+                    uint32_t s0 = 0, s1 = 0;
+                    const uint16_t* gc = nullptr;
+                    if (b <= b1) dc_segment(a, l, b, s0, s1, gc);
                     const uint32_t base = b << bl;
-                    for (uint32_t q = s0 + lane; q < s1; q += 64u) {
-                        const uint32_t u = base | (uint32_t)gc[q];
-                        if (u - a.dc_s0 < sw) atomicAdd(&h[C[u]], 1u);
+                    for (uint32_t q = s0 + gl; __ballot(q < s1); q += 64u) {
+                        uint32_t id[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) id[k] = q + 8u * k < s1 ? (uint32_t)gc[q + 8u * k] : 0xFFFFFFFFu;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            const uint32_t u = base | id[k];
+                            if (id[k] != 0xFFFFFFFFu && u - a.dc_s0 < sw) atomicAdd(&h[C[u]], 1u);
+                        }
                     }
                 }
                 dc_lds_wait();
