@@ -346,6 +346,25 @@ __device__ bool dc_stage_flush(const SweepArgs& a, DevState* st, DcStage& stg, u
     return true;
 }
 
+// x 16807 mod (2^31 - 1) for a minstd state x < 2^31: the product is below 2^46, one fold and one
+// conditional subtraction (minstd_mulmod's general form takes two folds of a 64-bit product).
+__device__ __forceinline__ uint32_t dc_mul16807(uint32_t x) {
+    const uint32_t lo = x * kMinstdA, hi = __umulhi(x, kMinstdA);
+    uint32_t r = (lo & kMinstdM) + ((hi << 1) | (lo >> 31));
+    return r >= kMinstdM ? r - kMinstdM : r;
+}
+// The smallest minstd state x in [1, 2^31 - 1) with minstd_canonical(x) >= f (2^31 - 1 if none):
+// canonical is non-decreasing in x, so u >= f <=> x >= this, exactly (a binary search over states).
+__device__ __forceinline__ uint32_t dc_canonical_at_least(float f) {
+    uint32_t lo = 1u, hi = kMinstdM;   // answer in [lo, hi]; hi = none
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (minstd_canonical(mid) >= f) hi = mid;
+        else lo = mid + 1u;
+    }
+    return lo;
+}
+
 constexpr uint32_t kDcLaneRows = 16;
 constexpr uint32_t kDcSpan = 64u * kDcLaneRows;
 template <int NW>
@@ -371,8 +390,13 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     const uint32_t nloc = a.v_end - a.v_begin;
     uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * nloc : nullptr;
     const float2* ew = nullptr;
+    __shared__ uint2 xkeep[256];   // the keep interval [E, S) of u as minstd states: [x_lo, x_hi)
     if (a.ewalk) {
-        for (uint32_t i = threadIdx.x; i < a.nCol; i += blockDim.x) ewl[i] = a.ewalk[i];
+        for (uint32_t i = threadIdx.x; i < a.nCol; i += blockDim.x) {
+            const float2 e = a.ewalk[i];
+            ewl[i] = e;
+            xkeep[i] = make_uint2(dc_canonical_at_least(e.x), dc_canonical_at_least(e.y));
+        }
         ew = ewl;
     }
     uint32_t fullw[NW];
@@ -445,11 +469,10 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
         if (ew != nullptr) {                                                                        \
             uint32_t x = xl;                                                                        \
             _Pragma("unroll") for (uint32_t j = 0; j < kDcLaneRows; j++) {                          \
-                if (j) x = minstd_mulmod(x, kMinstdA);                                              \
+                if (j) x = dc_mul16807(x);                                                          \
                 const uint32_t cv = (CW[j >> 2] >> (8u * (j & 3u))) & 0xFFu;                        \
-                const float u = minstd_canonical(x);                                                \
-                const float2 es = ew[cv];                                                           \
-                bool k = u >= es.x && es.y > u;                                                     \
+                const uint2 xk = xkeep[cv];   /* u >= E[cv] && S[cv] > u, as states */              \
+                bool k = x >= xk.x && x < xk.y;                                                     \
                 if (a.taboo != nullptr) k = k && tabw[j] == 0u;                                     \
                 keepm |= (k ? 1u : 0u) << j;                                                        \
             }                                                                                       \
