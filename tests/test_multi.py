@@ -366,3 +366,39 @@ def test_native_loopback_tailcut_generated_rows(M):
     assert_native(lp, st, r, 3)
     assert all(s.tailcutPasses == r.res.tailcutPasses for s in st)
     lp.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [4, 8])
+def test_part_bench_rank_stub(M, world):
+    """mcmc_part_bench_rank (bench.py --rank-share): rank 0 of a world-K partition over its own
+    generated rows, the exchange stubbed. Sweep 0 changes most colours, so its delta slot
+    overflows and the driver runs full-mode steps after it; once the colouring settles (mean degree
+    400, 32 colours: full masks) every step runs in delta mode (sweep + delta packing + footer +
+    part_commit) and none overflows."""
+    import ctypes
+
+    from mcmc_colorer_amd._lib import MCMCRunStats, check, lib, u32ptr
+    from mcmc_colorer_amd.distributed import plan_rows
+
+    n, p, steps = 40000, 0.01, 12
+    bounds = plan_rows(n, world)
+    g = M.Graph.er_fast(n, p, 3, rows=(0, int(bounds[1])))
+    prm = M.ColoringMCMCParams(nCol=32, maxRip=1000).to_c(3)
+    ctx = ctypes.c_void_p()
+    check(lib().mcmc_part_create(g.handle, ctypes.byref(prm), world, 0, u32ptr(bounds), None, ctypes.byref(ctx)))
+    try:
+        check(lib().mcmc_set_glibc_window(ctx, u32ptr(M.GlibcRand(1).window)))
+        check(lib().mcmc_init_coloring(ctx, None))
+        check(lib().mcmc_set_bench_mode(ctx, 1))
+        st = MCMCRunStats()
+        xs = [ctypes.c_uint64() for _ in range(4)]
+        check(lib().mcmc_part_bench_rank(ctx, 24, ctypes.byref(st)))   # warm-up: overflow, full mode
+        check(lib().mcmc_part_exchange_stats(ctx, *[ctypes.byref(x) for x in xs]))
+        assert xs[0].value + xs[1].value == 24 and xs[2].value <= 1
+        check(lib().mcmc_part_bench_rank(ctx, steps, ctypes.byref(st)))
+        check(lib().mcmc_part_exchange_stats(ctx, *[ctypes.byref(x) for x in xs]))
+        assert (xs[0].value, xs[1].value, xs[2].value) == (steps, 0, 0)
+        assert st.loopMs > 0.0
+    finally:
+        lib().mcmc_destroy(ctx)
