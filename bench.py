@@ -56,7 +56,9 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-KERNELS = {"dense": "dc_eval_kernel (one sweep: update + evaluation + commit)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
+KERNELS = {"dense": "dc_multi_kernel (persistent: the timed sweeps in one launch; solo sweeps on workgroup 0, "
+                    "full sweeps on the grid)",
+           "dense-part": "dc_eval_kernel (one sweep: update + evaluation + commit)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
            "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)",
            "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
@@ -399,6 +401,14 @@ def main() -> int:
         st = cr.run(0)
         cw = time.perf_counter() - t0
         tr = [int(x) for x in cr.trajectory()]
+        # the first sweep of a colouring alone (the dense sweep's count rebuild happens there), then
+        # one more: their difference is the rebuild's cost, paid once per colouring
+        cf = M.ColoringMCMC(g, M.GPURand(g.nNodes, a.seed, M.GlibcRand(1) if a.config != "c2" else
+                                         M.GlibcRand(1, n_req * (n_req + 1) // 2)), M.ColoringMCMCParams(nCol=a.ncol))
+        cf.init(0)
+        s1 = cf.step(1)
+        s2 = cf.step(1)
+        cf.close()
         conv = {"sweeps_to_zero_conflict": int(st.iter) if st.finalViol == 0 else None,
                 "converged": bool(st.finalViol == 0),
                 "status": (f"converged after {int(st.iter)} sweeps" if st.finalViol == 0 else
@@ -406,6 +416,13 @@ def main() -> int:
                 "iterations": int(st.iter), "max_iter_reached": bool(st.maxIterReached),
                 "final_Cviol": int(st.finalViol), "sweeps_run": int(st.sweepsRun),
                 "loop_ms": st.loopMs, "wall_s": round(cw, 4), "glibc_draws": int(st.glibcDraws),
+                "amortized_ms_per_sweep": st.loopMs / max(1, int(st.sweepsRun)),
+                "amortized_value": g.nNodes * int(st.sweepsRun) / (st.loopMs * 1e-3),
+                "first_sweep_ms": s1.loopMs, "second_sweep_ms": s2.loopMs,
+                "rebuild_ms": max(0.0, s1.loopMs - s2.loopMs),
+                "note": "loop_ms = device time of the whole reference loop (run(), every sweep incl. the first "
+                        "sweep's count rebuild); amortized_* = that loop per sweep; first/second_sweep_ms = one-sweep "
+                        "launches of a fresh colouring, their difference the rebuild paid once per colouring",
                 "trajectory": tr}
         cr.close()
     if ref and dist is not None:
@@ -496,18 +513,28 @@ def main() -> int:
         # dense mask, ids + colour gathers, an upper bound: their whole rows outside it); a rebuild
         # reads every row's arcs into the range and copies the local colours
         d = {k: dn1[k] - dn0[k] for k in ("incremental_sweeps", "rebuilds", "moved_vertices", "open_rows",
-                                          "changed_rows", "copy_sweeps")}
+                                          "changed_rows", "copy_sweeps", "solo_sweeps", "solo_evaluated")}
         S = max(1, d["incremental_sweeps"] + d["rebuilds"])
         nw = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
         deg = m / max(1, n)
         span = dn1["s1"] - dn1["s0"]
-        b_eval = n * (1.0 + nw / 8.0)
-        b_chg = d["changed_rows"] * 3.0 + d["copy_sweeps"] * 2.0 * n
+        # bytes from what the device counted (one definition for every dense line): a full sweep reads
+        # every row's colour and open bits; a solo sweep (dense_sparse.h) reads the colour and open word
+        # of each row it evaluates (candidates of the discrete-log window, open rows); a changed row
+        # writes its colour (both buffers in solo sweeps, restore in full ones) and a list entry; a
+        # moved vertex of S reads its local arcs (2 B ids) and moves two 4 B counts per arc; an open
+        # row reads its mask and its arcs outside S with their colours (3 B per arc); a rebuild reads
+        # the rows' arcs into S and writes counts, masks and a copy of the colours
+        full = S - d["solo_sweeps"]
+        b_eval = full * n * (1.0 + nw / 8.0) + d["solo_evaluated"] * 9.0
+        b_chg = d["changed_rows"] * 10.0 + d["copy_sweeps"] * 2.0 * n
         b_upd = d["moved_vertices"] * deg * 10.0
         b_open = d["open_rows"] * (4.0 * nw + deg * (1.0 - span / max(1, n)) * 3.0)
-        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 3.0 + n * a.ncol * 4.0 + n * nw * 4.0 + 2.0 * n)
-        b_alg = b_eval + (b_chg + b_upd + b_open + b_rebuild) / S
+        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 2.0 + n * a.ncol * 4.0 + n * nw * 4.0 + 2.0 * n)
+        b_alg = (b_eval + b_chg + b_upd + b_open + b_rebuild) / S
         dense = dict(d, sweeps_counted=S, dense_range=[dn1["s0"], dn1["s1"]],
+                     window_states=dn1["window_states"], persistent=dn1["persistent"],
+                     solo_evaluated_per_sweep=d["solo_evaluated"] / S,
                      moved_vertices_per_sweep=d["moved_vertices"] / S, open_rows_per_sweep=d["open_rows"] / S,
                      rebuild_threshold=dn1["rebuild_threshold"], bytes_per_sweep=b_alg,
                      changed_rows_per_sweep=d["changed_rows"] / S,
@@ -515,9 +542,12 @@ def main() -> int:
                             "open_rows": b_open / S, "rebuilds": b_rebuild / S},
                      note="dense-count sweep: every row keeps the counts of its neighbours' colours over a fixed "
                           "dense column range, moved each sweep by the vertices there that changed colour; a row "
-                          "whose dense mask holds every colour (open bit clear) is evaluated from its own colour "
-                          "alone, the rest scan their other column blocks; only rows that change colour are "
-                          "written. One launch per sweep. Bit-identical to the scan sweeps (tests/test_dense.py).")
+                          "whose dense mask holds every colour (open bit clear) keeps its colour unless its minstd "
+                          "state falls in the candidate window, whose rows are found by discrete logarithm "
+                          "(csrc/dense_sparse.h): a solo sweep evaluates only those and the open rows, on one "
+                          "workgroup of a persistent launch of all the timed sweeps; full sweeps (the count "
+                          "rebuild) run on the whole grid inside it. Bit-identical to the scan sweeps "
+                          "(tests/test_dense.py, tests/test_c3_full.py).")
         if not a.no_full_scan:
             # the same graph through the tiled scan sweep (MCMC_DENSE=0, the r03 early-exit kernel) and
             # the full scan (MCMC_FULL_SCAN=1): every sweep scans the layout
@@ -641,7 +671,8 @@ def main() -> int:
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,
-                     "kernel": KERNELS.get(variant, variant) + ("<REF>" if ref else "")
+                     "kernel": KERNELS.get(variant + ("-part" if (variant == "dense" and dist is not None) else ""), variant)
+                               + ("<REF>" if ref else "")
                                + ("" if world == 1 else " + exchange (per-rank step)"),
                      "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg,
                      "ref_layout_bytes": b_ref, "ref_layout_equiv_GBs": b_ref / (kernel_ms * 1e-3) / 1e9,

@@ -175,6 +175,10 @@ int mcmc_set_bench_mode(mcmc_ctx* c, int on);
  * list's rebuild threshold, local rows that changed colour (the restore lists; a list past its
  * capacity counts as its capacity), sweeps whose restore list overflowed}; all 0 when off. */
 int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[10]);
+/* The same plus the persistent dense sweep (csrc/dense_sparse.h): out[10] sweeps the leader ran
+ * alone (solo), out[11] candidate-window states, out[12] 1 if the context launches it, out[13] open
+ * mask words now nonzero, out[14] rows the solo sweeps evaluated. Test / bench statistics. */
+int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]);
 /* Diagnostics of the tiled sweep's scan (no reference counterpart): with stats on, every sweep adds
  * the 16-byte id quads it loaded and the (group, column block) pairs it staged (table + colour
  * slice); mcmc_set_scan_stats(c, 1) also zeroes them. The sweep stops scanning a row once its

@@ -56,6 +56,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_scan_stats_v2": (c_int, [c_void_p, _u64p]),
     "mcmc_get_wide_inc_stats": (c_int, [c_void_p, _u64p]),
     "mcmc_get_dense_stats": (c_int, [c_void_p, _u64p]),
+    "mcmc_get_dense_stats_v2": (c_int, [c_void_p, _u64p]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
     "mcmc_cdf_walk": (c_uint32, [_u32p, c_uint32, c_uint32, c_float, c_float, c_float]),
     "mcmc_refstruct_bench": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_double), _u64p]),

@@ -310,11 +310,13 @@ class ColoringMCMC:
         dense_counts.h): whether the context runs it, its dense column range, sweeps whose update moved
         the counts by the changed vertices, count rebuilds, vertices moved, rows that scanned past the
         range, the update list's rebuild threshold, rows that changed colour and restore-list overflows."""
-        out = (ctypes.c_uint64 * 10)()
-        check(lib().mcmc_get_dense_stats(self._ctx, out))
+        out = (ctypes.c_uint64 * 16)()
+        check(lib().mcmc_get_dense_stats_v2(self._ctx, out))
         return {"enabled": bool(out[0]), "s0": int(out[1]), "s1": int(out[2]), "incremental_sweeps": int(out[3]),
                 "rebuilds": int(out[4]), "moved_vertices": int(out[5]), "open_rows": int(out[6]),
-                "rebuild_threshold": int(out[7]), "changed_rows": int(out[8]), "copy_sweeps": int(out[9])}
+                "rebuild_threshold": int(out[7]), "changed_rows": int(out[8]), "copy_sweeps": int(out[9]),
+                "solo_sweeps": int(out[10]), "window_states": int(out[11]), "persistent": bool(out[12]),
+                "open_words": int(out[13]), "solo_evaluated": int(out[14])}
 
     def save(self, iteration: int) -> None:
         d = self.directory

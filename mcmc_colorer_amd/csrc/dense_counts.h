@@ -52,6 +52,17 @@ __device__ __forceinline__ uint32_t dc_fullw(uint32_t nCol, uint32_t i) {
     return nCol >= lo + 32u ? ~0u : (nCol > lo ? (1u << (nCol - lo)) - 1u : 0u);
 }
 
+// Open word wi (= (row >> 6) NW + mask word) went from o to n: when that crossed zero, flip its
+// summary bit and move the count of nonzero open words (dc_osum). Every change of an open word is
+// an atomic returning the old value, so the crossings of one word alternate in the order of its
+// atomics: the summary bit ends as (word != 0) and the count as the number of such words,
+// whatever the interleaving (both start consistent: all zero with the open words, setup_dense).
+__device__ __forceinline__ void dc_osum_note(const SweepArgs& a, size_t wi, unsigned long long o, unsigned long long n) {
+    if (a.dc_osum == nullptr || ((o == 0ull) == (n == 0ull))) return;
+    atomicXor(&a.dc_osum[1 + (wi >> 6)], 1ull << (wi & 63u));
+    atomicAdd(reinterpret_cast<uint32_t*>(a.dc_osum), o == 0ull ? 1u : 0xFFFFFFFFu);
+}
+
 // Row lw's count of colour c crossed zero: flip its mask bit, and its open bit when that changed
 // whether mask word c / 32 is full. Flips of one word are ordered by its atomics, so the open bit
 // ends as (word not full) whatever the interleaving.
@@ -59,8 +70,12 @@ template <int NW>
 __device__ __forceinline__ void dc_flip(const SweepArgs& a, uint32_t lw, uint32_t c) {
     const uint32_t i = c >> 5, bit = 1u << (c & 31u), fw = dc_fullw(a.nCol, i);
     const uint32_t o = atomicXor(&a.dc_mask[(size_t)lw * NW + i], bit);
-    if (((o & fw) == fw) != (((o ^ bit) & fw) == fw))
-        atomicXor(&a.dc_open[(size_t)(lw >> 6) * NW + i], 1ull << (lw & 63u));
+    if (((o & fw) == fw) != (((o ^ bit) & fw) == fw)) {
+        const size_t wi = (size_t)(lw >> 6) * NW + i;
+        const unsigned long long ob = 1ull << (lw & 63u);
+        const unsigned long long oo = atomicXor(&a.dc_open[wi], ob);
+        dc_osum_note(a, wi, oo, oo ^ ob);
+    }
 }
 
 // Vertex u of S moved from colour ca to cb: row lw's counts, dense mask and open bits.
@@ -98,8 +113,105 @@ __device__ __forceinline__ void dc_ctl_load(const SweepArgs& a, DcCtl& w) {
         w.len[q] = a.dc_ctl[kDcLen + q];
     }
 }
+// The rebuild of one chunk of a row group's rows (the streaming form, SweepArgs::dc_rbrows = rows
+// per chunk): rows [r0, r0 + rows) of group g. Per column block b overlapping S, the colours of
+// b's part of S go to LDS (the slice) and the chunk's segments of block b -- contiguous in tcol,
+// the rows following each other -- are streamed by the whole workgroup, a 16-byte quad (8 ids of
+// one row: segments are padded to multiples of 8) per thread and step, its row found by a binary
+// search of the segment starts; each real id in S adds 1 to its row's count of its colour in an
+// LDS histogram (two uint16 counts per word: setup_dense takes this form only when no row has
+// 65536 arcs). Then the counts, masks and open bits of the chunk's rows are written. Replaces a
+// wave per row (one chain of dependent loads each) by coalesced streaming of the ids.
+// lds: [histogram rows x hw words][segment starts rows + 1 words] (64 KiB) + [slice: 64 KiB].
 template <int NW>
-__device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, const DcCtl& w) {
+__device__ __forceinline__ void dc_rebuild_chunk(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t g,
+                                                 uint32_t r0, uint32_t rows, uint32_t* lds) {
+    const uint32_t R = a.grp_rows, bl = a.block_log2, nCol = a.nCol, hw = (nCol + 1u) >> 1;
+    uint32_t* const hist = lds;
+    uint32_t* const tab = lds + rows * hw;
+    uint8_t* const sl = reinterpret_cast<uint8_t*>(lds + kDcEvalLds / 4u);
+    for (uint32_t i = threadIdx.x; i < rows * hw; i += blockDim.x) hist[i] = 0u;
+    const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
+    const uint32_t sb0 = a.dc_s0 >> bl, sb1 = (a.dc_s1 - 1u) >> bl;
+    for (uint32_t b = sb0; b <= sb1; b++) {
+        const uint32_t blo = b << bl;
+        const uint32_t lo = max(blo, a.dc_s0) - blo, hi = min(blo + (1u << bl), a.dc_s1) - blo;   // S in block b
+        const uint32_t* ts = a.tseg + ((size_t)g * a.nblocks + b) * tseg_stride(R) + r0;
+        __syncthreads();   // the last block's readers of sl / tab are done
+        for (uint32_t j = threadIdx.x; j <= rows; j += blockDim.x) tab[j] = ts[j];
+        {   // the slice [lo, hi) of block b's colours (16-byte loads where aligned)
+            const uint32_t q0 = (lo + 15u) & ~15u, q1 = max(hi & ~15u, q0);
+            for (uint32_t i = q0 + 16u * threadIdx.x; i < q1; i += 16u * blockDim.x)
+                *reinterpret_cast<uint4*>(sl + i) = *reinterpret_cast<const uint4*>(C + blo + i);
+            for (uint32_t i = lo + threadIdx.x; i < min(q0, hi); i += blockDim.x) sl[i] = C[blo + i];
+            for (uint32_t i = max(q1, lo) + threadIdx.x; i < hi; i += blockDim.x) sl[i] = C[blo + i];
+        }
+        __syncthreads();
+        const uint32_t p0 = tab[0] & kTsegPos, p1 = tab[rows] & kTsegPos, nq = (p1 - p0) >> 3;
+        for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+            const uint32_t pos = p0 + 8u * q;
+            const uint4 v = *reinterpret_cast<const uint4*>(gc + pos);
+            uint32_t L = 0, H = rows;   // the row j with start(j) <= pos < start(j + 1)
+            while (H - L > 1u) {
+                const uint32_t mid = (L + H) >> 1;
+                if ((tab[mid] & kTsegPos) <= pos) L = mid;
+                else H = mid;
+            }
+            const uint32_t end = (tab[L + 1] & kTsegPos) - (tab[L] & 7u);
+            uint32_t* const hr = hist + L * hw;
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t id = (w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                if (pos + (uint32_t)k < end && id - lo < hi - lo) {
+                    const uint32_t c = sl[id];
+                    atomicAdd(&hr[c >> 1], 1u << (16u * (c & 1u)));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // write-out: counts (coalesced), masks, then the chunk's open words
+    const uint32_t l0 = g * R + r0;   // first local row of the chunk
+    uint32_t* const cnt = a.dc_cnt + (size_t)l0 * a.dc_cw;
+    for (uint32_t i = threadIdx.x; i < rows * nCol; i += blockDim.x) {
+        const uint32_t j = i / nCol, c = i - j * nCol;
+        cnt[(size_t)j * a.dc_cw + c] = (hist[j * hw + (c >> 1)] >> (16u * (c & 1u))) & 0xFFFFu;
+    }
+    // per (row, mask word): the mask word, and whether it is full; open bits gathered per open word
+    // in LDS (the slice is free now), then one AND + one OR per open word (the words at the chunk's
+    // ends are shared with the neighbouring chunks' rows)
+    const uint32_t w0 = l0 >> 6, nwo = ((l0 + rows - 1u) >> 6) - w0 + 1u;   // open words (per mask word)
+    unsigned long long* const ob = reinterpret_cast<unsigned long long*>(sl);   // [nwo][NW]
+    for (uint32_t i = threadIdx.x; i < nwo * NW; i += blockDim.x) ob[i] = 0ull;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < rows * NW; i += blockDim.x) {
+        const uint32_t j = i / NW, wi = i - j * NW;
+        uint32_t mw = 0;
+        for (uint32_t c = 32u * wi; c < min(nCol, 32u * wi + 32u); c++)
+            mw |= (((hist[j * hw + (c >> 1)] >> (16u * (c & 1u))) & 0xFFFFu) != 0u ? 1u : 0u) << (c & 31u);
+        a.dc_mask[(size_t)(l0 + j) * NW + wi] = mw;
+        const uint32_t fw = dc_fullw(nCol, wi);
+        if ((mw & fw) != fw) atomicOr(&ob[(((l0 + j) >> 6) - w0) * NW + wi], 1ull << ((l0 + j) & 63u));
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nwo * NW; i += blockDim.x) {
+        const uint32_t ow = i / NW, wi = i - ow * NW;
+        const uint32_t rlo = max((w0 + ow) << 6, l0), rhi = min(((w0 + ow) << 6) + 64u, l0 + rows);   // rows here
+        const unsigned long long span = (rhi - rlo >= 64u ? ~0ull : ((1ull << (rhi - rlo)) - 1ull)) << (rlo & 63u);
+        const unsigned long long nb = ob[i];
+        const size_t idx = (size_t)(w0 + ow) * NW + wi;
+        const unsigned long long o1 = atomicAnd(&a.dc_open[idx], ~span | nb);
+        dc_osum_note(a, idx, o1, o1 & (~span | nb));
+        if (nb) {
+            const unsigned long long o2 = atomicOr(&a.dc_open[idx], nb);
+            dc_osum_note(a, idx, o2, o2 | nb);
+        }
+    }
+}
+
+template <int NW>
+__device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, const DcCtl& w) {
     __shared__ uint32_t sh_k;
     const uint32_t p = t & 1u;
     const uint32_t mode = w.mode, copy = mode | w.ovf[p];
@@ -108,7 +220,9 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
     const uint32_t bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
     const uint32_t nmov_w = mode ? 0u : len * nbl;   // len <= |S| / 8 + 1 when incremental: no overflow
     const uint32_t n1 = copy ? (nloc + kDcCopyRows - 1u) / kDcCopyRows : (m + 1023u) / 1024u;
-    const uint32_t n2 = mode ? (nloc + kDcRebuildRows - 1u) / kDcRebuildRows : (nmov_w + 15u) / 16u;
+    const uint32_t R = a.grp_rows, Rc = a.dc_rbrows, cpg = Rc ? (R + Rc - 1u) / Rc : 0u;   // chunks per group
+    const uint32_t n2 = mode ? (Rc ? a.ngroups * cpg : (nloc + kDcRebuildRows - 1u) / kDcRebuildRows)
+                             : (nmov_w + 15u) / 16u;
     const uint32_t T = n1 + n2;
     if (T == 0u) return;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;   // C_t
@@ -136,6 +250,10 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
                 const uint32_t u = a.dc_chg[(size_t)p * a.dc_chg_cap + i];
                 Y[u] = C[u];
             }
+        } else if (mode && Rc) {   // the streaming rebuild of one chunk of a group's rows
+            const uint32_t k2 = k - n1, gg = k2 / cpg, r0 = (k2 - gg * cpg) * Rc;
+            const uint32_t grow = min(R, nloc - gg * R);   // rows of group gg
+            if (r0 < grow) dc_rebuild_chunk<NW>(a, C, gg, r0, min(Rc, grow - r0), lds);
         } else if (mode) {
             const uint32_t b0 = a.dc_s0 >> bl, b1 = (a.dc_s1 - 1u) >> bl, sw = a.dc_s1 - a.dc_s0;
             const uint32_t r0 = (k - n1) * kDcRebuildRows;
@@ -166,7 +284,8 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
                 uint32_t* cr = a.dc_cnt + (size_t)l * a.dc_cw;
                 for (uint32_t i = lane; i < a.dc_cw; i += 64u) cr[i] = h[i];
                 uint32_t* mk = a.dc_mask + (size_t)l * NW;
-                unsigned long long* ow = a.dc_open + (size_t)(l >> 6) * NW;
+                const size_t ow0 = (size_t)(l >> 6) * NW;
+                unsigned long long* ow = a.dc_open + ow0;
                 const unsigned long long obit = 1ull << (l & 63u);
                 for (uint32_t c0 = 0; c0 < 32u * NW; c0 += 64u) {
                     const uint32_t c = c0 + lane;
@@ -175,8 +294,13 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
                         for (uint32_t i = c0 >> 5; i < min((c0 >> 5) + 2u, (uint32_t)NW); i++) {
                             const uint32_t mw = (uint32_t)(bm >> (32u * (i - (c0 >> 5)))), fw = dc_fullw(a.nCol, i);
                             mk[i] = mw;
-                            if ((mw & fw) != fw) atomicOr(&ow[i], obit);
-                            else atomicAnd(&ow[i], ~obit);
+                            if ((mw & fw) != fw) {
+                                const unsigned long long o = atomicOr(&ow[i], obit);
+                                dc_osum_note(a, ow0 + i, o, o | obit);
+                            } else {
+                                const unsigned long long o = atomicAnd(&ow[i], ~obit);
+                                dc_osum_note(a, ow0 + i, o, o & ~obit);
+                            }
                         }
                     }
                 }
@@ -199,6 +323,10 @@ __device__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, c
                 }
             }
         }
+        // every wave drains its own stores (copies, rebuilt counts / masks) before the barrier:
+        // thread 0's agent release below writes back what has reached L2, so the stores of the
+        // other 15 waves must be complete first (MI355X_MICROARCH.md, "Valid forms": producer)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();   // the task's stores are complete before the next claim / the release
     }
     if (threadIdx.x == 0) {
@@ -305,7 +433,7 @@ __device__ __noinline__ DcMask<NW> dc_open_scan(DcScan d, const uint8_t* __restr
 // The workgroup's staged appends (DcStage, evaluate_lane) into the global lists, all threads: a
 // stage that never filled is copied behind one reservation per list; one that overflowed (its
 // holes are ~0u) entry by entry. Returns whether anything was appended (the workgroup releases).
-__device__ bool dc_stage_flush(const SweepArgs& a, DevState* st, DcStage& stg, uint32_t t) {
+__device__ __forceinline__ bool dc_stage_flush(const SweepArgs& a, DevState* st, DcStage& stg, uint32_t t) {
     __shared__ uint32_t base[3];
     const uint32_t q = (t + 1u) & 1u;
     const uint32_t caps[3] = {kDcStageChg, kDcStageS, kDcStageEv};
@@ -367,18 +495,38 @@ __device__ __forceinline__ uint32_t dc_canonical_at_least(float f) {
 
 constexpr uint32_t kDcLaneRows = 16;
 constexpr uint32_t kDcSpan = 64u * kDcLaneRows;
+// The per-launch tables of a dense sweep (LDS): fill_p's closed-form own-colour walk {E[c], S[c]}
+// and its keep interval [E, S) of u as minstd states, [x_lo, x_hi) (nullptr without ewalk).
+struct DcTabs {
+    const float2* ew;
+    const uint2* xkeep;
+};
+__device__ __forceinline__ DcTabs dc_tabs_load(const SweepArgs& a, float2* ewl, uint2* xkeep) {
+    if (a.ewalk) {
+        for (uint32_t i = threadIdx.x; i < a.nCol; i += blockDim.x) {
+            const float2 e = a.ewalk[i];
+            ewl[i] = e;
+            xkeep[i] = make_uint2(dc_canonical_at_least(e.x), dc_canonical_at_least(e.y));
+        }
+        return DcTabs{ewl, xkeep};
+    }
+    return DcTabs{nullptr, nullptr};
+}
+
+// One whole dense sweep by this workgroup as one of the grid's (every workgroup of the grid runs
+// it for the same sweep): the update tasks, its spans of the evaluation, the arrival; the last
+// workgroup to arrive commits. s4 = {t, done, x_t, err} as this workgroup read them. Returns
+// whether this workgroup committed. (dc_eval_kernel: one per launch; dc_multi_kernel: its full
+// sweeps, dense_sparse.h.) The caller has synchronised the workgroup after building `tb`.
 template <int NW>
-__global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
-    extern __shared__ uint4 dc_lds[];
+__device__ __forceinline__ bool dc_full_body(const SweepArgs& a, uint4 s4, DcTabs tb, uint32_t* dyn) {
     __shared__ TailShared sh;
-    __shared__ float2 ewl[256];
     __shared__ DcCtl sh_ctl;
     DevState* __restrict__ st = a.st;
-    const uint4 s4 = *reinterpret_cast<const uint4*>(st);   // {t, done, x_t, err}: one load
-    if (a.check_done && s4.y) return;
     if (threadIdx.x == 0) {
         sh.wg_viol = 0;
         sh.wg_ev = 0;
+        sh.wg_last = 0;
         sh.viol = 0;
         dc_ctl_load(a, sh_ctl);
     }
@@ -389,20 +537,13 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     uint8_t* __restrict__ Cs = (t & 1) ? a.colors0 : a.colors1;
     const uint32_t nloc = a.v_end - a.v_begin;
     uint8_t* const vf = a.vflags ? a.vflags + (size_t)(t & 1u) * nloc : nullptr;
-    const float2* ew = nullptr;
-    __shared__ uint2 xkeep[256];   // the keep interval [E, S) of u as minstd states: [x_lo, x_hi)
-    if (a.ewalk) {
-        for (uint32_t i = threadIdx.x; i < a.nCol; i += blockDim.x) {
-            const float2 e = a.ewalk[i];
-            ewl[i] = e;
-            xkeep[i] = make_uint2(dc_canonical_at_least(e.x), dc_canonical_at_least(e.y));
-        }
-        ew = ewl;
-    }
+    const float2* ew = tb.ew;
+    const uint2* xkeep = tb.xkeep;
     uint32_t fullw[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) fullw[i] = dc_fullw(a.nCol, (uint32_t)i);
     __syncthreads();
+    uint4* const dc_lds = reinterpret_cast<uint4*>(dyn);
     dc_update_tasks<NW>(a, t, reinterpret_cast<uint32_t*>(dc_lds), sh_ctl);
     // the list appends' stage (dc_lds is free between the update's histograms and the commit)
     __shared__ DcStage stg;
@@ -539,6 +680,18 @@ __global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
     if (dc_stage_flush(a, st, stg, t)) wave_ev = 1u;
     __syncthreads();   // ewl's and the stage's last readers are done before the commit may reuse LDS
     sweep_tail(a, st, sh, wave_viol, wave_ev, lane, reinterpret_cast<uint32_t*>(dc_lds), a.lds_sort_cap, t, err0);
+    return sh.wg_last != 0u;
+}
+
+template <int NW>
+__global__ __launch_bounds__(1024) void dc_eval_kernel(SweepArgs a) {
+    extern __shared__ uint4 dc_lds[];
+    __shared__ float2 ewl[256];
+    __shared__ uint2 xkeep[256];
+    const uint4 s4 = *reinterpret_cast<const uint4*>(a.st);   // {t, done, x_t, err}: one load
+    if (a.check_done && s4.y) return;
+    const DcTabs tb = dc_tabs_load(a, ewl, xkeep);
+    (void)dc_full_body<NW>(a, s4, tb, reinterpret_cast<uint32_t*>(dc_lds));
 }
 
 template <int NW>

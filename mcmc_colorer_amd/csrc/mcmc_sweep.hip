@@ -65,6 +65,7 @@ struct DevState {
     unsigned long long finalViol;
     uint32_t iter;
     uint32_t maxIterReached;
+    uint32_t lx;                // discrete log of x_t base 16807 (rng.h minstd_dlog): x_t = 16807^lx
 };
 
 struct SweepArgs {
@@ -231,8 +232,18 @@ struct SweepArgs {
     uint32_t* dc_chg;           // [2][dc_chg_cap] every local vertex whose colour changed (restore list)
     unsigned long long* dc_open;   // [ntiles][NW] bit j of word (tile, i): row 64 tile + j's mask word i not full
     uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max, dc_chg_cap;
+    uint32_t dc_rbrows;         // rows per chunk of the streaming count rebuild (0: a wave per row)
     uint32_t dc_commit_restore;  // restore lists up to this long are applied by the commit
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
+    // open summary (dense_counts.h dc_osum_note): word 0's low half = open words that are nonzero;
+    // then one bit per open word (its index (row >> 6) NW + mask word), set while it is nonzero
+    unsigned long long* dc_osum;
+    // the persistent dense sweep's candidate window (dense_sparse.h): every minstd state w whose draw
+    // may move a closed row, with its discrete log: {L(w), w}, dl_n entries
+    const uint2* dl_tab;
+    uint32_t dl_n;
+    unsigned long long* solo_ts;    // diagnostics (MCMC_SOLO_TRACE): the leader's stamps, [sweep of the launch][8]
+    uint32_t nmodN;             // n mod (2^31 - 2): the advance of DevState::lx per sweep
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
 constexpr uint32_t kIncMode = 0;     // the running sweep: 1 full (the tile scan recounts), 0 incremental
@@ -261,8 +272,18 @@ constexpr uint32_t kDcCommitRestore = 8192;   // restore lists up to this long: 
 constexpr uint32_t kDcTask = 20;   // the running sweep's update tasks claimed (dense_counts.h dc_update_tasks)
 constexpr uint32_t kDcDone = 21;   // and completed
 constexpr uint32_t kDcStat2 = 22;  // u32 [2]: rows on the restore lists (saturating), restore-list overflows
-constexpr uint32_t kDcWords = 24;
-constexpr uint32_t kDcEvalLds = 64u * 1024u;   // dc_eval_kernel's dynamic LDS: the commit's sort buffer
+// the persistent dense sweep (dense_sparse.h dc_multi_kernel); the leader resets them before it returns
+constexpr uint32_t kDcGen = 24;    // the leader's posted phase: seq << 2 | kind (1 full sweep, 2 exit)
+constexpr uint32_t kDcAck = 25;    // helpers that saw the exit
+constexpr uint32_t kDcCommitted = 26;   // full sweeps committed in this launch
+constexpr uint32_t kDcSoloStat = 28;    // u64: sweeps the leader ran alone (solo), statistics
+constexpr uint32_t kDcSoloEval = 30;    // u64: rows those sweeps evaluated (candidates + open rows)
+constexpr uint32_t kDcMvDone = 32;      // the persistent sweep's move phases: workgroup tasks completed
+constexpr uint32_t kDcMvN = 33;         // the posted move phase: vertices of S moved
+constexpr uint32_t kDcMvList = 34;      // and their (v, a << 16 | b), 16 pairs at most
+constexpr uint32_t kDcWords = 72;
+constexpr uint32_t kDcEvalLds = 64u * 1024u;   // the dense sweep's LDS scratch: stage, commit sort buffer
+constexpr uint32_t kDcRebuildLds = 2u * kDcEvalLds;   // + the streaming rebuild's colour slice (dc_eval_kernel's dynamic LDS)
 
 
 // The commit's bookkeeping of sweep t (thread 0, after the event replay listed its vertices of S):
@@ -284,7 +305,7 @@ __device__ __forceinline__ DcCommitWords dc_commit_load(const SweepArgs& a, uint
     w.mode = k[kDcMode];
     return w;
 }
-__device__ void dc_commit(const SweepArgs& a, uint32_t t, const DcCommitWords& w) {
+__device__ __forceinline__ void dc_commit(const SweepArgs& a, uint32_t t, const DcCommitWords& w) {
     uint32_t* k = a.dc_ctl;
     const uint32_t p = t & 1u;
     unsigned long long* s = reinterpret_cast<unsigned long long*>(k + kDcStat);
@@ -357,6 +378,7 @@ __device__ __forceinline__ uint32_t inc_list_global(const SweepArgs& a, uint32_t
     return deg;
 }
 
+constexpr uint32_t kTabooMax24 = (1u << 24) - 1u;   // tail-queue entries pack the taboo counter in 24 bits
 constexpr uint32_t kDeltaWords = 4096;  // MCMC delta slot per rank: head + (v, c) pairs (16 KiB)
 constexpr uint32_t kDeltaHead = 2;
 constexpr uint32_t kDeltaPairs = (kDeltaWords - kDeltaHead) / 2;
@@ -574,7 +596,7 @@ __device__ void bitonic_sort_block(uint32_t* s, uint32_t P) {
     } while (0)
 
 template <typename CT = uint8_t>
-__device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
+__device__ __forceinline__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint32_t E, uint32_t* lds,
                               uint32_t lds_cap, bool sorted = false) {
     DevState* st = a.st;
     __shared__ uint32_t inc_cc[2];   // incremental counts: rows the event replay changed, their arcs
@@ -717,6 +739,8 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
     if (threadIdx.x == 0) {
         st->glibc_draws += E;
         st->x_t = minstd_mulmod(st->x_t, a.aN);
+        const uint32_t lx = st->lx + a.nmodN;   // (both < 2^31 - 2: no wrap of 32 bits)
+        st->lx = lx >= kMinstdN ? lx - kMinstdN : lx;
         st->t = t + 1;
         st->viol = 0;
         st->ev_count = 0;
@@ -729,7 +753,7 @@ __device__ void commit_accept(const SweepArgs& a, uint32_t t, uint32_t* ev, uint
 // on Cviol_t <= z, otherwise accepts the sweep. All threads of one workgroup call it with the same
 // state values; thread 0 writes the state.
 template <typename CT = uint8_t>
-__device__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
+__device__ __forceinline__ void commit_control(const SweepArgs& a, uint32_t t, unsigned long long viol, uint32_t E, uint32_t err,
                                uint32_t* lds, uint32_t lds_cap, uint32_t* ev = nullptr, bool sorted = false) {
     DevState* st = a.st;
     if (threadIdx.x == 0 && t < a.traj_cap) a.traj[t] = viol;
@@ -1012,6 +1036,10 @@ __device__ bool wide_commit_fast(const SweepArgs& a) {
         st->glibc_head = 0;
         st->glibc_draws = draws0 + E;
         st->x_t = minstd_mulmod(x_t, a.aN);
+        {
+            const uint32_t lx = st->lx + a.nmodN;
+            st->lx = lx >= kMinstdN ? lx - kMinstdN : lx;
+        }
         st->t = t + 1;
         st->viol = 0;
         st->ev_count = 0;
@@ -3077,6 +3105,7 @@ __global__ __launch_bounds__(1024) void sweep_tiled_kernel(SweepArgs a) {
 }
 
 #include "dense_counts.h"
+#include "dense_sparse.h"
 
 // Layout construction lives in tiled_layout.hip.
 __global__ void segment_kernel(const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ col_idx,
@@ -3327,7 +3356,14 @@ struct mcmc_ctx {
     uint32_t* dc_cnt = nullptr;
     uint32_t* dc_mask = nullptr;
     unsigned long long* dc_open = nullptr;
-    uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1, dc_chg_cap = 0;
+    uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1, dc_chg_cap = 0, dc_rbrows = 0;
+    unsigned long long* dc_osum = nullptr;   // open summary (count + one bit per open word)
+    // the persistent dense sweep (dense_sparse.h): its launch (nullptr: one dc_eval_kernel per sweep)
+    // and the candidate window {L(w), w}
+    void (*dcm_launch)(const SweepArgs&, uint32_t, dim3, hipStream_t) = nullptr;
+    uint2* dl_tab = nullptr;
+    uint32_t dl_n = 0;
+    unsigned long long* solo_ts = nullptr;   // MCMC_SOLO_TRACE diagnostics (4096 x 8 stamps)
 };
 
 namespace {
@@ -3367,6 +3403,7 @@ int upload_state(mcmc_ctx* c, uint32_t t) {
     DevState h{};
     h.t = t;
     h.x_t = c->x0;
+    h.lx = minstd_dlog(c->x0);
     h.glibc_head = 0;
     for (int i = 0; i < 31; i++) h.glibc_ring[i] = c->glibc.r[i];
     MCMC_HIP_TRY(hipMemcpyAsync(c->st, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
@@ -3398,10 +3435,12 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     a.v_begin = c->v_begin;
     a.v_end = c->v_end;
     a.nCol = c->p.nCol;
-    a.tabooIteration = c->p.tabooIteration;
+    // the tail queue's 24-bit counters (create_impl): a clamped copy, c->p keeps the caller's value
+    a.tabooIteration = (c->tq_l && c->p.tabooIteration > kTabooMax24) ? c->p.maxRip + 2u : c->p.tabooIteration;
     a.maxRip = c->p.maxRip;
     a.z = c->z;
     a.aN = minstd_pow(kMinstdA, c->n);
+    a.nmodN = c->n % kMinstdN;
     a.a256 = minstd_pow(kMinstdA, 256);
     a.eps = c->p.epsilon;
     a.hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;   // fill_p :406, no contraction
@@ -3542,6 +3581,11 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.dc_max = c->dc_max;
         a.dc_apow = c->dc_apow;
         a.lds_sort_cap = kDcEvalLds / 4u;
+        a.dc_osum = c->dc_osum;
+        a.dc_rbrows = c->dc_rbrows;
+        a.dl_tab = c->dl_tab;
+        a.dl_n = c->dl_n;
+        a.solo_ts = c->solo_ts;
     }
     a.phase_ts = c->phase_ts;
     a.pair_trace = c->pair_trace;
@@ -3591,13 +3635,25 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
+// K sweeps on the context stream: one persistent dense launch (dc_multi_kernel) where the context
+// has it (setup_dense_window; MCMC_DENSE_MULTI=0: never) and the arguments allow it (single context,
+// committing in the sweep; no taboo, no tail-cut flags, no diagnostics); else K (sweep, commit) pairs.
+void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
+    if (c->dcm_launch && a.fused == 1 && !c->part && a.taboo == nullptr && a.vflags == nullptr &&
+        a.scan_stats == nullptr && a.phase_ts == nullptr && a.pair_trace == nullptr) {
+        if (K) c->dcm_launch(a, K, c->grid, c->stream);
+        return;
+    }
+    for (uint32_t i = 0; i < K; i++) launch_pair(c, a);
+}
+
 int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
     if (c->batch_exec && c->batch == batch) return MCMC_OK;
     if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }
     SweepArgs a = make_args(c, 1);
     hipGraph_t graph;
     MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (uint32_t i = 0; i < batch; i++) launch_pair(c, a);
+    launch_sweeps(c, a, batch);
     MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
     hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
@@ -3762,6 +3818,66 @@ int simple_symmetric(GraphDev& gd, uint32_t vb, uint32_t ve, hipStream_t stream,
     return MCMC_OK;
 }
 
+// The smallest minstd state x in [1, 2^31 - 1) with canonical(x) >= f (2^31 - 1 if none): the host
+// twin of dense_counts.h dc_canonical_at_least (canonical is non-decreasing in x).
+uint32_t host_canonical_at_least(float f) {
+    uint32_t lo = 1u, hi = kMinstdM;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (minstd_canonical(mid) >= f) hi = mid;
+        else lo = mid + 1u;
+    }
+    return lo;
+}
+
+constexpr uint32_t kDlMax = 1u << 16;   // candidate-window states of the persistent dense sweep
+
+// The persistent dense sweep's pieces (dense_sparse.h): the open summary, and -- where the
+// closed-form walk exists, no taboo, the context's ids below 2^31 - 2 and the window small -- the
+// window's logarithm table. MCMC_DENSE_MULTI=0: neither (one dc_eval_kernel per sweep).
+int setup_dense_window(mcmc_ctx* c) {
+    const char* dm = getenv("MCMC_DENSE_MULTI");
+    if (dm && atoi(dm) == 0) return MCMC_OK;
+    const size_t nloc = c->v_end - c->v_begin;
+    const size_t owords = (nloc + 63u) / 64u * c->nw;
+    const size_t sbytes = sizeof(unsigned long long) * (1u + (owords + 63u) / 64u);
+    MCMC_HIP_TRY(hipMalloc(&c->dc_osum, sbytes));
+    MCMC_HIP_TRY(hipMemsetAsync(c->dc_osum, 0, sbytes, c->stream));
+    if (!c->ewalk || c->p.tabooIteration != 0u || c->v_end > kMinstdN || c->part) return MCMC_OK;
+    std::vector<float2> ew(c->p.nCol);
+    MCMC_HIP_TRY(hipMemcpy(ew.data(), c->ewalk, sizeof(float2) * ew.size(), hipMemcpyDeviceToHost));
+    uint32_t lo = 1u, hi = kMinstdM;   // the keep interval common to every colour: [lo, hi)
+    for (const float2& e : ew) {
+        lo = std::max(lo, host_canonical_at_least(e.x));
+        hi = std::min(hi, host_canonical_at_least(e.y));
+    }
+    if (hi <= lo) return MCMC_OK;
+    const uint64_t nwin = (uint64_t)(lo - 1u) + (uint64_t)(kMinstdM - hi);
+    uint64_t dlmax = kDlMax;
+    if (const char* e = getenv("MCMC_DL_MAX")) dlmax = strtoull(e, nullptr, 10);   // tests: larger windows
+    if (nwin > dlmax) return MCMC_OK;   // (eps far above the reference's 1e-8: the per-sweep kernel)
+    uint32_t* err = nullptr;
+    MCMC_HIP_TRY(hipMalloc(&c->dl_tab, sizeof(uint2) * std::max<uint64_t>(nwin, 1)));
+    MCMC_HIP_TRY(hipMalloc(&err, sizeof(uint32_t)));
+    uint32_t herr = 0;
+    hipError_t e = hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream);
+    if (e == hipSuccess && nwin) {
+        dl_table_kernel<<<(uint32_t)((nwin + 255u) / 256u), 256, 0, c->stream>>>(c->dl_tab, lo, hi, (uint32_t)nwin, err);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&herr, err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(err);
+    if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("dense window: ") + hipGetErrorString(e));
+    if (herr) return fail(MCMC_E_DEVICE, "dense window: a discrete logarithm failed its check");
+    c->dl_n = (uint32_t)nwin;
+    if (getenv("MCMC_SOLO_TRACE")) {
+        MCMC_HIP_TRY(hipMalloc(&c->solo_ts, sizeof(unsigned long long) * 8u * 4096u));
+        MCMC_HIP_TRY(hipMemset(c->solo_ts, 0, sizeof(unsigned long long) * 8u * 4096u));
+    }
+    return MCMC_OK;
+}
+
 // The dense-count sweep of a tiled context (dense_counts.h), when the graph allows it and
 // MCMC_DENSE is not 0: S = the first |S| local rows, |S| such that a row's expected neighbours in
 // S number nCol (ln nCol + K), K below (MCMC_DENSE_ROWS overrides |S|); counts, masks and lists allocated.
@@ -3773,24 +3889,43 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     if (!ok) return MCMC_OK;
     const uint32_t nCol = c->p.nCol;
     const double dbar = (double)c->tl->arcs / (double)nloc;
-    // K = 10: a row misses a colour in S with probability ~e^-10. Each sweep with an open row pays
-    // a chain of dependent loads (~6 us) in the wave holding it, while every unit of K costs the
-    // rebuild nloc nCol more counted arcs (~2.3 ms at C3, ~12 us at C2): small contexts take
-    // K = ln(nloc) + 3 (an open row in ~5 % of sweeps), large ones keep 10.
-    double K = 10.0;
-    if ((double)nloc * nCol <= 2e7) K = std::max(K, std::log((double)nloc) + 3.0);
+    // K = ln(nloc) + 3: a row misses a colour in S with probability ~nloc^-1 e^-3, so the context
+    // has an open row in ~5 % of its colourings. An open row costs every sweep a chain of dependent
+    // loads (the scan of its other column blocks) and keeps the persistent sweep's leader from
+    // running alone past kDcSoloOpenWords of them (dense_sparse.h); a unit of K costs the count
+    // rebuild nloc nCol more counted arcs, once per colouring (C3: K 19.1, |S| ~ 7.2e5; r04 took
+    // K = 10 there, 431 open rows in every sweep).
+    double K = std::max(10.0, std::log((double)nloc) + 3.0);
+    if (const char* dk = getenv("MCMC_DENSE_K")) K = atof(dk);
     const double target = (double)nCol * (std::log((double)nCol) + K);
     uint64_t S = dbar > 0.0 ? (uint64_t)std::ceil(target * (double)c->n / dbar) : nloc;
     if (const char* dr = getenv("MCMC_DENSE_ROWS")) S = (uint64_t)std::max(1, atoi(dr));
     S = std::max<uint64_t>(1, std::min<uint64_t>(S, nloc));
     const size_t cnt_bytes = (size_t)nloc * nCol * sizeof(uint32_t);
     if (cnt_bytes > (64ull << 30)) return MCMC_OK;   // counts beyond 64 GiB: the scan sweep
+    // and only with room to spare on the device: the counts must not take the memory that later
+    // allocations (tail queue, tail-cut buffers, the caller's tensors) need -- at most half of
+    // what is free now, else the scan sweep
+    {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && cnt_bytes > fr / 2) return MCMC_OK;
+        (void)hipGetLastError();
+    }
     c->dc_s0 = c->v_begin;
     c->dc_s1 = c->v_begin + (uint32_t)S;
     c->dc_cap = (uint32_t)S;
     c->dc_max = std::max<uint32_t>(64u, (uint32_t)(S / 8u));
     c->dc_apow = minstd_pow(kMinstdA, 64ull * c->grid.x * (c->block.x / 64u));
     c->dc_chg_cap = std::max<uint32_t>(4096u, nloc / 32u);   // past it: a full copy of the local rows
+    // the streaming count rebuild (dense_counts.h dc_rebuild_chunk): chunks of rows whose uint16
+    // count pairs and segment starts fill 64 KiB of LDS; its counts hold up to 65535 (every row
+    // below that many arcs), else a wave per row (MCMC_DENSE_RB=0 too)
+    {
+        const uint32_t hw = (nCol + 1u) / 2u, R = c->tl->grp_rows;
+        const uint32_t rc = std::min<uint32_t>(R, (kDcEvalLds / 4u - 1u) / (hw + 1u));
+        const char* rb = getenv("MCMC_DENSE_RB");
+        c->dc_rbrows = (c->g->maxDeg > 0 && c->g->maxDeg < 65536u && rc >= 1u && !(rb && atoi(rb) == 0)) ? rc : 0u;
+    }
     if (const char* cc = getenv("MCMC_DENSE_CHG_CAP")) c->dc_chg_cap = (uint32_t)std::max(2, atoi(cc));   // tests
     const size_t open_bytes = sizeof(unsigned long long) * (((size_t)nloc + 63u) / 64u) * c->nw;
     hipError_t e = hipMalloc(&c->dc_ctl, sizeof(uint32_t) * (kDcWords + 4ull * S + 2ull * c->dc_chg_cap));
@@ -3811,7 +3946,7 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     c->dc = true;
     e = dc_reset(c);
     if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("dense counts: ") + hipGetErrorString(e));
-    return MCMC_OK;
+    return setup_dense_window(c);
 }
 
 }  // namespace
@@ -3847,12 +3982,6 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     const GraphDev& gd = g->g;
     if (p->nCol == 0) return fail(MCMC_E_ARG, "nCol must be >= 1");
     if (v_begin > v_end || v_end > gd.n) return fail(MCMC_E_ARG, "bad vertex range");
-    // The tail queue packs a row's taboo counter in 24 bits (own colour | counter << 8). A counter
-    // past the loop's last sweep never expires within the loop, so a larger tabooIteration is
-    // clamped to maxRip + 2 (the same run); with a loop that long it is refused.
-    constexpr uint32_t kTabooMax = (1u << 24) - 1u;
-    if (p->tabooIteration > kTabooMax && (uint64_t)p->maxRip + 2u > kTabooMax)
-        return fail(MCMC_E_ARG, "tabooIteration >= 2^24 needs maxRip + 2 < 2^24 (24-bit taboo counters)");
     // nCol > 256: the wide sweep (uint16 replicas, sweep_wide.h); MCMC_GATHER=wide forces it
     const char* gv = getenv("MCMC_GATHER");
     const std::string gsel = gv ? gv : "";
@@ -3881,7 +4010,6 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     mcmc_ctx* c = new mcmc_ctx();
     c->g = &gd;
     c->p = *p;
-    if (c->p.tabooIteration > kTabooMax) c->p.tabooIteration = p->maxRip + 2u;
     c->n = gd.n;
     c->v_begin = v_begin;
     c->v_end = v_end;
@@ -4140,6 +4268,15 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                 return fail(MCMC_E_NOMEM, std::string("tail queue: ") + hipGetErrorString(qe));
             }
             c->tq_dense = tqd;
+            // The tail queue packs a row's taboo counter in 24 bits (own colour | counter << 8). A
+            // counter past the loop's last sweep never expires within the loop, so the sweeps of
+            // such a context see a larger tabooIteration as maxRip + 2 (make_args; c->p keeps the
+            // caller's value); with a loop that long it is refused.
+            if (p->tabooIteration > kTabooMax24 && (uint64_t)p->maxRip + 2u > kTabooMax24) {
+                mcmc_destroy(c);
+                return fail(MCMC_E_ARG, "tabooIteration >= 2^24 needs maxRip + 2 < 2^24 (24-bit taboo counters "
+                                        "of the tail queue)");
+            }
         }
         c->own_buf_bytes = resident ? 0u : (uint32_t)own_bytes(R);
         if (ref) {
@@ -4160,9 +4297,15 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             static const SweepLaunch tab[4] = {launch_dc<1>, launch_dc<2>, launch_dc<4>, launch_dc<8>};
             c->sweep = tab[wi];
             c->sweep_diag = nullptr;
-            c->lds = kDcEvalLds;
+            c->lds = kDcRebuildLds;
             ea = wi == 0 ? allow_lds_dc<1>(c->lds) : wi == 1 ? allow_lds_dc<2>(c->lds)
                : wi == 2 ? allow_lds_dc<4>(c->lds) : allow_lds_dc<8>(c->lds);
+            if (c->dc_osum) {   // the persistent launch (dense_sparse.h)
+                static const decltype(c->dcm_launch) tabm[4] = {launch_dcm<1>, launch_dcm<2>, launch_dcm<4>, launch_dcm<8>};
+                c->dcm_launch = tabm[wi];
+                if (ea == hipSuccess)
+                    ea = wi == 0 ? allow_lds_dcm<1>() : wi == 1 ? allow_lds_dcm<2>() : wi == 2 ? allow_lds_dcm<4>() : allow_lds_dcm<8>();
+            }
         } else if (c->early) {   // the early-exit instantiations
             if (resident) {
                 static const SweepLaunch tab[4] = {launch_tiled<1, true, false, true>, launch_tiled<2, true, false, true>,
@@ -4512,7 +4655,8 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
             launched += batch;
         } else {
             SweepArgs a = make_args(c, 1);
-            for (; launched < total; launched++) launch_pair(c, a);
+            launch_sweeps(c, a, total - launched);
+            launched = total;
             MCMC_HIP_TRY(hipGetLastError());
         }
         rc = download_state(c, &h);
@@ -4654,6 +4798,24 @@ int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[10]) {
     out[7] = c->dc_max;
     out[8] = h[kDcStat2];
     out[9] = h[kDcStat2 + 1];
+    return MCMC_OK;
+}
+
+int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    for (int i = 0; i < 16; i++) out[i] = 0;
+    int rc = mcmc_get_dense_stats(c, out);
+    if (rc || !c->dc) return rc;
+    uint32_t h[kDcWords];
+    MCMC_HIP_TRY(hipMemcpyAsync(h, c->dc_ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    unsigned long long os = 0;
+    if (c->dc_osum) MCMC_HIP_TRY(hipMemcpyAsync(&os, c->dc_osum, sizeof(os), hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    out[10] = reinterpret_cast<const unsigned long long*>(h + kDcSoloStat)[0];   // solo sweeps
+    out[11] = c->dl_n;                                                           // window states
+    out[12] = c->dcm_launch ? 1u : 0u;                                           // persistent launch
+    out[13] = (uint32_t)os;                                                      // nonzero open words now
+    out[14] = reinterpret_cast<const unsigned long long*>(h + kDcSoloEval)[0];   // rows solo sweeps evaluated
     return MCMC_OK;
 }
 
@@ -4831,7 +4993,7 @@ int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
     a.bench = 1;   // a convergent run (C5) keeps sweeping from its proper colouring
     hipGraph_t graph;
     MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (uint32_t i = 0; i < sweeps; i++) launch_pair(c, a);
+    launch_sweeps(c, a, sweeps);
     MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
     hipError_t e = hipGraphInstantiate(&c->bench_exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
@@ -4867,6 +5029,14 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
         MCMC_HIP_TRY(hipMemcpy(h_tr.data(), c->pair_trace, h_tr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("MCMC_PAIR_TRACE"), "wb")) {
             fwrite(h_tr.data(), sizeof(unsigned long long), h_tr.size(), f);
+            fclose(f);
+        }
+    }
+    if (c->solo_ts) {   // diagnostics: the persistent launch's per-sweep stamps of its leader
+        std::vector<unsigned long long> h_ts(8u * 4096u);
+        MCMC_HIP_TRY(hipMemcpy(h_ts.data(), c->solo_ts, h_ts.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("MCMC_SOLO_TRACE"), "wb")) {
+            fwrite(h_ts.data(), sizeof(unsigned long long), h_ts.size(), f);
             fclose(f);
         }
     }
@@ -5004,6 +5174,9 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dc_cnt);
     (void)hipFree(c->dc_mask);
     (void)hipFree(c->dc_open);
+    (void)hipFree(c->dc_osum);
+    (void)hipFree(c->dl_tab);
+    (void)hipFree(c->solo_ts);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
@@ -5111,6 +5284,9 @@ int part_sweep(mcmc_ctx* c, bool delta) {
 
 int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
     if (!c || !c->part || !part_solo(c) || !c->initialized || steps == 0) return 1;
+    // the legacy null stream (mcmc_part_attach with torch's default stream) cannot be captured:
+    // the caller's per-step path then
+    if (c->stream == nullptr) return 1;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     c->ran = true;
     const uint32_t key = 0x80000000u | steps;   // (c->batch: the one-GPU run's batches are plain counts)
@@ -5120,7 +5296,10 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
         a.dcap = 0u;
         a.fused = c->wide ? 0 : 1;   // as part_sweep's world-1 step
         hipGraph_t graph;
-        MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            (void)hipGetLastError();
+            return 1;   // capture unsupported on this stream: the per-step path
+        }
         for (uint32_t i = 0; i < steps; i++) launch_pair(c, a);
         MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
         hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
@@ -5245,6 +5424,10 @@ void part_tail_done(mcmc_ctx* c, uint64_t cviol, uint32_t passes) {
     c->tail_done = true;
     c->tail_passes = passes;
     c->tail_viol = cviol;
+    // the passes changed colours outside a sweep: dense counts and incremental violation counts
+    // start over, as after mcmc_run's tail cut
+    if (c->dc) (void)dc_reset(c);
+    if (c->inc) (void)inc_reset(c);
 }
 
 int part_spill_buffer(mcmc_ctx* c, uint32_t stride, uint32_t** buf) {

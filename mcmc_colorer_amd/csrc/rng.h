@@ -44,6 +44,37 @@ MCMC_HD uint32_t minstd_pow(uint32_t a, uint64_t e) {
     return r;
 }
 
+// Discrete logarithm base 16807 modulo 2^31 - 1: the L in [0, N), N = 2^31 - 2, with 16807^L = x.
+// 16807 is a primitive root of the prime 2^31 - 1 (the reason minstd uses it: Park & Miller), so
+// every state x in [1, 2^31 - 2] has exactly one. N = 2 * 3^2 * 7 * 11 * 31 * 151 * 331 is smooth:
+// Pohlig-Hellman -- per prime power q^e, L mod q^e is the d < q^e with (16807^(N/q^e))^d =
+// x^(N/q^e), found by stepping; the Chinese remainder theorem assembles L. About 900 mulmods.
+// Returns 0xFFFFFFFF for x outside the group (0 or >= 2^31 - 1).
+// Use: engine draw j after state x_t is x_t 16807^j = 16807^(L(x_t) + j), so the vertices whose
+// draw lands in a given set of states follow from the states' logarithms (dense_sparse.h).
+constexpr uint32_t kMinstdN = kMinstdM - 1u;   // the multiplicative group's order
+MCMC_HD uint32_t minstd_dlog(uint32_t x) {
+    if (x == 0u || x >= kMinstdM) return 0xFFFFFFFFu;
+    const uint32_t qe[7] = {2u, 9u, 7u, 11u, 31u, 151u, 331u};
+    uint64_t L = 0;
+    for (int i = 0; i < 7; i++) {
+        const uint32_t q = qe[i], m = kMinstdN / q;
+        const uint32_t g = minstd_pow(kMinstdA, m), h = minstd_pow(x, m);
+        uint32_t y = 1u, d = 0u;
+        while (y != h && d < q) {
+            y = minstd_mulmod(y, g);
+            d++;
+        }
+        if (d == q) return 0xFFFFFFFFu;
+        // CRT coefficient: m (m^-1 mod q), so it is 1 mod q and 0 mod the other prime powers
+        const uint32_t mr = m % q;
+        uint32_t inv = 1u;
+        while ((uint64_t)mr * inv % q != 1u) inv++;
+        L = (L + (uint64_t)d * ((uint64_t)m * inv % kMinstdN)) % kMinstdN;
+    }
+    return (uint32_t)L;
+}
+
 // linear_congruential_engine::seed(s): x0 = s mod m, or 1 when that is 0.
 MCMC_HD uint32_t minstd_seed_state(uint32_t seed) {
     uint32_t s = seed % kMinstdM;

@@ -1,0 +1,21 @@
+"""Summarise MCMC_SOLO_TRACE stamps (dense_sparse.h dc_leader_solo, wall_clock64 at 100 MHz):
+per solo sweep [0] start, [1] before the evaluation, [2] evaluation done, [3] accepted; sweeps
+with a move phase also [7] the helpers' moves done. Medians in us."""
+import sys
+
+import numpy as np
+
+ts = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+r = ts[(ts[:, 0] > 0) & (ts[:, 3] > 0)]
+if len(r) < 2:
+    print("no solo sweeps traced")
+    sys.exit(0)
+us = lambda x: float(np.median(x)) / 100.0
+mv = r[:, 7] > 0
+per = np.diff(r[:, 0])
+print(f"solo sweeps traced: {len(r)}, with a move phase: {int(mv.sum())}")
+print(f"  setup {us(r[~mv,1]-r[~mv,0]):.2f} us, evaluation {us(r[:,2]-r[:,1]):.2f} us, accept {us(r[:,3]-r[:,2]):.2f} us, "
+      f"period median {us(per):.2f} us, mean {np.mean(per)/100:.2f} us")
+if mv.any():
+    m = r[mv]
+    print(f"  move phase (post -> helpers done) {us(m[:,7]-m[:,0]):.2f} us, to evaluation {us(m[:,1]-m[:,0]):.2f} us")

@@ -170,3 +170,72 @@ def test_dense_partitioned_loopback(M, monkeypatch, world):
     b = plan_rows(3000, world)
     assert out[0] == 1 and out[1] == b[world - 1] and out[2] == b[world - 1] + 150 and out[3] > 0
     lp.close()
+
+
+def dense_stats_v2(col):
+    return col.dense_stats()
+
+
+@pytest.mark.parametrize("n,p,ncol,seed,eps,maxrip,srows,solo_min", [
+    (3000, 0.3, 16, 31, 1e-8, 60, None, 58),    # C2-like (every row full): every sweep but the rebuild solo
+    (1500, 0.6, 48, 55, 1e-8, 40, None, 1),     # NW = 2
+    (2000, 0.5, 100, 52, 1e-8, 30, None, 1),    # NW = 4, a few open rows (evaluated by the leader)
+    (2500, 0.8, 200, 53, 1e-8, 20, None, 1),    # NW = 8
+    (3000, 0.3, 16, 54, 1e-8, 30, 40, 0),       # |S| = 40: most rows open, full sweeps inside the launch
+])
+def test_dense_persistent_matches_oracle(M, monkeypatch, n, p, ncol, seed, eps, maxrip, srows, solo_min):
+    """The persistent dense sweep (csrc/dense_sparse.h): the leader's solo sweeps evaluate only the
+    candidate rows of the discrete-log window and the open rows; full sweeps (the count rebuild, open
+    rows past the solo limit) run on the whole grid inside the same launch. Bit-exact vs the oracle."""
+    if srows is not None:
+        monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, maxRip=maxrip)
+    col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=maxrip)
+    assert_same(col, st, r)
+    ds = dense_stats_v2(col)
+    assert ds["enabled"] and ds["persistent"] and ds["window_states"] > 0
+    assert ds["solo_sweeps"] >= solo_min, ds
+
+
+def test_dense_persistent_off_matches(M, monkeypatch):
+    """MCMC_DENSE_MULTI=0: one dc_eval_kernel per sweep, the same results."""
+    monkeypatch.setenv("MCMC_DENSE_MULTI", "0")
+    off, idx, nc, r = oracle_case(3000, 0.02, 16, 31, epsilon=1e-8, maxRip=60)
+    col, st, _ = gpu_run(M, off, idx, nc, 31, 3000 * 3001 // 2, maxRip=60)
+    assert_same(col, st, r)
+    ds = dense_stats_v2(col)
+    assert ds["enabled"] and not ds["persistent"] and ds["solo_sweeps"] == 0
+
+
+@pytest.mark.parametrize("eps", [1e-8, 1e-3])
+def test_dense_persistent_generated_graph(M, eps):
+    """The generated G(n, p) (n = 150000, mean degree 450, 32 colours): 40 sweeps of the persistent
+    launch (eps 1e-8: solo sweeps; 1e-3: the window is too large, the per-sweep kernel) equal the oracle."""
+    n, p, seed = 150000, 0.003, 8
+    off, idx = O.er_fast(n, p, seed)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 32, seed, epsilon=eps, maxRip=39, nthreads=8)
+    g = M.Graph.er_fast(n, p, seed)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=32, epsilon=eps, maxRip=39))
+    st = col.run(0)
+    assert_same(col, st, r)
+    ds = dense_stats_v2(col)
+    assert (ds["window_states"] > 0) == (eps < 1e-6)   # eps 1e-3: no closed-form walk, no window
+    if eps < 1e-6:
+        assert ds["solo_sweeps"] >= 30, ds
+
+
+@pytest.mark.parametrize("rb", ["0", "1"])
+@pytest.mark.parametrize("n,p,ncol,seed,eps,srows", [(3000, 0.02, 16, 61, 1e-3, 1000), (2500, 0.1, 200, 62, 1e-3, 700),
+                                                     (2000, 0.05, 33, 63, 3.3e6, None)])
+def test_dense_rebuild_forms(M, monkeypatch, rb, n, p, ncol, seed, eps, srows):
+    """The count rebuild two ways -- a wave per row (MCMC_DENSE_RB=0) and the streaming chunks of a
+    row group (dense_counts.h dc_rebuild_chunk, the default) -- over list overflows (eps 3.3e6:
+    every sweep rebuilds) and partial column blocks of S: the same colourings as the oracle."""
+    monkeypatch.setenv("MCMC_DENSE_RB", rb)
+    if srows:
+        monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
+    off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, maxRip=20)
+    col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=20)
+    assert_same(col, st, r)
+    assert dense_stats_v2(col)["rebuilds"] >= 1
