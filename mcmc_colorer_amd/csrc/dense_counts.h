@@ -133,6 +133,10 @@ __device__ __forceinline__ void dc_rebuild_chunk(const SweepArgs& a, const uint8
     for (uint32_t i = threadIdx.x; i < rows * hw; i += blockDim.x) hist[i] = 0u;
     const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
     const uint32_t sb0 = a.dc_s0 >> bl, sb1 = (a.dc_s1 - 1u) >> bl;
+    // diagnostics (MCMC_SOLO_TRACE): workgroup 0's first chunk, stamps at the end of solo_ts
+    unsigned long long* const rts = (a.solo_ts && blockIdx.x == 0 && threadIdx.x == 0 && a.solo_ts[8u * 4096u - 1u] == 0ull)
+                                        ? a.solo_ts + 8u * 4096u - 64u : nullptr;
+    if (rts) rts[0] = wall_clock64();
     for (uint32_t b = sb0; b <= sb1; b++) {
         const uint32_t blo = b << bl;
         const uint32_t lo = max(blo, a.dc_s0) - blo, hi = min(blo + (1u << bl), a.dc_s1) - blo;   // S in block b
@@ -147,27 +151,45 @@ __device__ __forceinline__ void dc_rebuild_chunk(const SweepArgs& a, const uint8
             for (uint32_t i = max(q1, lo) + threadIdx.x; i < hi; i += blockDim.x) sl[i] = C[blo + i];
         }
         __syncthreads();
+        if (rts && b - sb0 < 28u) rts[1u + 2u * (b - sb0)] = wall_clock64();
         const uint32_t p0 = tab[0] & kTsegPos, p1 = tab[rows] & kTsegPos, nq = (p1 - p0) >> 3;
-        for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
-            const uint32_t pos = p0 + 8u * q;
-            const uint4 v = *reinterpret_cast<const uint4*>(gc + pos);
-            uint32_t L = 0, H = rows;   // the row j with start(j) <= pos < start(j + 1)
-            while (H - L > 1u) {
-                const uint32_t mid = (L + H) >> 1;
-                if ((tab[mid] & kTsegPos) <= pos) L = mid;
-                else H = mid;
-            }
-            const uint32_t end = (tab[L + 1] & kTsegPos) - (tab[L] & 7u);
-            uint32_t* const hr = hist + L * hw;
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        // kRbQ quads per thread in flight (one HBM round trip for a block's whole chunk at C3: ~7
+        // quads per thread), then their rows (independent binary searches) and histogram adds
+        constexpr uint32_t kRbQ = 8;
+        for (uint32_t q0 = 0; q0 < nq; q0 += kRbQ * blockDim.x) {
+            uint4 v[kRbQ];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t id = (w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                if (pos + (uint32_t)k < end && id - lo < hi - lo) {
-                    const uint32_t c = sl[id];
-                    atomicAdd(&hr[c >> 1], 1u << (16u * (c & 1u)));
+            for (uint32_t r = 0; r < kRbQ; r++) {
+                const uint32_t q = q0 + r * blockDim.x + threadIdx.x;
+                v[r] = q < nq ? *reinterpret_cast<const uint4*>(gc + p0 + 8u * q) : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < kRbQ; r++) {
+                const uint32_t q = q0 + r * blockDim.x + threadIdx.x;
+                if (q >= nq) continue;
+                const uint32_t pos = p0 + 8u * q;
+                uint32_t L = 0, H = rows;   // the row j with start(j) <= pos < start(j + 1)
+                while (H - L > 1u) {
+                    const uint32_t mid = (L + H) >> 1;
+                    if ((tab[mid] & kTsegPos) <= pos) L = mid;
+                    else H = mid;
+                }
+                const uint32_t end = (tab[L + 1] & kTsegPos) - (tab[L] & 7u);
+                uint32_t* const hr = hist + L * hw;
+                const uint32_t w4[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t id = (w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    if (pos + (uint32_t)k < end && id - lo < hi - lo) {
+                        const uint32_t c = sl[id];
+                        atomicAdd(&hr[c >> 1], 1u << (16u * (c & 1u)));
+                    }
                 }
             }
+        }
+        if (rts && b - sb0 < 28u) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            rts[2u + 2u * (b - sb0)] = wall_clock64();
         }
     }
     __syncthreads();
@@ -207,6 +229,11 @@ __device__ __forceinline__ void dc_rebuild_chunk(const SweepArgs& a, const uint8
             const unsigned long long o2 = atomicOr(&a.dc_open[idx], nb);
             dc_osum_note(a, idx, o2, o2 | nb);
         }
+    }
+    if (rts) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        rts[62] = wall_clock64();
+        rts[63] = 1ull;   // (only the first chunk is traced)
     }
 }
 

@@ -6,7 +6,7 @@ timeout -k 10 600 python3 -u -m pytest tests/test_dense.py -x -q --timeout 300 -
 rc=$?; tail -3 $O/dense.log; [ $rc -ne 0 ] && { grep -n "Error\|assert\|FAIL" $O/dense.log | head -30; exit $rc; }
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-MCMC_SOLO_TRACE=$O/solo.bin timeout -k 10 600 python3 -u bench.py --steps 200 --warmup 5 --no-refstruct --no-cpu-baseline --no-full-scan --no-convergence > $O/c3_trace.log 2>&1 || { tail -20 $O/c3_trace.log; exit 1; }
+MCMC_SOLO_TRACE=$O/solo.bin timeout -k 10 600 python3 -u bench.py --steps 200 --warmup 0 --no-refstruct --no-cpu-baseline --no-full-scan --no-convergence > $O/c3_trace.log 2>&1 || { tail -20 $O/c3_trace.log; exit 1; }
 python3 scripts/solo_trace.py $O/solo.bin
 timeout -k 10 600 python3 -u bench.py --steps 20 --warmup 5 --no-refstruct --no-cpu-baseline --no-full-scan > $O/c3.log 2>&1 || { tail -20 $O/c3.log; exit 1; }
 python3 - $O/c3.log <<'PY'

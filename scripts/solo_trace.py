@@ -19,3 +19,12 @@ print(f"  setup {us(r[~mv,1]-r[~mv,0]):.2f} us, evaluation {us(r[:,2]-r[:,1]):.2
 if mv.any():
     m = r[mv]
     print(f"  move phase (post -> helpers done) {us(m[:,7]-m[:,0]):.2f} us, to evaluation {us(m[:,1]-m[:,0]):.2f} us")
+rb = ts.reshape(-1)[8 * 4096 - 64:]
+if rb[63] == 1:
+    t0 = rb[0]
+    blocks = [(rb[1 + 2 * i] - t0, rb[2 + 2 * i] - t0) for i in range(28) if rb[2 + 2 * i] > 0]
+    st = [blocks[0][0]] + [blocks[i][0] - blocks[i - 1][1] for i in range(1, len(blocks))]
+    sm = [b[1] - b[0] for b in blocks]
+    print(f"rebuild chunk (workgroup 0): {len(blocks)} blocks, stage+barrier median {np.median(st)/100:.2f} us, "
+          f"stream median {np.median(sm)/100:.2f} us, write-out {(rb[62] - t0 - blocks[-1][1])/100:.2f} us, "
+          f"total {(rb[62] - t0)/100:.2f} us")
