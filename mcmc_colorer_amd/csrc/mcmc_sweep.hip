@@ -4300,7 +4300,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             c->lds = kDcRebuildLds;
             ea = wi == 0 ? allow_lds_dc<1>(c->lds) : wi == 1 ? allow_lds_dc<2>(c->lds)
                : wi == 2 ? allow_lds_dc<4>(c->lds) : allow_lds_dc<8>(c->lds);
-            if (c->dc_osum) {   // the persistent launch (dense_sparse.h)
+            if (c->dc_osum && c->dl_n) {   // the persistent launch (dense_sparse.h), where sweeps can run solo
                 static const decltype(c->dcm_launch) tabm[4] = {launch_dcm<1>, launch_dcm<2>, launch_dcm<4>, launch_dcm<8>};
                 c->dcm_launch = tabm[wi];
                 if (ea == hipSuccess)

@@ -572,6 +572,18 @@ void oracle_canonical_at(uint32_t seed, const uint64_t* pos, uint64_t k, float* 
     for (uint64_t i = 0; i < k; i++) out[i] = canonical_from_state(mulmod(x0, powmod(kA, pos[i])));
 }
 
+// u of the k consecutive engine draws start, start + 1, ... of default_random_engine(seed): the bulk
+// draw of one sweep (coloringMCMC_CPU.cpp:139), one skip-ahead then sequential minstd steps.
+void oracle_canonical_from(uint32_t seed, uint64_t start, uint64_t k, float* out) {
+    uint64_t x0 = (uint64_t)seed % kM;
+    if (x0 == 0) x0 = 1;
+    uint64_t x = k ? mulmod(x0, powmod(kA, start)) : 0;
+    for (uint64_t i = 0; i < k; i++) {
+        out[i] = canonical_from_state(x);
+        x = mulmod(x, kA);
+    }
+}
+
 // One vertex of loop 1 (coloringMCMC_CPU.cpp:183-204) from its neighbours' colours: violation flag
 // (violation_count :329-351: own colour used by a neighbour), count_free_colors (:361-383), fill_p
 // (:392-481, colorIdx the identity) and extract_new_color (:492-528, taboo 0). Returns 1 for a CDF

@@ -84,6 +84,7 @@ void     oracle_free(void* p);
 // ---- per-vertex pieces for sampled checks at sizes where the whole run cannot be restated ----
 // u of engine draw pos[i] (1-based) of default_random_engine(seed) (coloringMCMC_CPU.cpp:139).
 void     oracle_canonical_at(uint32_t seed, const uint64_t* pos, uint64_t k, float* out);
+void     oracle_canonical_from(uint32_t seed, uint64_t start, uint64_t k, float* out);
 // One vertex of the sweep from its neighbours' colours (violation_count, count_free_colors, fill_p,
 // extract_new_color with taboo 0). Returns 1 on a CDF overflow (colour from rand()), else 0.
 int      oracle_vertex_update(uint32_t nCol, float epsilon, uint32_t cv, const uint32_t* nbr_colors, uint64_t deg,

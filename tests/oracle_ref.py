@@ -61,6 +61,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_er_rows.argtypes = [c_uint32, ctypes.c_double, c_uint64, c_void_p, c_uint32, c_int,
                                      POINTER(POINTER(c_uint64)), POINTER(POINTER(c_uint32))]
         L.oracle_canonical_at.argtypes = [c_uint32, c_void_p, c_uint64, c_void_p]
+        L.oracle_canonical_from.argtypes = [c_uint32, c_uint64, c_uint64, c_void_p]
         L.oracle_vertex_update.argtypes = [c_uint32, c_float, c_uint32, c_void_p, c_uint64, c_float,
                                            POINTER(c_uint32), POINTER(c_int)]
         L.oracle_free.argtypes = [c_void_p]
@@ -144,6 +145,13 @@ def canonical_at(seed: int, positions) -> np.ndarray:
     pos = np.ascontiguousarray(positions, dtype=np.uint64)
     out = np.zeros(len(pos), dtype=np.float32)
     lib().oracle_canonical_at(seed & 0xFFFFFFFF, _p(pos), len(pos), _p(out))
+    return out
+
+
+def canonical_from(seed: int, start: int, count: int) -> np.ndarray:
+    """u of engine draws start, start + 1, ..., start + count - 1 (1-based) of default_random_engine(seed)."""
+    out = np.zeros(count, dtype=np.float32)
+    lib().oracle_canonical_from(seed & 0xFFFFFFFF, start, count, _p(out))
     return out
 
 

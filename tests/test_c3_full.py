@@ -123,3 +123,42 @@ def test_c3_full_size_every_vertex_eps_1e3(hip_lib):
     assert col.trajectory().tolist()[:3] == [N, N, N]
     col.close()
     g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c3_full_size_reference_loop_every_vertex(hip_lib):
+    """The bench's exact reference loop at full C3 size -- run() from the initial colouring to its
+    maxRip cap (251 accepted sweeps + the count-only pass, coloringMCMC_CPU.cpp:136-270) -- at the
+    default eps (the persistent dense sweep: discrete-log candidate rows, solo sweeps, move phases
+    for the ~60 vertices of the dense range that change over the run) and at eps = 1e-3 (no
+    closed-form walk: one dense sweep per launch, ~13 000 vertices of the dense range moving per
+    sweep, incremental count updates over hundreds of sweeps). Every vertex of the final colouring
+    C_251, the glibc draws and the whole Cviol trajectory equal tests/c3_expect.py's streamed
+    restatement of the all-full case."""
+    import mcmc_colorer_amd.colorer as M
+
+    g = M.Graph.er_fast(N, P, SEED)
+    for eps in (EPS, 1e-3):
+        t0 = time.perf_counter()
+        col = M.ColoringMCMC(g, M.GPURand(N, SEED, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=NCOL, epsilon=eps))
+        st = col.run(0)
+        got = col.coloring()
+        traj = col.trajectory()
+        ds = col.dense_stats()
+        t1 = time.perf_counter()
+        C3X.pin_walk(NCOL, eps)
+        E, k0, evs = C3X.expected_final(251, eps)
+        print(f"\neps {eps}: loop {st.loopMs:.1f} ms ({t1 - t0:.1f} s with set-up), restatement "
+              f"{time.perf_counter() - t1:.1f} s; glibc draws {st.glibcDraws}, events {sum(evs)}; dense {ds}", flush=True)
+        assert (st.iter, bool(st.maxIterReached), st.sweepsRun) == (251, True, 252)
+        assert st.initDraws == k0
+        assert st.glibcDraws == sum(evs)
+        assert traj.tolist() == [N] * 252
+        bad = np.nonzero(got != E)[0]
+        assert len(bad) == 0, f"eps {eps}: {len(bad)} vertices of C_251 differ, first {bad[:5].tolist()}"
+        assert ds["incremental_sweeps"] >= 200 and ds["moved_vertices"] > 0
+        if eps == EPS:
+            assert ds["solo_sweeps"] >= 240, ds
+        col.close()
+    g.close()
