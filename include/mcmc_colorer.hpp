@@ -25,6 +25,8 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <numeric>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -115,12 +117,34 @@ public:
                                      neighs.size(), device, &h_));
         info();
     }
-    ~Graph() { mcmc_graph_destroy(h_); }
+    // A host-only graph (no device copy): the CSR as the reference's host Graph holds it, for
+    // ColoringMCMC_CPU's per-vertex hooks and violation_count without a GPU; run() needs a device graph.
+    struct HostOnly {};
+    Graph(HostOnly, const std::vector<uint64_t>& cumulDegs, const std::vector<node>& neighs, float prob_ = 0.0f)
+        : prob(prob_) {
+        n_ = (node)(cumulDegs.size() - 1);
+        m_ = neighs.size();
+        str_.nNodes = n_;
+        str_.nEdges = m_;
+        str_.cumulDegsV = cumulDegs;
+        str_.neighsV = neighs.empty() ? std::vector<node>(1) : neighs;
+        str_.cumulDegs = str_.cumulDegsV.data();
+        str_.neighs = str_.neighsV.data();
+        maxDeg_ = 0;
+        minDeg_ = n_ ? ~node(0) : 0;
+        for (node i = 0; i < n_; i++) {   // doStats (graphCPU.cpp:432-450)
+            maxDeg_ = std::max<node>(maxDeg_, (node)str_.deg(i));
+            minDeg_ = std::min<node>(minDeg_, (node)str_.deg(i));
+        }
+    }
+    ~Graph() {
+        if (h_) mcmc_graph_destroy(h_);
+    }
     Graph(const Graph&) = delete;
     Graph& operator=(const Graph&) = delete;
 
     GraphStruct<nodeW, edgeW>* getStruct() {
-        if (!str_.cumulDegs) {
+        if (!str_.cumulDegs && h_) {
             str_.nNodes = n_;
             str_.nEdges = m_;
             str_.cumulDegsV.resize((size_t)n_ + 1);
@@ -137,6 +161,7 @@ public:
     node getMinNodeDeg() const { return minDeg_; }
     float getMeanNodeDeg() const { return n_ ? (float)m_ / (float)n_ : 0.0f; }
     const mcmc_graph* handle() const { return h_; }
+    bool onDevice() const { return h_ != nullptr; }
     int device() const { return device_; }
     float prob{0.0f};
     // Row-partial graphs (ErFast with a row range: one rank's rows) describe only their rows; the
@@ -330,16 +355,36 @@ private:
 // ---- ColoringMCMC_CPU's class surface (graph_coloring/coloringMCMC_CPU.h:15-31) ----------------
 // The reference's --mcmccpu colorer, run by the same HIP sweep as ColoringMCMC (its semantics ARE
 // the CPU colorer's: bit-identical colouring, iteration count and glibc stream). Kept: the ctor
-// (graph, params, seed -- main.cu:171 passes seed + repetition), run(), show_histogram(),
-// violation_count() (on the GPU: mcmc_count_violations of the given colouring), saveStats() and
-// saveColor() in the reference's layout (coloringMCMC_CPUutils.cpp:70-109), getC(). The per-vertex
-// GoogleTest hooks of the reference (count_free_colors, fill_p, extract_new_color, fill_qstar) act on
-// the CPU class's private buffers and have no counterpart: the sweep computes them in registers.
+// (graph, params, seed -- main.cu:171 passes seed + repetition; it draws the initial colouring C
+// with default_random_engine(seed) and uniform_int_distribution, coloringMCMC_CPU.cpp:53-61), run(),
+// show_histogram(), violation_count() (on the GPU for a device graph, else on the host), saveStats()
+// and saveColor() in the reference's layout (coloringMCMC_CPUutils.cpp:70-109), and the per-vertex
+// hooks the reference made public for its GoogleTest (coloringMCMC_CPU.h:20-28): count_free_colors,
+// fill_p, extract_new_color, fill_qstar -- host restatements of coloringMCMC_CPU.cpp:362-551 over
+// the class's own buffers (p, q, qstar, freeColors, Cviols, taboo, colorIdx = identity), CDF
+// overflows drawing rand() from the process-global glibc window like the sweep. With the dbg
+// accessors (getC, getCstar, getp, ...) a test drives loop 1 of run() vertex by vertex.
 template <typename nodeW, typename edgeW>
 class ColoringMCMC_CPU {
 public:
     ColoringMCMC_CPU(Graph<nodeW, edgeW>* g, ColoringMCMCParams params, uint32_t seed)
-        : graph(g), param(params), seed(seed) {}
+        : graph(g), param(params), seed(seed), nCol(params.nCol), epsilon(params.epsilon) {
+        const size_t n = g->getNNodes();
+        gen.seed(seed);
+        std::uniform_int_distribution<uint32_t> unifInitColors(0, nCol - 1);
+        C.resize(n);
+        for (size_t i = 0; i < n; i++) C[i] = unifInitColors(gen);   // coloringMCMC_CPU.cpp:61
+        Cstar.assign(n, 0);
+        p.assign(nCol, 0.0f);
+        q.assign(n, 0.0f);
+        qstar.assign(n, 0.0f);
+        freeColors.assign(nCol, false);
+        Cviols.assign(n, false);
+        Cstarviols.assign(n, false);
+        taboo.assign(n, 0);
+        colorIdx.resize(nCol);
+        std::iota(colorIdx.begin(), colorIdx.end(), (size_t)0);
+    }
     ~ColoringMCMC_CPU() {
         if (ctx) mcmc_destroy(ctx);
     }
@@ -347,8 +392,8 @@ public:
     void run() {
         if (ctx) mcmc_destroy(ctx);
         ctx = nullptr;
-        mcmc_params p = to_params();
-        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &ctx));
+        mcmc_params p_ = to_params();
+        MCMC_CHECK(mcmc_create(graph->handle(), &p_, 0, graph->getNNodes(), &ctx));
         MCMC_CHECK(mcmc_set_glibc_window(ctx, mcmc::glibc_global().w));   // rand(): the process stream
         if (param.tailcutRepair) MCMC_CHECK(mcmc_set_tailcut_repair(ctx, param.tailcutRepair));
         MCMC_CHECK(mcmc_init_coloring(ctx, nullptr));
@@ -367,11 +412,25 @@ public:
     }
 
     // Vertices with a neighbour of their own colour in `currentColoring` (coloringMCMC_CPU.cpp:329-351),
-    // their flags in `violations`; counted on the GPU.
+    // their flags in `violations`; counted on the GPU for a device graph, else on the host.
     size_t violation_count(const std::vector<uint32_t>& currentColoring, std::vector<bool>& violations) {
-        mcmc_params p = to_params();
+        if (!graph->onDevice()) {
+            const GraphStruct<nodeW, edgeW>* str = graph->getStruct();
+            violations.assign(currentColoring.size(), false);
+            size_t count = 0;
+            for (size_t i = 0; i < currentColoring.size(); i++) {
+                for (uint64_t k = str->cumulDegs[i]; k < str->cumulDegs[i + 1]; k++)
+                    if (currentColoring[str->neighs[k]] == currentColoring[i]) {
+                        violations[i] = true;
+                        count++;
+                        break;
+                    }
+            }
+            return count;
+        }
+        mcmc_params p_ = to_params();
         mcmc_ctx* vc = nullptr;
-        MCMC_CHECK(mcmc_create(graph->handle(), &p, 0, graph->getNNodes(), &vc));
+        MCMC_CHECK(mcmc_create(graph->handle(), &p_, 0, graph->getNNodes(), &vc));
         MCMC_CHECK(mcmc_init_coloring(vc, currentColoring.data()));
         uint64_t count = 0;
         std::vector<uint8_t> flags(graph->getNNodes());
@@ -381,8 +440,79 @@ public:
         return (size_t)count;
     }
 
+    // count_free_colors (coloringMCMC_CPU.cpp:362-383): freeColors[c] = no neighbour of `node_` has
+    // colour c in currentColoring; returns how many are free (Zvcomp).
+    size_t count_free_colors(const size_t node_, const std::vector<uint32_t>& currentColoring,
+                             std::vector<bool>& freeCols) {
+        const GraphStruct<nodeW, edgeW>* str = graph->getStruct();
+        std::fill(std::begin(freeCols), std::end(freeCols), true);
+        for (uint64_t k = str->cumulDegs[node_]; k < str->cumulDegs[node_ + 1]; k++) freeCols[currentColoring[str->neighs[k]]] = false;
+        return (size_t)std::count(std::begin(freeCols), std::end(freeCols), true);
+    }
+
+    // fill_p (coloringMCMC_CPU.cpp:393-481, the baseline branch): p from C[currentNode], Cviols and
+    // the member freeColors (count_free_colors(node, C, freeColors) fills it), Zv = occupied colours.
+    void fill_p(const size_t currentNode, const size_t Zv) {
+        const size_t Zvcomp = nCol - Zv;
+        const uint32_t currentColor = C[currentNode];
+        if (Cviols[currentNode]) {
+            const int nFreeColors = std::accumulate(std::begin(freeColors), std::end(freeColors), 0);
+            if (nFreeColors == 0) {
+                for (size_t idx = 0; idx < p.size(); idx++) p[idx] = idx == currentColor ? 1.0f - (nCol - 1) * epsilon : epsilon;
+                return;
+            }
+            for (size_t idx = 0; idx < p.size(); idx++)
+                p[idx] = freeColors[idx] ? (1.0f - epsilon * Zv) / (float)Zvcomp : epsilon;
+        } else {
+            for (size_t idx = 0; idx < p.size(); idx++) p[idx] = colorIdx[idx] == currentColor ? 1.0f - (nCol - 1) * epsilon : epsilon;
+        }
+    }
+
+    // extract_new_color (coloringMCMC_CPU.cpp:493-528): taboo; else the first colour whose fp32 CDF
+    // passes the vertex's draw (strict >), on overflow rand() % (nCol - 1) from the process-global
+    // glibc window; qVect[currentNode] = p of the colour chosen; taboo set when the colour stays.
+    void extract_new_color(const size_t currentNode, const std::vector<float>& pVect,
+                           const std::vector<float>& experimentVect, std::vector<float>& qVect,
+                           std::vector<uint32_t>& newColoring) {
+        if (taboo[currentNode] > 0) {
+            taboo[currentNode]--;
+            newColoring[currentNode] = C[currentNode];
+            qVect[currentNode] = (1.0f - (nCol - 1) * epsilon);
+            return;
+        }
+        const float experimentThrsh = experimentVect[currentNode];
+        float cdf = 0;
+        size_t idx;
+        for (idx = 0; idx < pVect.size(); idx++) {
+            cdf += pVect[idx];
+            if (cdf > experimentThrsh) break;
+        }
+        if (idx >= nCol) {
+            uint32_t r = 0;
+            MCMC_CHECK(mcmc_glibc_draw(mcmc::glibc_global().w, 1, &r));
+            idx = r % (nCol - 1);
+        }
+        qVect[currentNode] = pVect[idx];
+        newColoring[currentNode] = (uint32_t)idx;
+        taboo[currentNode] = (newColoring[currentNode] == C[currentNode]) * param.tabooIteration;
+    }
+
+    // fill_qstar (coloringMCMC_CPU.cpp:532-551): the Hastings term of the new colour, into the member
+    // qstar (as the reference: its qVect argument is not written).
+    void fill_qstar(const size_t currentNode, const size_t Zv, const std::vector<uint32_t>& newColoring,
+                    const std::vector<uint32_t>& oldColoring, const std::vector<bool>& freeCols,
+                    const std::vector<bool>& newColoringViols, std::vector<float>& /*qVect*/) {
+        const size_t Zvcomp = nCol - Zv;
+        const uint32_t currentColor = newColoring[currentNode];
+        if (newColoringViols[currentNode]) {
+            qstar[currentNode] = freeCols[currentColor] ? (1.0f - epsilon * Zv) / (float)Zvcomp : epsilon;
+        } else {
+            qstar[currentNode] = newColoring[currentNode] == oldColoring[currentNode] ? 1.0f - (nCol - 1) * epsilon : epsilon;
+        }
+    }
+
     void saveStats(size_t it, float duration, std::ofstream& outFile) const {
-        const uint32_t nCol = param.nCol;
+        const uint32_t nCol_ = param.nCol;
         outFile << "MCMC Colorer - CPU version - Report" << std::endl;
         outFile << "-------------------------------------------" << std::endl;
         outFile << "GRAPH INFO" << std::endl;
@@ -399,21 +529,21 @@ public:
         outFile << "Max iteration reached: " << (maxIterReached ? "yes" : "no") << std::endl;
         outFile << "-------------------------------------------" << std::endl;
         outFile << "Color histogram:" << std::endl;
-        std::vector<size_t> hist(nCol, 0);
+        std::vector<size_t> hist(nCol_, 0);
         for (uint32_t c : C) hist[c]++;
         size_t used = 0;
-        for (size_t i = 0; i < nCol; i++) {
+        for (size_t i = 0; i < nCol_; i++) {
             outFile << i << ": " << hist[i] << std::endl;
             if (hist[i]) used++;
         }
-        outFile << "Number of colors: " << nCol << " - Used colors: " << used << std::endl;
+        outFile << "Number of colors: " << nCol_ << " - Used colors: " << used << std::endl;
         outFile << "Color ratio: " << param.numColorRatio << std::endl;
         size_t total = 0;
         for (size_t h : hist) total += h;
-        const float mean = (float)(int)total / (float)nCol;   // std::accumulate(..., 0): an int sum
+        const float mean = (float)(int)total / (float)nCol_;   // std::accumulate(..., 0): an int sum
         float var = 0;
         for (size_t h : hist) var += ((h - mean) * (h - mean));
-        var /= (float)nCol;
+        var /= (float)nCol_;
         outFile << "Average number of nodes for each color: " << mean << std::endl;
         outFile << "Variance: " << var << std::endl;
         outFile << "StD: " << std::sqrt(var) << std::endl;
@@ -423,30 +553,47 @@ public:
         for (size_t i = 0; i < C.size(); i++) outfile << i << " " << C[i] << std::endl;
     }
 
+    // the dbg accessors (coloringMCMC_CPU.h:34-51)
     std::vector<uint32_t>* getC() { return &C; }
+    std::vector<uint32_t>* getCstar() { return &Cstar; }
+    std::vector<float>* getp() { return &p; }
+    std::vector<float>* getq() { return &q; }
+    std::vector<float>* getqstar() { return &qstar; }
+    std::vector<bool>* getfreeColors() { return &freeColors; }
+    std::vector<bool>* getCviols() { return &Cviols; }
+    std::vector<bool>* getCstarviols() { return &Cstarviols; }
+    std::vector<uint32_t>* getTaboo() { return &taboo; }
+    uint32_t* getnCol() { return &nCol; }
+    float* getepsilon() { return &epsilon; }
     const mcmc_run_stats& getStats() const { return stats; }
 
 private:
     mcmc_params to_params() const {
-        mcmc_params p{};
-        p.nCol = param.nCol;
-        p.epsilon = param.epsilon;
-        p.lambda = param.lambda;
-        p.ratioFreezed = param.ratioFreezed;
-        p.numColorRatio = param.numColorRatio;
-        p.maxRip = param.maxRip;
-        p.tabooIteration = param.tabooIteration;
-        p.tailcut = param.tailcut;
-        p.seed = seed;
-        return p;
+        mcmc_params p_{};
+        p_.nCol = param.nCol;
+        p_.epsilon = param.epsilon;
+        p_.lambda = param.lambda;
+        p_.ratioFreezed = param.ratioFreezed;
+        p_.numColorRatio = param.numColorRatio;
+        p_.maxRip = param.maxRip;
+        p_.tabooIteration = param.tabooIteration;
+        p_.tailcut = param.tailcut;
+        p_.seed = seed;
+        return p_;
     }
 
     Graph<nodeW, edgeW>* graph;
     ColoringMCMCParams param;
     uint32_t seed;
+    uint32_t nCol;
+    float epsilon;
+    std::default_random_engine gen;
     mcmc_ctx* ctx{nullptr};
     mcmc_run_stats stats{};
-    std::vector<uint32_t> C;
+    std::vector<uint32_t> C, Cstar, taboo;
+    std::vector<float> p, q, qstar;
+    std::vector<bool> freeColors, Cviols, Cstarviols;
+    std::vector<size_t> colorIdx;
     uint32_t iter{0};
     bool maxIterReached{false};
 };

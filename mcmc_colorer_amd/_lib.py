@@ -162,13 +162,58 @@ class MCMCError(RuntimeError):
 _lib = None
 
 
+def _hip_runtimes() -> set:
+    """Paths of the HIP runtimes (libamdhip64) mapped into this process."""
+    try:
+        with open("/proc/self/maps") as f:
+            return {ln.split()[-1] for ln in f if "libamdhip64" in ln and ln.split()[-1].startswith("/")}
+    except OSError:
+        return set()
+
+
+def _process_hip_runtime():
+    """The HIP runtime this process has or will have: one already mapped (torch imported first), else
+    the one torch bundles when torch is installed (it carries its own libamdhip64.so with the soname
+    libamdhip64.so.7 and its own HSA runtime), else None (the library's /opt/rocm runtime)."""
+    mapped = _hip_runtimes()
+    if mapped:
+        return sorted(mapped)[0]
+    import importlib.util
+
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is not None and spec.origin:
+        cand = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+        if cand.exists():
+            return str(cand)
+    return None
+
+
 def lib() -> ctypes.CDLL:
-    """Loads libmcmc_hip.so once. Raises (never falls back) when it is missing."""
+    """Loads libmcmc_hip.so once. Raises (never falls back) when it is missing.
+
+    One HIP runtime per process: the library needs libamdhip64.so.7, which torch's bundled runtime
+    also provides under that soname. Loaded first, the library would bring /opt/rocm's runtime and
+    a later `import torch` its own -- two HSA runtimes, and one of them finds no GPU. So the
+    runtime torch uses is loaded (RTLD_GLOBAL) before the library, which then binds to it; torch,
+    imported later, finds its runtime already mapped. Two runtimes mapped anyway is an error."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
             raise MCMCError(f"{LIB_PATH} not found: build it with `python -m mcmc_colorer_amd.build`")
+        rt = _process_hip_runtime()
+        if rt is not None and os.environ.get("MCMC_OWN_HIP_RUNTIME") != "1":
+            ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+            rccl = Path(rt).parent / "librccl.so"   # (soname librccl.so.1: the library's RCCL too)
+            if rccl.exists():
+                ctypes.CDLL(str(rccl), mode=ctypes.RTLD_GLOBAL)
         L = ctypes.CDLL(str(LIB_PATH))
+        both = _hip_runtimes()
+        if len(both) > 1:
+            raise MCMCError(f"two HIP runtimes in one process ({', '.join(sorted(both))}): load "
+                            f"libmcmc_hip.so after the runtime the process uses (import torch first)")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
