@@ -146,7 +146,7 @@ class MCMCCtxInfo(ctypes.Structure):
         ("ref_bytes", c_uint64),
     ]
 
-    VARIANTS = {0: "lds", 1: "blocked", 2: "global", 3: "tiled", 4: "wide", 5: "ref-wide"}
+    VARIANTS = {0: "lds", 1: "blocked", 2: "global", 3: "tiled", 4: "wide", 5: "ref-wide", 6: "wide-tiled"}
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}

@@ -3164,6 +3164,7 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
 }
 
 #include "sweep_wide.h"
+#include "wide_tiled.h"
 #include "ref_wide.h"
 
 // ----------------------------------------------------------------------------------------------
@@ -3323,6 +3324,7 @@ struct mcmc_ctx {
     uint32_t own_buf_bytes = 0;
     // wide sweep (variant 4: nCol > 256, uint16 colour replicas; sweep_wide.h)
     bool wide = false;
+    bool wide_tiled = false;        // variant 6: nCol > 256 over the tiled layout (wide_tiled.h)
     uint32_t cbytes = 1;            // bytes per colour in the replicas
     uint32_t* chunk_row = nullptr;
     uint32_t nchunks = 0;
@@ -3565,6 +3567,11 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.inc_thresh = c->inc_thresh;
         }
     }
+    if (c->wide_tiled) {
+        a.etab = c->etab;
+        a.walk_tie = c->walk_tie;
+        a.fused = 0;
+    }
     if (c->dc) {
         a.dc_ctl = c->dc_ctl;
         a.dc_list = c->dc_ctl + kDcWords;
@@ -3631,7 +3638,7 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     launch_tiled_or_diag(c, a);
     if (a.fused) return;
     if (c->refwide) refw_commit_kernel<<<1, 1024, 0, c->stream>>>(a);
-    else if (c->wide) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
+    else if (c->wide || c->wide_tiled) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
 }
 
@@ -3986,18 +3993,23 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     const char* gv = getenv("MCMC_GATHER");
     const std::string gsel = gv ? gv : "";
     // REF: a colour may equal nCol (initColoring at u = 1.0f), so uint8 replicas hold nCol <= 255
-    const bool wide = ref ? p->nCol > 255 : (p->nCol > 256 || gsel == "wide");
+    const bool wide = ref ? p->nCol > 255 : (p->nCol > 256 || gsel == "wide" || gsel == "wide-tiled");
+    // nCol > 256 on a generated graph (no CSR): its CSR is built from the tiled layout when it fits
+    // beside it (the wide sweep's slabs and violator walks come from one); otherwise -- C3 at the
+    // reference's default nCol = maxDeg, main.cu:162: 4.0e11 B of ids beside a 2.2e11 B layout --
+    // the wide sweep over the tiled layout itself (wide_tiled.h). MCMC_GATHER=wide-tiled forces that
+    // one, MCMC_GATHER=wide the CSR.
+    bool wide_tiled = wide && !ref && gsel == "wide-tiled";
     if (wide) {
         if (p->nCol > kWideMaxCol) return fail(MCMC_E_ARG, "nCol > 65535 is not supported (uint16 colour replicas)");
-        // the wide sweep scans a CSR (its slab layout and violator walks are built from one): a
-        // generated graph gets its CSR from the tiled layout here, when it fits beside the layout
-        // (the reference's default nCol = maxDeg, main.cu:162, on --simulate graphs); C3 on one
-        // device does not (4.0e11 B of ids + 2.2e11 B of layout > 288 GB) and fails with the sizes
-        if (!gd.row_off) {
+        if (!gd.row_off && !wide_tiled) {
             int mr = mcmc_graph_materialize_csr(const_cast<mcmc_graph*>(g));
-            if (mr) return fail(mr, std::string("nCol > 256 on a generated graph: ") + mcmc_last_error());
+            if (mr == MCMC_E_NOMEM && !ref && gsel != "wide" && v_begin == 0 && v_end == gd.n) wide_tiled = true;
+            else if (mr) return fail(mr, std::string("nCol > 256 on a generated graph: ") + mcmc_last_error());
         }
     }
+    if (wide_tiled && (v_begin != 0 || v_end != gd.n))
+        return fail(MCMC_E_ARG, "the wide tiled sweep: whole-graph contexts only (no partitions)");
     if (ref) {
         if (p->nCol < 2) return fail(MCMC_E_ARG, "reference-GPU mode: nCol >= 2");
         if (v_begin != 0 || v_end != gd.n) return fail(MCMC_E_ARG, "reference-GPU mode: whole-graph contexts");
@@ -4051,7 +4063,13 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
     c->variant = (gsel == "global") ? 2 : (gsel == "blocked") ? 1 : (gsel == "lds") ? 0 : 3;
     if (c->variant == 0 && lds_bytes > kMaxLdsBytes) c->variant = 3;
     if (!gd.row_off || ref) c->variant = 3;   // generated graph / REF: tiled layout only
-    if (wide && ref) {   // REF over the CSR with uint16 replicas (ref_wide.h)
+    if (wide_tiled) {   // the wide sweep over the tiled layout (wide_tiled.h)
+        c->variant = 6;
+        c->wide_tiled = true;
+        c->cbytes = 2;
+        c->fused = 0;
+        c->sweep = launch_wide_tiled;
+    } else if (wide && ref) {   // REF over the CSR with uint16 replicas (ref_wide.h)
         c->variant = 5;
         c->refwide = true;
         c->cbytes = 2;
@@ -4084,7 +4102,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->lds = (size_t)(1u << c->block_log2) + (size_t)c->chunk_rows * c->nw * 4u;
         ea = wi == 0 ? allow_lds_blocked<1>(c->lds) : wi == 1 ? allow_lds_blocked<2>(c->lds)
            : wi == 2 ? allow_lds_blocked<4>(c->lds) : allow_lds_blocked<8>(c->lds);
-    } else if (c->variant == 4 || c->variant == 5) {
+    } else if (c->variant == 4 || c->variant == 5 || c->variant == 6) {
         // geometry and tables below
     } else if (c->variant == 3) {
         const char* bl = getenv("MCMC_BLOCK_LOG2");
@@ -4347,6 +4365,30 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(ea));
         }
+    } else if (c->variant == 6) {
+        // one wave per row over the tiled layout (64 KiB column blocks; a CSR graph's layout is built
+        // here with 1024-row groups, a generated graph's comes with it)
+        c->block_log2 = 16;
+        const char* gr = getenv("MCMC_GROUP_ROWS");
+        const uint32_t R = gr ? (uint32_t)std::max(1, std::min((int)kTileRowsMax, atoi(gr))) : 1024u;
+        int rs = get_tiled_layout(const_cast<mcmc_graph*>(g), v_begin, v_end, R, c->block_log2, c->stream, &c->tl);
+        if (rs) { mcmc_destroy(c); return rs; }
+        c->nblocks = c->tl->nblocks;
+        const uint32_t W = wide_tiled_waves(p->nCol), NWW = (p->nCol + 31u) >> 5;
+        c->block = dim3(64u * W);
+        c->grid = dim3((uint32_t)cus * wide_tiled_wgs_per_cu(p->nCol));
+        c->lds = (size_t)W * (2u * NWW + 1u) * 4u;
+        if (const char* e = getenv("MCMC_WALK_TIE")) c->walk_tie = (uint32_t)strtoul(e, nullptr, 10);
+        std::vector<float> et((size_t)p->nCol + 1);
+        eps_table(p->epsilon, p->nCol, et.data());
+        hipError_t ew = hipFuncSetAttribute((const void*)wide_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)c->lds);
+        if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
+        if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
+        if (ew != hipSuccess) {
+            mcmc_destroy(c);
+            return fail(MCMC_E_HIP, std::string("wide tiled sweep setup: ") + hipGetErrorString(ew));
+        }
     } else if (c->variant == 4) {
         c->grid = dim3((uint32_t)cus);   // launch_wide scales it per kernel
         c->block = dim3(256);
@@ -4492,7 +4534,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         c->block = dim3(256);
         c->grid = dim3((uint32_t)cus * 8u);
     }
-    if (c->variant != 3 && c->variant != 4 && c->variant != 5) {
+    if (c->variant != 3 && c->variant != 4 && c->variant != 5 && c->variant != 6) {
         const uint32_t W = c->variant == 1 ? c->grid.x : c->grid.x * (c->block.x / 64);
         hipError_t ew = hipMalloc(&c->wave_start, sizeof(uint32_t) * (W + 1));
         if (ew != hipSuccess) {
@@ -4582,7 +4624,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
         std::vector<uint8_t> h((size_t)n * c->cbytes);
         for (uint32_t v = 0; v < n; v++) {
-            if (c->wide) reinterpret_cast<uint16_t*>(h.data())[v] = (uint16_t)C0[v];
+            if (c->cbytes == 2) reinterpret_cast<uint16_t*>(h.data())[v] = (uint16_t)C0[v];
             else h[v] = (uint8_t)C0[v];
         }
         int rc = upload_colors(c, c->colors[0], h.data());
@@ -4593,7 +4635,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
         MCMC_HIP_TRY(hipMemcpyAsync(c->st, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
         const UniformIntConst k = uniform_int_const(c->p.nCol);
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255) / 256, 4096u));
-        if (c->wide)
+        if (c->cbytes == 2)
             init_coloring_wide_kernel<<<blocks, 256, 0, c->stream>>>(reinterpret_cast<uint16_t*>(c->colors[0]), n, s0,
                                                                      k, c->st);
         else
@@ -4611,7 +4653,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
             for (uint32_t v = 0; v < n; v++) {
                 uint32_t r;
                 do { x = minstd_mulmod(x, kMinstdA); r = x - 1u; draws++; } while (r >= k.past);
-                if (c->wide) reinterpret_cast<uint16_t*>(hc.data())[v] = (uint16_t)(r / k.scaling);
+                if (c->cbytes == 2) reinterpret_cast<uint16_t*>(hc.data())[v] = (uint16_t)(r / k.scaling);
                 else hc[v] = (uint8_t)(r / k.scaling);
             }
             rc = upload_colors(c, c->colors[0], hc.data());
@@ -5102,7 +5144,7 @@ int mcmc_get_info(mcmc_ctx* c, mcmc_ctx_info* out) {
         i.sub_log2 = c->sub_log2;
         const uint64_t segb = 4ull * tseg_stride(t.grp_rows) * t.ngroups * t.nblocks + 8ull * (t.ngroups + 1);
         i.layout_bytes = 2 * t.ids + segb;
-        i.sweep_bytes = i.layout_bytes + c->n + nloc + taboo + ref_extra;
+        i.sweep_bytes = i.layout_bytes + (uint64_t)c->cbytes * (c->n + nloc) + taboo + ref_extra;
     } else if (c->wide && c->xs) {
         // slab entries + chunk base rows; colour replica read once; per own vertex the flag, the
         // colour read and the colour write (1 + 2 + 2 B)
@@ -5449,7 +5491,7 @@ extern "C" {
 // The replica element size mcmc_create picks for nCol (the wide sweep: uint16).
 uint32_t mcmc_color_bytes(uint32_t nCol) {
     const char* gv = getenv("MCMC_GATHER");
-    return (nCol > 256 || (gv && std::string(gv) == "wide")) ? 2u : 1u;
+    return (nCol > 256 || (gv && (std::string(gv) == "wide" || std::string(gv) == "wide-tiled"))) ? 2u : 1u;
 }
 
 int mcmc_part_plan_rows(uint32_t n, uint32_t world, uint32_t* bounds) {

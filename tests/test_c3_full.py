@@ -162,3 +162,64 @@ def test_c3_full_size_reference_loop_every_vertex(hip_lib):
             assert ds["solo_sweeps"] >= 240, ds
         col.close()
     g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1100)
+def test_c3_default_ncol_maxdeg_sampled_rows(hip_lib):
+    """C3 at the reference's default colour count (`--mcmcgpu --simulate-fast 0.001 -n 10000000
+    --seed 1`: nCol = maxDeg, main.cu:162 -- about 10 400 colours): no CSR fits beside the 2.2e11 B
+    layout, so the wide sweep runs over the layout itself (csrc/wide_tiled.h). C_0 is checked on every
+    vertex; for sweeps 0..2 every one of ~1000 sampled rows (three column blocks) equals the oracle's
+    one-vertex update on its regenerated row, and so do the recount's violation flags; the fused
+    Cviol_t equals the recount of C_t."""
+    import mcmc_colorer_amd.colorer as M
+
+    g = M.Graph.er_fast(N, P, SEED)
+    ncol = M.default_ncol(g, M.ColoringMCMCParams(nCol=0))
+    assert ncol == g.maxDeg > 256
+    rng = np.random.default_rng(77)
+    rows = []
+    for X in (0, 76, (N - 1) // T):
+        lo, hi = X * T, min(N, (X + 1) * T)
+        rows += [lo, lo + 1, hi - 1] + rng.integers(lo, hi, 330).tolist()
+    rows = np.unique(np.array(rows, dtype=np.uint32))
+    t0 = time.perf_counter()
+    ref = O.er_rows(N, P, SEED, rows)
+    print(f"\nnCol = maxDeg = {ncol}; oracle rows: {len(rows)} in {time.perf_counter() - t0:.1f} s", flush=True)
+    col = M.ColoringMCMC(g, M.GPURand(N, SEED, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol))
+    assert col.info()["variant"] == "wide-tiled"
+    col.init(0)
+    C = [col.coloring()]
+    exp0 = np.zeros(N, dtype=np.uint32)
+    k0 = int(O.lib().oracle_uniform_int_seq(SEED, ncol, N, O._p(exp0)))
+    assert np.array_equal(C[0], exp0), "initial colouring"
+    counts, flags, ms = [], [], []
+    for t in range(3):
+        c, f = col.count_violations(flags=True)
+        counts.append(c)
+        flags.append(f[rows])
+        t1 = time.perf_counter()
+        st = col.step(1)
+        ms.append((time.perf_counter() - t1) * 1e3)
+        C.append(col.coloring())
+    assert st.initDraws == k0
+    traj = col.trajectory()
+    print(f"Cviol trajectory {traj.tolist()}, recount {counts}; step wall ms {[round(x, 1) for x in ms]}", flush=True)
+    assert traj.tolist() == counts, "fused Cviol_t != recount of C_t"
+    checked = events = moved = 0
+    for t in range(3):
+        u = O.canonical_at(SEED, k0 + t * N + rows.astype(np.uint64) + 1)
+        for i, v in enumerate(rows.tolist()):
+            c, viol = O.vertex_update(ncol, EPS, int(C[t][v]), C[t][ref[i]], float(u[i]))
+            assert bool(flags[t][i]) == viol, f"violation flag of {v} at sweep {t}"
+            if c is None:
+                events += 1
+            else:
+                assert int(C[t + 1][v]) == c, f"C_{t + 1}[{v}]"
+                checked += 1
+                moved += int(c != int(C[t][v]))
+    print(f"checked {checked} vertex updates ({moved} moved, {events} CDF overflows skipped)", flush=True)
+    assert checked >= 2900 and moved > 500
+    col.close()
+    g.close()

@@ -208,7 +208,7 @@ def M(hip_lib):
     return M
 
 
-def run_both(M, off, idx, ncol, seed=1, **kw):
+def run_both(M, off, idx, ncol, seed=1, variant="wide", **kw):
     g = M.Graph.from_csr(off, idx)
     params = M.ColoringMCMCParams(nCol=ncol, epsilon=kw.get("epsilon", 1e-8), maxRip=kw.get("maxRip", 250),
                                   tabooIteration=kw.get("tabooIteration", 0), tailcut=kw.get("tailcut", False))
@@ -216,7 +216,7 @@ def run_both(M, off, idx, ncol, seed=1, **kw):
     st = col.run(0)
     O.srand(1)   # both glibc streams at srand(1), no draws
     r = O.mcmc_run(off, idx, ncol, seed, **kw)
-    assert col.info()["variant"] == "wide"
+    assert col.info()["variant"] == variant
     assert col.coloring().tolist() == r.colors.tolist()
     assert col.trajectory().tolist() == r.traj.tolist()
     assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws, st.initDraws) == (
@@ -281,6 +281,71 @@ def test_wide_forced_small_ncol(M, monkeypatch, ncol, eps, taboo):
     O.srand(1)
     off, idx = O.setup_rnd2(2000, 0.05)
     run_both(M, off, idx, ncol, epsilon=eps, tabooIteration=taboo, maxRip=60)
+
+
+# The wide sweep over the tiled layout (variant 6, csrc/wide_tiled.h): what a generated graph too
+# large for a CSR beside its layout runs at nCol > 256 (C3 at nCol = maxDeg, tests/test_c3_full.py).
+# MCMC_GATHER=wide-tiled forces it on CSR graphs (the layout is built from the CSR) and on small nCol.
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncol,eps,taboo,tailcut", [(300, 1e-8, 0, False), (1000, 1e-8, 2, False),
+                                                     (700, 1e-3, 0, False), (4000, 1e-8, 0, True),
+                                                     (65535, 1e-8, 0, False)])
+def test_wide_tiled_sparse(M, monkeypatch, ncol, eps, taboo, tailcut):
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    O.srand(1)
+    off, idx = O.setup_rnd2(3000, 0.01)
+    run_both(M, off, idx, ncol, variant="wide-tiled", epsilon=eps, tabooIteration=taboo, tailcut=tailcut)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncol,eps,taboo", [(16, 1e-8, 0), (16, 1e-3, 0), (7, 1e-8, 3), (256, 1e-2, 0)])
+def test_wide_tiled_forced_small_ncol(M, monkeypatch, ncol, eps, taboo):
+    """Every vertex violates (C2-like): the mask walk on every row, CDF overflow events, taboo."""
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    O.srand(1)
+    off, idx = O.setup_rnd2(2000, 0.05)
+    run_both(M, off, idx, ncol, variant="wide-tiled", epsilon=eps, tabooIteration=taboo, maxRip=60)
+
+
+@pytest.mark.gpu
+def test_wide_tiled_dense_default_ncol(M, monkeypatch):
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    O.srand(1)
+    off, idx = O.setup_rnd2(1200, 0.3)
+    run_both(M, off, idx, O.max_deg(off), variant="wide-tiled")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", ["1", "7", "1024"])
+def test_wide_tiled_skewed_degrees(M, monkeypatch, rows):
+    """A hub row of ~4 000 arcs beside empty ones, several group sizes of the layout."""
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    monkeypatch.setenv("MCMC_GROUP_ROWS", rows)
+    off, idx = _hub_graph()
+    run_both(M, off, idx, O.max_deg(off), variant="wide-tiled")
+    run_both(M, off, idx, 300, variant="wide-tiled", maxRip=30)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p,seed", [(4000, 0.1, 7), (70000, 0.01, 3)])
+def test_wide_tiled_generated_graph(M, monkeypatch, n, p, seed):
+    """The build's generated G(n, p) at nCol = maxDeg over its own layout (no CSR at all; the second
+    graph spans two 64 Ki column blocks), against the oracle's run on its restatement of the graph."""
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    off, idx = O.er_fast(n, p, seed)
+    ncol = O.max_deg(off)
+    g = M.Graph.er_fast(n, p, seed)
+    col = M.ColoringMCMC(g, M.GPURand(n, seed, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=12))
+    st = col.run(0)
+    assert col.info()["variant"] == "wide-tiled"
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, seed, maxRip=12)
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, st.finalViol, st.glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+    col.close()
 
 
 def _hub_graph(n=5000):
