@@ -243,6 +243,7 @@ struct SweepArgs {
     const uint2* dl_tab;
     uint32_t dl_n;
     unsigned long long* solo_ts;    // diagnostics (MCMC_SOLO_TRACE): the leader's stamps, [sweep of the launch][8]
+    unsigned long long* wt_tick;    // wide tiled sweep: clock ticks per block step of the last sweep (0: none yet)
     uint32_t nmodN;             // n mod (2^31 - 2): the advance of DevState::lx per sweep
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -3366,6 +3367,7 @@ struct mcmc_ctx {
     uint2* dl_tab = nullptr;
     uint32_t dl_n = 0;
     unsigned long long* solo_ts = nullptr;   // MCMC_SOLO_TRACE diagnostics (4096 x 8 stamps)
+    unsigned long long* wt_tick = nullptr;   // wide tiled sweep's block rotation clock (wide_tiled.h)
 };
 
 namespace {
@@ -3568,6 +3570,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         }
     }
     if (c->wide_tiled) {
+        a.wt_tick = c->wt_tick;
         a.etab = c->etab;
         a.walk_tie = c->walk_tie;
         a.fused = 0;
@@ -4385,6 +4388,11 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
                                             (int)c->lds);
         if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
         if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
+        const char* rot = getenv("MCMC_WT_ROTATE");   // 0: every row scans blocks 0, 1, ... (A/B runs)
+        if (ew == hipSuccess && !(rot && atoi(rot) == 0)) {
+            ew = hipMalloc(&c->wt_tick, sizeof(unsigned long long));
+            if (ew == hipSuccess) ew = hipMemset(c->wt_tick, 0, sizeof(unsigned long long));
+        }
         if (ew != hipSuccess) {
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("wide tiled sweep setup: ") + hipGetErrorString(ew));
@@ -5219,6 +5227,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dc_osum);
     (void)hipFree(c->dl_tab);
     (void)hipFree(c->solo_ts);
+    (void)hipFree(c->wt_tick);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -51,7 +51,13 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     uint32_t* const pre = mask + NWW;
     const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2;
     const uint32_t grp = lane >> 4, gl = lane & 15u;
-    uint32_t wave_viol = 0;
+    uint32_t wave_viol = 0, nrows = 0;
+    // Block rotation: a row's mask is an OR, so its blocks may be scanned in any cyclic order. Each
+    // row starts at the block a common clock points to (one block per tick, the tick measured on
+    // the previous sweep), so all waves gather from a narrow window of colour slices at any time --
+    // one XCD's L2 holds it, where the 2 B x n replica (20 MB at C3) does not fit.
+    const unsigned long long tick = a.wt_tick != nullptr ? *a.wt_tick : 0ull;
+    const unsigned long long t_begin = wall_clock64();
     for (uint32_t l = blockIdx.x * nwv + wave; l < nloc; l += gridDim.x * nwv) {
         const uint32_t v = a.v_begin + l;
         for (uint32_t i = lane; i < NWW; i += 64u) mask[i] = 0u;
@@ -59,10 +65,13 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
         const uint32_t g = l / R, r = l - g * R;
         const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
         uint64_t deg = 0;
+        const uint32_t bs = tick ? (uint32_t)((wall_clock64() / tick) % nb) : 0u;
+        nrows++;
         for (uint32_t b0 = 0; b0 < nb; b0 += 4u) {
-            const uint32_t b = b0 + grp;
+            const uint32_t bi = b0 + grp;
+            const uint32_t b = bi + bs < nb ? bi + bs : bi + bs - nb;
             uint32_t s0 = 0, s1 = 0;
-            if (b < nb) {
+            if (bi < nb) {
                 const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
                 const uint32_t raw = ts[r];
                 s0 = raw & kTsegPos;
@@ -113,6 +122,10 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
         wave_lds_sync();   // the walk's LDS reads are done before the next row clears the mask
     }
     if (lane == 0 && wave_viol) atomicAdd(&sh_viol, wave_viol);
+    if (a.wt_tick != nullptr && blockIdx.x == 0 && threadIdx.x == 0 && nrows > 0) {   // next sweep's tick
+        const unsigned long long d = (wall_clock64() - t_begin) / ((unsigned long long)nrows * nb);
+        *a.wt_tick = d > 0 ? d : 1ull;
+    }
     __syncthreads();
     if (threadIdx.x == 0 && sh_viol) atomicAdd(&st->viol, (unsigned long long)sh_viol);
 }
