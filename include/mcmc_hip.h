@@ -201,6 +201,15 @@ int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]);
  * changed colour, [4] their arcs. Results are the same either way; MCMC_WIDE_INC=0 at mcmc_create
  * turns it off. */
 int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]);
+/* The persistent wide sweep for nearly proper colourings (csrc/wide_solo.h; no reference
+ * counterpart -- the same sweeps as the per-sweep path, bit for bit): [0] 1 if the context runs it
+ * (whole graph, incremental counts, eps > 0, no taboo; MCMC_WIDE_SOLO=0 at mcmc_create: off),
+ * [1] candidate-window states, then cumulative [2] sweeps it ran, [3] phases it handed to the
+ * grid, [4] violators its leader walked, [5] walk phases, [6] count-move phases, [7] violator
+ * collections, [8] candidate rows evaluated, [9] rows that changed colour; diagnostics [10] the
+ * watchdog word (nonzero: a phase never completed, the run failed), [11] / [12] the leader's last
+ * sweep of a launch and its step, [13] the phase flag word. */
+int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[14]);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

@@ -55,6 +55,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_scan_stats_ex": (c_int, [c_void_p, _u64p, _u64p, _u64p]),
     "mcmc_get_scan_stats_v2": (c_int, [c_void_p, _u64p]),
     "mcmc_get_wide_inc_stats": (c_int, [c_void_p, _u64p]),
+    "mcmc_get_wide_solo_stats": (c_int, [c_void_p, _u64p]),
     "mcmc_get_dense_stats": (c_int, [c_void_p, _u64p]),
     "mcmc_get_dense_stats_v2": (c_int, [c_void_p, _u64p]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),

@@ -305,6 +305,17 @@ class ColoringMCMC:
         return {"enabled": bool(out[0]), "incremental_sweeps": int(out[1]), "full_sweeps": int(out[2]),
                 "changed_rows": int(out[3]), "changed_arcs": int(out[4])}
 
+    def wide_solo_stats(self) -> dict:
+        """The persistent wide sweep (mcmc_get_wide_solo_stats; csrc/wide_solo.h): whether the
+        context runs it, its candidate-window states, and cumulative sweeps, phases handed to the
+        grid, violators walked by its leader, walk / count-move / collection phases, candidate rows
+        evaluated and rows that changed colour."""
+        out = (ctypes.c_uint64 * 14)()
+        check(lib().mcmc_get_wide_solo_stats(self._ctx, out))
+        keys = ("enabled", "window_states", "sweeps", "phases", "leader_walks", "walk_phases", "delta_phases",
+                "collects", "candidates", "changed_rows", "watchdog", "dbg_sweep", "dbg_step", "dbg_gen")
+        return {k: int(v) for k, v in zip(keys, out)}
+
     def dense_stats(self) -> dict:
         """The dense-count sweep since the colouring was initialised (mcmc_get_dense_stats; csrc/
         dense_counts.h): whether the context runs it, its dense column range, sweeps whose update moved

@@ -305,8 +305,11 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
                 a.dc_ctl[kDcLen + p] = 0u;
                 sv.st_listed += len;
                 sv.len = 0;
-                while (dc_ld(&a.dc_ctl[kDcMvDone]) < mvexp) __builtin_amdgcn_s_sleep(1);
-                if (a.solo_ts && k < 4096u) a.solo_ts[8u * k + 7u] = wall_clock64();
+            }
+            if (threadIdx.x < 64u) {   // wave 0 waits (a wave-uniform spin loop: see dc_multi_kernel)
+                const uint32_t ex = __builtin_amdgcn_readfirstlane(mvexp);
+                while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcMvDone])) < ex) __builtin_amdgcn_s_sleep(1);
+                if (threadIdx.x == 0 && a.solo_ts && k < 4096u) a.solo_ts[8u * k + 7u] = wall_clock64();
             }
             __syncthreads();
         }
@@ -552,14 +555,16 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
-        } else if (threadIdx.x == 0) {
+        } else if (threadIdx.x < 64u) {
+            // wave 0 polls: a wave-uniform spin loop (a spin loop in one lane beside barriers in the
+            // other waves lets the compiler's structurizer run the rest of the wave ahead of it)
             uint32_t g;
-            while ((g = dc_ld(&a.dc_ctl[kDcGen])) == last) __builtin_amdgcn_s_sleep(4);
+            while ((g = __builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcGen]))) == last) __builtin_amdgcn_s_sleep(4);
             if ((g & 3u) == 1u) {   // a full sweep reads plain data of the last phases: acquire
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            sh_g = g;
+            if (threadIdx.x == 0) sh_g = g;
         }
         __syncthreads();
         const uint32_t g = sh_g;
@@ -575,24 +580,24 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
         const bool mine = dc_full_body<NW>(a, s4, tb, dyn);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) {
-            if (mine) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                atomicAdd(&a.dc_ctl[kDcCommitted], 1u);
-            }
-            if (leader) {   // the sweep is committed (its data released) before the leader plans the next
-                while (dc_ld(&a.dc_ctl[kDcCommitted]) < nfull) __builtin_amdgcn_s_sleep(2);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+        if (threadIdx.x == 0 && mine) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicAdd(&a.dc_ctl[kDcCommitted], 1u);
+        }
+        if (leader && threadIdx.x < 64u) {   // the sweep is committed (its data released) before the leader plans the next
+            const uint32_t nf = __builtin_amdgcn_readfirstlane(nfull);
+            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcCommitted])) < nf) __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
         if (leader) k++;
     }
     if (leader) {
-        if (threadIdx.x == 0) {   // every helper saw the exit: the words are reset for the next launch
-            while (dc_ld(&a.dc_ctl[kDcAck]) < gridDim.x - 1u) __builtin_amdgcn_s_sleep(2);
+        if (threadIdx.x < 64u)   // every helper saw the exit (wave 0 waits, wave-uniform)
+            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcAck])) < gridDim.x - 1u) __builtin_amdgcn_s_sleep(2);
+        if (threadIdx.x == 0) {   // the words are reset for the next launch
             a.dc_ctl[kDcGen] = 0u;
             a.dc_ctl[kDcAck] = 0u;
             a.dc_ctl[kDcCommitted] = 0u;

@@ -3166,6 +3166,7 @@ __global__ void init_coloring_kernel(uint8_t* C, uint32_t n, uint32_t x0, Unifor
 
 #include "sweep_wide.h"
 #include "wide_tiled.h"
+#include "wide_solo.h"
 #include "ref_wide.h"
 
 // ----------------------------------------------------------------------------------------------
@@ -3184,7 +3185,8 @@ void launch_wide(const SweepArgs& a, dim3 g, dim3, size_t, hipStream_t s) {
     }
     else if (a.xs_ent) wide_xscan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
     else wide_scan_kernel<<<g.x * 8u, 256, 0, s>>>(a);
-    wide_eval_kernel<<<a.evnblk + kWalkBlocks, 256, wide_walk_lds(a.nCol), s>>>(a);
+    if (a.dcap) wide_eval_kernel<true><<<a.evnblk + kWalkBlocks, 256, wide_walk_lds(a.nCol), s>>>(a);
+    else wide_eval_kernel<false><<<a.evnblk + kWalkBlocks, 256, wide_walk_lds(a.nCol), s>>>(a);
 }
 // REF wide (ref_wide.h): grid = 8 blocks per CU (g.x = CUs) for the list kernels; masks of nCol bits
 // per violator in LDS (at most 32 KiB per 256-thread block)
@@ -3326,6 +3328,10 @@ struct mcmc_ctx {
     // wide sweep (variant 4: nCol > 256, uint16 colour replicas; sweep_wide.h)
     bool wide = false;
     bool wide_tiled = false;        // variant 6: nCol > 256 over the tiled layout (wide_tiled.h)
+    uint32_t* ws_buf = nullptr;     // the persistent wide sweep's lists and window (wide_solo.h)
+    WsArgs wsa{};                   // (wsa.ctl != nullptr: set up)
+    uint32_t* ws_dbg_host = nullptr; // MCMC_WS_DEBUG: the progress words (host memory, device-mapped)
+    uint32_t ws_grid = 0;
     uint32_t cbytes = 1;            // bytes per colour in the replicas
     uint32_t* chunk_row = nullptr;
     uint32_t nchunks = 0;
@@ -3649,6 +3655,11 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
 // has it (setup_dense_window; MCMC_DENSE_MULTI=0: never) and the arguments allow it (single context,
 // committing in the sweep; no taboo, no tail-cut flags, no diagnostics); else K (sweep, commit) pairs.
 void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
+    if (c->wsa.ctl && !c->part && a.taboo == nullptr && a.vflags == nullptr && a.scan_stats == nullptr &&
+        a.phase_ts == nullptr && a.pair_trace == nullptr && a.inc != nullptr) {
+        if (K) ws_kernel<<<c->ws_grid, 1024, kWsLds, c->stream>>>(a, c->wsa, K);
+        return;
+    }
     if (c->dcm_launch && a.fused == 1 && !c->part && a.taboo == nullptr && a.vflags == nullptr &&
         a.scan_stats == nullptr && a.phase_ts == nullptr && a.pair_trace == nullptr) {
         if (K) c->dcm_launch(a, K, c->grid, c->stream);
@@ -3985,6 +3996,102 @@ int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out) {
 }
 
 // ref != nullptr: a reference-GPU-semantics context (tiled REF sweep) over ref's XORWOW states.
+// The persistent wide sweep (wide_solo.h) for a whole-graph context with incremental counts, eps > 0
+// and no taboo: its lists, and the candidate window sorted by logarithm with a bucket index. The
+// window is [1, w_lo) U [w_hi, 2^31 - 1): the states whose canonical draw is below E[nCol - 1] or
+// at least hi (a case (iii) row keeps its colour exactly outside it). MCMC_WIDE_SOLO=0: off;
+// MCMC_WS_MAX: window states allowed (default 2^24); MCMC_WS_LEAD_ARCS: changed arcs the leader
+// moves itself; MCMC_WS_LIGHT: violator arcs walked on one wave.
+static uint32_t first_state_at_least(float thr) {
+    uint32_t lo = 1, hi = kMinstdM;   // states 1 .. 2^31 - 2; hi = none
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (minstd_canonical(mid) >= thr) hi = mid; else lo = mid + 1u;
+    }
+    return lo;
+}
+static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
+    const char* e = getenv("MCMC_WIDE_SOLO");
+    if ((e && atoi(e) == 0) || !c->inc || c->part || c->v_begin != 0 || c->v_end != c->n || c->p.tabooIteration > 0 ||
+        !(c->p.epsilon > 0.0f) || !c->etab || c->p.nCol < 2)
+        return MCMC_OK;
+    const float hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;
+    if (!(c->emax < hi)) return MCMC_OK;
+    const uint32_t wlo = first_state_at_least(c->emax), whi = first_state_at_least(hi);
+    const uint64_t nw = (uint64_t)(wlo - 1u) + (uint64_t)(kMinstdM - whi);
+    uint64_t wmax = 1ull << 24;
+    if (const char* m = getenv("MCMC_WS_MAX")) wmax = strtoull(m, nullptr, 10);
+    if (nw == 0 || nw > wmax) return MCMC_OK;
+    const size_t nloc = c->v_end - c->v_begin;
+    const size_t words = kWsWords + 2 * nloc + (nloc + 3) / 4 + 2 * nloc + 2 * nloc + (nloc + 1) + nloc + nloc +
+                         2 * nw + (kWsNB + 1);
+    size_t fr = 0, tot = 0;
+    MCMC_HIP_TRY(hipMemGetInfo(&fr, &tot));
+    if (4 * words + 16 * nw + (256ull << 20) > fr) return MCMC_OK;   // (the sort's scratch too)
+    MCMC_HIP_TRY(hipMalloc(&c->ws_buf, 4 * words));
+    uint32_t* b = c->ws_buf;
+    WsArgs& w = c->wsa;
+    w.ctl = b; b += kWsWords;
+    w.vl = b; b += 2 * nloc;
+    w.flag = b; b += (nloc + 3) / 4;
+    w.res = b; b += 2 * nloc;
+    w.chg = b; b += 2 * nloc;
+    w.pre = b; b += nloc + 1;
+    w.tch = b; b += nloc;
+    w.heavy = b; b += nloc;
+    uint32_t* wL = b; b += nw;
+    uint32_t* ww = b; b += nw;
+    uint32_t* boff = b;
+    w.wL = wL;
+    w.ww = ww;
+    w.boff = boff;
+    w.nw = (uint32_t)nw;
+    w.lead_arcs = 4096;
+    if (const char* m = getenv("MCMC_WS_LEAD_ARCS")) w.lead_arcs = (uint32_t)strtoul(m, nullptr, 10);
+    w.light_arcs = 4096;
+    if (const char* m = getenv("MCMC_WS_LIGHT")) w.light_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(m, nullptr, 10));
+    w.sets = std::min<uint32_t>(16u, kWsLds / (4u * walk_set_words(c->p.nCol)));
+    if (getenv("MCMC_WS_DEBUG")) {
+        MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->ws_dbg_host), 4096 * sizeof(uint32_t),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
+        memset(c->ws_dbg_host, 0, 4096 * sizeof(uint32_t));
+        MCMC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&w.dbg), c->ws_dbg_host, 0));
+    }
+    c->ws_grid = cus;
+    // the window: (L, w) pairs, sorted by L, bucketed
+    uint32_t *tk = nullptr, *tv = nullptr, *err = nullptr;
+    void* tmp = nullptr;
+    size_t tb = 0;
+    hipError_t he = hipMalloc(&tk, sizeof(uint32_t) * nw);
+    if (he == hipSuccess) he = hipMalloc(&tv, sizeof(uint32_t) * nw);
+    if (he == hipSuccess) he = hipMalloc(&err, sizeof(uint32_t));
+    if (he == hipSuccess) he = hipMemsetAsync(err, 0, sizeof(uint32_t), c->stream);
+    if (he == hipSuccess) {
+        ws_table_kernel<<<(uint32_t)((nw + 255) / 256), 256, 0, c->stream>>>(tk, tv, wlo, whi, (uint32_t)nw, err);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, tk, wL, tv, ww, (int)nw, 0, 31, c->stream);
+    if (he == hipSuccess) he = hipMalloc(&tmp, std::max<size_t>(tb, 1));
+    if (he == hipSuccess) he = hipcub::DeviceRadixSort::SortPairs(tmp, tb, tk, wL, tv, ww, (int)nw, 0, 31, c->stream);
+    if (he == hipSuccess) {
+        ws_bucket_kernel<<<(kWsNB + 1u + 255u) / 256u, 256, 0, c->stream>>>(wL, (uint32_t)nw, boff);
+        he = hipGetLastError();
+    }
+    if (he == hipSuccess) he = hipMemsetAsync(w.ctl, 0, sizeof(uint32_t) * kWsWords, c->stream);
+    uint32_t herr = 0;
+    if (he == hipSuccess) he = hipMemcpyAsync(&herr, err, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    (void)hipFree(tk);
+    (void)hipFree(tv);
+    (void)hipFree(err);
+    (void)hipFree(tmp);
+    if (he == hipSuccess) he = hipFuncSetAttribute(reinterpret_cast<const void*>(&ws_kernel),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWsLds);
+    if (he != hipSuccess) return fail(MCMC_E_HIP, std::string("persistent wide sweep setup: ") + hipGetErrorString(he));
+    if (herr) return fail(MCMC_E_DEVICE, "persistent wide sweep: a window state's logarithm failed its check");
+    return MCMC_OK;
+}
+
 static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_begin, uint32_t v_end,
                        mcmc_gpurand* ref, mcmc_ctx** out) {
     if (!g || !p || !out) return fail(MCMC_E_ARG, "NULL argument");
@@ -4519,6 +4626,10 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             mcmc_destroy(c);
             return fail(MCMC_E_HIP, std::string("wide sweep setup: ") + hipGetErrorString(ew));
         }
+        if (int rw = setup_wide_solo(c, (uint32_t)cus)) {
+            mcmc_destroy(c);
+            return rw;
+        }
     } else if (c->variant == 5) {
         c->grid = dim3((uint32_t)cus);   // launch_ref_wide scales it per kernel
         c->block = dim3(256);
@@ -4741,6 +4852,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
         rc = run_tailcut(c, h, &s.finalViol, &s.tailcutPasses);
         if (rc) return rc;
         if (c->dc) MCMC_HIP_TRY(dc_reset(c));   // the passes changed colours outside a sweep
+        if (c->inc) MCMC_HIP_TRY(inc_reset(c));
     }
     c->last = s;
     // keep the host copy of the glibc window in step with the device stream
@@ -4826,6 +4938,37 @@ int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
     MCMC_HIP_TRY(hipMemcpy(h, c->inc + kIncStat, sizeof(h), hipMemcpyDeviceToHost));
     out[0] = 1;
     for (int i = 0; i < 4; i++) out[1 + i] = h[i];
+    return MCMC_OK;
+}
+
+// The persistent wide sweep (wide_solo.h): [0] set up, [1] window states, [2] its sweeps, [3] phases
+// posted, [4] violators the leader walked, [5] walk phases, [6] delta phases, [7] violator
+// collections, [8] candidate rows evaluated, [9] changed rows; diagnostics: [10] the watchdog word,
+// [11] / [12] the leader's last sweep of a launch and its step, [13] the phase flag word.
+int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[14]) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    for (int i = 0; i < 14; i++) out[i] = 0;
+    if (!c->wsa.ctl) return MCMC_OK;
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    uint32_t h[kWsWords];
+    MCMC_HIP_TRY(hipMemcpyAsync(h, c->wsa.ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(h + kWsStat);
+    out[0] = 1;
+    out[1] = c->wsa.nw;
+    for (int i = 0; i < 8; i++) out[2 + i] = q[i];
+    out[10] = h[kWsErr];
+    out[11] = h[kWsDbg];
+    out[12] = h[kWsDbg + 1];
+    out[13] = h[kWsGen];
+    return MCMC_OK;
+}
+
+// Diagnostics (MCMC_WS_DEBUG at mcmc_create): the persistent wide sweep's progress words, read from
+// host memory without touching the device (callable while a launch runs).
+int mcmc_ws_debug(mcmc_ctx* c, uint32_t* out, uint32_t n) {
+    if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
+    for (uint32_t i = 0; i < n; i++) out[i] = c->ws_dbg_host && i < 4096 ? __atomic_load_n(&c->ws_dbg_host[i], __ATOMIC_RELAXED) : 0u;
     return MCMC_OK;
 }
 
@@ -5228,6 +5371,8 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dl_tab);
     (void)hipFree(c->solo_ts);
     (void)hipFree(c->wt_tick);
+    (void)hipFree(c->ws_buf);
+    if (c->ws_dbg_host) (void)hipHostFree(c->ws_dbg_host);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);

@@ -692,6 +692,7 @@ __device__ __forceinline__ void wide_delta_one(const SweepArgs& a, uint32_t t, u
 // 256-thread workgroup: word prefix counts, then one wave walks them. cv = C_t[v] and x = u_v's
 // minstd state come in (loaded beside the task's first loads); deg = v's arcs. Overflow events go
 // to the global list. All threads call it; it ends with an LDS barrier.
+template <bool PART>
 __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t cv, uint32_t x, uint32_t deg,
                             uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* wsum,
                             uint32_t* islot, uint32_t* ic) {
@@ -742,7 +743,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
                 if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
             }
             if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
-            if (a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
+            if (PART && a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
             if (event) {
                 const uint32_t idx = atomicAdd(&st->ev_count, 1u);
@@ -776,6 +777,7 @@ __device__ __forceinline__ void walk_gather_wave(const SweepArgs& a, const uint1
 
 // walk_finish for one wave and its own mask set (a light walk): the word prefix counts by the
 // wave's 64 lanes, then the same walk and stores. All 64 lanes call it.
+template <bool PART>
 __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t cv, uint32_t x, uint32_t deg,
                                  uint16_t* __restrict__ Cs, const uint32_t* mask, uint32_t* pre, uint32_t* islot,
                                  uint32_t* ic, uint32_t lane) {
@@ -815,7 +817,7 @@ __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uin
             if (a.fp_live) ((t & 1) ? a.wfp0 : a.wfp1)[v] = (uint8_t)nv;
         }
         if (islot != nullptr && nv != cv) atomicAdd(&ic[1], inc_list_deg(a, l, t, islot, a.inc_wslot_n, &ic[0], deg));
-        if (a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
+        if (PART && a.dcap && nv != cv) wide_delta_one(a, t, v, nv);
         if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
         if (event) {
             const uint32_t idx = atomicAdd(&st->ev_count, 1u);
@@ -854,6 +856,7 @@ __host__ __device__ inline uint32_t walk_waves(uint32_t nCol) {
 // (atomicExch: read and clear for the next sweep) and walks. Software-pipelined: the next task's list
 // entry is loaded beside this task's row offsets, own colour and first gathers, and LDS hand-offs
 // use walk_sync, so a task costs its offsets, ids and colours round trips (~3), not ~7.
+template <bool PART>
 __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t t, uint32_t x_t) {
     // the occupancy mask and its word prefix counts: dynamic LDS sized for nCol (wide_walk_lds), so
     // the evaluation launch's workgroups are not all sized for 65 536 colours
@@ -929,7 +932,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
             walk_gather(a, C, mask, rb, re);
             walk_sync();
             const unsigned long long tt1 = a.phase_ts ? wall_clock64() : 0ull;
-            walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
+            walk_finish<PART>(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
             if (a.phase_ts && threadIdx.x == 0) walk_task_stamp(a, cnt + task, tt0, tt1, re - rb, 1u);
         } else {
             const uint32_t ntk = (uint32_t)((re - rb + SA - 1) / SA);
@@ -955,7 +958,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
                     __threadfence();
                     for (uint32_t w = threadIdx.x; w < NWW; w += blockDim.x) mask[w] = atomicExch(&gm[w], 0u);
                     walk_sync();
-                    walk_finish(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
+                    walk_finish<PART>(a, v, t, cv, x, (uint32_t)(re - rb), Cs, mask, pre, wsum, islot, ic);
                 }
                 if (a.phase_ts && threadIdx.x == 0) walk_task_stamp(a, cnt + task, tt0, tt1, re - rb, sh_last ? 3u : 2u);
                 walk_sync();   // sh_last and mask are reused by the next task
@@ -989,7 +992,7 @@ __device__ void walk_tasks(const SweepArgs& a, uint32_t b, uint32_t nb, uint32_t
             walk_gather_wave(a, C, wm, rb, re, lane);
             wave_lds_sync();
             const unsigned long long tt1 = a.phase_ts ? wall_clock64() : 0ull;
-            walk_finish_wave(a, lv, t, cv, x, (uint32_t)(re - rb), Cs, wm, wp, islot, ic, lane);
+            walk_finish_wave<PART>(a, lv, t, cv, x, (uint32_t)(re - rb), Cs, wm, wp, islot, ic, lane);
             if (a.phase_ts && lane == 0) walk_task_stamp(a, k, tt0, tt1, re - rb, 0u);
             nlight++;
             lv = nv;
@@ -1022,6 +1025,9 @@ inline size_t wide_walk_lds(uint32_t nCol) { return 4u * (size_t)walk_waves(nCol
 // Grid: kWalkBlocks walk workgroups (walk_tasks; first, so that they start at once), then evnblk =
 // ceil(nloc / (256 * kWideEvalPer)) evaluation workgroups of 256; lane `tid` of evaluation
 // workgroup eb takes the vertices eb * 2048 + j * 256 + tid, j < 8 (coalesced per j).
+// PART: a partitioned rank's sweep (the delta exchange's slot writes, a.dcap); the single-context
+// instantiation carries none of that code.
+template <bool PART>
 __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol, sh_nev;
     __shared__ uint32_t sh_ev[kEvSlot];   // this workgroup's overflow events (ordered at the end)
@@ -1029,7 +1035,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     if (blockIdx.x < kWalkBlocks) {   // the walks, beside the evaluation (dispatched first)
-        walk_tasks(a, blockIdx.x, kWalkBlocks, st->t, st->x_t);
+        walk_tasks<PART>(a, blockIdx.x, kWalkBlocks, st->t, st->x_t);
         return;
     }
     const uint32_t eb = blockIdx.x - kWalkBlocks;   // evaluation workgroup
@@ -1134,7 +1140,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
                 dnv = nv;
             }
         }
-        if (a.dcap) {   // partitioned delta exchange: one slot atomic per wave
+        if (PART && a.dcap) {   // partitioned delta exchange: one slot atomic per wave
             const uint64_t db = __ballot(dch);
             if (db) {
                 uint32_t* dl = (t & 1) ? a.dlt0 : a.dlt1;

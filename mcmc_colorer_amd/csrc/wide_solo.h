@@ -1,0 +1,867 @@
+// mcmc_colorer_amd/csrc/wide_solo.h -- the persistent wide sweep (ws_kernel): nCol > 256 once the
+// colouring is nearly proper. Included by mcmc_sweep.hip inside namespace mcmc, after sweep_wide.h.
+//
+// The per-sweep wide launches (sweep_wide.h) evaluate all n rows every sweep, so a converged sweep
+// at C5 (4.2e6 rows, ~1 200 of them changing) costs four launches and ~60 us of fixed work. Which
+// rows can change is known before any row is read, as for the dense sweep (dense_sparse.h):
+//   * a violator (its count of same-coloured neighbours is > 0) resamples from its occupancy mask
+//     (fill_p cases (ii)/(i), coloringMCMC_CPU.cpp:414-420, 402-412);
+//   * any other row is in case (iii) (own colour hi, others eps): it keeps its colour exactly when
+//     its draw u_v lies in [E[nCol-1], hi) (sweep_wide.h wide_eval_kernel's range test), i.e. when
+//     its minstd state lies outside the window W = [1, w_lo) U [w_hi, 2^31 - 1) -- C5 (eps 1e-8,
+//     nCol 29 438): 1.26e6 of the 2^31 - 2 states. Vertex v draws state 16807^(lx_t + v + 1) in
+//     sweep t (lx_t = log x_t), so the window's states sorted by logarithm L hand out sweep t's
+//     candidate rows as the entries with L in [lx_t + 1, lx_t + 1 + n) mod (2^31 - 2): one or two
+//     contiguous runs of the table (a bucket index finds them), ~n |W| / 2^31 rows (C5: ~2 500).
+// The counts (SweepArgs::inc_vcnt, the incremental counts of sweep_wide.h) are kept exact across
+// sweeps: each changed row moves both ends of its arcs by [C_t+1 equal] - [C_t equal]. So a sweep
+// reads the candidates, the violators and the changed rows' arcs -- nothing else.
+//
+// One launch runs K sweeps, one 1024-thread workgroup per CU. Workgroup 0 (the leader) runs each
+// sweep: loop control (:136, :259-269; Cviol_t = the violator list's length), its own small walks
+// and the candidates' own-colour walks, the overflow events' glibc draws in ascending vertex order
+// (:517-520) and the changed rows' writes (into BOTH colour buffers, which stay equal), and hands
+// the grid-sized parts to the other workgroups as phases (posted through a flag word, completion
+// counted on another): many violators' walks (a wave each, workgroups for heavy rows), count moves
+// of many changed arcs, a full violator collection, the recount of a new colouring. Results come
+// back through device-scope atomics and plain stores bracketed by release/acquire (the dense
+// sweep's hand-off rules, dense_sparse.h).
+// Entry from the per-sweep launches: a full recount pending (kIncMode) is run here; a pending
+// change list of the last per-sweep commit is applied; the violator list is collected unless the
+// last persistent launch left it valid for this t. Exit: the per-sweep path's next flag pass visits
+// every row (kIncTchOvf) and its delta lists are empty -- both paths may alternate freely.
+
+constexpr uint32_t kWsGen = 0, kWsDone = 1, kWsAck = 2, kWsT = 3;
+constexpr uint32_t kWsVn = 4;        // [2] violator-list lengths, by parity of t
+constexpr uint32_t kWsResN = 6;      // results of the running sweep
+constexpr uint32_t kWsTchN = 7, kWsTchOvf = 8;
+constexpr uint32_t kWsHeavyN = 9, kWsChgN = 10, kWsArgT = 11, kWsArgP = 12;
+constexpr uint32_t kWsStat = 16;     // u64 [8]: solo sweeps, phases, leader walks, walk phases,
+                                     // delta phases, collects, candidates, changed rows
+constexpr uint32_t kWsErr = 32;      // watchdog: (phase sequence << 8) | where (a wait that never completed)
+constexpr uint32_t kWsDbg = 33;      // [2] the leader's sweep of the launch and its step (diagnostics)
+constexpr uint32_t kWsWords = 48;
+// Watchdogs (wall clock, 100 MHz): a leader wait or an acknowledgement pending this long flags
+// DevState::err and ends the launch instead of spinning forever; an idle helper leaves after kWsIdle.
+constexpr unsigned long long kWsWaitTicks = 200000000ull;    // 2 s
+constexpr unsigned long long kWsIdleTicks = 1000000000ull;   // 10 s
+constexpr uint32_t kWsBShift = 16;   // window buckets: L >> 16
+constexpr uint32_t kWsNB = ((kMinstdN - 1u) >> kWsBShift) + 1u;
+constexpr uint32_t kWsCandCap = 4096;      // candidate rows per round (leader LDS)
+constexpr uint32_t kWsEvLds = 8192;        // overflow events sorted in LDS (more: in global memory)
+constexpr uint32_t kWsLeadSets = 4;        // the leader's walk mask sets (violators it walks itself)
+constexpr uint32_t kWsLeadList = 16384;    // violator-list updates the leader does itself
+constexpr uint32_t kWsPreLds = 16384;      // delta phase: changed rows whose arc prefix sits in LDS
+constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
+enum : uint32_t { kWsRecount = 1, kWsExit = 2, kWsDelta = 3, kWsWalkLight = 4, kWsWalkHeavy = 5, kWsCopy = 6,
+                  kWsCollect = 7, kWsPending = 8, kWsZero = 9 };
+
+struct WsArgs {
+    uint32_t* ctl;
+    uint32_t* vl;          // [2][nloc] violator lists (parity of t)
+    uint32_t* flag;        // [nloc] bytes: row in the current violator list
+    uint32_t* res;         // [2 nloc] the sweep's results (l, cv | nc << 16; nc = nCol: an overflow)
+    uint32_t* chg;         // [2 nloc] its changed rows (l, cov | cnv << 16)
+    uint32_t* pre;         // [nloc + 1] their arcs' exclusive prefix
+    uint32_t* tch;         // [nloc] rows whose count left 0
+    uint32_t* heavy;       // [nloc] violators walked by a workgroup; then the events' drawn colours (by row)
+    const uint32_t* wL;    // window logarithms, ascending
+    const uint32_t* ww;    // the window states, same order
+    const uint32_t* boff;  // [kWsNB + 1] first entry of each bucket
+    uint32_t nw;           // window states
+    uint32_t lead_arcs;    // changed arcs the leader moves itself (more: a delta phase)
+    uint32_t light_arcs;   // violators of at most this many arcs walk on one wave
+    uint32_t sets;         // wave mask sets per workgroup
+    uint32_t* dbg;         // diagnostics (MCMC_WS_DEBUG): host-visible progress words, or nullptr
+};
+// Progress words in host memory (MCMC_WS_DEBUG): readable while a launch runs.
+__device__ __forceinline__ void ws_dbg(const WsArgs& w, uint32_t i, uint32_t v) {
+    if (w.dbg != nullptr) __hip_atomic_store(&w.dbg[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// w[i] = the i-th state of the window [1, lo) U [hi, 2^31 - 1), L[i] = its logarithm; err |= 1 if a
+// logarithm fails its check 16807^L = w.
+__global__ __launch_bounds__(256) void ws_table_kernel(uint32_t* __restrict__ L, uint32_t* __restrict__ w, uint32_t lo,
+                                                       uint32_t hi, uint32_t nw, uint32_t* __restrict__ err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nw) return;
+    const uint32_t s = i < lo - 1u ? 1u + i : hi + (i - (lo - 1u));
+    const uint32_t l = minstd_dlog(s);
+    if (l == 0xFFFFFFFFu || minstd_pow(kMinstdA, l) != s) atomicOr(err, 1u);
+    L[i] = l;
+    w[i] = s;
+}
+// boff[b] = first i with L[i] >= b << kWsBShift (b <= kWsNB)
+__global__ __launch_bounds__(256) void ws_bucket_kernel(const uint32_t* __restrict__ L, uint32_t nw,
+                                                        uint32_t* __restrict__ boff) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > kWsNB) return;
+    const uint64_t key = (uint64_t)b << kWsBShift;
+    uint32_t lo = 0, hi = nw;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)L[mid] < key) lo = mid + 1u; else hi = mid;
+    }
+    boff[b] = lo;
+}
+
+// Prefix counts of a mask (one wave: word runs per lane) and the walk of fill_p case (ii) / (i) --
+// walk_finish_wave's selection without its writes. All 64 lanes call it; returns the new colour or
+// nCol (an overflow), the same on every lane.
+__device__ __forceinline__ uint32_t ws_mask_walk(const SweepArgs& a, const uint32_t* mask, uint32_t* pre, uint32_t cv,
+                                                 float u, uint32_t lane) {
+    const uint32_t NWW = (a.nCol + 31u) >> 5, per = (NWW + 63u) >> 6, w0 = lane * per;
+    uint32_t s = 0;
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) s += __popc(mask[w]);
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    uint32_t run = inc - s;
+    for (uint32_t w = w0; w < w0 + per && w < NWW; w++) {
+        pre[w] = run;
+        run += __popc(mask[w]);
+    }
+    if (lane == 63u) pre[NWW] = inc;
+    wave_lds_sync();
+    const uint32_t P = pre[NWW], Zvcomp = a.nCol - P;
+    uint32_t nc;
+    if (Zvcomp > 0) {   // case (ii)
+        const float pf = (1.0f - a.eps * (float)P) / (float)Zvcomp;
+        nc = walk_mask_pre(mask, pre, a.nCol, a.eps, pf, u, a.walk_tie != 0u);
+    } else {            // case (i)
+        nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+    }
+    wave_lds_sync();
+    return __builtin_amdgcn_readfirstlane(nc);
+}
+
+// A result (lane's row l: colour cv -> nc), wave-aggregated into the global list.
+__device__ __forceinline__ void ws_push(const WsArgs& w, bool want, uint32_t l, uint32_t cv, uint32_t nc, uint32_t lane) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const int lead = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == lead) base = atomicAdd(&w.ctl[kWsResN], (uint32_t)__popcll(m));
+    base = __shfl(base, lead, 64);
+    if (want) {
+        const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        w.res[2u * j] = l;
+        w.res[2u * j + 1u] = cv | (nc << 16);
+    }
+}
+__device__ __forceinline__ void ws_touch(const SweepArgs& a, const WsArgs& w, uint32_t l) {
+    const uint32_t idx = atomicAdd(&w.ctl[kWsTchN], 1u);
+    if (idx < a.v_end - a.v_begin) w.tch[idx] = l;
+    else atomicOr(&w.ctl[kWsTchOvf], 1u);
+}
+
+// One light violator on one wave: its occupancy mask in the wave's set, its walk, the result.
+__device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ C,
+                                              uint32_t x_t, uint32_t l, uint32_t* mask, uint32_t lane) {
+    const uint32_t NWW = (a.nCol + 31u) >> 5;
+    uint32_t* pre = mask + ((NWW + 3u) & ~3u);
+    const uint32_t cv = C[l];
+    const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)l + 1ull));   // u_v (:139)
+    for (uint32_t i = lane; i < NWW; i += 64u) mask[i] = 0u;
+    wave_lds_sync();
+    walk_gather_wave(a, C, mask, a.row_off[l], a.row_off[l + 1], lane);
+    wave_lds_sync();
+    const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
+    if (lane == 0 && nc != cv) {
+        const uint32_t j = atomicAdd(&w.ctl[kWsResN], 1u);
+        w.res[2u * j] = l;
+        w.res[2u * j + 1u] = cv | (nc << 16);
+    }
+}
+// One heavy violator on the whole workgroup (mask set 0); all threads call it.
+__device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ C,
+                                              uint32_t x_t, uint32_t l, uint32_t* mask) {
+    const uint32_t NWW = (a.nCol + 31u) >> 5, lane = threadIdx.x & 63u;
+    uint32_t* pre = mask + ((NWW + 3u) & ~3u);
+    for (uint32_t i = threadIdx.x; i < NWW; i += blockDim.x) mask[i] = 0u;
+    __syncthreads();
+    walk_gather(a, C, mask, a.row_off[l], a.row_off[l + 1]);
+    __syncthreads();
+    if (threadIdx.x < 64u) {
+        const uint32_t cv = C[l];
+        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)l + 1ull));
+        const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
+        if (lane == 0 && nc != cv) {
+            const uint32_t j = atomicAdd(&w.ctl[kWsResN], 1u);
+            w.res[2u * j] = l;
+            w.res[2u * j + 1u] = cv | (nc << 16);
+        }
+    }
+    __syncthreads();
+}
+
+// Arcs [k, k1) (step) of the flattened changed-row arcs: both ends' counts move by [Cn equal] -
+// [Cp equal] (an arc whose other end changed too only from the smaller end; self-arcs never move).
+// pre: the prefix (LDS or global), nch changed rows.
+__device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ Cp,
+                                              const uint16_t* __restrict__ Cn, const uint32_t* pre, uint32_t nch,
+                                              uint32_t k, uint32_t k1, uint32_t step) {
+    const uint32_t nloc = a.v_end - a.v_begin;
+    for (; k < k1; k += step) {
+        uint32_t lo = 0, hi = nch;   // the changed row i with pre[i] <= k < pre[i + 1]
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= k) lo = mid; else hi = mid;
+        }
+        const uint32_t v = w.chg[2u * lo], ab = w.chg[2u * lo + 1u];
+        const uint32_t cov = ab & 0xFFFFu, cnv = ab >> 16;
+        const uint32_t u = a.col_idx[a.row_off[v] + (k - pre[lo])];
+        if (u == v) continue;
+        const uint32_t ou = Cp[u], nu = Cn[u];
+        if (ou != nu && u < v) continue;
+        const int d = (int)(nu == cnv) - (int)(ou == cov);
+        if (d == 0) continue;
+        if (u < nloc) {
+            const uint32_t old = atomicAdd(&a.inc_vcnt[u], (uint32_t)d);
+            if (d > 0 && old == 0u) ws_touch(a, w, u);
+        }
+        const uint32_t old = atomicAdd(&a.inc_vcnt[v], (uint32_t)d);
+        if (d > 0 && old == 0u) ws_touch(a, w, v);
+    }
+}
+
+// ---- helper phases (workgroups 1..G-1; h = blockIdx.x - 1 of H) ---------------------------------
+__device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uint32_t kind, uint32_t* dyn) {
+    const uint32_t H = gridDim.x - 1u, h = blockIdx.x - 1u, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t gt = h * blockDim.x + threadIdx.x, GT = H * blockDim.x;
+    const uint32_t nloc = a.v_end - a.v_begin;
+    const uint32_t t = w.ctl[kWsArgT], P = w.ctl[kWsArgP];
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);   // C_t
+    uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
+    if (kind == kWsZero) {   // counts to zero (a recount follows)
+        for (uint32_t l = gt; l < nloc; l += GT) a.inc_vcnt[l] = 0u;
+    } else if (kind == kWsCopy) {   // the other buffer = C_t (whole replica, 16 B at a time)
+        const uint32_t n4 = (a.n * 2u + 15u) / 16u;
+        const uint4* s = reinterpret_cast<const uint4*>(C);
+        uint4* d = reinterpret_cast<uint4*>(Cs);
+        for (uint32_t i = gt; i < n4; i += GT) d[i] = s[i];
+    } else if (kind == kWsRecount) {   // every arc (r, u) with C_t[u] = C_t[r]: count of r (violation_count, :329-351)
+        const uint64_t* __restrict__ ro = a.row_off;
+        const uint64_t a0 = a.arc_begin, m = a.arc_count;
+        const uint32_t gw = gt >> 6, nwv = GT >> 6;
+        for (uint32_t ch = gw; ch < a.nchunks; ch += nwv) {
+            const uint64_t k0 = (uint64_t)ch * kWideChunk + 4u * lane;
+            if (k0 >= m) continue;
+            const uint4 q = *reinterpret_cast<const uint4*>(a.col_idx + a0 + k0);
+            uint32_t id[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 1; i < 4; i++)
+                if (k0 + i >= m) id[i] = 0u;
+            uint32_t nc[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) nc[i] = C[id[i]];
+            uint32_t lo = a.chunk_row[ch], hi = a.chunk_row[ch + 1];
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1u) >> 1;
+                if (ro[mid] - a0 <= k0) lo = mid; else hi = mid - 1u;
+            }
+            uint32_t r = lo;
+            uint64_t rend = ro[r + 1] - a0;
+            uint32_t own = C[r];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint64_t k = k0 + i;
+                if (k >= m) break;
+                if (rend <= k) {
+                    do { r++; rend = ro[r + 1] - a0; } while (rend <= k);
+                    own = C[r];
+                }
+                if (nc[i] == own) atomicAdd(&a.inc_vcnt[r], 1u);
+            }
+        }
+    } else if (kind == kWsCollect) {   // the violator list P and the flags, from the counts
+        for (uint32_t q0 = gt & ~63u; q0 * 4u < nloc; q0 += GT) {
+            const uint32_t q = q0 + lane, l0 = 4u * q;
+            uint32_t f = 0, fl[4] = {0, 0, 0, 0};
+            if (l0 < nloc) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    fl[i] = (l0 + i < nloc && a.inc_vcnt[l0 + i] > 0u) ? 1u : 0u;
+                    f |= fl[i] << (8 * i);
+                }
+                w.flag[q] = f;
+            }
+            const uint32_t cnt = __popc(f);
+            uint32_t inc = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            uint32_t base = 0;
+            const uint32_t tot = __shfl(inc, 63, 64);
+            if (lane == 63u && tot) base = atomicAdd(&w.ctl[kWsVn + P], tot);
+            base = __shfl(base, 63, 64) + inc - cnt;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (fl[i]) w.vl[(size_t)P * nloc + base++] = l0 + i;
+        }
+    } else if (kind == kWsWalkLight) {   // violator list P: light rows a wave each, heavy ones listed
+        const uint32_t Vn = w.ctl[kWsVn + P];
+        const uint32_t* vl = w.vl + (size_t)P * nloc;
+        if (wv < w.sets) {
+            uint32_t* mask = dyn + wv * walk_set_words(a.nCol);
+            for (uint32_t i = h * w.sets + wv; i < Vn; i += H * w.sets) {
+                const uint32_t l = vl[i];
+                const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
+                if (deg > w.light_arcs) {
+                    if (lane == 0) w.heavy[atomicAdd(&w.ctl[kWsHeavyN], 1u)] = l;
+                    continue;
+                }
+                ws_walk_light(a, w, C, w.ctl[kWsArgP + 1], l, mask, lane);
+            }
+        }
+    } else if (kind == kWsWalkHeavy) {
+        const uint32_t hn = w.ctl[kWsHeavyN];
+        for (uint32_t j = h; j < hn; j += H) ws_walk_heavy(a, w, C, w.ctl[kWsArgP + 1], w.heavy[j], dyn);
+    } else if (kind == kWsDelta) {   // the changed rows' arcs (prefix cached in LDS where it fits)
+        const uint32_t nch = w.ctl[kWsChgN];
+        const uint32_t* pre = w.pre;
+        if (nch + 1u <= kWsPreLds) {
+            for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) dyn[i] = w.pre[i];
+            __syncthreads();
+            pre = dyn;
+        }
+        ws_delta_arcs(a, w, C, Cs, pre, nch, gt, pre[nch], GT);
+    } else if (kind == kWsPending) {   // the last per-sweep commit's changed rows: C_t-1 (buffer of t-1) -> C_t
+        const uint32_t p = t & 1u;
+        const uint16_t* Cp = Cs;   // the buffer of C_t-1 (sweep t writes it next)
+        const uint32_t nd = a.inc[kIncDenseN + p], nh = a.inc[kIncHubN + p];
+        for (uint32_t i = h; i < nh; i += H) {   // hubs: a workgroup each
+            const uint32_t v = a.inc_hub[(size_t)p * a.inc_lcap + i];
+            int dv = inc_arcs(a, Cp, C, v, Cp[v], C[v], a.row_off_g[v] + threadIdx.x, a.row_off_g[v + 1], blockDim.x, t);
+            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+            if (lane == 0 && dv != 0) {
+                const uint32_t old = atomicAdd(&a.inc_vcnt[v], (uint32_t)dv);
+                (void)old;
+            }
+        }
+        const uint32_t gw = gt >> 6, nwv = GT >> 6;
+        const uint32_t* dn = a.inc_dense + (size_t)p * a.inc_lcap;
+        for (uint32_t i = gw; i < nd; i += nwv) {   // other rows: a wave each
+            const uint32_t v = dn[i];
+            int dv = inc_arcs(a, Cp, C, v, Cp[v], C[v], a.row_off_g[v] + lane, a.row_off_g[v + 1], 64u, t);
+            for (int o = 32; o > 0; o >>= 1) dv += __shfl_xor(dv, o, 64);
+            if (lane == 0 && dv != 0) atomicAdd(&a.inc_vcnt[v], (uint32_t)dv);
+        }
+    }
+}
+
+// The leader's loop state (LDS).
+struct WsState {
+    uint32_t t, x_t, lx, done, err, nres;
+    uint32_t ring[31];
+    unsigned long long draws;
+    unsigned long long st[8];
+    unsigned long long arcs;        // the changed rows' arcs (the incremental statistics)
+    uint32_t recounts;
+};
+
+// Exclusive scan of one value per thread over the workgroup; *tot = the sum. All threads call it.
+__device__ __forceinline__ uint32_t ws_scan(uint32_t v, uint32_t* wsum, uint32_t* tot) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t off = 0, s = 0;
+    for (uint32_t k = 0; k < nwv; k++) {
+        if (k < wv) off += wsum[k];
+        s += wsum[k];
+    }
+    *tot = s;
+    __syncthreads();
+    return off + inc - v;
+}
+
+__global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_t K) {
+    extern __shared__ uint4 ws_lds[];
+    uint32_t* const dyn = reinterpret_cast<uint32_t*>(ws_lds);
+    __shared__ uint32_t sh_g;
+    DevState* __restrict__ st = a.st;
+    const uint32_t nloc = a.v_end - a.v_begin, G = gridDim.x;
+    if (blockIdx.x != 0) {   // helpers: phases until the exit post
+        uint32_t last = 0;
+        for (;;) {
+            // the whole of wave 0 polls (a wave-uniform loop: a spin loop in one lane beside barriers
+            // in the others lets the compiler's structurizer run the other lanes of the wave ahead)
+            if (threadIdx.x < 64u) {
+                uint32_t g;
+                const unsigned long long t0 = wall_clock64();
+                for (;;) {
+                    g = __builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsGen]));
+                    if (g != last) break;
+                    if (wall_clock64() - t0 > kWsIdleTicks) { g = kWsExit; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (threadIdx.x == 0) sh_g = g;
+            }
+            __syncthreads();
+            const uint32_t g = sh_g;
+            last = g;
+            __syncthreads();
+            if ((g & 15u) == kWsExit) break;
+            if (threadIdx.x == 0) ws_dbg(w, 64u + blockIdx.x, (g << 4) | 1u);
+            ws_help(a, w, g & 15u, dyn);
+            if (threadIdx.x == 0) ws_dbg(w, 64u + blockIdx.x, (g << 4) | 2u);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                atomicAdd(&w.ctl[kWsDone], 1u);
+            }
+        }
+        if (threadIdx.x == 0) atomicAdd(&w.ctl[kWsAck], 1u);
+        return;
+    }
+    // ---- the leader ----
+    __shared__ WsState s;
+    __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_wsum[16], s_heavy[kWsLeadSets], s_nh, s_vq, s_w[4];
+    uint32_t* const cand = dyn;                              // [2 kWsCandCap]
+    uint32_t* const evl = dyn + 2u * kWsCandCap;             // [kWsEvLds]
+    uint32_t* const sets = evl + kWsEvLds;                   // kWsLeadSets mask sets
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    // a phase for the helpers: every wave's stores drained, release, the flag; then wait for all
+    auto post = [&](uint32_t kind) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0 && (s.err == 0u || kind == kWsExit)) {
+            s_seq++;
+            s_exp += G - 1u;
+            s.st[1]++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&w.ctl[kWsGen], (s_seq << 4) | kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    };
+    auto wait = [&]() {   // wave 0 waits (a wave-uniform loop, as the helpers poll)
+        if (threadIdx.x < 64u && __builtin_amdgcn_readfirstlane(s.err) == 0u) {
+            const unsigned long long t0 = wall_clock64();
+            const uint32_t ex = __builtin_amdgcn_readfirstlane(s_exp);
+            for (;;) {
+                const uint32_t d = __builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsDone]));
+                if (d >= ex) break;
+                if (w.dbg != nullptr && threadIdx.x == 0) {
+                    ws_dbg(w, 3, d);
+                    ws_dbg(w, 4, ex);
+                }
+                if (wall_clock64() - t0 > kWsWaitTicks) {   // a phase that never completed: flag and leave
+                    if (threadIdx.x == 0) {
+                        w.ctl[kWsErr] = (s_seq << 8) | 1u;
+                        st->err |= 1u;
+                        s.err = 1u;
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    };
+    auto mark = [&](uint32_t k, uint32_t step) {
+        if (threadIdx.x == 0) {
+            w.ctl[kWsDbg] = k;
+            w.ctl[kWsDbg + 1] = step;
+            ws_dbg(w, 0, k);
+            ws_dbg(w, 1, step);
+            ws_dbg(w, 2, s_seq);
+        }
+    };
+    if (threadIdx.x == 0) {   // take over the loop state
+        const uint32_t head = st->glibc_head;
+        s.t = st->t;
+        s.done = st->done;
+        s.err = st->err;
+        s.x_t = st->x_t;
+        s.lx = st->lx;
+        for (uint32_t i = 0; i < 31u; i++) s.ring[i] = st->glibc_ring[(head + i) % 31u];
+        s.draws = st->glibc_draws;
+        for (int i = 0; i < 8; i++) s.st[i] = 0;
+        s.arcs = 0;
+        s.recounts = 0;
+        s_seq = 0;
+        s_exp = 0;
+    }
+    __syncthreads();
+    const bool go = !(s.done || s.err);
+    mark(0xFFFFu, 100u);
+    if (go) {
+        const uint32_t t = s.t, p = t & 1u;
+        if (threadIdx.x == 0) {
+            s_w[0] = a.inc[kIncMode];
+            s_w[1] = a.inc[kIncDenseN + p] + a.inc[kIncHubN + p];
+            s_w[2] = w.ctl[kWsT] == t + 1u ? 1u : 0u;
+            w.ctl[kWsArgT] = t;
+            w.ctl[kWsArgP + 1] = s.x_t;
+        }
+        __syncthreads();
+        const uint32_t mode = s_w[0], pend = s_w[1];
+        bool valid = s_w[2] != 0u;
+        __syncthreads();
+        mark(0xFFFFu, 101u + (mode ? 10u : 0u) + (pend ? 20u : 0u) + (valid ? 40u : 0u));
+        if (mode) {   // a new colouring: recount (both buffers = C_t first)
+            post(kWsZero);
+            wait();
+            post(kWsCopy);
+            wait();
+            post(kWsRecount);
+            wait();
+            valid = false;
+            if (threadIdx.x == 0) s.recounts = 1;
+        } else if (pend) {   // the last per-sweep commit's changes: their counts, then both buffers = C_t
+            post(kWsPending);
+            wait();
+            post(kWsCopy);
+            wait();
+            valid = false;
+        }
+        if (threadIdx.x == 0) {
+            a.inc[kIncMode] = 0u;
+            a.inc[kIncDenseN + p] = a.inc[kIncHubN + p] = 0u;
+            w.ctl[kWsTchN] = 0u;
+            w.ctl[kWsTchOvf] = 0u;
+        }
+        if (!valid) {
+            if (threadIdx.x == 0) {
+                w.ctl[kWsVn + p] = 0u;
+                w.ctl[kWsArgP] = p;
+                s.st[5]++;
+            }
+            post(kWsCollect);
+            wait();
+        }
+    }
+    const uint32_t SW = walk_set_words(a.nCol);
+    for (uint32_t k = 0; go && k < K; k++) {
+        if (s.done || s.err) break;
+        const uint32_t t = s.t, p = t & 1u, q = p ^ 1u;
+        const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>(p ? a.colors1 : a.colors0);   // C_t
+        uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>(p ? a.colors0 : a.colors1);          // = C_t too
+        mark(k, 1);
+        if (threadIdx.x == 0) s_w[3] = dc_ld(&w.ctl[kWsVn + p]);
+        __syncthreads();
+        const uint32_t Vn = s_w[3];
+        const uint32_t* vl = w.vl + (size_t)p * nloc;
+        // loop control (:136, :259-269): Cviol_t = the violators
+        const unsigned long long viol = Vn;
+        const bool stop = t == a.maxRip + 1u || (!a.bench && viol <= a.z);
+        if (threadIdx.x == 0) {
+            if (t < a.traj_cap) a.traj[t] = viol;
+            if (stop) {
+                st->done = 1u;
+                st->iter = t;
+                st->maxIterReached = t == a.maxRip + 1u ? 1u : 0u;
+                st->finalViol = viol;
+                s.done = 1u;
+            }
+            w.ctl[kWsResN] = 0u;
+            w.ctl[kWsHeavyN] = 0u;
+            w.ctl[kWsArgT] = t;
+            w.ctl[kWsArgP] = p;
+            w.ctl[kWsArgP + 1] = s.x_t;
+            s_nh = 0;
+        }
+        __syncthreads();
+        if (stop) break;
+        // violators: the leader's waves walk a few light ones, else a walk phase (overlapping the candidates)
+        bool walking = false;
+        if (Vn > 0u && Vn <= kWsLeadSets) {
+            if (wv < Vn) {
+                const uint32_t l = vl[wv];
+                const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
+                if (deg > w.light_arcs) {
+                    if (lane == 0) s_heavy[atomicAdd(&s_nh, 1u)] = l;
+                } else {
+                    ws_walk_light(a, w, C, s.x_t, l, sets + wv * SW, lane);
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = 0; i < s_nh; i++) ws_walk_heavy(a, w, C, s.x_t, s_heavy[i], sets);
+            if (threadIdx.x == 0) s.st[2] += Vn;
+        } else if (Vn > 0u) {
+            post(kWsWalkLight);
+            walking = true;
+            if (threadIdx.x == 0) s.st[3]++;
+        }
+        mark(k, 2);
+        // the candidates: window entries with L in [lx + 1, lx + 1 + n) mod N, in one or two runs
+        {
+            const uint32_t lo = s.lx + 1u >= kMinstdN ? s.lx + 1u - kMinstdN : s.lx + 1u;
+            for (uint32_t run = 0; run < 2u; run++) {
+                uint32_t r0, r1;
+                if (run == 0) { r0 = lo; r1 = (uint32_t)min<uint64_t>((uint64_t)lo + nloc, kMinstdN); }
+                else { r0 = 0; r1 = (uint64_t)lo + nloc > kMinstdN ? (uint32_t)((uint64_t)lo + nloc - kMinstdN) : 0u; }
+                if (r1 <= r0) continue;
+                const uint32_t e0 = w.boff[r0 >> kWsBShift], e1 = w.boff[((r1 - 1u) >> kWsBShift) + 1u];
+                const uint32_t base = run == 0 ? lo : lo - kMinstdN;   // v = L - base (mod 2^32)
+                for (uint32_t c0 = e0; c0 < e1; c0 += kWsCandCap) {
+                    if (threadIdx.x == 0) s_nc = 0;
+                    __syncthreads();
+                    for (uint32_t j = c0 + threadIdx.x; j < min(e1, c0 + kWsCandCap); j += blockDim.x) {
+                        const uint32_t L = w.wL[j];
+                        if (L >= r0 && L < r1) {
+                            const uint32_t kk = atomicAdd(&s_nc, 1u);
+                            cand[2u * kk] = L - base;
+                            cand[2u * kk + 1u] = w.ww[j];
+                        }
+                    }
+                    __syncthreads();
+                    const uint32_t nc = s_nc;
+                    if (threadIdx.x == 0) s.st[6] += nc;
+                    for (uint32_t b = wv * 64u; b < nc; b += nwv * 64u) {
+                        const uint32_t kk = b + lane;
+                        const bool valid = kk < nc;
+                        const uint32_t l = valid ? cand[2u * kk] : 0u, x = valid ? cand[2u * kk + 1u] : 1u;
+                        uint32_t cv = 0, cnt = 1;
+                        if (valid) {
+                            cv = C[l];
+                            cnt = dc_ld(&a.inc_vcnt[l]);
+                        }
+                        uint32_t ncol = cv;
+                        if (valid && cnt == 0u) {   // case (iii); a violator is walked above
+                            const float u = minstd_canonical(x);
+                            if (u < a.emax && x - 1u < a.ftab_n) {
+                                const uint32_t F = a.ftab[x - 1u];
+                                ncol = F <= cv ? F - 1u : cv;
+                            } else {
+                                ncol = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+                            }
+                        }
+                        ws_push(w, valid && ncol != cv, l, cv, ncol, lane);
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        mark(k, 3);
+        if (walking) {
+            wait();
+            if (threadIdx.x == 0) s_w[0] = dc_ld(&w.ctl[kWsHeavyN]);
+            __syncthreads();
+            if (s_w[0] > 0u) {
+                post(kWsWalkHeavy);
+                wait();
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        mark(k, 4);
+        // the results: overflow events in ascending vertex order take the next glibc draws (:517-520)
+        if (threadIdx.x == 0) {
+            s.nres = dc_ld(&w.ctl[kWsResN]);
+            s_ne = 0;
+        }
+        __syncthreads();
+        const uint32_t N = s.nres;
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+            const uint32_t e = w.res[2u * i + 1u];
+            if ((e >> 16) == a.nCol) {
+                const uint32_t j = atomicAdd(&s_ne, 1u);
+                const uint32_t l = w.res[2u * i];
+                if (j < kWsEvLds) evl[j] = l;
+                a.events[j] = l;
+            }
+        }
+        __syncthreads();
+        const uint32_t E = s_ne;
+        if (E) {
+            uint32_t P2 = 1;
+            while (P2 < E) P2 <<= 1;
+            uint32_t* sv = P2 <= kWsEvLds ? evl : a.events;
+            for (uint32_t i = E + threadIdx.x; i < P2; i += blockDim.x) sv[i] = 0xFFFFFFFFu;
+            __syncthreads();
+            bitonic_sort_block(sv, P2);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t head = 0;
+                for (uint32_t i = 0; i < E; i++) w.heavy[sv[i]] = glibc_next(s.ring, head) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                uint32_t r[31];
+                for (uint32_t i = 0; i < 31u; i++) r[i] = s.ring[(head + i) % 31u];
+                for (uint32_t i = 0; i < 31u; i++) {
+                    s.ring[i] = r[i];
+                    st->glibc_ring[i] = r[i];
+                }
+                st->glibc_head = 0u;
+                s.draws += E;
+                st->glibc_draws = s.draws;
+            }
+            __syncthreads();
+        }
+        // the changed rows: C_t+1 into the other buffer, listed with their arcs' prefix (per-thread
+        // runs of the results, workgroup scans of their counts and arcs)
+        uint32_t nch = 0, arcs = 0;
+        {
+            const uint32_t per = (N + blockDim.x - 1u) / blockDim.x, i0 = min(N, threadIdx.x * per), i1 = min(N, i0 + per);
+            uint32_t mc = 0, ma = 0;
+            for (uint32_t i = i0; i < i1; i++) {
+                const uint32_t l = w.res[2u * i], e = w.res[2u * i + 1u];
+                const uint32_t cv = e & 0xFFFFu, nc = (e >> 16) == a.nCol ? w.heavy[l] : (e >> 16);
+                if (nc != cv) {
+                    Cs[l] = (uint16_t)nc;
+                    mc++;
+                    ma += (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                }
+            }
+            const uint32_t oc = ws_scan(mc, s_wsum, &nch);
+            const uint32_t oa = ws_scan(ma, s_wsum, &arcs);
+            uint32_t j = oc, run = oa;
+            for (uint32_t i = i0; i < i1; i++) {
+                const uint32_t l = w.res[2u * i], e = w.res[2u * i + 1u];
+                const uint32_t cv = e & 0xFFFFu, nc = (e >> 16) == a.nCol ? w.heavy[l] : (e >> 16);
+                if (nc != cv) {
+                    w.chg[2u * j] = l;
+                    w.chg[2u * j + 1u] = cv | (nc << 16);
+                    w.pre[j] = run;
+                    run += (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                    j++;
+                }
+            }
+            if (threadIdx.x == 0) {
+                w.pre[nch] = arcs;
+                w.ctl[kWsChgN] = nch;
+                s.st[7] += nch;
+                s.arcs += arcs;
+            }
+        }
+        mark(k, 5);
+        // the counts move: by the leader's threads when few arcs, else a delta phase
+        if (nch) {
+            if (arcs <= w.lead_arcs) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                const uint32_t* pre = w.pre;
+                if (nch + 1u <= 2u * kWsCandCap) {   // the prefix into LDS (the candidates' buffer)
+                    for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) cand[i] = w.pre[i];
+                    __syncthreads();
+                    pre = cand;
+                }
+                ws_delta_arcs(a, w, C, Cs, pre, nch, threadIdx.x, arcs, blockDim.x);
+            } else {
+                post(kWsDelta);
+                wait();
+                if (threadIdx.x == 0) s.st[4]++;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            // both buffers = C_t+1
+            for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x)
+                const_cast<uint16_t*>(C)[w.chg[2u * j]] = (uint16_t)(w.chg[2u * j + 1u] >> 16);
+        }
+        mark(k, 6);
+        // the violators of C_t+1: those of C_t still counted and the touched rows (flags dedupe)
+        {
+            if (threadIdx.x == 0) {
+                s_w[0] = dc_ld(&w.ctl[kWsTchN]);
+                s_w[1] = dc_ld(&w.ctl[kWsTchOvf]);
+            }
+            __syncthreads();
+            const uint32_t tn = s_w[0], tovf = s_w[1];
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                w.ctl[kWsVn + q] = 0u;
+                w.ctl[kWsTchN] = 0u;
+                w.ctl[kWsTchOvf] = 0u;
+                s_vq = 0;
+            }
+            __syncthreads();
+            if (!tovf && Vn + tn <= kWsLeadList) {
+                uint32_t* vq = w.vl + (size_t)q * nloc;
+                for (uint32_t i = threadIdx.x; i < Vn + tn; i += blockDim.x) {
+                    const bool old = i < Vn;
+                    const uint32_t l = old ? vl[i] : w.tch[i - Vn];
+                    const bool on = dc_ld(&a.inc_vcnt[l]) > 0u;
+                    const uint32_t bit = 1u << (8u * (l & 3u));
+                    bool add = false;
+                    if (old) {
+                        if (on) add = true;
+                        else atomicAnd(&w.flag[l >> 2], ~bit);
+                    } else if (on) {
+                        add = (atomicOr(&w.flag[l >> 2], bit) & bit) == 0u;
+                    }
+                    const uint64_t m = __ballot(add);
+                    if (m) {
+                        const int lead = __ffsll((long long)m) - 1;
+                        uint32_t b = 0;
+                        if ((int)lane == lead) b = atomicAdd(&s_vq, (uint32_t)__popcll(m));
+                        b = __shfl(b, lead, 64);
+                        if (add) vq[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = l;
+                    }
+                }
+                __syncthreads();
+                if (threadIdx.x == 0) w.ctl[kWsVn + q] = s_vq;
+            } else {
+                if (threadIdx.x == 0) {
+                    w.ctl[kWsArgP] = q;
+                    s.st[5]++;
+                }
+                post(kWsCollect);
+                wait();
+            }
+        }
+        mark(k, 7);
+        // accept: the RNG advances by n draws (:139), lx with it
+        if (threadIdx.x == 0) {
+            s.t = t + 1u;
+            s.x_t = minstd_mulmod(s.x_t, a.aN);
+            const uint32_t lx = s.lx + a.nmodN;
+            s.lx = lx >= kMinstdN ? lx - kMinstdN : lx;
+            st->t = s.t;
+            st->x_t = s.x_t;
+            st->lx = s.lx;
+            w.ctl[kWsT] = s.t + 1u;
+            s.st[0]++;
+        }
+        __syncthreads();
+    }
+    // exit: the helpers leave; the per-sweep path finds its delta lists empty and visits every row
+    mark(0xFFFFu, 200u);
+    post(kWsExit);
+    if (threadIdx.x < 64u) {   // (wave-uniform, as the waits)
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+            if (__builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsAck])) >= G - 1u) break;
+            if (wall_clock64() - t0 > kWsWaitTicks) {
+                if (threadIdx.x == 0) {
+                    w.ctl[kWsErr] = (s_seq << 8) | 2u;
+                    st->err |= 1u;
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        w.ctl[kWsGen] = 0u;
+        w.ctl[kWsAck] = 0u;
+        w.ctl[kWsDone] = 0u;
+        const uint32_t p = s.t & 1u;
+        if (go) {
+            a.inc[kIncTchOvf + p] = 1u;
+            a.inc[kIncDenseN + p] = 0u;
+            a.inc[kIncHubN + p] = 0u;
+            unsigned long long* is = reinterpret_cast<unsigned long long*>(a.inc + kIncStat);
+            is[0] += s.st[0];
+            is[1] += s.recounts;
+            is[2] += s.st[7];
+            is[3] += s.arcs;
+        }
+        unsigned long long* ss = reinterpret_cast<unsigned long long*>(w.ctl + kWsStat);
+        for (int i = 0; i < 8; i++) ss[i] += s.st[i];
+    }
+}

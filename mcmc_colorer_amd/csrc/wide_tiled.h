@@ -106,7 +106,7 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
                 a.taboo[l] = tab - 1u;
             }
         } else if (viol) {   // case (ii) / (i): the walk over the mask (writes Cs, taboo, the event)
-            walk_finish_wave(a, v, t, cv, x, (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu), Cs, mask, pre, nullptr, nullptr,
+            walk_finish_wave<false>(a, v, t, cv, x, (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu), Cs, mask, pre, nullptr, nullptr,
                              lane);
         } else if (lane == 0) {   // case (iii)
             const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(x));

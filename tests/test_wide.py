@@ -435,6 +435,87 @@ def test_wide_incremental_counts(M, monkeypatch, mode, case):
     col.close()
 
 
+WS_CASES = {
+    # name: (graph, nCol, run kwargs, env, what the stats must show)
+    "rmat-300": ("rmat", 300, {"maxRip": 25}, {}, "walk_phases"),
+    "rmat-phases": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_LEAD_ARCS": "0", "MCMC_WS_LIGHT": "8"}, "delta_phases"),
+    "rmat-maxdeg": ("rmat", None, {}, {}, "sweeps"),
+    "hub-300": ("hub", 300, {"maxRip": 30}, {}, "sweeps"),
+    "hub-heavy": ("hub", 300, {"maxRip": 30}, {"MCMC_WS_LIGHT": "1", "MCMC_WS_LEAD_ARCS": "0"}, "delta_phases"),
+    "dense-maxdeg": ("dense", None, {}, {}, "sweeps"),
+    "sparse-eps": ("sparse", 1000, {"epsilon": 2e-6, "maxRip": 40}, {}, "candidates"),
+    "sparse-65535": ("sparse", 65535, {"maxRip": 40}, {}, "sweeps"),
+    "all-change-16": ("dense16", 16, {"maxRip": 30}, {"MCMC_GATHER": "wide"}, "walk_phases"),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(WS_CASES))
+def test_wide_persistent(M, monkeypatch, case):
+    """The persistent wide sweep (csrc/wide_solo.h): candidate rows from the discrete-log window,
+    violators walked by the leader or by walk phases (a wave each, heavy rows a workgroup), counts
+    moved by the leader or by delta phases, the violator list kept or recollected. Every case equals
+    the oracle's run (colouring, trajectory, iter, glibc draws); the statistics show the path ran."""
+    graph, ncol, kw, env, key = WS_CASES[case]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if graph == "rmat":
+        off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    elif graph == "hub":
+        off, idx = _hub_graph()
+    elif graph == "sparse":
+        O.srand(1)
+        off, idx = O.setup_rnd2(3000, 0.01)
+    elif graph == "dense16":
+        O.srand(1)
+        off, idx = O.setup_rnd2(2000, 0.05)
+    else:
+        O.srand(1)
+        off, idx = O.setup_rnd2(1200, 0.3)
+    ncol = ncol or O.max_deg(off)
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, epsilon=kw.get("epsilon", 1e-8), maxRip=kw.get("maxRip", 250))
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    st = col.run(0)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, 1, **kw)
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws) == (
+        r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws)
+    ws = col.wide_solo_stats()
+    assert ws["enabled"] == 1 and ws["sweeps"] >= 1 and ws[key] > 0, ws
+    # the same run from the same colouring with the per-sweep path only
+    monkeypatch.setenv("MCMC_WIDE_SOLO", "0")
+    col2 = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    st2 = col2.run(0)
+    assert col2.wide_solo_stats()["enabled"] == 0
+    assert col2.coloring().tolist() == r.colors.tolist() and st2.iter == st.iter
+    col.close()
+    col2.close()
+
+
+@pytest.mark.gpu
+def test_wide_persistent_steps_alternate(M, monkeypatch):
+    """step() batches of 1, 3, 16 and 2 sweeps through the persistent launch (each entry finds the
+    violator list the last launch left): the trajectory and colouring equal one uninterrupted
+    oracle run of 22 sweeps."""
+    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    ncol = 300
+    g = M.Graph.from_csr(off, idx)
+    params = M.ColoringMCMCParams(nCol=ncol, maxRip=40)
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    col.init(0)
+    for k in (1, 3, 16, 2):
+        col.step(k)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, ncol, 1, maxRip=40, sweep_limit=22)
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist()[:22] == r.traj.tolist()[:22]
+    assert col.wide_solo_stats()["sweeps"] >= 20
+    col.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("scan", ["lds", "l2", "csr"])
 def test_wide_rmat_both_scans(M, monkeypatch, scan):
