@@ -439,6 +439,7 @@ def main() -> int:
             check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
         check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
         inc0 = None if ref else col.wide_inc_stats()
+        ws0 = None if ref else col.wide_solo_stats()
         dn0 = None if ref else col.dense_stats()
         t0 = time.perf_counter()
         check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
@@ -446,6 +447,7 @@ def main() -> int:
         kernel_ms = ker.value
         info = col.info()
         inc1 = None if ref else col.wide_inc_stats()
+        ws1 = None if ref else col.wide_solo_stats()
         dn1 = None if ref else col.dense_stats()
     else:
         import torch
@@ -628,8 +630,14 @@ def main() -> int:
         # full recount sweep (the first, or after many changes) by the layout's B_fmt
         d = {k: inc1[k] - inc0[k] for k in ("incremental_sweeps", "full_sweeps", "changed_rows", "changed_arcs")}
         S = max(1, d["incremental_sweeps"] + d["full_sweeps"])
-        b_alg = (3.0 * g.nNodes * d["incremental_sweeps"] + 30.0 * d["changed_rows"] + 8.0 * d["changed_arcs"]
-                 + b_fmt * d["full_sweeps"]) / S
+        # persistent sweeps (csrc/wide_solo.h) read no per-vertex state: per candidate row of the
+        # discrete-log window its table entry, colour and count (14 B), per violator its row's ids and
+        # colours as the walks do (priced with the changed arcs: 8 B per arc)
+        pw = {k: ws1[k] - ws0[k] for k in ("sweeps", "phases", "leader_walks", "walk_phases", "delta_phases",
+                                            "collects", "candidates", "changed_rows")} if ws1 and ws1["enabled"] else None
+        nws = pw["sweeps"] if pw else 0
+        b_alg = (3.0 * g.nNodes * max(0, d["incremental_sweeps"] - nws) + 14.0 * (pw["candidates"] if pw else 0)
+                 + 30.0 * d["changed_rows"] + 8.0 * d["changed_arcs"] + b_fmt * d["full_sweeps"]) / S
         wide_inc = dict(d, sweeps_counted=S, changed_rows_per_sweep=d["changed_rows"] / S,
                         changed_arcs_per_sweep=d["changed_arcs"] / S, bytes_per_sweep=b_alg,
                         layout_bytes_full_sweep=b_fmt,
@@ -638,6 +646,17 @@ def main() -> int:
                              "many change); bit-identical to the full scan (tests/test_wide.py::"
                              "test_wide_incremental_counts). The roofline prices the sweep by these bytes: it "
                              "is bound by launch and dependent-latency chains, not by HBM.")
+        if pw:
+            wide_inc["persistent"] = dict(pw, window_states=ws1["window_states"],
+                                          candidates_per_sweep=pw["candidates"] / max(1, nws),
+                                          step_us_per_sweep={k: (ws1["step_us"][k] - ws0["step_us"][k]) / max(1, nws)
+                                                             for k in ws1["step_us"]},
+                                          probe_us_per_sweep=[(x - y) / max(1, nws)
+                                                              for x, y in zip(ws1["probe_us"], ws0["probe_us"])],
+                                          note="persistent wide sweep (csrc/wide_solo.h): one launch for the timed "
+                                               "sweeps; a sweep evaluates the violators and the discrete-log "
+                                               "window's candidate rows only, and moves the counts by the "
+                                               "changed rows' arcs")
     achieved = b_alg / (kernel_ms * 1e-3) / 1e9
     key = f"{a.config}/{variant}" if (world == 1 and (a.config in ("c3", "c5") or n_req == 100000)) else None
     if key and ref:

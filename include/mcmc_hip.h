@@ -208,8 +208,10 @@ int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]);
  * grid, [4] violators its leader walked, [5] walk phases, [6] count-move phases, [7] violator
  * collections, [8] candidate rows evaluated, [9] rows that changed colour; diagnostics [10] the
  * watchdog word (nonzero: a phase never completed, the run failed), [11] / [12] the leader's last
- * sweep of a launch and its step, [13] the phase flag word. */
-int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[14]);
+ * sweep of a launch and its step, [13] the phase flag word, [14..21] wall-clock ticks (100 MHz) of
+ * its sweeps' steps: walks, candidates, walk wait, events, changed rows, count moves, violator
+ * list, whole sweeps; [22..29] finer probes of those steps (diagnostics). */
+int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[30]);
 
 /* Test hook (no reference counterpart): the wide sweep's exact fp32 CDF walk (csrc/cdf_walk.h,
  * extract_new_color coloringMCMC_CPU.cpp:505-520 over runs of equal p) evaluated on the host.

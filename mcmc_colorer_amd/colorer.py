@@ -310,11 +310,15 @@ class ColoringMCMC:
         context runs it, its candidate-window states, and cumulative sweeps, phases handed to the
         grid, violators walked by its leader, walk / count-move / collection phases, candidate rows
         evaluated and rows that changed colour."""
-        out = (ctypes.c_uint64 * 14)()
+        out = (ctypes.c_uint64 * 30)()
         check(lib().mcmc_get_wide_solo_stats(self._ctx, out))
         keys = ("enabled", "window_states", "sweeps", "phases", "leader_walks", "walk_phases", "delta_phases",
                 "collects", "candidates", "changed_rows", "watchdog", "dbg_sweep", "dbg_step", "dbg_gen")
-        return {k: int(v) for k, v in zip(keys, out)}
+        d = {k: int(v) for k, v in zip(keys, out)}
+        steps = ("walks", "candidates", "walk_wait", "events", "changes", "count_moves", "violator_list", "sweep")
+        d["step_us"] = {k: out[14 + i] / 100.0 for i, k in enumerate(steps)}   # summed over its sweeps
+        d["probe_us"] = [out[22 + i] / 100.0 for i in range(8)]   # finer probes (csrc/wide_solo.h)
+        return d
 
     def dense_stats(self) -> dict:
         """The dense-count sweep since the colouring was initialised (mcmc_get_dense_stats; csrc/

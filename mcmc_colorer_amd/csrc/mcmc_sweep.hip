@@ -4023,7 +4023,7 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     if (const char* m = getenv("MCMC_WS_MAX")) wmax = strtoull(m, nullptr, 10);
     if (nw == 0 || nw > wmax) return MCMC_OK;
     const size_t nloc = c->v_end - c->v_begin;
-    const size_t words = kWsWords + 2 * nloc + (nloc + 3) / 4 + 2 * nloc + 2 * nloc + (nloc + 1) + nloc + nloc +
+    const size_t words = 4 + kWsWords + 2 * nloc + (nloc + 3) / 4 + 2 * nloc + 4 * nloc + (nloc + 1) + nloc + nloc + 3 * nloc +
                          2 * nw + (kWsNB + 1);
     size_t fr = 0, tot = 0;
     MCMC_HIP_TRY(hipMemGetInfo(&fr, &tot));
@@ -4035,10 +4035,12 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     w.vl = b; b += 2 * nloc;
     w.flag = b; b += (nloc + 3) / 4;
     w.res = b; b += 2 * nloc;
-    w.chg = b; b += 2 * nloc;
+    b += (4u - ((b - c->ws_buf) & 3u)) & 3u;   // (16-byte entries)
+    w.chg = b; b += 4 * nloc;
     w.pre = b; b += nloc + 1;
     w.tch = b; b += nloc;
     w.heavy = b; b += nloc;
+    w.gcand = b; b += 3 * nloc;
     uint32_t* wL = b; b += nw;
     uint32_t* ww = b; b += nw;
     uint32_t* boff = b;
@@ -4051,6 +4053,8 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     w.light_arcs = 4096;
     if (const char* m = getenv("MCMC_WS_LIGHT")) w.light_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(m, nullptr, 10));
     w.sets = std::min<uint32_t>(16u, kWsLds / (4u * walk_set_words(c->p.nCol)));
+    w.poll = 1;
+    if (const char* m = getenv("MCMC_WS_POLL")) w.poll = (uint32_t)strtoul(m, nullptr, 10);
     if (getenv("MCMC_WS_DEBUG")) {
         MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->ws_dbg_host), 4096 * sizeof(uint32_t),
                                    hipHostMallocMapped | hipHostMallocCoherent));
@@ -4944,10 +4948,12 @@ int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
 // The persistent wide sweep (wide_solo.h): [0] set up, [1] window states, [2] its sweeps, [3] phases
 // posted, [4] violators the leader walked, [5] walk phases, [6] delta phases, [7] violator
 // collections, [8] candidate rows evaluated, [9] changed rows; diagnostics: [10] the watchdog word,
-// [11] / [12] the leader's last sweep of a launch and its step, [13] the phase flag word.
-int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[14]) {
+// [11] / [12] the leader's last sweep of a launch and its step, [13] the phase flag word; [14..21]
+// wall-clock ticks (100 MHz) of its sweeps' steps: walks, candidates, walk wait, events, changed
+// rows, count moves, violator list, whole sweeps; [22..29] finer probes (diagnostics, wide_solo.h).
+int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[30]) {
     if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
-    for (int i = 0; i < 14; i++) out[i] = 0;
+    for (int i = 0; i < 30; i++) out[i] = 0;
     if (!c->wsa.ctl) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     uint32_t h[kWsWords];
@@ -4961,6 +4967,8 @@ int mcmc_get_wide_solo_stats(mcmc_ctx* c, uint64_t out[14]) {
     out[11] = h[kWsDbg];
     out[12] = h[kWsDbg + 1];
     out[13] = h[kWsGen];
+    const unsigned long long* tq = reinterpret_cast<const unsigned long long*>(h + kWsTime);
+    for (int i = 0; i < 16; i++) out[14 + i] = tq[i];
     return MCMC_OK;
 }
 

@@ -31,25 +31,32 @@
 // last persistent launch left it valid for this t. Exit: the per-sweep path's next flag pass visits
 // every row (kIncTchOvf) and its delta lists are empty -- both paths may alternate freely.
 
-constexpr uint32_t kWsGen = 0, kWsDone = 1, kWsAck = 2, kWsT = 3;
+constexpr uint32_t kWsDone = 1, kWsAck = 2, kWsT = 3;
+constexpr uint32_t kWsGen = 80;      // the phase flag the helpers poll: a cache line of its own
 constexpr uint32_t kWsVn = 4;        // [2] violator-list lengths, by parity of t
 constexpr uint32_t kWsResN = 6;      // results of the running sweep
 constexpr uint32_t kWsTchN = 7, kWsTchOvf = 8;
-constexpr uint32_t kWsHeavyN = 9, kWsChgN = 10, kWsArgT = 11, kWsArgP = 12;
+constexpr uint32_t kWsHeavyN = 9, kWsChgN = 10, kWsArgT = 11, kWsArgP = 12;   // [13]: x_t of the sweep
+constexpr uint32_t kWsCandN = 14, kWsArgL = 15;   // the next sweep's changing candidates, its minstd log
 constexpr uint32_t kWsStat = 16;     // u64 [8]: solo sweeps, phases, leader walks, walk phases,
                                      // delta phases, collects, candidates, changed rows
 constexpr uint32_t kWsErr = 32;      // watchdog: (phase sequence << 8) | where (a wait that never completed)
 constexpr uint32_t kWsDbg = 33;      // [2] the leader's sweep of the launch and its step (diagnostics)
-constexpr uint32_t kWsWords = 48;
+constexpr uint32_t kWsTime = 48;     // u64 [16]: wall-clock ticks (100 MHz) per step of the leader's sweeps,
+                                     // then finer probes (diagnostics)
+constexpr uint32_t kWsWords = 96;
 // Watchdogs (wall clock, 100 MHz): a leader wait or an acknowledgement pending this long flags
 // DevState::err and ends the launch instead of spinning forever; an idle helper leaves after kWsIdle.
 constexpr unsigned long long kWsWaitTicks = 200000000ull;    // 2 s
 constexpr unsigned long long kWsIdleTicks = 1000000000ull;   // 10 s
 constexpr uint32_t kWsBShift = 16;   // window buckets: L >> 16
 constexpr uint32_t kWsNB = ((kMinstdN - 1u) >> kWsBShift) + 1u;
-constexpr uint32_t kWsCandCap = 4096;      // candidate rows per round (leader LDS)
-constexpr uint32_t kWsEvLds = 8192;        // overflow events sorted in LDS (more: in global memory)
-constexpr uint32_t kWsLeadSets = 4;        // the leader's walk mask sets (violators it walks itself)
+constexpr uint32_t kWsCandCap = 2048;      // changing candidate rows the leader holds (more: no prefetch)
+constexpr uint32_t kWsResLds = 4096;       // results the leader keeps in LDS (more: the global list)
+constexpr uint32_t kWsEvLds = 4096;        // overflow events sorted in LDS (more: in global memory)
+constexpr uint32_t kWsRankMax = 1024;      // events ranked and drawn in parallel (more: bitonic + sequential)
+constexpr uint32_t kWsLeadLight = 256;     // violator arcs the leader walks on one wave (more: the workgroup)
+constexpr uint32_t kWsLeadSets = 2;        // the leader's walk mask sets (violators it walks itself)
 constexpr uint32_t kWsLeadList = 16384;    // violator-list updates the leader does itself
 constexpr uint32_t kWsPreLds = 16384;      // delta phase: changed rows whose arc prefix sits in LDS
 constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
@@ -61,7 +68,7 @@ struct WsArgs {
     uint32_t* vl;          // [2][nloc] violator lists (parity of t)
     uint32_t* flag;        // [nloc] bytes: row in the current violator list
     uint32_t* res;         // [2 nloc] the sweep's results (l, cv | nc << 16; nc = nCol: an overflow)
-    uint32_t* chg;         // [2 nloc] its changed rows (l, cov | cnv << 16)
+    uint32_t* chg;         // [4 nloc] its changed rows (l, cov | cnv << 16, row start lo, hi)
     uint32_t* pre;         // [nloc + 1] their arcs' exclusive prefix
     uint32_t* tch;         // [nloc] rows whose count left 0
     uint32_t* heavy;       // [nloc] violators walked by a workgroup; then the events' drawn colours (by row)
@@ -73,7 +80,46 @@ struct WsArgs {
     uint32_t light_arcs;   // violators of at most this many arcs walk on one wave
     uint32_t sets;         // wave mask sets per workgroup
     uint32_t* dbg;         // diagnostics (MCMC_WS_DEBUG): host-visible progress words, or nullptr
+    uint32_t poll;         // an idle helper's poll interval (s_sleep 2 units; MCMC_WS_POLL)
+    uint32_t* gcand;       // [3 nloc] the next sweep's candidates that change colour in case (iii)
+                           // (l, x, cv | nc << 16), found by the helpers during a delta phase
 };
+
+// The candidates of the sweep whose minstd log is lxv: window entries with L in [lxv + 1,
+// lxv + 1 + n) mod (2^31 - 2) -- one or two runs of the table. Entry j (< *tot) of the runs: its
+// row l (the vertex drawing state x) when it lies in them.
+struct WsRuns {
+    uint32_t lo, r1a, r1b, ea0, ea1, eb1, tot;
+};
+__device__ __forceinline__ WsRuns ws_runs(const WsArgs& w, uint32_t lxv, uint32_t nloc) {
+    WsRuns r;
+    r.lo = lxv + 1u >= kMinstdN ? lxv + 1u - kMinstdN : lxv + 1u;
+    r.r1a = (uint32_t)min<uint64_t>((uint64_t)r.lo + nloc, kMinstdN);
+    r.r1b = (uint64_t)r.lo + nloc > kMinstdN ? (uint32_t)((uint64_t)r.lo + nloc - kMinstdN) : 0u;
+    r.ea0 = w.boff[r.lo >> kWsBShift];
+    r.ea1 = w.boff[((r.r1a - 1u) >> kWsBShift) + 1u];
+    r.eb1 = r.r1b ? w.boff[((r.r1b - 1u) >> kWsBShift) + 1u] : 0u;
+    r.tot = (r.ea1 - r.ea0) + r.eb1;
+    return r;
+}
+__device__ __forceinline__ bool ws_entry(const WsArgs& w, const WsRuns& r, uint32_t j0, uint32_t& l, uint32_t& x) {
+    const bool ra = j0 < r.ea1 - r.ea0;
+    const uint32_t j = ra ? r.ea0 + j0 : j0 - (r.ea1 - r.ea0);
+    const uint32_t L = w.wL[j];
+    x = w.ww[j];
+    l = ra ? L - r.lo : L + (kMinstdN - r.lo);
+    return ra ? (L >= r.lo && L < r.r1a) : (L < r.r1b);
+}
+// fill_p case (iii) (own colour hi, others eps) for a row of colour cv and state x: the new colour
+// (nCol: an overflow).
+__device__ __forceinline__ uint32_t ws_own_walk(const SweepArgs& a, uint32_t cv, uint32_t x) {
+    const float u = minstd_canonical(x);
+    if (u < a.emax && x - 1u < a.ftab_n) {
+        const uint32_t F = a.ftab[x - 1u];
+        return F <= cv ? F - 1u : cv;
+    }
+    return walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
+}
 // Progress words in host memory (MCMC_WS_DEBUG): readable while a launch runs.
 __device__ __forceinline__ void ws_dbg(const WsArgs& w, uint32_t i, uint32_t v) {
     if (w.dbg != nullptr) __hip_atomic_store(&w.dbg[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -158,8 +204,9 @@ __device__ __forceinline__ void ws_touch(const SweepArgs& a, const WsArgs& w, ui
 }
 
 // One light violator on one wave: its occupancy mask in the wave's set, its walk, the result.
-__device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ C,
-                                              uint32_t x_t, uint32_t l, uint32_t* mask, uint32_t lane) {
+// Results go to (rcnt, rbuf): the global list (helpers) or the leader's LDS list.
+__device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t x_t,
+                                              uint32_t l, uint32_t* mask, uint32_t lane, uint32_t* rcnt, uint32_t* rbuf) {
     const uint32_t NWW = (a.nCol + 31u) >> 5;
     uint32_t* pre = mask + ((NWW + 3u) & ~3u);
     const uint32_t cv = C[l];
@@ -170,28 +217,41 @@ __device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const WsArgs& 
     wave_lds_sync();
     const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
     if (lane == 0 && nc != cv) {
-        const uint32_t j = atomicAdd(&w.ctl[kWsResN], 1u);
-        w.res[2u * j] = l;
-        w.res[2u * j + 1u] = cv | (nc << 16);
+        const uint32_t j = atomicAdd(rcnt, 1u);
+        rbuf[2u * j] = l;
+        rbuf[2u * j + 1u] = cv | (nc << 16);
     }
 }
 // One heavy violator on the whole workgroup (mask set 0); all threads call it.
-__device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ C,
-                                              uint32_t x_t, uint32_t l, uint32_t* mask) {
+__device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t x_t,
+                                              uint32_t l, uint32_t* mask, uint32_t* rcnt, uint32_t* rbuf) {
     const uint32_t NWW = (a.nCol + 31u) >> 5, lane = threadIdx.x & 63u;
     uint32_t* pre = mask + ((NWW + 3u) & ~3u);
     for (uint32_t i = threadIdx.x; i < NWW; i += blockDim.x) mask[i] = 0u;
     __syncthreads();
-    walk_gather(a, C, mask, a.row_off[l], a.row_off[l + 1]);
+    {   // the row's occupancy: 16 gathers per thread in flight (a hub: ~2 rounds at C5)
+        const uint64_t k0 = a.row_off[l], k1 = a.row_off[l + 1];
+        for (uint64_t k = k0 + threadIdx.x; k < k1; k += 16u * blockDim.x) {
+            uint32_t c[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint64_t kk = k + (uint64_t)j * blockDim.x;
+                c[j] = kk < k1 ? (uint32_t)C[a.col_idx[kk]] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
+        }
+    }
     __syncthreads();
     if (threadIdx.x < 64u) {
         const uint32_t cv = C[l];
         const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)l + 1ull));
         const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
         if (lane == 0 && nc != cv) {
-            const uint32_t j = atomicAdd(&w.ctl[kWsResN], 1u);
-            w.res[2u * j] = l;
-            w.res[2u * j + 1u] = cv | (nc << 16);
+            const uint32_t j = atomicAdd(rcnt, 1u);
+            rbuf[2u * j] = l;
+            rbuf[2u * j + 1u] = cv | (nc << 16);
         }
     }
     __syncthreads();
@@ -210,9 +270,9 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
             const uint32_t mid = (lo + hi) >> 1;
             if (pre[mid] <= k) lo = mid; else hi = mid;
         }
-        const uint32_t v = w.chg[2u * lo], ab = w.chg[2u * lo + 1u];
-        const uint32_t cov = ab & 0xFFFFu, cnv = ab >> 16;
-        const uint32_t u = a.col_idx[a.row_off[v] + (k - pre[lo])];
+        const uint4 ch = reinterpret_cast<const uint4*>(w.chg)[lo];
+        const uint32_t v = ch.x, cov = ch.y & 0xFFFFu, cnv = ch.y >> 16;
+        const uint32_t u = a.col_idx[(((uint64_t)ch.w << 32) | ch.z) + (k - pre[lo])];
         if (u == v) continue;
         const uint32_t ou = Cp[u], nu = Cn[u];
         if (ou != nu && u < v) continue;
@@ -302,24 +362,36 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
             for (int i = 0; i < 4; i++)
                 if (fl[i]) w.vl[(size_t)P * nloc + base++] = l0 + i;
         }
-    } else if (kind == kWsWalkLight) {   // violator list P: light rows a wave each, heavy ones listed
-        const uint32_t Vn = w.ctl[kWsVn + P];
+    } else if (kind == kWsWalkLight) {
+        // violator list P: entries h, h + H, ... of this workgroup; its waves walk the light ones
+        // (one each), then the whole workgroup the heavy ones (listed in LDS)
+        const uint32_t Vn = w.ctl[kWsVn + P], x_t = w.ctl[kWsArgP + 1];
         const uint32_t* vl = w.vl + (size_t)P * nloc;
+        __shared__ uint32_t s_hn, s_hv[64];
+        if (threadIdx.x == 0) s_hn = 0;
+        __syncthreads();
         if (wv < w.sets) {
             uint32_t* mask = dyn + wv * walk_set_words(a.nCol);
-            for (uint32_t i = h * w.sets + wv; i < Vn; i += H * w.sets) {
+            for (uint32_t i = h + H * wv; i < Vn; i += H * w.sets) {
                 const uint32_t l = vl[i];
-                const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
-                if (deg > w.light_arcs) {
-                    if (lane == 0) w.heavy[atomicAdd(&w.ctl[kWsHeavyN], 1u)] = l;
+                if (a.row_off[l + 1] - a.row_off[l] > w.light_arcs) {
+                    if (lane == 0) {
+                        const uint32_t j = atomicAdd(&s_hn, 1u);
+                        if (j < 64u) s_hv[j] = l;
+                        else w.heavy[atomicAdd(&w.ctl[kWsHeavyN], 1u)] = l;
+                    }
                     continue;
                 }
-                ws_walk_light(a, w, C, w.ctl[kWsArgP + 1], l, mask, lane);
+                ws_walk_light(a, C, x_t, l, mask, lane, &w.ctl[kWsResN], w.res);
             }
         }
+        __syncthreads();
+        const uint32_t hn = min(s_hn, 64u);
+        for (uint32_t j = 0; j < hn; j++) ws_walk_heavy(a, C, x_t, s_hv[j], dyn, &w.ctl[kWsResN], w.res);
     } else if (kind == kWsWalkHeavy) {
         const uint32_t hn = w.ctl[kWsHeavyN];
-        for (uint32_t j = h; j < hn; j += H) ws_walk_heavy(a, w, C, w.ctl[kWsArgP + 1], w.heavy[j], dyn);
+        for (uint32_t j = h; j < hn; j += H)
+            ws_walk_heavy(a, C, w.ctl[kWsArgP + 1], w.heavy[j], dyn, &w.ctl[kWsResN], w.res);
     } else if (kind == kWsDelta) {   // the changed rows' arcs (prefix cached in LDS where it fits)
         const uint32_t nch = w.ctl[kWsChgN];
         const uint32_t* pre = w.pre;
@@ -329,6 +401,30 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
             pre = dyn;
         }
         ws_delta_arcs(a, w, C, Cs, pre, nch, gt, pre[nch], GT);
+        // meanwhile the next sweep's candidates (its colours: C_t+1, in Cs): those that change
+        // colour unless they turn out violators, into gcand
+        const WsRuns r = ws_runs(w, w.ctl[kWsArgL], nloc);
+        for (uint32_t j0 = gt & ~63u; j0 < r.tot; j0 += GT) {   // (wave-uniform bounds)
+            uint32_t l = 0, x = 1, cv = 0, nc = 0;
+            bool in = j0 + lane < r.tot && ws_entry(w, r, j0 + lane, l, x);
+            if (in) {
+                cv = Cs[l];
+                nc = ws_own_walk(a, cv, x);
+                in = nc != cv;
+            }
+            const uint64_t m = __ballot(in);
+            if (m == 0) continue;
+            const int ld = __ffsll((long long)m) - 1;
+            uint32_t b = 0;
+            if ((int)lane == ld) b = atomicAdd(&w.ctl[kWsCandN], (uint32_t)__popcll(m));
+            b = __shfl(b, ld, 64);
+            if (in) {
+                const uint32_t k = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                w.gcand[3u * k] = l;
+                w.gcand[3u * k + 1u] = x;
+                w.gcand[3u * k + 2u] = cv | (nc << 16);
+            }
+        }
     } else if (kind == kWsPending) {   // the last per-sweep commit's changed rows: C_t-1 (buffer of t-1) -> C_t
         const uint32_t p = t & 1u;
         const uint16_t* Cp = Cs;   // the buffer of C_t-1 (sweep t writes it next)
@@ -361,6 +457,8 @@ struct WsState {
     unsigned long long st[8];
     unsigned long long arcs;        // the changed rows' arcs (the incremental statistics)
     uint32_t recounts;
+    unsigned long long tm[16], t0, ts, tp;   // ticks per step: walks, candidates, walk wait, events, changes,
+                                    // count moves, violator list, whole sweeps
 };
 
 // Exclusive scan of one value per thread over the workgroup; *tot = the sum. All threads call it.
@@ -372,14 +470,14 @@ __device__ __forceinline__ uint32_t ws_scan(uint32_t v, uint32_t* wsum, uint32_t
         if (lane >= (uint32_t)o) inc += y;
     }
     if (lane == 63u) wsum[wv] = inc;
-    __syncthreads();
+    dc_lbar();
     uint32_t off = 0, s = 0;
     for (uint32_t k = 0; k < nwv; k++) {
         if (k < wv) off += wsum[k];
         s += wsum[k];
     }
     *tot = s;
-    __syncthreads();
+    dc_lbar();
     return off + inc - v;
 }
 
@@ -401,7 +499,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     g = __builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsGen]));
                     if (g != last) break;
                     if (wall_clock64() - t0 > kWsIdleTicks) { g = kWsExit; break; }
-                    __builtin_amdgcn_s_sleep(2);
+                    for (uint32_t z = 0; z < w.poll; z++) __builtin_amdgcn_s_sleep(2);   // (0: spin)
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -428,11 +526,14 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
     }
     // ---- the leader ----
     __shared__ WsState s;
-    __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_wsum[16], s_heavy[kWsLeadSets], s_nh, s_vq, s_w[4];
-    uint32_t* const cand = dyn;                              // [2 kWsCandCap]
-    uint32_t* const evl = dyn + 2u * kWsCandCap;             // [kWsEvLds]
+    __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_nr, s_wsum[16], s_nh, s_vq, s_w[4], s_pf, s_gn;
+    __shared__ uint32_t s_ring[31];
+    uint32_t* const cand = dyn;                              // [3 kWsCandCap] candidates (l, x, cv | nc << 16)
+    uint32_t* const tmp = cand + 3u * kWsCandCap;            // [kWsResLds] raw draws, event vertices, degrees
+    uint32_t* const lres = tmp + kWsResLds;                  // [2 kWsResLds] the sweep's results
+    uint32_t* const evl = lres + 2u * kWsResLds;             // [kWsEvLds] overflow events (result indices)
     uint32_t* const sets = evl + kWsEvLds;                   // kWsLeadSets mask sets
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // a phase for the helpers: every wave's stores drained, release, the flag; then wait for all
     auto post = [&](uint32_t kind) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -473,8 +574,20 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         }
         __syncthreads();
     };
+    auto probe = [&](uint32_t i) {   // tm[8 + i] += ticks since the last probe (i = 0: restart)
+        if (threadIdx.x == 0) {
+            const unsigned long long now = wall_clock64();
+            if (i) s.tm[8 + i] += now - s.tp;
+            s.tp = now;
+        }
+    };
     auto mark = [&](uint32_t k, uint32_t step) {
         if (threadIdx.x == 0) {
+            const unsigned long long now = wall_clock64();
+            if (step >= 2u && step <= 8u) s.tm[step - 2u] += now - s.t0;
+            if (step == 8u) s.tm[7] += now - s.ts;
+            if (step == 1u) s.ts = now;
+            if (step >= 1u && step <= 8u) s.t0 = now;
             w.ctl[kWsDbg] = k;
             w.ctl[kWsDbg + 1] = step;
             ws_dbg(w, 0, k);
@@ -494,6 +607,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         for (int i = 0; i < 8; i++) s.st[i] = 0;
         s.arcs = 0;
         s.recounts = 0;
+        for (int i = 0; i < 16; i++) s.tm[i] = 0;
         s_seq = 0;
         s_exp = 0;
     }
@@ -547,6 +661,90 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         }
     }
     const uint32_t SW = walk_set_words(a.nCol);
+    // The candidates of the sweep whose minstd log is lxv: window entries with L in [lxv + 1,
+    // lxv + 1 + n) mod N (one or two runs of the table), their colours in Cb and the colour a case
+    // (iii) walk gives them (fill_p own colour hi, others eps) into cand; s_nc = their number, or
+    // 0xFFFFFFFF if more than the LDS holds (the sweep then runs them in rounds, rounds()).
+    auto fetch = [&](uint32_t lxv, const uint16_t* __restrict__ Cb) {
+        probe(0);
+        const uint32_t lo = lxv + 1u >= kMinstdN ? lxv + 1u - kMinstdN : lxv + 1u;
+        const uint32_t r1a = (uint32_t)min<uint64_t>((uint64_t)lo + nloc, kMinstdN);
+        const uint32_t r1b = (uint64_t)lo + nloc > kMinstdN ? (uint32_t)((uint64_t)lo + nloc - kMinstdN) : 0u;
+        const uint32_t ea0 = w.boff[lo >> kWsBShift], ea1 = w.boff[((r1a - 1u) >> kWsBShift) + 1u];
+        const uint32_t eb1 = r1b ? w.boff[((r1b - 1u) >> kWsBShift) + 1u] : 0u;
+        if (threadIdx.x == 0) s_nc = 0u;
+        dc_lbar();
+        probe(1);   // [9] the bucket bounds
+        // 4 entries per thread per round, every load of a stage issued before the next stage's
+        // (table entries -> colours and F(u) -> the eps-prefix walks)
+        const uint32_t tot = (ea1 - ea0) + eb1;
+        for (uint32_t b0 = 0; b0 < tot; b0 += 4u * blockDim.x) {
+            uint32_t L[4], x[4], l[4], cv[4], F[4];
+            bool in[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t j0 = b0 + (uint32_t)q * blockDim.x + threadIdx.x;
+                const bool ra = j0 < ea1 - ea0;
+                const uint32_t j = ra ? ea0 + j0 : j0 - (ea1 - ea0);
+                in[q] = j0 < tot;
+                L[q] = in[q] ? w.wL[j] : 0u;
+                x[q] = in[q] ? w.ww[j] : 1u;
+                in[q] = in[q] && (ra ? (L[q] >= lo && L[q] < r1a) : (L[q] < r1b));
+                l[q] = ra ? L[q] - lo : L[q] + (kMinstdN - lo);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                cv[q] = in[q] ? (uint32_t)Cb[l[q]] : 0u;
+                const bool tab = in[q] && minstd_canonical(x[q]) < a.emax && x[q] - 1u < a.ftab_n;
+                F[q] = tab ? (uint32_t)a.ftab[x[q] - 1u] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t ncol = cv[q];
+                if (!in[q]) continue;
+                if (F[q] != 0xFFFFFFFFu) ncol = F[q] <= cv[q] ? F[q] - 1u : cv[q];
+                else ncol = walk_own_tab(a.etab, a.nCol, cv[q], a.eps, a.hi, minstd_canonical(x[q]));
+                in[q] = in[q] && ncol != cv[q];   // (candidates that keep their colour need nothing)
+                cv[q] |= ncol << 16;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {   // appends: one LDS atomic per wave
+                const uint64_t m = __ballot(in[q]);
+                if (m == 0) continue;
+                const int lead = __ffsll((long long)m) - 1;
+                uint32_t b = 0;
+                if ((int)(threadIdx.x & 63u) == lead) b = atomicAdd(&s_nc, (uint32_t)__popcll(m));
+                b = __shfl(b, lead, 64);
+                const uint32_t kk = b + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull));
+                if (in[q] && kk < kWsCandCap) {
+                    cand[3u * kk] = l[q];
+                    cand[3u * kk + 1u] = x[q];
+                    cand[3u * kk + 2u] = cv[q];
+                }
+            }
+        }
+        dc_lbar();
+        probe(2);   // [10] the entries, colours, walks
+        if (threadIdx.x == 0) {
+            s.st[6] += (ea1 - ea0) + eb1;
+            if (s_nc > kWsCandCap) s_nc = 0xFFFFFFFFu;
+        }
+        dc_lbar();
+    };
+    // a result of the leader into its LDS list (past it: the global one)
+    auto push = [&](uint32_t l, uint32_t e) {
+        const uint32_t j = atomicAdd(&s_nr, 1u);
+        if (j < kWsResLds) {
+            lres[2u * j] = l;
+            lres[2u * j + 1u] = e;
+        } else {
+            const uint32_t g = atomicAdd(&w.ctl[kWsResN], 1u);
+            w.res[2u * g] = l;
+            w.res[2u * g + 1u] = e;
+        }
+    };
+    if (threadIdx.x == 0) s_pf = 0xFFFFFFFFu;   // no prefetched candidates yet
+    __syncthreads();
     for (uint32_t k = 0; go && k < K; k++) {
         if (s.done || s.err) break;
         const uint32_t t = s.t, p = t & 1u, q = p ^ 1u;
@@ -554,7 +752,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>(p ? a.colors0 : a.colors1);          // = C_t too
         mark(k, 1);
         if (threadIdx.x == 0) s_w[3] = dc_ld(&w.ctl[kWsVn + p]);
-        __syncthreads();
+        dc_lbar();
         const uint32_t Vn = s_w[3];
         const uint32_t* vl = w.vl + (size_t)p * nloc;
         // loop control (:136, :259-269): Cviol_t = the violators
@@ -575,23 +773,25 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             w.ctl[kWsArgP] = p;
             w.ctl[kWsArgP + 1] = s.x_t;
             s_nh = 0;
+            s_nr = 0;
         }
         __syncthreads();
         if (stop) break;
-        // violators: the leader's waves walk a few light ones, else a walk phase (overlapping the candidates)
+        // violators: the leader's waves walk a few light ones (the workgroup the heavier), else a walk
+        // phase (overlapping the candidates). The leader's results go to its LDS list.
         bool walking = false;
-        if (Vn > 0u && Vn <= kWsLeadSets) {
-            if (wv < Vn) {
+        bool lead = Vn > 0u && Vn <= kWsLeadSets;
+        if (lead) {   // the leader walks them only if all are light (a heavy one: the grid, beside the candidates)
+            if (wv < Vn && lane == 0) {
                 const uint32_t l = vl[wv];
-                const uint64_t deg = a.row_off[l + 1] - a.row_off[l];
-                if (deg > w.light_arcs) {
-                    if (lane == 0) s_heavy[atomicAdd(&s_nh, 1u)] = l;
-                } else {
-                    ws_walk_light(a, w, C, s.x_t, l, sets + wv * SW, lane);
-                }
+                if (a.row_off[l + 1] - a.row_off[l] > kWsLeadLight) atomicAdd(&s_nh, 1u);
             }
-            __syncthreads();
-            for (uint32_t i = 0; i < s_nh; i++) ws_walk_heavy(a, w, C, s.x_t, s_heavy[i], sets);
+            dc_lbar();
+            lead = s_nh == 0u;
+        }
+        if (lead) {
+            if (wv < Vn) ws_walk_light(a, C, s.x_t, vl[wv], sets + wv * SW, lane, &s_nr, lres);
+            dc_lbar();
             if (threadIdx.x == 0) s.st[2] += Vn;
         } else if (Vn > 0u) {
             post(kWsWalkLight);
@@ -599,8 +799,37 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             if (threadIdx.x == 0) s.st[3]++;
         }
         mark(k, 2);
-        // the candidates: window entries with L in [lx + 1, lx + 1 + n) mod N, in one or two runs
-        {
+        // the candidates (fetched while the last sweep's counts moved, where they fit): those that are
+        // not violators keep the colour their case (iii) walk gave; more than the LDS holds: in rounds
+        const bool pre_g = s_pf == s.lx;   // the helpers found them during the last delta phase
+        if (!pre_g) fetch(s.lx, C);
+        if (pre_g || s_nc != 0xFFFFFFFFu) {
+            const uint32_t nc = pre_g ? s_gn : s_nc;
+            const uint32_t* cl = pre_g ? w.gcand : cand;
+            for (uint32_t b0 = wv * 64u; b0 < nc; b0 += blockDim.x) {   // (wave-uniform bounds)
+                const uint32_t kk = b0 + lane;
+                const uint32_t l = kk < nc ? cl[3u * kk] : 0u;
+                const bool keep = kk < nc && dc_ld(&a.inc_vcnt[l]) == 0u;   // a violator: walked above
+                const uint64_t m = __ballot(keep);
+                if (m == 0) continue;
+                const int ld = __ffsll((long long)m) - 1;
+                uint32_t b = 0;
+                if ((int)lane == ld) b = atomicAdd(&s_nr, (uint32_t)__popcll(m));
+                b = __shfl(b, ld, 64);
+                const uint32_t j = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (keep) {
+                    const uint32_t e = cl[3u * kk + 2u];
+                    if (j < kWsResLds) {
+                        lres[2u * j] = l;
+                        lres[2u * j + 1u] = e;
+                    } else {
+                        const uint32_t g = atomicAdd(&w.ctl[kWsResN], 1u);
+                        w.res[2u * g] = l;
+                        w.res[2u * g + 1u] = e;
+                    }
+                }
+            }
+        } else {
             const uint32_t lo = s.lx + 1u >= kMinstdN ? s.lx + 1u - kMinstdN : s.lx + 1u;
             for (uint32_t run = 0; run < 2u; run++) {
                 uint32_t r0, r1;
@@ -609,49 +838,29 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 if (r1 <= r0) continue;
                 const uint32_t e0 = w.boff[r0 >> kWsBShift], e1 = w.boff[((r1 - 1u) >> kWsBShift) + 1u];
                 const uint32_t base = run == 0 ? lo : lo - kMinstdN;   // v = L - base (mod 2^32)
-                for (uint32_t c0 = e0; c0 < e1; c0 += kWsCandCap) {
-                    if (threadIdx.x == 0) s_nc = 0;
-                    __syncthreads();
-                    for (uint32_t j = c0 + threadIdx.x; j < min(e1, c0 + kWsCandCap); j += blockDim.x) {
-                        const uint32_t L = w.wL[j];
-                        if (L >= r0 && L < r1) {
-                            const uint32_t kk = atomicAdd(&s_nc, 1u);
-                            cand[2u * kk] = L - base;
-                            cand[2u * kk + 1u] = w.ww[j];
-                        }
+                if (threadIdx.x == 0) s.st[6] += e1 - e0;
+                for (uint32_t j = e0 + threadIdx.x; j < e1; j += blockDim.x) {
+                    const uint32_t L = w.wL[j];
+                    if (!(L >= r0 && L < r1)) continue;
+                    const uint32_t l = L - base, x = w.ww[j];
+                    const uint32_t cv = C[l];
+                    if (dc_ld(&a.inc_vcnt[l]) != 0u) continue;   // a violator: walked above
+                    const float u = minstd_canonical(x);
+                    uint32_t ncol;
+                    if (u < a.emax && x - 1u < a.ftab_n) {
+                        const uint32_t F = a.ftab[x - 1u];
+                        ncol = F <= cv ? F - 1u : cv;
+                    } else {
+                        ncol = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
                     }
-                    __syncthreads();
-                    const uint32_t nc = s_nc;
-                    if (threadIdx.x == 0) s.st[6] += nc;
-                    for (uint32_t b = wv * 64u; b < nc; b += nwv * 64u) {
-                        const uint32_t kk = b + lane;
-                        const bool valid = kk < nc;
-                        const uint32_t l = valid ? cand[2u * kk] : 0u, x = valid ? cand[2u * kk + 1u] : 1u;
-                        uint32_t cv = 0, cnt = 1;
-                        if (valid) {
-                            cv = C[l];
-                            cnt = dc_ld(&a.inc_vcnt[l]);
-                        }
-                        uint32_t ncol = cv;
-                        if (valid && cnt == 0u) {   // case (iii); a violator is walked above
-                            const float u = minstd_canonical(x);
-                            if (u < a.emax && x - 1u < a.ftab_n) {
-                                const uint32_t F = a.ftab[x - 1u];
-                                ncol = F <= cv ? F - 1u : cv;
-                            } else {
-                                ncol = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, u);
-                            }
-                        }
-                        ws_push(w, valid && ncol != cv, l, cv, ncol, lane);
-                    }
-                    __syncthreads();
+                    if (ncol != cv) push(l, cv | (ncol << 16));
                 }
             }
         }
         mark(k, 3);
         if (walking) {
             wait();
-            if (threadIdx.x == 0) s_w[0] = dc_ld(&w.ctl[kWsHeavyN]);
+            if (threadIdx.x == 0) s_w[0] = dc_ld(&w.ctl[kWsHeavyN]);   // heavy rows past a workgroup's 64
             __syncthreads();
             if (s_w[0] > 0u) {
                 post(kWsWalkHeavy);
@@ -661,35 +870,97 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         mark(k, 4);
-        // the results: overflow events in ascending vertex order take the next glibc draws (:517-520)
+        // the results in one list: the global one (walk phases, LDS overflow) appended to the LDS one
+        // where it fits, else the LDS one appended to the global one
         if (threadIdx.x == 0) {
-            s.nres = dc_ld(&w.ctl[kWsResN]);
+            s_w[0] = dc_ld(&w.ctl[kWsResN]);
             s_ne = 0;
         }
-        __syncthreads();
-        const uint32_t N = s.nres;
-        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
-            const uint32_t e = w.res[2u * i + 1u];
-            if ((e >> 16) == a.nCol) {
-                const uint32_t j = atomicAdd(&s_ne, 1u);
-                const uint32_t l = w.res[2u * i];
-                if (j < kWsEvLds) evl[j] = l;
-                a.events[j] = l;
-            }
+        dc_lbar();
+        probe(0);
+        const uint32_t Ng = s_w[0], Nl = min(s_nr, kWsResLds);
+        const bool inl = Nl + Ng <= kWsResLds;
+        uint32_t* const R = inl ? lres : w.res;
+        const uint32_t N = Nl + Ng;
+        if (inl) {
+            for (uint32_t i = threadIdx.x; i < 2u * Ng; i += blockDim.x) lres[2u * Nl + i] = w.res[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < 2u * Nl; i += blockDim.x) w.res[2u * Ng + i] = lres[i];
         }
-        __syncthreads();
+        if (inl) dc_lbar(); else __syncthreads();
+        probe(3);   // [11] merge
+        // overflow events in ascending vertex order take the next glibc draws (:517-520): up to
+        // kWsRankMax ranked and drawn in parallel (draw r = sum_m T[m][r] ring[m], the commit's table),
+        // more sorted (bitonic) and drawn in sequence
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+            if ((R[2u * i + 1u] >> 16) == a.nCol) {
+                const uint32_t j = atomicAdd(&s_ne, 1u);
+                if (j < kWsEvLds) evl[j] = i;
+                a.events[j] = R[2u * i];
+            }
+        if (threadIdx.x < 31u) s_ring[threadIdx.x] = s.ring[threadIdx.x];
+        dc_lbar();
+        probe(4);   // [12] the events' collection
         const uint32_t E = s_ne;
-        if (E) {
+
+        if (E > 0u && E <= kWsRankMax) {
+            // (vertex, result index) pairs sorted in LDS (bitonic), then draw r on thread r (the
+            // table's columns side by side) for the event of rank r
             uint32_t P2 = 1;
             while (P2 < E) P2 <<= 1;
-            uint32_t* sv = P2 <= kWsEvLds ? evl : a.events;
+            unsigned long long* const kv = reinterpret_cast<unsigned long long*>(tmp);   // [P2]
+            uint32_t* const raw = evl;   // [E] raw draws by rank (the indices are in kv)
+            for (uint32_t i = threadIdx.x; i < P2; i += blockDim.x)
+                kv[i] = i < E ? (((unsigned long long)R[2u * evl[i]] << 32) | evl[i]) : ~0ull;
+            dc_lbar();
+            probe(5);   // [13] the keys
+            for (uint32_t kb = 2; kb <= P2; kb <<= 1) {
+                for (uint32_t jb = kb >> 1; jb > 0; jb >>= 1) {
+                    for (uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
+                        const uint32_t ixj = i ^ jb;
+                        if (ixj > i) {
+                            const bool up = (i & kb) == 0;
+                            const unsigned long long x0 = kv[i], y0 = kv[ixj];
+                            if ((x0 > y0) == up) { kv[i] = y0; kv[ixj] = x0; }
+                        }
+                    }
+                    dc_lbar();
+                }
+            }
+            probe(6);   // [14] the sort
+            if (threadIdx.x < E) {
+                const uint32_t r = threadIdx.x, ii = (uint32_t)kv[r];
+                uint32_t acc = 0;
+#pragma unroll
+                for (int m = 0; m < 31; m++) acc += kGlibcTab[m * kGlibcTabK + r] * s_ring[m];
+                raw[r] = acc;
+                const uint32_t c = (acc >> 1) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                R[2u * ii + 1u] = (R[2u * ii + 1u] & 0xFFFFu) | (c << 16);
+            }
+            dc_lbar();
+            probe(7);   // [15] the draws
+            if (threadIdx.x < 31u) {   // the window after E draws, oldest first
+                const uint32_t nw = (E < 31u && threadIdx.x < 31u - E) ? s_ring[E + threadIdx.x] : raw[E + threadIdx.x - 31u];
+                s.ring[threadIdx.x] = nw;
+                st->glibc_ring[threadIdx.x] = nw;
+            }
+            if (threadIdx.x == 0) {
+                st->glibc_head = 0u;
+                s.draws += E;
+                st->glibc_draws = s.draws;
+            }
+            if (inl) dc_lbar(); else __syncthreads();
+        } else if (E > 0u) {
+            uint32_t P2 = 1;
+            while (P2 < E) P2 <<= 1;
+            uint32_t* sv = a.events;   // vertex ids
             for (uint32_t i = E + threadIdx.x; i < P2; i += blockDim.x) sv[i] = 0xFFFFFFFFu;
             __syncthreads();
             bitonic_sort_block(sv, P2);
             __syncthreads();
             if (threadIdx.x == 0) {
                 uint32_t head = 0;
-                for (uint32_t i = 0; i < E; i++) w.heavy[sv[i]] = glibc_next(s.ring, head) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                for (uint32_t i = 0; i < E; i++) w.heavy[sv[i]] = glibc_next(s.ring, head) % (a.nCol - 1u);
                 uint32_t r[31];
                 for (uint32_t i = 0; i < 31u; i++) r[i] = s.ring[(head + i) % 31u];
                 for (uint32_t i = 0; i < 31u; i++) {
@@ -701,33 +972,41 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 st->glibc_draws = s.draws;
             }
             __syncthreads();
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+                if ((R[2u * i + 1u] >> 16) == a.nCol)
+                    R[2u * i + 1u] = (R[2u * i + 1u] & 0xFFFFu) | (w.heavy[R[2u * i]] << 16);
+            __syncthreads();
         }
+        mark(k, 5);
         // the changed rows: C_t+1 into the other buffer, listed with their arcs' prefix (per-thread
         // runs of the results, workgroup scans of their counts and arcs)
         uint32_t nch = 0, arcs = 0;
         {
             const uint32_t per = (N + blockDim.x - 1u) / blockDim.x, i0 = min(N, threadIdx.x * per), i1 = min(N, i0 + per);
+            uint32_t* const dg = tmp;   // degrees by result index (LDS results only)
             uint32_t mc = 0, ma = 0;
             for (uint32_t i = i0; i < i1; i++) {
-                const uint32_t l = w.res[2u * i], e = w.res[2u * i + 1u];
-                const uint32_t cv = e & 0xFFFFu, nc = (e >> 16) == a.nCol ? w.heavy[l] : (e >> 16);
+                const uint32_t l = R[2u * i], e = R[2u * i + 1u];
+                const uint32_t cv = e & 0xFFFFu, nc = e >> 16;
                 if (nc != cv) {
                     Cs[l] = (uint16_t)nc;
+                    const uint32_t d = (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                    if (inl) dg[i] = d;
                     mc++;
-                    ma += (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                    ma += d;
                 }
             }
             const uint32_t oc = ws_scan(mc, s_wsum, &nch);
             const uint32_t oa = ws_scan(ma, s_wsum, &arcs);
             uint32_t j = oc, run = oa;
             for (uint32_t i = i0; i < i1; i++) {
-                const uint32_t l = w.res[2u * i], e = w.res[2u * i + 1u];
-                const uint32_t cv = e & 0xFFFFu, nc = (e >> 16) == a.nCol ? w.heavy[l] : (e >> 16);
+                const uint32_t l = R[2u * i], e = R[2u * i + 1u];
+                const uint32_t cv = e & 0xFFFFu, nc = e >> 16;
                 if (nc != cv) {
-                    w.chg[2u * j] = l;
-                    w.chg[2u * j + 1u] = cv | (nc << 16);
+                    const uint64_t r0 = a.row_off[l];
+                    reinterpret_cast<uint4*>(w.chg)[j] = make_uint4(l, e, (uint32_t)r0, (uint32_t)(r0 >> 32));
                     w.pre[j] = run;
-                    run += (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                    run += inl ? dg[i] : (uint32_t)(a.row_off[l + 1] - r0);
                     j++;
                 }
             }
@@ -738,47 +1017,57 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 s.arcs += arcs;
             }
         }
-        mark(k, 5);
+        mark(k, 6);
         // the counts move: by the leader's threads when few arcs, else a delta phase
         if (nch) {
             if (arcs <= w.lead_arcs) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 const uint32_t* pre = w.pre;
-                if (nch + 1u <= 2u * kWsCandCap) {   // the prefix into LDS (the candidates' buffer)
+                if (nch + 1u <= 3u * kWsCandCap) {   // the prefix into LDS (the candidates' buffer: gone)
                     for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) cand[i] = w.pre[i];
                     __syncthreads();
                     pre = cand;
                 }
                 ws_delta_arcs(a, w, C, Cs, pre, nch, threadIdx.x, arcs, blockDim.x);
+                if (threadIdx.x == 0) s_pf = 0xFFFFFFFFu;
             } else {
+                // the helpers move the counts and find the next sweep's candidates (its log is lx + n,
+                // its colours are C_t+1, in Cs); only those candidates' counts must wait
+                const uint32_t lxn = s.lx + a.nmodN >= kMinstdN ? s.lx + a.nmodN - kMinstdN : s.lx + a.nmodN;
+                if (threadIdx.x == 0) {
+                    w.ctl[kWsArgL] = lxn;
+                    w.ctl[kWsCandN] = 0u;
+                }
                 post(kWsDelta);
                 wait();
-                if (threadIdx.x == 0) s.st[4]++;
+                if (threadIdx.x == 0) {
+                    s.st[4]++;
+                    s_pf = lxn;
+                    s_gn = dc_ld(&w.ctl[kWsCandN]);
+                }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             // both buffers = C_t+1
             for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x)
-                const_cast<uint16_t*>(C)[w.chg[2u * j]] = (uint16_t)(w.chg[2u * j + 1u] >> 16);
+                const_cast<uint16_t*>(C)[w.chg[4u * j]] = (uint16_t)(w.chg[4u * j + 1u] >> 16);
         }
-        mark(k, 6);
+        mark(k, 7);
         // the violators of C_t+1: those of C_t still counted and the touched rows (flags dedupe)
         {
             if (threadIdx.x == 0) {
                 s_w[0] = dc_ld(&w.ctl[kWsTchN]);
                 s_w[1] = dc_ld(&w.ctl[kWsTchOvf]);
+                s_vq = 0;
             }
-            __syncthreads();
+            dc_lbar();
             const uint32_t tn = s_w[0], tovf = s_w[1];
-            __syncthreads();
             if (threadIdx.x == 0) {
                 w.ctl[kWsVn + q] = 0u;
                 w.ctl[kWsTchN] = 0u;
                 w.ctl[kWsTchOvf] = 0u;
-                s_vq = 0;
             }
-            __syncthreads();
             if (!tovf && Vn + tn <= kWsLeadList) {
                 uint32_t* vq = w.vl + (size_t)q * nloc;
                 for (uint32_t i = threadIdx.x; i < Vn + tn; i += blockDim.x) {
@@ -802,7 +1091,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                         if (add) vq[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = l;
                     }
                 }
-                __syncthreads();
+                dc_lbar();
                 if (threadIdx.x == 0) w.ctl[kWsVn + q] = s_vq;
             } else {
                 if (threadIdx.x == 0) {
@@ -813,7 +1102,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 wait();
             }
         }
-        mark(k, 7);
+        mark(k, 8);
         // accept: the RNG advances by n draws (:139), lx with it
         if (threadIdx.x == 0) {
             s.t = t + 1u;
@@ -863,5 +1152,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         }
         unsigned long long* ss = reinterpret_cast<unsigned long long*>(w.ctl + kWsStat);
         for (int i = 0; i < 8; i++) ss[i] += s.st[i];
+        unsigned long long* tt = reinterpret_cast<unsigned long long*>(w.ctl + kWsTime);
+        for (int i = 0; i < 16; i++) tt[i] += s.tm[i];
     }
 }

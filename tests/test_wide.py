@@ -500,8 +500,10 @@ def test_wide_persistent_steps_alternate(M, monkeypatch):
     """step() batches of 1, 3, 16 and 2 sweeps through the persistent launch (each entry finds the
     violator list the last launch left): the trajectory and colouring equal one uninterrupted
     oracle run of 22 sweeps."""
-    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
-    ncol = 300
+    monkeypatch.setenv("MCMC_GATHER", "wide")   # nCol 16 on a dense graph: violators every sweep
+    O.srand(1)
+    off, idx = O.setup_rnd2(2000, 0.05)
+    ncol = 16
     g = M.Graph.from_csr(off, idx)
     params = M.ColoringMCMCParams(nCol=ncol, maxRip=40)
     col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
