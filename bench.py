@@ -63,6 +63,33 @@ KERNELS = {"dense": "dc_multi_kernel (persistent: the timed sweeps in one launch
            "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
 
+def ctx_stats(ctx) -> tuple:
+    """(dense, wide incremental, persistent wide) device statistics of a context handle -- a single
+    context or a partitioned rank: the bench prices a sweep by what these count, on every line."""
+    from mcmc_colorer_amd._lib import check, lib
+
+    def q(fn, k):
+        out = (ctypes.c_uint64 * k)()
+        check(getattr(lib(), fn)(ctx, out))
+        return [int(x) for x in out]
+    d = q("mcmc_get_dense_stats_v2", 16)
+    dense = {"enabled": bool(d[0]), "s0": d[1], "s1": d[2], "incremental_sweeps": d[3], "rebuilds": d[4],
+             "moved_vertices": d[5], "open_rows": d[6], "rebuild_threshold": d[7], "changed_rows": d[8],
+             "copy_sweeps": d[9], "solo_sweeps": d[10], "window_states": d[11], "persistent": bool(d[12]),
+             "open_words": d[13], "solo_evaluated": d[14]}
+    i = q("mcmc_get_wide_inc_stats", 5)
+    inc = {"enabled": bool(i[0]), "incremental_sweeps": i[1], "full_sweeps": i[2], "changed_rows": i[3],
+           "changed_arcs": i[4]}
+    w = q("mcmc_get_wide_solo_stats", 30)
+    keys = ("enabled", "window_states", "sweeps", "phases", "leader_walks", "walk_phases", "delta_phases",
+            "collects", "candidates", "changed_rows")
+    ws = {k: v for k, v in zip(keys, w)}
+    steps = ("walks", "candidates", "walk_wait", "events", "changes", "count_moves", "violator_list", "sweep")
+    ws["step_us"] = {k: w[14 + j] / 100.0 for j, k in enumerate(steps)}
+    ws["probe_us"] = [w[22 + j] / 100.0 for j in range(8)]
+    return dense, inc, ws
+
+
 def load_traffic(key: str):
     """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary (or None)."""
     p = ROOT / "profiles" / "pmc_summary.json"
@@ -438,17 +465,13 @@ def main() -> int:
         if a.warmup:
             check(lib().mcmc_bench_sweeps(col._ctx, a.warmup, ctypes.byref(tot), ctypes.byref(ker)))
         check(lib().mcmc_bench_prepare(col._ctx, a.steps))   # graph instantiation outside the timed region
-        inc0 = None if ref else col.wide_inc_stats()
-        ws0 = None if ref else col.wide_solo_stats()
-        dn0 = None if ref else col.dense_stats()
+        dn0, inc0, ws0 = (None, None, None) if ref else ctx_stats(col._ctx)
         t0 = time.perf_counter()
         check(lib().mcmc_bench_sweeps(col._ctx, a.steps, ctypes.byref(tot), ctypes.byref(ker)))
         wall = time.perf_counter() - t0
         kernel_ms = ker.value
         info = col.info()
-        inc1 = None if ref else col.wide_inc_stats()
-        ws1 = None if ref else col.wide_solo_stats()
-        dn1 = None if ref else col.dense_stats()
+        dn1, inc1, ws1 = (None, None, None) if ref else ctx_stats(col._ctx)
     else:
         import torch
 
@@ -462,10 +485,12 @@ def main() -> int:
         st = MCMCRunStats()
         if a.warmup:
             check(lib().mcmc_part_run(arr, 1, a.warmup, ctypes.byref(st)))
+        dn0, inc0, ws0 = ctx_stats(drv._ctx)
         barrier()
         t0 = time.perf_counter()
         check(lib().mcmc_part_run(arr, 1, a.steps, ctypes.byref(st)))   # sweeps + RCCL exchanges + commits
         barrier()
+        dn1, inc1, ws1 = ctx_stats(drv._ctx)
         wall = time.perf_counter() - t0
         kernel_ms = st.loopMs / a.steps   # device time of one whole step on this rank's stream
         xs = [ctypes.c_uint64() for _ in range(4)]
@@ -494,20 +519,12 @@ def main() -> int:
     variant = info["variant"]
     scan = None
     b_alg = b_fmt
-    if dist is not None:
-        dn0 = dn1 = None
-        if not ref:
-            out8 = (ctypes.c_uint64 * 10)()
-            check(lib().mcmc_get_dense_stats(drv._ctx, out8))
-            dn1 = {"enabled": bool(out8[0])}
     dense_on = bool(dn1 and dn1["enabled"])
     if dense_on:
         variant = "dense"
-        if dist is not None:   # this rank's evaluation bytes: its rows' colours and open words
-            nwd = 1 if a.ncol <= 32 else 2 if a.ncol <= 64 else 4 if a.ncol <= 128 else 8
-            b_alg = int(bounds[rank + 1] - bounds[rank]) * (1 + nwd / 8)
+    nrows = g.nNodes if dist is None else int(bounds[rank + 1] - bounds[rank])   # this context's rows
     dense = None
-    if dense_on and dist is None:
+    if dense_on:
         # the dense-count sweep (csrc/dense_counts.h): per sweep every row's own colour and its open
         # bits (NW bits) read; per row that changed colour its new colour written, and the restore
         # (read + write) into the next sweep's buffer; per vertex of the dense range that changed
@@ -527,12 +544,14 @@ def main() -> int:
         # moved vertex of S reads its local arcs (2 B ids) and moves two 4 B counts per arc; an open
         # row reads its mask and its arcs outside S with their colours (3 B per arc); a rebuild reads
         # the rows' arcs into S and writes counts, masks and a copy of the colours
+        # (this context's rows: a partitioned rank prices its own rows the same way)
         full = S - d["solo_sweeps"]
-        b_eval = full * n * (1.0 + nw / 8.0) + d["solo_evaluated"] * 9.0
-        b_chg = d["changed_rows"] * 10.0 + d["copy_sweeps"] * 2.0 * n
-        b_upd = d["moved_vertices"] * deg * 10.0
+        b_eval = full * nrows * (1.0 + nw / 8.0) + d["solo_evaluated"] * 9.0
+        b_chg = d["changed_rows"] * 10.0 + d["copy_sweeps"] * 2.0 * nrows
+        b_upd = d["moved_vertices"] * deg * (nrows / max(1, n)) * 10.0
         b_open = d["open_rows"] * (4.0 * nw + deg * (1.0 - span / max(1, n)) * 3.0)
-        b_rebuild = d["rebuilds"] * (n * deg * span / max(1, n) * 2.0 + n * a.ncol * 4.0 + n * nw * 4.0 + 2.0 * n)
+        b_rebuild = d["rebuilds"] * (nrows * deg * span / max(1, n) * 2.0 + nrows * a.ncol * 4.0 + nrows * nw * 4.0
+                                     + 2.0 * nrows)
         b_alg = (b_eval + b_chg + b_upd + b_open + b_rebuild) / S
         dense = dict(d, sweeps_counted=S, dense_range=[dn1["s0"], dn1["s1"]],
                      window_states=dn1["window_states"], persistent=dn1["persistent"],
@@ -550,7 +569,7 @@ def main() -> int:
                           "workgroup of a persistent launch of all the timed sweeps; full sweeps (the count "
                           "rebuild) run on the whole grid inside it. Bit-identical to the scan sweeps "
                           "(tests/test_dense.py, tests/test_c3_full.py).")
-        if not a.no_full_scan:
+        if not a.no_full_scan and dist is None:
             # the same graph through the tiled scan sweep (MCMC_DENSE=0, the r03 early-exit kernel) and
             # the full scan (MCMC_FULL_SCAN=1): every sweep scans the layout
             for label, env in (("scan_sweep", "MCMC_DENSE"), ("full_scan", "MCMC_FULL_SCAN")):
@@ -622,7 +641,7 @@ def main() -> int:
                                  "frac": b_fmt / (ker2.value * 1e-3) / 1e9 / HBM_PEAK_GBS}
             cf.close()
     wide_inc = None
-    if dist is None and not ref and variant == "wide" and inc1 and inc1["enabled"]:
+    if not ref and variant == "wide" and inc1 and inc1["enabled"]:
         # incremental violation counts (sweep_wide.h wide_inc_*): a sweep moves the counts by the rows
         # that changed colour instead of scanning the slab layout, so it is priced by what it reads:
         # per vertex its flag and colour (3 B), per changed row its offsets, list entries and the
@@ -636,7 +655,7 @@ def main() -> int:
         pw = {k: ws1[k] - ws0[k] for k in ("sweeps", "phases", "leader_walks", "walk_phases", "delta_phases",
                                             "collects", "candidates", "changed_rows")} if ws1 and ws1["enabled"] else None
         nws = pw["sweeps"] if pw else 0
-        b_alg = (3.0 * g.nNodes * max(0, d["incremental_sweeps"] - nws) + 14.0 * (pw["candidates"] if pw else 0)
+        b_alg = (3.0 * nrows * max(0, d["incremental_sweeps"] - nws) + 14.0 * (pw["candidates"] if pw else 0)
                  + 30.0 * d["changed_rows"] + 8.0 * d["changed_arcs"] + b_fmt * d["full_sweeps"]) / S
         wide_inc = dict(d, sweeps_counted=S, changed_rows_per_sweep=d["changed_rows"] / S,
                         changed_arcs_per_sweep=d["changed_arcs"] / S, bytes_per_sweep=b_alg,

@@ -125,6 +125,12 @@ __device__ __forceinline__ void ws_dbg(const WsArgs& w, uint32_t i, uint32_t v) 
     if (w.dbg != nullptr) __hip_atomic_store(&w.dbg[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A colour read coherently across workgroups without an acquire fence (a relaxed agent-scope load:
+// no L2 invalidation, see ws_kernel's hand-off notes).
+__device__ __forceinline__ uint32_t ld16c(const uint16_t* p) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned short*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // w[i] = the i-th state of the window [1, lo) U [hi, 2^31 - 1), L[i] = its logarithm; err |= 1 if a
 // logarithm fails its check 16807^L = w.
 __global__ __launch_bounds__(256) void ws_table_kernel(uint32_t* __restrict__ L, uint32_t* __restrict__ w, uint32_t lo,
@@ -204,16 +210,31 @@ __device__ __forceinline__ void ws_touch(const SweepArgs& a, const WsArgs& w, ui
 }
 
 // One light violator on one wave: its occupancy mask in the wave's set, its walk, the result.
-// Results go to (rcnt, rbuf): the global list (helpers) or the leader's LDS list.
+// Results go to (rcnt, rbuf): the global list (helpers) or the leader's LDS list. COH: colours read
+// with coherent loads (a helper phase without an acquire).
+template <bool COH>
 __device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t x_t,
                                               uint32_t l, uint32_t* mask, uint32_t lane, uint32_t* rcnt, uint32_t* rbuf) {
     const uint32_t NWW = (a.nCol + 31u) >> 5;
     uint32_t* pre = mask + ((NWW + 3u) & ~3u);
-    const uint32_t cv = C[l];
+    const uint32_t cv = COH ? ld16c(&C[l]) : C[l];
     const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)l + 1ull));   // u_v (:139)
     for (uint32_t i = lane; i < NWW; i += 64u) mask[i] = 0u;
     wave_lds_sync();
-    walk_gather_wave(a, C, mask, a.row_off[l], a.row_off[l + 1], lane);
+    {   // walk_gather_wave with the colour loads COH
+        const uint64_t k0 = a.row_off[l], k1 = a.row_off[l + 1];
+        for (uint64_t k = k0 + lane; k < k1; k += 8u * 64u) {
+            uint32_t c[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint64_t kk = k + (uint64_t)j * 64u;
+                c[j] = kk < k1 ? (COH ? ld16c(&C[a.col_idx[kk]]) : (uint32_t)C[a.col_idx[kk]]) : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (c[j] != 0xFFFFFFFFu) atomicOr(&mask[c[j] >> 5], 1u << (c[j] & 31u));
+        }
+    }
     wave_lds_sync();
     const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
     if (lane == 0 && nc != cv) {
@@ -223,6 +244,7 @@ __device__ __forceinline__ void ws_walk_light(const SweepArgs& a, const uint16_t
     }
 }
 // One heavy violator on the whole workgroup (mask set 0); all threads call it.
+template <bool COH>
 __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t* __restrict__ C, uint32_t x_t,
                                               uint32_t l, uint32_t* mask, uint32_t* rcnt, uint32_t* rbuf) {
     const uint32_t NWW = (a.nCol + 31u) >> 5, lane = threadIdx.x & 63u;
@@ -236,7 +258,7 @@ __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t
 #pragma unroll
             for (int j = 0; j < 16; j++) {
                 const uint64_t kk = k + (uint64_t)j * blockDim.x;
-                c[j] = kk < k1 ? (uint32_t)C[a.col_idx[kk]] : 0xFFFFFFFFu;
+                c[j] = kk < k1 ? (COH ? ld16c(&C[a.col_idx[kk]]) : (uint32_t)C[a.col_idx[kk]]) : 0xFFFFFFFFu;
             }
 #pragma unroll
             for (int j = 0; j < 16; j++)
@@ -245,7 +267,7 @@ __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t
     }
     __syncthreads();
     if (threadIdx.x < 64u) {
-        const uint32_t cv = C[l];
+        const uint32_t cv = COH ? ld16c(&C[l]) : C[l];
         const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)l + 1ull));
         const uint32_t nc = ws_mask_walk(a, mask, pre, cv, minstd_canonical(x), lane);
         if (lane == 0 && nc != cv) {
@@ -260,6 +282,7 @@ __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t
 // Arcs [k, k1) (step) of the flattened changed-row arcs: both ends' counts move by [Cn equal] -
 // [Cp equal] (an arc whose other end changed too only from the smaller end; self-arcs never move).
 // pre: the prefix (LDS or global), nch changed rows.
+template <bool COH>   // COH: the list and the colours read with coherent loads (a helper, no acquire)
 __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ Cp,
                                               const uint16_t* __restrict__ Cn, const uint32_t* pre, uint32_t nch,
                                               uint32_t k, uint32_t k1, uint32_t step) {
@@ -270,11 +293,19 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
             const uint32_t mid = (lo + hi) >> 1;
             if (pre[mid] <= k) lo = mid; else hi = mid;
         }
-        const uint4 ch = reinterpret_cast<const uint4*>(w.chg)[lo];
+        uint4 ch;
+        if (COH) {
+            ch.x = dc_ld(&w.chg[4u * lo]);
+            ch.y = dc_ld(&w.chg[4u * lo + 1u]);
+            ch.z = dc_ld(&w.chg[4u * lo + 2u]);
+            ch.w = dc_ld(&w.chg[4u * lo + 3u]);
+        } else {
+            ch = reinterpret_cast<const uint4*>(w.chg)[lo];
+        }
         const uint32_t v = ch.x, cov = ch.y & 0xFFFFu, cnv = ch.y >> 16;
         const uint32_t u = a.col_idx[(((uint64_t)ch.w << 32) | ch.z) + (k - pre[lo])];
         if (u == v) continue;
-        const uint32_t ou = Cp[u], nu = Cn[u];
+        const uint32_t ou = COH ? ld16c(&Cp[u]) : Cp[u], nu = COH ? ld16c(&Cn[u]) : Cn[u];
         if (ou != nu && u < v) continue;
         const int d = (int)(nu == cnv) - (int)(ou == cov);
         if (d == 0) continue;
@@ -292,7 +323,7 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
     const uint32_t H = gridDim.x - 1u, h = blockIdx.x - 1u, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gt = h * blockDim.x + threadIdx.x, GT = H * blockDim.x;
     const uint32_t nloc = a.v_end - a.v_begin;
-    const uint32_t t = w.ctl[kWsArgT], P = w.ctl[kWsArgP];
+    const uint32_t t = dc_ld(&w.ctl[kWsArgT]), P = dc_ld(&w.ctl[kWsArgP]);
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);   // C_t
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     if (kind == kWsZero) {   // counts to zero (a recount follows)
@@ -365,7 +396,7 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
     } else if (kind == kWsWalkLight) {
         // violator list P: entries h, h + H, ... of this workgroup; its waves walk the light ones
         // (one each), then the whole workgroup the heavy ones (listed in LDS)
-        const uint32_t Vn = w.ctl[kWsVn + P], x_t = w.ctl[kWsArgP + 1];
+        const uint32_t Vn = dc_ld(&w.ctl[kWsVn + P]), x_t = dc_ld(&w.ctl[kWsArgP + 1]);
         const uint32_t* vl = w.vl + (size_t)P * nloc;
         __shared__ uint32_t s_hn, s_hv[64];
         if (threadIdx.x == 0) s_hn = 0;
@@ -373,7 +404,7 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         if (wv < w.sets) {
             uint32_t* mask = dyn + wv * walk_set_words(a.nCol);
             for (uint32_t i = h + H * wv; i < Vn; i += H * w.sets) {
-                const uint32_t l = vl[i];
+                const uint32_t l = dc_ld(&vl[i]);
                 if (a.row_off[l + 1] - a.row_off[l] > w.light_arcs) {
                     if (lane == 0) {
                         const uint32_t j = atomicAdd(&s_hn, 1u);
@@ -382,33 +413,40 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
                     }
                     continue;
                 }
-                ws_walk_light(a, C, x_t, l, mask, lane, &w.ctl[kWsResN], w.res);
+                ws_walk_light<true>(a, C, x_t, l, mask, lane, &w.ctl[kWsResN], w.res);
             }
         }
         __syncthreads();
         const uint32_t hn = min(s_hn, 64u);
-        for (uint32_t j = 0; j < hn; j++) ws_walk_heavy(a, C, x_t, s_hv[j], dyn, &w.ctl[kWsResN], w.res);
+        for (uint32_t j = 0; j < hn; j++) ws_walk_heavy<true>(a, C, x_t, s_hv[j], dyn, &w.ctl[kWsResN], w.res);
     } else if (kind == kWsWalkHeavy) {
-        const uint32_t hn = w.ctl[kWsHeavyN];
+        const uint32_t hn = dc_ld(&w.ctl[kWsHeavyN]), x_t = dc_ld(&w.ctl[kWsArgP + 1]);
         for (uint32_t j = h; j < hn; j += H)
-            ws_walk_heavy(a, C, w.ctl[kWsArgP + 1], w.heavy[j], dyn, &w.ctl[kWsResN], w.res);
-    } else if (kind == kWsDelta) {   // the changed rows' arcs (prefix cached in LDS where it fits)
-        const uint32_t nch = w.ctl[kWsChgN];
+            ws_walk_heavy<true>(a, C, x_t, dc_ld(&w.heavy[j]), dyn, &w.ctl[kWsResN], w.res);
+    } else if (kind == kWsDelta) {
+        // the changed rows' arcs (prefix cached in LDS where it fits). This phase runs without an
+        // acquire (no L2 invalidation on every XCD per sweep): what the leader wrote for it -- the
+        // list, the prefix, the colours of C_t+1 -- is read with coherent loads
+        const uint32_t nch = dc_ld(&w.ctl[kWsChgN]);
         const uint32_t* pre = w.pre;
         if (nch + 1u <= kWsPreLds) {
-            for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) dyn[i] = w.pre[i];
+            for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) dyn[i] = dc_ld(&w.pre[i]);
             __syncthreads();
             pre = dyn;
         }
-        ws_delta_arcs(a, w, C, Cs, pre, nch, gt, pre[nch], GT);
+        // arcs dealt round-robin over the workgroups (h, h + H, ...): a few thousand random reads
+        // spread over every CU rather than filling the first few
+        const uint32_t tot = nch + 1u <= kWsPreLds ? pre[nch] : dc_ld(&w.pre[nch]);
+        ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * blockDim.x);
         // meanwhile the next sweep's candidates (its colours: C_t+1, in Cs): those that change
-        // colour unless they turn out violators, into gcand
-        const WsRuns r = ws_runs(w, w.ctl[kWsArgL], nloc);
-        for (uint32_t j0 = gt & ~63u; j0 < r.tot; j0 += GT) {   // (wave-uniform bounds)
+        // colour unless they turn out violators, into gcand -- a slice of the entries per workgroup
+        const WsRuns r = ws_runs(w, dc_ld(&w.ctl[kWsArgL]), nloc);
+        const uint32_t per = (r.tot + H - 1u) / H, jb = min(r.tot, h * per), je = min(r.tot, jb + per);
+        for (uint32_t j0 = jb + wv * 64u; j0 < je; j0 += blockDim.x) {   // (wave-uniform bounds)
             uint32_t l = 0, x = 1, cv = 0, nc = 0;
-            bool in = j0 + lane < r.tot && ws_entry(w, r, j0 + lane, l, x);
+            bool in = j0 + lane < je && ws_entry(w, r, j0 + lane, l, x);
             if (in) {
-                cv = Cs[l];
+                cv = ld16c(&Cs[l]);
                 nc = ws_own_walk(a, cv, x);
                 in = nc != cv;
             }
@@ -457,7 +495,7 @@ struct WsState {
     unsigned long long st[8];
     unsigned long long arcs;        // the changed rows' arcs (the incremental statistics)
     uint32_t recounts;
-    unsigned long long tm[16], t0, ts, tp;   // ticks per step: walks, candidates, walk wait, events, changes,
+    unsigned long long tm[16], t0, ts, tp, tc;   // ticks per step: walks, candidates, walk wait, events, changes,
                                     // count moves, violator list, whole sweeps
 };
 
@@ -501,8 +539,11 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     if (wall_clock64() - t0 > kWsIdleTicks) { g = kWsExit; break; }
                     for (uint32_t z = 0; z < w.poll; z++) __builtin_amdgcn_s_sleep(2);   // (0: spin)
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if ((g & 15u) != kWsDelta && (g & 15u) != kWsWalkLight && (g & 15u) != kWsWalkHeavy) {
+                    // (the per-sweep phases read what the leader wrote coherently instead)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
                 if (threadIdx.x == 0) sh_g = g;
             }
             __syncthreads();
@@ -548,7 +589,9 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         }
         __syncthreads();
     };
-    auto wait = [&]() {   // wave 0 waits (a wave-uniform loop, as the helpers poll)
+    // acq: an acquire after the phase (L2 invalidation): the rare phases whose plain writes the
+    // leader then reads plainly; the per-sweep ones are read back with coherent loads instead
+    auto wait = [&](bool acq = true) {   // wave 0 waits (a wave-uniform loop, as the helpers poll)
         if (threadIdx.x < 64u && __builtin_amdgcn_readfirstlane(s.err) == 0u) {
             const unsigned long long t0 = wall_clock64();
             const uint32_t ex = __builtin_amdgcn_readfirstlane(s_exp);
@@ -569,8 +612,10 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (acq) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
         __syncthreads();
     };
@@ -585,8 +630,14 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         if (threadIdx.x == 0) {
             const unsigned long long now = wall_clock64();
             if (step >= 2u && step <= 8u) s.tm[step - 2u] += now - s.t0;
-            if (step == 8u) s.tm[7] += now - s.ts;
-            if (step == 1u) s.ts = now;
+            if (step == 8u) {
+                s.tm[7] += now - s.ts;
+                s.tm[8] += __builtin_amdgcn_s_memtime() - s.tc;   // [8] shader clocks of the sweeps
+            }
+            if (step == 1u) {
+                s.ts = now;
+                s.tc = __builtin_amdgcn_s_memtime();
+            }
             if (step >= 1u && step <= 8u) s.t0 = now;
             w.ctl[kWsDbg] = k;
             w.ctl[kWsDbg + 1] = step;
@@ -790,7 +841,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             lead = s_nh == 0u;
         }
         if (lead) {
-            if (wv < Vn) ws_walk_light(a, C, s.x_t, vl[wv], sets + wv * SW, lane, &s_nr, lres);
+            if (wv < Vn) ws_walk_light<false>(a, C, s.x_t, vl[wv], sets + wv * SW, lane, &s_nr, lres);
             dc_lbar();
             if (threadIdx.x == 0) s.st[2] += Vn;
         } else if (Vn > 0u) {
@@ -808,7 +859,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             const uint32_t* cl = pre_g ? w.gcand : cand;
             for (uint32_t b0 = wv * 64u; b0 < nc; b0 += blockDim.x) {   // (wave-uniform bounds)
                 const uint32_t kk = b0 + lane;
-                const uint32_t l = kk < nc ? cl[3u * kk] : 0u;
+                const uint32_t l = kk < nc ? (pre_g ? dc_ld(&cl[3u * kk]) : cl[3u * kk]) : 0u;
                 const bool keep = kk < nc && dc_ld(&a.inc_vcnt[l]) == 0u;   // a violator: walked above
                 const uint64_t m = __ballot(keep);
                 if (m == 0) continue;
@@ -818,7 +869,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 b = __shfl(b, ld, 64);
                 const uint32_t j = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (keep) {
-                    const uint32_t e = cl[3u * kk + 2u];
+                    const uint32_t e = pre_g ? dc_ld(&cl[3u * kk + 2u]) : cl[3u * kk + 2u];
                     if (j < kWsResLds) {
                         lres[2u * j] = l;
                         lres[2u * j + 1u] = e;
@@ -858,13 +909,13 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             }
         }
         mark(k, 3);
-        if (walking) {
-            wait();
+        if (walking) {   // (their results are read back coherently: no acquire)
+            wait(false);
             if (threadIdx.x == 0) s_w[0] = dc_ld(&w.ctl[kWsHeavyN]);   // heavy rows past a workgroup's 64
             __syncthreads();
             if (s_w[0] > 0u) {
                 post(kWsWalkHeavy);
-                wait();
+                wait(false);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -883,8 +934,13 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         uint32_t* const R = inl ? lres : w.res;
         const uint32_t N = Nl + Ng;
         if (inl) {
-            for (uint32_t i = threadIdx.x; i < 2u * Ng; i += blockDim.x) lres[2u * Nl + i] = w.res[i];
+            for (uint32_t i = threadIdx.x; i < 2u * Ng; i += blockDim.x) lres[2u * Nl + i] = dc_ld(&w.res[i]);
         } else {
+            if (threadIdx.x == 0) {   // (the global list is read plainly from here: acquire)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
             for (uint32_t i = threadIdx.x; i < 2u * Nl; i += blockDim.x) w.res[2u * Ng + i] = lres[i];
         }
         if (inl) dc_lbar(); else __syncthreads();
@@ -904,41 +960,49 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         const uint32_t E = s_ne;
 
         if (E > 0u && E <= kWsRankMax) {
-            // (vertex, result index) pairs sorted in LDS (bitonic), then draw r on thread r (the
-            // table's columns side by side) for the event of rank r
-            uint32_t P2 = 1;
-            while (P2 < E) P2 <<= 1;
-            unsigned long long* const kv = reinterpret_cast<unsigned long long*>(tmp);   // [P2]
-            uint32_t* const raw = evl;   // [E] raw draws by rank (the indices are in kv)
-            for (uint32_t i = threadIdx.x; i < P2; i += blockDim.x)
-                kv[i] = i < E ? (((unsigned long long)R[2u * evl[i]] << 32) | evl[i]) : ~0ull;
+            // ranks by vertex: a counting sort over 1024 buckets of the row range (events are few
+            // and spread: a bucket holds about one), then the order inside each bucket; beside it
+            // the E raw draws, one per thread (glibc's r_i = r_i-31 + r_i-3 as a table of powers)
+            uint32_t* const bc = tmp;               // [1024] events per bucket, then their offsets
+            uint32_t* const bf = tmp + 1024u;       // [1024] fill counters
+            uint32_t* const sl = tmp + 2048u;       // [E] the events' vertices, bucket by bucket
+            uint32_t* const raw = evl + kWsRankMax; // [E] raw draws in order (rand() = raw >> 1)
+            bc[threadIdx.x] = 0u;
+            bf[threadIdx.x] = 0u;
             dc_lbar();
-            probe(5);   // [13] the keys
-            for (uint32_t kb = 2; kb <= P2; kb <<= 1) {
-                for (uint32_t jb = kb >> 1; jb > 0; jb >>= 1) {
-                    for (uint32_t i = threadIdx.x; i < P2; i += blockDim.x) {
-                        const uint32_t ixj = i ^ jb;
-                        if (ixj > i) {
-                            const bool up = (i & kb) == 0;
-                            const unsigned long long x0 = kv[i], y0 = kv[ixj];
-                            if ((x0 > y0) == up) { kv[i] = y0; kv[ixj] = x0; }
-                        }
-                    }
-                    dc_lbar();
-                }
-            }
-            probe(6);   // [14] the sort
+            uint32_t ii = 0, v = 0, bk = 0;
             if (threadIdx.x < E) {
-                const uint32_t r = threadIdx.x, ii = (uint32_t)kv[r];
+                ii = evl[threadIdx.x];
+                v = R[2u * ii];
+                bk = (uint32_t)(((uint64_t)v * 1024u) / nloc);
+                atomicAdd(&bc[bk], 1u);
+            }
+            if (threadIdx.x < E) {   // raw draw r on thread r: sum_m T[m][r] ring[m] (the commit's table)
+                const uint32_t rr = threadIdx.x;
+                uint32_t tv[31];
+#pragma unroll
+                for (int m = 0; m < 31; m++) tv[m] = kGlibcTab[m * kGlibcTabK + rr];
                 uint32_t acc = 0;
 #pragma unroll
-                for (int m = 0; m < 31; m++) acc += kGlibcTab[m * kGlibcTabK + r] * s_ring[m];
-                raw[r] = acc;
-                const uint32_t c = (acc >> 1) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
+                for (int m = 0; m < 31; m++) acc += tv[m] * s_ring[m];
+                raw[rr] = acc;
+            }
+            dc_lbar();
+            uint32_t tot = 0;
+            const uint32_t off = ws_scan(bc[threadIdx.x], s_wsum, &tot);
+            bc[threadIdx.x] = off;
+            dc_lbar();
+            if (threadIdx.x < E) sl[bc[bk] + atomicAdd(&bf[bk], 1u)] = v;
+            dc_lbar();
+            probe(6);   // [14] buckets
+            if (threadIdx.x < E) {
+                uint32_t rk = bc[bk];
+                for (uint32_t j = bc[bk], je = bc[bk] + bf[bk]; j < je; j++) rk += sl[j] < v ? 1u : 0u;
+                const uint32_t c = (raw[rk] >> 1) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
                 R[2u * ii + 1u] = (R[2u * ii + 1u] & 0xFFFFu) | (c << 16);
             }
             dc_lbar();
-            probe(7);   // [15] the draws
+            probe(7);   // [15] ranks and colours
             if (threadIdx.x < 31u) {   // the window after E draws, oldest first
                 const uint32_t nw = (E < 31u && threadIdx.x < 31u - E) ? s_ring[E + threadIdx.x] : raw[E + threadIdx.x - 31u];
                 s.ring[threadIdx.x] = nw;
@@ -978,8 +1042,9 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             __syncthreads();
         }
         mark(k, 5);
-        // the changed rows: C_t+1 into the other buffer, listed with their arcs' prefix (per-thread
-        // runs of the results, workgroup scans of their counts and arcs)
+        // the changed rows: C_t+1 into the other buffer; every result listed (by result index) with
+        // its row start and its arcs' prefix (an unchanged one -- an overflow that drew its own
+        // colour -- with no arcs), per-thread runs of the results, workgroup scans
         uint32_t nch = 0, arcs = 0;
         {
             const uint32_t per = (N + blockDim.x - 1u) / blockDim.x, i0 = min(N, threadIdx.x * per), i1 = min(N, i0 + per);
@@ -988,31 +1053,29 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             for (uint32_t i = i0; i < i1; i++) {
                 const uint32_t l = R[2u * i], e = R[2u * i + 1u];
                 const uint32_t cv = e & 0xFFFFu, nc = e >> 16;
+                uint32_t d = 0;
+                uint64_t r0 = 0;
                 if (nc != cv) {
                     Cs[l] = (uint16_t)nc;
-                    const uint32_t d = (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
-                    if (inl) dg[i] = d;
+                    r0 = a.row_off[l];
+                    d = (uint32_t)(a.row_off[l + 1] - r0);
                     mc++;
-                    ma += d;
                 }
+                reinterpret_cast<uint4*>(w.chg)[i] = make_uint4(l, e, (uint32_t)r0, (uint32_t)(r0 >> 32));
+                if (inl) dg[i] = d;
+                else w.pre[i] = d;
+                ma += d;
             }
-            const uint32_t oc = ws_scan(mc, s_wsum, &nch);
-            const uint32_t oa = ws_scan(ma, s_wsum, &arcs);
-            uint32_t j = oc, run = oa;
+            (void)ws_scan(mc, s_wsum, &nch);
+            uint32_t run = ws_scan(ma, s_wsum, &arcs);
             for (uint32_t i = i0; i < i1; i++) {
-                const uint32_t l = R[2u * i], e = R[2u * i + 1u];
-                const uint32_t cv = e & 0xFFFFu, nc = e >> 16;
-                if (nc != cv) {
-                    const uint64_t r0 = a.row_off[l];
-                    reinterpret_cast<uint4*>(w.chg)[j] = make_uint4(l, e, (uint32_t)r0, (uint32_t)(r0 >> 32));
-                    w.pre[j] = run;
-                    run += inl ? dg[i] : (uint32_t)(a.row_off[l + 1] - r0);
-                    j++;
-                }
+                const uint32_t d = inl ? dg[i] : w.pre[i];
+                w.pre[i] = run;
+                run += d;
             }
             if (threadIdx.x == 0) {
-                w.pre[nch] = arcs;
-                w.ctl[kWsChgN] = nch;
+                w.pre[N] = arcs;
+                w.ctl[kWsChgN] = N;
                 s.st[7] += nch;
                 s.arcs += arcs;
             }
@@ -1020,16 +1083,17 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         mark(k, 6);
         // the counts move: by the leader's threads when few arcs, else a delta phase
         if (nch) {
+            const uint32_t nl = N;   // listed results (changed or not)
             if (arcs <= w.lead_arcs) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 const uint32_t* pre = w.pre;
-                if (nch + 1u <= 3u * kWsCandCap) {   // the prefix into LDS (the candidates' buffer: gone)
-                    for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) cand[i] = w.pre[i];
+                if (nl + 1u <= 3u * kWsCandCap) {   // the prefix into LDS (the candidates' buffer: gone)
+                    for (uint32_t i = threadIdx.x; i <= nl; i += blockDim.x) cand[i] = w.pre[i];
                     __syncthreads();
                     pre = cand;
                 }
-                ws_delta_arcs(a, w, C, Cs, pre, nch, threadIdx.x, arcs, blockDim.x);
+                ws_delta_arcs<false>(a, w, C, Cs, pre, nl, threadIdx.x, arcs, blockDim.x);
                 if (threadIdx.x == 0) s_pf = 0xFFFFFFFFu;
             } else {
                 // the helpers move the counts and find the next sweep's candidates (its log is lx + n,
@@ -1040,7 +1104,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     w.ctl[kWsCandN] = 0u;
                 }
                 post(kWsDelta);
-                wait();
+                wait(false);   // (candidates and touched rows read back coherently)
                 if (threadIdx.x == 0) {
                     s.st[4]++;
                     s_pf = lxn;
@@ -1050,8 +1114,10 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             // both buffers = C_t+1
-            for (uint32_t j = threadIdx.x; j < nch; j += blockDim.x)
-                const_cast<uint16_t*>(C)[w.chg[4u * j]] = (uint16_t)(w.chg[4u * j + 1u] >> 16);
+            for (uint32_t j = threadIdx.x; j < nl; j += blockDim.x) {
+                const uint32_t e = w.chg[4u * j + 1u];
+                if ((e >> 16) != (e & 0xFFFFu)) const_cast<uint16_t*>(C)[w.chg[4u * j]] = (uint16_t)(e >> 16);
+            }
         }
         mark(k, 7);
         // the violators of C_t+1: those of C_t still counted and the touched rows (flags dedupe)
@@ -1072,7 +1138,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 uint32_t* vq = w.vl + (size_t)q * nloc;
                 for (uint32_t i = threadIdx.x; i < Vn + tn; i += blockDim.x) {
                     const bool old = i < Vn;
-                    const uint32_t l = old ? vl[i] : w.tch[i - Vn];
+                    const uint32_t l = old ? vl[i] : dc_ld(&w.tch[i - Vn]);
                     const bool on = dc_ld(&a.inc_vcnt[l]) > 0u;
                     const uint32_t bit = 1u << (8u * (l & 3u));
                     bool add = false;
