@@ -3251,10 +3251,12 @@ struct mcmc_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipGraphExec_t batch_exec = nullptr;
+    hipGraphExec_t batch_exec_ws = nullptr;   // the same batch through the persistent wide sweep
     hipGraphExec_t bench_exec = nullptr;   // mcmc_bench_prepare
     uint32_t bench_n = 0;
     bool borrowed_stream = false;
     uint32_t batch = 0;
+    uint32_t batch_ws = 0;
     GlibcWindow glibc{};
     bool initialized = false;
     bool ran = false;
@@ -3332,6 +3334,11 @@ struct mcmc_ctx {
     WsArgs wsa{};                   // (wsa.ctl != nullptr: set up)
     uint32_t* ws_dbg_host = nullptr; // MCMC_WS_DEBUG: the progress words (host memory, device-mapped)
     uint32_t ws_grid = 0;
+    bool ws_on = false;             // launch_sweeps takes the persistent wide sweep
+    bool bench_ws = false;          // ws_on when bench_exec was captured
+    bool traj_ok = false;           // traj[t - 1] holds Cviol_{t-1} of the current chain (mcmc_run)
+    long long ws_enter = 512;       // MCMC_WS_ENTER: largest Cviol a batch enters the persistent sweep
+                                    // with (< 0: every batch, the colouring's first included)
     uint32_t cbytes = 1;            // bytes per colour in the replicas
     uint32_t* chunk_row = nullptr;
     uint32_t nchunks = 0;
@@ -3652,15 +3659,17 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
 }
 
 // K sweeps on the context stream: one persistent dense launch (dc_multi_kernel) where the context
-// has it (setup_dense_window; MCMC_DENSE_MULTI=0: never) and the arguments allow it (single context,
-// committing in the sweep; no taboo, no tail-cut flags, no diagnostics); else K (sweep, commit) pairs.
+// has it (setup_dense_window; MCMC_DENSE_MULTI=0: never) and the arguments allow it (single context
+// or a world-1 partition, committing in the sweep; no taboo, no tail-cut flags, no diagnostics); the
+// persistent wide sweep (wide_solo.h) where set up and chosen (ws_choose); else K (sweep, commit) pairs.
 void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
-    if (c->wsa.ctl && !c->part && a.taboo == nullptr && a.vflags == nullptr && a.scan_stats == nullptr &&
+    const bool solo = !c->part || c->world == 1;   // nothing leaves the context
+    if (c->wsa.ctl && c->ws_on && solo && a.dcap == 0u && a.taboo == nullptr && a.vflags == nullptr && a.scan_stats == nullptr &&
         a.phase_ts == nullptr && a.pair_trace == nullptr && a.inc != nullptr) {
         if (K) ws_kernel<<<c->ws_grid, 1024, kWsLds, c->stream>>>(a, c->wsa, K);
         return;
     }
-    if (c->dcm_launch && a.fused == 1 && !c->part && a.taboo == nullptr && a.vflags == nullptr &&
+    if (c->dcm_launch && a.fused == 1 && solo && a.dcap == 0u && a.taboo == nullptr && a.vflags == nullptr &&
         a.scan_stats == nullptr && a.phase_ts == nullptr && a.pair_trace == nullptr) {
         if (K) c->dcm_launch(a, K, c->grid, c->stream);
         return;
@@ -3668,18 +3677,50 @@ void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
     for (uint32_t i = 0; i < K; i++) launch_pair(c, a);
 }
 
+// The batch graph of the path c->ws_on selects (one cached graph per path: a run switches once,
+// from the per-sweep path to the persistent sweep, when the violators have thinned out)
 int build_batch_graph(mcmc_ctx* c, uint32_t batch) {
-    if (c->batch_exec && c->batch == batch) return MCMC_OK;
-    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }
+    hipGraphExec_t& ex = c->ws_on ? c->batch_exec_ws : c->batch_exec;
+    uint32_t& key = c->ws_on ? c->batch_ws : c->batch;
+    if (ex && key == batch) return MCMC_OK;
+    if (ex) { (void)hipGraphExecDestroy(ex); ex = nullptr; }
     SweepArgs a = make_args(c, 1);
     hipGraph_t graph;
     MCMC_HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     launch_sweeps(c, a, batch);
     MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
-    hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
+    hipError_t e = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-    c->batch = batch;
+    key = batch;
+    return MCMC_OK;
+}
+
+void drop_graphs(mcmc_ctx* c) {
+    if (c->batch_exec) (void)hipGraphExecDestroy(c->batch_exec);
+    if (c->batch_exec_ws) (void)hipGraphExecDestroy(c->batch_exec_ws);
+    if (c->bench_exec) (void)hipGraphExecDestroy(c->bench_exec);
+    c->batch_exec = c->batch_exec_ws = c->bench_exec = nullptr;
+    c->batch = c->batch_ws = c->bench_n = 0;
+}
+
+// Path choice for the next batch of a whole-graph run. The persistent wide sweep (wide_solo.h)
+// rebuilds its violator lists and counts on entry and walks the violators on a few workgroups, so it
+// beats the per-sweep path only near convergence (C5: 53 vs 66 us per converged sweep, but 2.1 vs
+// 1.0 ms per sweep at nCol = maxDeg / 4 where every sweep has ~10^4 violators): it takes batches
+// whose latest Cviol is at most ws_enter. last_viol < 0: unknown (a fresh colouring).
+void ws_choose(mcmc_ctx* c, long long last_viol) {
+    if (!c->wsa.ctl) { c->ws_on = false; return; }
+    c->ws_on = c->ws_enter < 0 || (last_viol >= 0 && last_viol <= c->ws_enter);
+}
+
+// Cviol of the latest accepted colouring from the trajectory, -1 when it is not known
+int last_cviol(mcmc_ctx* c, const DevState& h, long long* out) {
+    *out = -1;
+    if (!c->wsa.ctl || !c->traj_ok || h.t == 0 || h.t - 1u >= c->traj_cap) return MCMC_OK;
+    unsigned long long v = 0;
+    MCMC_HIP_TRY(hipMemcpy(&v, c->traj + (h.t - 1u), sizeof(v), hipMemcpyDeviceToHost));
+    *out = (long long)v;
     return MCMC_OK;
 }
 
@@ -4022,6 +4063,7 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     uint64_t wmax = 1ull << 24;
     if (const char* m = getenv("MCMC_WS_MAX")) wmax = strtoull(m, nullptr, 10);
     if (nw == 0 || nw > wmax) return MCMC_OK;
+    if (const char* m = getenv("MCMC_WS_ENTER")) c->ws_enter = strtoll(m, nullptr, 10);
     const size_t nloc = c->v_end - c->v_begin;
     const size_t words = 4 + kWsWords + 2 * nloc + (nloc + 3) / 4 + 2 * nloc + 4 * nloc + (nloc + 1) + nloc + nloc + 3 * nloc +
                          2 * nw + (kWsNB + 1);
@@ -4740,6 +4782,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     const uint32_t n = c->n;
     const uint32_t s0 = minstd_seed_state(c->p.seed);
     if (c->wflag) MCMC_HIP_TRY(hipMemsetAsync(c->wflag, 0, std::max<uint32_t>(c->v_end - c->v_begin, 1u), c->stream));
+    c->traj_ok = false;
     if (c->inc) MCMC_HIP_TRY(inc_reset(c));
     if (c->dc) MCMC_HIP_TRY(dc_reset(c));
     if (C0) {
@@ -4808,15 +4851,24 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     const uint32_t total = max_sweeps ? max_sweeps : c->p.maxRip + 2;   // +1 final count pass
     const uint32_t batch = std::min<uint32_t>(16u, total);
-    int rc = build_batch_graph(c, batch);
+    DevState h{};
+    long long lv = -1;
+    int rc = MCMC_OK;
+    if (c->wsa.ctl && c->ran) {
+        rc = download_state(c, &h);
+        if (rc == MCMC_OK) rc = last_cviol(c, h, &lv);
+        if (rc) return rc;
+    }
+    ws_choose(c, lv);
+    rc = build_batch_graph(c, batch);
     if (rc) return rc;
     c->ran = true;
+    c->traj_ok = true;
     MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
     uint32_t launched = 0;
-    DevState h{};
     while (launched < total) {
         if (total - launched >= batch) {
-            MCMC_HIP_TRY(hipGraphLaunch(c->batch_exec, c->stream));
+            MCMC_HIP_TRY(hipGraphLaunch(c->ws_on ? c->batch_exec_ws : c->batch_exec, c->stream));
             launched += batch;
         } else {
             SweepArgs a = make_args(c, 1);
@@ -4827,6 +4879,12 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
         rc = download_state(c, &h);
         if (rc) return rc;
         if (h.done || h.err) break;
+        if (c->wsa.ctl && !c->ws_on && launched < total) {   // near convergence: the persistent sweep
+            rc = last_cviol(c, h, &lv);
+            if (rc) return rc;
+            ws_choose(c, lv);
+            if (c->ws_on && (rc = build_batch_graph(c, batch))) return rc;
+        }
     }
     MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
     MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
@@ -4899,8 +4957,7 @@ int mcmc_set_scan_stats(mcmc_ctx* c, int on) {
     if (on && !c->scan_stats) MCMC_HIP_TRY(hipMalloc(&c->scan_stats, 6 * sizeof(unsigned long long)));
     if (on) MCMC_HIP_TRY(hipMemsetAsync(c->scan_stats, 0, 6 * sizeof(unsigned long long), c->stream));
     c->scan_stats_on = on != 0;
-    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
-    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
+    drop_graphs(c);
     return MCMC_OK;
 }
 
@@ -5023,7 +5080,7 @@ int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]) {
 int mcmc_set_bench_mode(mcmc_ctx* c, int on) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     c->bench_mode = on ? 1 : 0;
-    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
+    drop_graphs(c);
     return MCMC_OK;
 }
 
@@ -5038,10 +5095,7 @@ int mcmc_set_tailcut_repair(mcmc_ctx* c, uint32_t max_passes) {
     }
     if ((max_passes != 0) != (c->tailcut_max != 0)) {
         // captured sweeps carry the flag pointer: re-capture with the new setting
-        if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }
-        if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
-        c->batch = 0;
-        c->bench_n = 0;
+        drop_graphs(c);
     }
     c->tailcut_max = max_passes;
     return MCMC_OK;
@@ -5054,9 +5108,7 @@ int mcmc_ref_init(mcmc_ctx* c) {
     const uint32_t n = c->n, nCol = c->p.nCol;
     // run() (coloringMCMC_main.cu:101-158): taboo cleared, colours from the states' next draw
     c->rand_base = c->rand->cur;
-    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; }   // states moved
-    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
-    c->batch = c->bench_n = 0;
+    drop_graphs(c);   // states moved
     MCMC_HIP_TRY(hipMemsetAsync(c->hist, 0, sizeof(uint32_t) * 2u * c->hist_words, c->stream));
     if (c->taboo) MCMC_HIP_TRY(hipMemsetAsync(c->taboo, 0, sizeof(uint32_t) * n, c->stream));
     int rc = upload_state(c, 0);
@@ -5182,8 +5234,17 @@ int mcmc_get_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len)
 int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (sweeps == 0) return fail(MCMC_E_ARG, "sweeps must be > 0");
-    if (c->bench_exec && c->bench_n == sweeps) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    long long lv = -1;
+    if (c->wsa.ctl && c->ran && c->ws_enter >= 0) {
+        // the path for the colouring the timed sweeps start from: its violators, recounted
+        uint64_t cv = 0;
+        int rc = mcmc_count_violations(c, &cv, nullptr);
+        if (rc) return rc;
+        lv = (long long)cv;
+    }
+    ws_choose(c, lv);
+    if (c->bench_exec && c->bench_n == sweeps && c->bench_ws == c->ws_on) return MCMC_OK;
     if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; }
     // Throughput mode: the loop body with the stop tests disabled (no cap, no convergence stop:
     // a sweep from a proper colouring still resamples every vertex), `sweeps` launches captured
@@ -5202,15 +5263,20 @@ int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
     MCMC_HIP_TRY(hipGraphUpload(c->bench_exec, c->stream));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     c->bench_n = sweeps;
+    c->bench_ws = c->ws_on;
     return MCMC_OK;
 }
 
 int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
-    int rc = mcmc_bench_prepare(c, sweeps);   // no-op when already prepared for `sweeps`
-    if (rc) return rc;
+    if (!(c->bench_exec && c->bench_n == sweeps)) {   // (prepared for `sweeps`: as captured)
+        int rc = mcmc_bench_prepare(c, sweeps);
+        if (rc) return rc;
+    }
+    int rc = MCMC_OK;
     c->ran = true;
+    c->traj_ok = false;   // throughput mode keeps no trajectory
     // one graph replay between two events on the sweep stream: total = device wall of the loop,
     // per-launch average = total / sweeps (each launch is one fused sweep, gap included)
     MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -5330,8 +5396,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->g->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->batch_exec) (void)hipGraphExecDestroy(c->batch_exec);
-    if (c->bench_exec) (void)hipGraphExecDestroy(c->bench_exec);
+    drop_graphs(c);
     (void)hipFree(c->own_colors[0]);
     (void)hipFree(c->own_colors[1]);
     (void)hipFree(c->taboo);
@@ -5492,8 +5557,19 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
     // the caller's per-step path then
     if (c->stream == nullptr) return 1;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (c->wsa.ctl) {   // the persistent wide sweep near convergence (ws_choose; one sync per batch)
+        DevState h{};
+        long long lv = -1;
+        if (c->ran) {
+            if (int rc = download_state(c, &h)) return rc;
+            if (int rc = last_cviol(c, h, &lv)) return rc;
+        }
+        ws_choose(c, lv);
+    }
     c->ran = true;
-    const uint32_t key = 0x80000000u | steps;   // (c->batch: the one-GPU run's batches are plain counts)
+    c->traj_ok = true;
+    // (c->batch: the one-GPU run's batches are plain counts)
+    const uint32_t key = 0x80000000u | (c->ws_on ? 0x40000000u : 0u) | steps;
     if (!(c->batch_exec && c->batch == key)) {
         if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
         SweepArgs a = make_args(c, 1);
@@ -5504,7 +5580,7 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
             (void)hipGetLastError();
             return 1;   // capture unsupported on this stream: the per-step path
         }
-        for (uint32_t i = 0; i < steps; i++) launch_pair(c, a);
+        launch_sweeps(c, a, steps);   // the persistent launches of the one-GPU run where they apply
         MCMC_HIP_TRY(hipStreamEndCapture(c->stream, &graph));
         hipError_t e = hipGraphInstantiate(&c->batch_exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);
@@ -5758,8 +5834,7 @@ int mcmc_part_attach(mcmc_ctx* c, uint32_t world, uint32_t rank, const uint32_t*
     if (c->stream && !c->borrowed_stream) (void)hipStreamDestroy(c->stream);
     c->stream = static_cast<hipStream_t>(stream);
     c->borrowed_stream = true;
-    if (c->batch_exec) { (void)hipGraphExecDestroy(c->batch_exec); c->batch_exec = nullptr; c->batch = 0; }
-    if (c->bench_exec) { (void)hipGraphExecDestroy(c->bench_exec); c->bench_exec = nullptr; c->bench_n = 0; }
+    drop_graphs(c);
     return MCMC_OK;
 }
 

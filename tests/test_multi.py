@@ -172,6 +172,36 @@ def test_native_loopback_wide(M, monkeypatch, world, inc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("enter", ["-1", "1000000000"])
+def test_native_loopback_wide_world1(M, monkeypatch, enter):
+    """A world-1 partition of the wide sweep takes the one-GPU run's launches through the driver:
+    its 8-step batches go through the persistent wide sweep (every batch, or from the second batch
+    on, MCMC_WS_ENTER), equal to the oracle."""
+    import oracle_np as NP
+
+    from mcmc_colorer_amd.distributed import plan_csr
+
+    monkeypatch.setenv("MCMC_WS_ENTER", enter)
+    off, idx = NP.rmat(11, 8, 0.5, 0.2, 0.2, 3)
+    ncol = int(np.diff(off.astype(np.int64)).max())
+    for nc, mr in ((ncol, 6), (300, 30)):
+        O.srand(1)
+        r = O.mcmc_run(off, idx, nc, 1, maxRip=mr)
+        lp, st, _ = loopback(M, off, idx, nc, 1, plan_csr(off, 1), 0, maxRip=mr)
+        assert_native(lp, st, r, 1)
+        import ctypes
+
+        from mcmc_colorer_amd._lib import check, lib
+
+        ws = (ctypes.c_uint64 * 30)()
+        check(lib().mcmc_get_wide_solo_stats(lp._ctx[0], ws))
+        assert ws[0] == 1, list(ws)[:10]
+        if enter == "-1" or r.res.iter > 9:
+            assert ws[2] > 0, list(ws)[:10]   # persistent sweeps run
+        lp.close()
+
+
+@pytest.mark.gpu
 def test_native_loopback_er_fast_rows(M):
     """Each rank generates only its rows of an uneven plan (mcmc_graph_er_fast_rows)."""
     n, p, ncol, seed = 150000, 0.003, 16, 8

@@ -457,6 +457,7 @@ def test_wide_persistent(M, monkeypatch, case):
     moved by the leader or by delta phases, the violator list kept or recollected. Every case equals
     the oracle's run (colouring, trajectory, iter, glibc draws); the statistics show the path ran."""
     graph, ncol, kw, env, key = WS_CASES[case]
+    monkeypatch.setenv("MCMC_WS_ENTER", "-1")   # every batch (default: only once Cviol <= 512)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     if graph == "rmat":
@@ -496,11 +497,14 @@ def test_wide_persistent(M, monkeypatch, case):
 
 
 @pytest.mark.gpu
-def test_wide_persistent_steps_alternate(M, monkeypatch):
+@pytest.mark.parametrize("enter", ["-1", "1000000000"])
+def test_wide_persistent_steps_alternate(M, monkeypatch, enter):
     """step() batches of 1, 3, 16 and 2 sweeps through the persistent launch (each entry finds the
     violator list the last launch left): the trajectory and colouring equal one uninterrupted
-    oracle run of 22 sweeps."""
+    oracle run of 22 sweeps. enter = 1e9: the first batch of a fresh colouring (Cviol unknown) takes
+    the per-sweep path, the later ones the persistent sweep."""
     monkeypatch.setenv("MCMC_GATHER", "wide")   # nCol 16 on a dense graph: violators every sweep
+    monkeypatch.setenv("MCMC_WS_ENTER", enter)
     O.srand(1)
     off, idx = O.setup_rnd2(2000, 0.05)
     ncol = 16
@@ -514,7 +518,35 @@ def test_wide_persistent_steps_alternate(M, monkeypatch):
     r = O.mcmc_run(off, idx, ncol, 1, maxRip=40, sweep_limit=22)
     assert col.coloring().tolist() == r.colors.tolist()
     assert col.trajectory().tolist()[:22] == r.traj.tolist()[:22]
-    assert col.wide_solo_stats()["sweeps"] >= 20
+    assert col.wide_solo_stats()["sweeps"] >= (20 if enter == "-1" else 19)
+    col.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("enter", [None, "1000000000"])
+def test_wide_persistent_hybrid(M, monkeypatch, enter):
+    """The default path choice: a run's first batch (16 sweeps) takes the per-sweep path, later
+    batches the persistent sweep once Cviol <= MCMC_WS_ENTER (default 512); one run switching paths
+    equals the oracle's run."""
+    if enter is not None:
+        monkeypatch.setenv("MCMC_WS_ENTER", enter)
+    off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+    g = M.Graph.from_csr(off, idx)
+    kw = {"maxRip": 40}
+    params = M.ColoringMCMCParams(nCol=300, maxRip=40)
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    st = col.run(0)
+    O.srand(1)
+    r = O.mcmc_run(off, idx, 300, 1, **kw)
+    assert col.coloring().tolist() == r.colors.tolist()
+    assert col.trajectory().tolist() == r.traj.tolist()
+    assert (st.iter, st.finalViol, st.glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+    ws = col.wide_solo_stats()
+    traj = r.traj.tolist()
+    if enter is not None and len(traj) > 17:
+        assert 1 <= ws["sweeps"] <= len(traj) - 16, (ws, len(traj))
+    elif len(traj) <= 16 or min(traj[15:]) > 512:
+        assert ws["sweeps"] == 0, ws
     col.close()
 
 
