@@ -58,7 +58,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 KERNELS = {"dense": "dc_multi_kernel (persistent: the timed sweeps in one launch; solo sweeps on workgroup 0, "
                     "full sweeps on the grid)",
-           "dense-part": "dc_eval_kernel (one sweep: update + evaluation + commit)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
+           "dense-part": "dc_eval_kernel (one sweep: update + evaluation + commit; world 1: dc_multi_kernel)",
+           "wide-persistent": "ws_kernel (persistent wide sweep: the timed sweeps in one launch)", "lds": "sweep_kernel<NW,true>", "global": "sweep_kernel<NW,false>", "blocked": "sweep_blocked_kernel",
            "tiled": "sweep_tiled_kernel", "wide": "wide_tscan+wide_eval(+walks)+commit (one sweep)",
            "ref-wide": "refw_scan+refw_rows+refw_walk+refw_commit (one sweep)"}
 
@@ -91,13 +92,14 @@ def ctx_stats(ctx) -> tuple:
 
 
 def load_traffic(key: str):
-    """HBM bytes per sweep-kernel launch from the committed rocprofv3 PMC summary (or None)."""
+    """HBM bytes per sweep from the committed rocprofv3 PMC summary (or None): a persistent launch's
+    bytes divided by the sweeps it ran (make_pmc_summary.py sweeps-per-launch)."""
     p = ROOT / "profiles" / "pmc_summary.json"
     if not p.exists():
         return None
     try:
-        d = json.loads(p.read_text())
-        return d.get(key, {}).get("hbm_bytes_per_launch")
+        e = json.loads(p.read_text()).get(key, {})
+        return e.get("hbm_bytes_per_sweep", e.get("hbm_bytes_per_launch"))
     except Exception:
         return None
 
@@ -709,7 +711,9 @@ def main() -> int:
                    "graph_gen_s": round(t_gen, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(key) if key else None,
-                     "kernel": KERNELS.get(variant + ("-part" if (variant == "dense" and dist is not None) else ""), variant)
+                     "kernel": KERNELS.get(variant + ("-part" if (variant == "dense" and dist is not None) else "")
+                                           + ("-persistent" if (wide_inc and "persistent" in wide_inc
+                                                                and wide_inc["persistent"]["sweeps"]) else ""), variant)
                                + ("<REF>" if ref else "")
                                + ("" if world == 1 else " + exchange (per-rank step)"),
                      "kernel_ms": kernel_ms, "algorithmic_bytes": b_alg,
