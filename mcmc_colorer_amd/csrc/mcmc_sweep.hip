@@ -4092,7 +4092,7 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     w.nw = (uint32_t)nw;
     w.lead_arcs = 4096;
     if (const char* m = getenv("MCMC_WS_LEAD_ARCS")) w.lead_arcs = (uint32_t)strtoul(m, nullptr, 10);
-    w.light_arcs = 4096;
+    w.light_arcs = 512;   // (a wave gathers 512 arcs per round; a longer row: the workgroup, one round)
     if (const char* m = getenv("MCMC_WS_LIGHT")) w.light_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(m, nullptr, 10));
     w.sets = std::min<uint32_t>(16u, kWsLds / (4u * walk_set_words(c->p.nCol)));
     w.poll = 1;

@@ -56,7 +56,7 @@ constexpr uint32_t kWsResLds = 4096;       // results the leader keeps in LDS (m
 constexpr uint32_t kWsEvLds = 4096;        // overflow events sorted in LDS (more: in global memory)
 constexpr uint32_t kWsRankMax = 1024;      // events ranked and drawn in parallel (more: bitonic + sequential)
 constexpr uint32_t kWsLeadLight = 256;     // violator arcs the leader walks on one wave (more: the workgroup)
-constexpr uint32_t kWsLeadSets = 2;        // the leader's walk mask sets (violators it walks itself)
+constexpr uint32_t kWsLeadSets = 6;        // the leader's walk mask sets at most (as many as fit the LDS)
 constexpr uint32_t kWsLeadList = 16384;    // violator-list updates the leader does itself
 constexpr uint32_t kWsPreLds = 16384;      // delta phase: changed rows whose arc prefix sits in LDS
 constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
@@ -568,12 +568,12 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
     // ---- the leader ----
     __shared__ WsState s;
     __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_nr, s_wsum[16], s_nh, s_vq, s_w[4], s_pf, s_gn;
-    __shared__ uint32_t s_ring[31];
+    __shared__ uint32_t s_ring[31], s_rawok;
     uint32_t* const cand = dyn;                              // [3 kWsCandCap] candidates (l, x, cv | nc << 16)
     uint32_t* const tmp = cand + 3u * kWsCandCap;            // [kWsResLds] raw draws, event vertices, degrees
     uint32_t* const lres = tmp + kWsResLds;                  // [2 kWsResLds] the sweep's results
     uint32_t* const evl = lres + 2u * kWsResLds;             // [kWsEvLds] overflow events (result indices)
-    uint32_t* const sets = evl + kWsEvLds;                   // kWsLeadSets mask sets
+    uint32_t* const sets = evl + kWsEvLds;                   // lead_sets mask sets
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // a phase for the helpers: every wave's stores drained, release, the flag; then wait for all
     auto post = [&](uint32_t kind) {
@@ -626,6 +626,20 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             s.tp = now;
         }
     };
+    // The next kWsRankMax raw glibc draws from the window s.ring (draw r = sum_m T[m][r] ring[m], the
+    // commit's table) into raw = evl + kWsRankMax, one per thread. They depend on the window only, so
+    // the leader computes them while the helpers move the last sweep's counts (s_rawok: valid for
+    // the current window), off the event step's critical path.
+    auto draws = [&]() {
+        uint32_t tv[31];
+#pragma unroll
+        for (int m = 0; m < 31; m++) tv[m] = kGlibcTab[m * kGlibcTabK + threadIdx.x];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int m = 0; m < 31; m++) acc += tv[m] * s.ring[m];
+        evl[kWsRankMax + threadIdx.x] = acc;
+    };
+    static_assert(kWsRankMax == 1024u && kWsEvLds >= 2u * kWsRankMax, "one draw per leader thread");
     auto mark = [&](uint32_t k, uint32_t step) {
         if (threadIdx.x == 0) {
             const unsigned long long now = wall_clock64();
@@ -661,6 +675,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         for (int i = 0; i < 16; i++) s.tm[i] = 0;
         s_seq = 0;
         s_exp = 0;
+        s_rawok = 0;
     }
     __syncthreads();
     const bool go = !(s.done || s.err);
@@ -831,7 +846,8 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         // violators: the leader's waves walk a few light ones (the workgroup the heavier), else a walk
         // phase (overlapping the candidates). The leader's results go to its LDS list.
         bool walking = false;
-        bool lead = Vn > 0u && Vn <= kWsLeadSets;
+        const uint32_t lead_sets = min(kWsLeadSets, (kWsLds / 4u - (uint32_t)(sets - dyn)) / SW);
+        bool lead = Vn > 0u && Vn <= lead_sets;
         if (lead) {   // the leader walks them only if all are light (a heavy one: the grid, beside the candidates)
             if (wv < Vn && lane == 0) {
                 const uint32_t l = vl[wv];
@@ -977,16 +993,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 bk = (uint32_t)(((uint64_t)v * 1024u) / nloc);
                 atomicAdd(&bc[bk], 1u);
             }
-            if (threadIdx.x < E) {   // raw draw r on thread r: sum_m T[m][r] ring[m] (the commit's table)
-                const uint32_t rr = threadIdx.x;
-                uint32_t tv[31];
-#pragma unroll
-                for (int m = 0; m < 31; m++) tv[m] = kGlibcTab[m * kGlibcTabK + rr];
-                uint32_t acc = 0;
-#pragma unroll
-                for (int m = 0; m < 31; m++) acc += tv[m] * s_ring[m];
-                raw[rr] = acc;
-            }
+            if (!s_rawok) draws();   // (computed during the last count moves where there were any)
             dc_lbar();
             uint32_t tot = 0;
             const uint32_t off = ws_scan(bc[threadIdx.x], s_wsum, &tot);
@@ -1012,6 +1019,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 st->glibc_head = 0u;
                 s.draws += E;
                 st->glibc_draws = s.draws;
+                s_rawok = 0;
             }
             if (inl) dc_lbar(); else __syncthreads();
         } else if (E > 0u) {
@@ -1034,6 +1042,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 st->glibc_head = 0u;
                 s.draws += E;
                 st->glibc_draws = s.draws;
+                s_rawok = 0;
             }
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
@@ -1104,6 +1113,11 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     w.ctl[kWsCandN] = 0u;
                 }
                 post(kWsDelta);
+                if (!s_rawok) {   // the next sweep's draws while the helpers work (E > kWsRankMax: the
+                    draws();      // event list overwrote them; the window is that of sweep t + 1)
+                    __syncthreads();
+                    if (threadIdx.x == 0) s_rawok = 1;
+                }
                 wait(false);   // (candidates and touched rows read back coherently)
                 if (threadIdx.x == 0) {
                     s.st[4]++;

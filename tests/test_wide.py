@@ -446,6 +446,8 @@ WS_CASES = {
     "sparse-eps": ("sparse", 1000, {"epsilon": 2e-6, "maxRip": 40}, {}, "candidates"),
     "sparse-65535": ("sparse", 65535, {"maxRip": 40}, {}, "sweeps"),
     "all-change-16": ("dense16", 16, {"maxRip": 30}, {"MCMC_GATHER": "wide"}, "walk_phases"),
+    "rmat-poll-debug": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_POLL": "8", "MCMC_WS_DEBUG": "1"}, "walk_phases"),
+    "rmat-light-4096": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_LIGHT": "4096"}, "walk_phases"),
 }
 
 
@@ -486,6 +488,13 @@ def test_wide_persistent(M, monkeypatch, case):
         r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws)
     ws = col.wide_solo_stats()
     assert ws["enabled"] == 1 and ws["sweeps"] >= 1 and ws[key] > 0, ws
+    col.close()
+    # MCMC_WS_MAX below the window: no persistent sweep, the same run
+    monkeypatch.setenv("MCMC_WS_MAX", "1")
+    col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+    col.run(0)
+    assert col.wide_solo_stats()["enabled"] == 0 and col.coloring().tolist() == r.colors.tolist()
+    monkeypatch.delenv("MCMC_WS_MAX")
     # the same run from the same colouring with the per-sweep path only
     monkeypatch.setenv("MCMC_WIDE_SOLO", "0")
     col2 = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
