@@ -876,6 +876,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             for (uint32_t b0 = wv * 64u; b0 < nc; b0 += blockDim.x) {   // (wave-uniform bounds)
                 const uint32_t kk = b0 + lane;
                 const uint32_t l = kk < nc ? (pre_g ? dc_ld(&cl[3u * kk]) : cl[3u * kk]) : 0u;
+                const uint32_t e = kk < nc ? (pre_g ? dc_ld(&cl[3u * kk + 2u]) : cl[3u * kk + 2u]) : 0u;
                 const bool keep = kk < nc && dc_ld(&a.inc_vcnt[l]) == 0u;   // a violator: walked above
                 const uint64_t m = __ballot(keep);
                 if (m == 0) continue;
@@ -885,7 +886,6 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 b = __shfl(b, ld, 64);
                 const uint32_t j = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (keep) {
-                    const uint32_t e = pre_g ? dc_ld(&cl[3u * kk + 2u]) : cl[3u * kk + 2u];
                     if (j < kWsResLds) {
                         lres[2u * j] = l;
                         lres[2u * j + 1u] = e;
@@ -1055,28 +1055,43 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         // its row start and its arcs' prefix (an unchanged one -- an overflow that drew its own
         // colour -- with no arcs), per-thread runs of the results, workgroup scans
         uint32_t nch = 0, arcs = 0;
+        probe(0);
         {
             const uint32_t per = (N + blockDim.x - 1u) / blockDim.x, i0 = min(N, threadIdx.x * per), i1 = min(N, i0 + per);
             uint32_t* const dg = tmp;   // degrees by result index (LDS results only)
             uint32_t mc = 0, ma = 0;
-            for (uint32_t i = i0; i < i1; i++) {
-                const uint32_t l = R[2u * i], e = R[2u * i + 1u];
-                const uint32_t cv = e & 0xFFFFu, nc = e >> 16;
-                uint32_t d = 0;
-                uint64_t r0 = 0;
-                if (nc != cv) {
-                    Cs[l] = (uint16_t)nc;
-                    r0 = a.row_off[l];
-                    d = (uint32_t)(a.row_off[l + 1] - r0);
-                    mc++;
+            for (uint32_t ib = i0; ib < i1; ib += 4u) {   // 4 rows' offsets in flight per thread
+                uint32_t l[4], e[4];
+                uint64_t r0[4], r1[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t i = ib + (uint32_t)u;
+                    l[u] = i < i1 ? R[2u * i] : 0u;
+                    e[u] = i < i1 ? R[2u * i + 1u] : 0u;
+                    const bool chg = i < i1 && (e[u] >> 16) != (e[u] & 0xFFFFu);
+                    r0[u] = chg ? a.row_off[l[u]] : 0ull;
+                    r1[u] = chg ? a.row_off[l[u] + 1u] : 0ull;
                 }
-                reinterpret_cast<uint4*>(w.chg)[i] = make_uint4(l, e, (uint32_t)r0, (uint32_t)(r0 >> 32));
-                if (inl) dg[i] = d;
-                else w.pre[i] = d;
-                ma += d;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t i = ib + (uint32_t)u;
+                    if (i >= i1) break;
+                    const uint32_t cv = e[u] & 0xFFFFu, nc = e[u] >> 16;
+                    const uint32_t d = (uint32_t)(r1[u] - r0[u]);
+                    if (nc != cv) {
+                        Cs[l[u]] = (uint16_t)nc;
+                        mc++;
+                    }
+                    reinterpret_cast<uint4*>(w.chg)[i] = make_uint4(l[u], e[u], (uint32_t)r0[u], (uint32_t)(r0[u] >> 32));
+                    if (inl) dg[i] = d;
+                    else w.pre[i] = d;
+                    ma += d;
+                }
             }
+            probe(1);   // [9] rows' offsets
             (void)ws_scan(mc, s_wsum, &nch);
             uint32_t run = ws_scan(ma, s_wsum, &arcs);
+            probe(2);   // [10] scans
             for (uint32_t i = i0; i < i1; i++) {
                 const uint32_t d = inl ? dg[i] : w.pre[i];
                 w.pre[i] = run;
@@ -1088,6 +1103,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 s.st[7] += nch;
                 s.arcs += arcs;
             }
+            probe(5);   // [13] prefix stores
         }
         mark(k, 6);
         // the counts move: by the leader's threads when few arcs, else a delta phase

@@ -4,7 +4,7 @@ ratios per access pattern (profiles/r05/fetch_calib.json).
   python scripts/fetch_calib.py <dir with probe.log, pmc1/, pmc2/> <out.json>
 
 probe.log is fetch_probe's stdout; pmc1 / pmc2 hold rocprofv3's counter_collection.csv of the two
-passes. Dispatches other than flush_kernel are, in order: stream16, stream4, stream2, gather2,
+passes. The probe's own dispatches (not flush_kernel, not the runtime's fills) are, in order: stream16, stream4, stream2, gather2,
 gather4, gather16, scatter2.
 """
 import csv
@@ -13,12 +13,13 @@ import sys
 from pathlib import Path
 
 ORDER = ["stream16", "stream4", "stream2", "gather2", "gather4", "gather16", "scatter2"]
+PROBES = ("stream_kernel", "gather_kernel", "scatter2_kernel")   # (not flush_kernel, not hipMemset's fills)
 
 
 def per_dispatch(path: Path, counter: str) -> list[float]:
     rows = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "flush_kernel" in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in PROBES):
             continue
         d = int(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(rows))
         rows[d] = rows.get(d, 0.0) + float(r["Counter_Value"])
