@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from ctypes import POINTER, byref, c_char_p, c_double, c_float, c_int, c_int32, c_uint32, c_uint64, c_void_p
 from pathlib import Path
 
@@ -204,6 +205,19 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not LIB_PATH.exists():
             raise MCMCError(f"{LIB_PATH} not found: build it with `python -m mcmc_colorer_amd.build`")
+        if "torch" not in sys.modules and os.environ.get("MCMC_NO_TORCH_FIRST") != "1":
+            # torch installed: import it first, so the process initialises its (shared) HIP runtime in
+            # torch's order. Loaded the other way round (runtime by path, the library, a sweep, then
+            # torch), both work but the process aborted at exit ("double free or corruption" in the
+            # runtime's teardown, r05 GPU box); MCMC_NO_TORCH_FIRST=1 skips this
+            import importlib.util
+
+            try:
+                has_torch = importlib.util.find_spec("torch") is not None
+            except (ImportError, ValueError):
+                has_torch = False
+            if has_torch:
+                import torch  # noqa: F401
         rt = _process_hip_runtime()
         if rt is not None and os.environ.get("MCMC_OWN_HIP_RUNTIME") != "1":
             ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)

@@ -1,0 +1,7 @@
+#!/bin/bash
+# r05: runtime exit probe, then the full-size -m gpu files
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/${1:-r05q}; mkdir -p $O
+timeout -k 10 300 python -u scripts/rt_exit_probe.py > $O/rt.log 2>&1; cat $O/rt.log
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests/test_c5_full.py tests/test_c3_full.py tests/test_c4_full.py tests/test_rccl_world.py > $O/t.log 2>&1; rc=$?
+tail -5 $O/t.log; exit $rc
