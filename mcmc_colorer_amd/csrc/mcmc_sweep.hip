@@ -3662,15 +3662,23 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
 // has it (setup_dense_window; MCMC_DENSE_MULTI=0: never) and the arguments allow it (single context
 // or a world-1 partition, committing in the sweep; no taboo, no tail-cut flags, no diagnostics); the
 // persistent wide sweep (wide_solo.h) where set up and chosen (ws_choose); else K (sweep, commit) pairs.
-void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
+// The persistent launch K sweeps of these arguments take, if any: 2 the wide one, 1 the dense one
+int persistent_path(const mcmc_ctx* c, const SweepArgs& a) {
     const bool solo = !c->part || c->world == 1;   // nothing leaves the context
-    if (c->wsa.ctl && c->ws_on && solo && a.dcap == 0u && a.taboo == nullptr && a.vflags == nullptr && a.scan_stats == nullptr &&
-        a.phase_ts == nullptr && a.pair_trace == nullptr && a.inc != nullptr) {
+    const bool plain = solo && a.dcap == 0u && a.taboo == nullptr && a.vflags == nullptr && a.scan_stats == nullptr &&
+                       a.phase_ts == nullptr && a.pair_trace == nullptr;
+    if (c->wsa.ctl && c->ws_on && plain && a.inc != nullptr) return 2;
+    if (c->dcm_launch && a.fused == 1 && plain) return 1;
+    return 0;
+}
+
+void launch_sweeps(mcmc_ctx* c, const SweepArgs& a, uint32_t K) {
+    const int pp = persistent_path(c, a);
+    if (pp == 2) {
         if (K) ws_kernel<<<c->ws_grid, 1024, kWsLds, c->stream>>>(a, c->wsa, K);
         return;
     }
-    if (c->dcm_launch && a.fused == 1 && solo && a.dcap == 0u && a.taboo == nullptr && a.vflags == nullptr &&
-        a.scan_stats == nullptr && a.phase_ts == nullptr && a.pair_trace == nullptr) {
+    if (pp == 1) {
         if (K) c->dcm_launch(a, K, c->grid, c->stream);
         return;
     }
@@ -5568,6 +5576,16 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
     }
     c->ran = true;
     c->traj_ok = true;
+    {   // a persistent path: one launch for the batch, no graph (nothing to capture once per size)
+        SweepArgs a = make_args(c, 1);
+        a.dcap = 0u;
+        a.fused = c->wide ? 0 : 1;
+        if (persistent_path(c, a)) {
+            launch_sweeps(c, a, steps);
+            MCMC_HIP_TRY(hipGetLastError());
+            return MCMC_OK;
+        }
+    }
     // (c->batch: the one-GPU run's batches are plain counts)
     const uint32_t key = 0x80000000u | (c->ws_on ? 0x40000000u : 0u) | steps;
     if (!(c->batch_exec && c->batch == key)) {

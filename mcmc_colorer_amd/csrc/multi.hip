@@ -71,6 +71,7 @@ int exchange_mode() {
 }
 constexpr uint32_t kFullAfterOverflow = 16;
 constexpr uint32_t kStepsPerPoll = 8;   // steps enqueued per batch; the host polls one batch behind
+constexpr uint32_t kSoloStepsPerPoll = 64;   // world 1: one persistent launch per batch
 
 struct Driver {
     std::vector<mcmc_ctx*> ctx;
@@ -478,13 +479,14 @@ int part_run_impl(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
     Ev e0{D.res0->ev[1]}, e1{D.res0->ev[2]};
     Ev batch_ev[2] = {{D.res0->ev[3]}, {D.res0->ev[4]}};
     MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
-    MCMC_HIP_TRY(hipEventRecord(e0.e, D.d[0].stream));
     // the loop continues from the device's sweep counter (a second call resumes where the first
     // stopped: the exchange's buffer parity is the device's)
     int32_t dn0 = 0;
     uint32_t t = 0, err0 = 0;
     if (int rc = mcmc_part_state(D.ctx[0], &dn0, &t, &err0)) return rc;
     if (err0 & 6u) return fail(MCMC_E_STATE, "an exchange of a paused sweep is pending");
+    MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
+    MCMC_HIP_TRY(hipEventRecord(e0.e, D.d[0].stream));   // (after the state read: the loop's device time)
     const uint32_t t_begin = t;
     // host-side exchange policy, identical on every rank (it sees the same device decisions)
     uint32_t full_left = 0;                // steps to run in full mode after a delta overflow
@@ -520,7 +522,8 @@ int part_run_impl(mcmc_ctx** ctxs, uint32_t k, uint32_t max_sweeps, mcmc_run_sta
     while (!done) {
         const uint32_t left = limit - std::min(limit, t - t_begin);
         if (left && inflight < 2) {
-            if (int rc = enqueue(std::min(kStepsPerPoll, left))) return rc;
+            const bool solo1 = D.d.size() == 1 && D.world == 1 && !D.stub;
+            if (int rc = enqueue(std::min(solo1 ? kSoloStepsPerPoll : kStepsPerPoll, left))) return rc;
             MCMC_HIP_TRY(hipSetDevice(D.d[0].device));
             MCMC_HIP_TRY(hipEventRecord(batch_ev[(cur + inflight) & 1].e, D.d[0].stream));
             inflight++;
