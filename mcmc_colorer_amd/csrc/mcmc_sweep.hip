@@ -3350,7 +3350,8 @@ struct mcmc_ctx {
     uint32_t* gmask = nullptr;      // split walks: masks, then kSplitMax task counters
     uint32_t split_arcs = kSplitArcs;   // MCMC_SPLIT_ARCS (tests)
     uint32_t walk_light = kWalkLight;   // MCMC_WALK_LIGHT (0: every walk by a whole workgroup)
-    uint32_t walk_tie = 0;              // MCMC_WALK_TIE (device tie-binade scan; off until measured on the GPU)
+    uint32_t walk_tie = 1;              // MCMC_WALK_TIE: tie binades by word functions (r05 default: violator-heavy
+                                        // C5 sweeps 0.265 -> 0.216 ms, converged unchanged; 0 = run by run)
     float* etab = nullptr;
     float emax = 0.0f;
     uint16_t* ftab = nullptr;       // F(u) table of the evaluation (ftab_n entries)
@@ -4102,6 +4103,8 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     if (const char* m = getenv("MCMC_WS_LEAD_ARCS")) w.lead_arcs = (uint32_t)strtoul(m, nullptr, 10);
     w.light_arcs = 512;   // (a wave gathers 512 arcs per round; a longer row: the workgroup, one round)
     if (const char* m = getenv("MCMC_WS_LIGHT")) w.light_arcs = std::max<uint32_t>(1u, (uint32_t)strtoul(m, nullptr, 10));
+    w.lead_heavy = 0;   // (measured: a hub walk on the leader costs ~40 us, the walk phase overlaps it)
+    if (const char* m = getenv("MCMC_WS_LEAD_HEAVY")) w.lead_heavy = (uint32_t)strtoul(m, nullptr, 10);
     w.sets = std::min<uint32_t>(16u, kWsLds / (4u * walk_set_words(c->p.nCol)));
     w.poll = 1;
     if (const char* m = getenv("MCMC_WS_POLL")) w.poll = (uint32_t)strtoul(m, nullptr, 10);

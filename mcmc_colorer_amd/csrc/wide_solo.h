@@ -78,6 +78,7 @@ struct WsArgs {
     uint32_t nw;           // window states
     uint32_t lead_arcs;    // changed arcs the leader moves itself (more: a delta phase)
     uint32_t light_arcs;   // violators of at most this many arcs walk on one wave
+    uint32_t lead_heavy;   // heavier violators' arcs (in all) the leader walks itself, a workgroup each
     uint32_t sets;         // wave mask sets per workgroup
     uint32_t* dbg;         // diagnostics (MCMC_WS_DEBUG): host-visible progress words, or nullptr
     uint32_t poll;         // an idle helper's poll interval (s_sleep 2 units; MCMC_WS_POLL)
@@ -437,12 +438,18 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         // arcs dealt round-robin over the workgroups (h, h + H, ...): a few thousand random reads
         // spread over every CU rather than filling the first few
         const uint32_t tot = nch + 1u <= kWsPreLds ? pre[nch] : dc_ld(&w.pre[nch]);
-        ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * blockDim.x);
-        // meanwhile the next sweep's candidates (its colours: C_t+1, in Cs): those that change
-        // colour unless they turn out violators, into gcand -- a slice of the entries per workgroup
+        // the last wave of every workgroup takes the next sweep's candidates, the others the arcs:
+        // the two dependent-load chains run side by side instead of one after the other
+        const uint32_t na = blockDim.x - 64u;
+        if (wv != (blockDim.x >> 6) - 1u) {
+            ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * na);
+            return;
+        }
+        // the next sweep's candidates (its colours: C_t+1, in Cs): those that change colour unless
+        // they turn out violators, into gcand -- a slice of the entries per workgroup
         const WsRuns r = ws_runs(w, dc_ld(&w.ctl[kWsArgL]), nloc);
         const uint32_t per = (r.tot + H - 1u) / H, jb = min(r.tot, h * per), je = min(r.tot, jb + per);
-        for (uint32_t j0 = jb + wv * 64u; j0 < je; j0 += blockDim.x) {   // (wave-uniform bounds)
+        for (uint32_t j0 = jb; j0 < je; j0 += 64u) {   // (wave-uniform bounds)
             uint32_t l = 0, x = 1, cv = 0, nc = 0;
             bool in = j0 + lane < je && ws_entry(w, r, j0 + lane, l, x);
             if (in) {
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
     // ---- the leader ----
     __shared__ WsState s;
     __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_nr, s_wsum[16], s_nh, s_vq, s_w[4], s_pf, s_gn;
-    __shared__ uint32_t s_ring[31], s_rawok;
+    __shared__ uint32_t s_ring[31], s_rawok, s_ha, s_hl[kWsLeadSets];
     uint32_t* const cand = dyn;                              // [3 kWsCandCap] candidates (l, x, cv | nc << 16)
     uint32_t* const tmp = cand + 3u * kWsCandCap;            // [kWsResLds] raw draws, event vertices, degrees
     uint32_t* const lres = tmp + kWsResLds;                  // [2 kWsResLds] the sweep's results
@@ -840,6 +847,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             w.ctl[kWsArgP + 1] = s.x_t;
             s_nh = 0;
             s_nr = 0;
+            s_ha = 0;
         }
         __syncthreads();
         if (stop) break;
@@ -848,16 +856,28 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         bool walking = false;
         const uint32_t lead_sets = min(kWsLeadSets, (kWsLds / 4u - (uint32_t)(sets - dyn)) / SW);
         bool lead = Vn > 0u && Vn <= lead_sets;
-        if (lead) {   // the leader walks them only if all are light (a heavy one: the grid, beside the candidates)
-            if (wv < Vn && lane == 0) {
-                const uint32_t l = vl[wv];
-                if (a.row_off[l + 1] - a.row_off[l] > kWsLeadLight) atomicAdd(&s_nh, 1u);
+        if (lead) {   // the leader walks them if the heavy ones (a workgroup each) are few arcs in all
+            bool heavy = false;
+            uint32_t l = 0;
+            if (wv < Vn) {
+                l = vl[wv];
+                const uint32_t d = (uint32_t)(a.row_off[l + 1] - a.row_off[l]);
+                heavy = d > kWsLeadLight;
+                if (heavy && lane == 0) {
+                    s_hl[atomicAdd(&s_nh, 1u)] = l;
+                    atomicAdd(&s_ha, d);
+                }
             }
             dc_lbar();
-            lead = s_nh == 0u;
+            lead = s_nh == 0u || s_ha <= w.lead_heavy;
+            if (lead) {
+                if (wv < Vn && !heavy) ws_walk_light<false>(a, C, s.x_t, l, sets + wv * SW, lane, &s_nr, lres);
+                __syncthreads();
+                const uint32_t nh = s_nh;
+                for (uint32_t j = 0; j < nh; j++) ws_walk_heavy<false>(a, C, s.x_t, s_hl[j], sets, &s_nr, lres);
+            }
         }
         if (lead) {
-            if (wv < Vn) ws_walk_light<false>(a, C, s.x_t, vl[wv], sets + wv * SW, lane, &s_nr, lres);
             dc_lbar();
             if (threadIdx.x == 0) s.st[2] += Vn;
         } else if (Vn > 0u) {

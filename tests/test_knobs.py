@@ -5,7 +5,7 @@ Knobs covered here (the others have their own tests: MCMC_GATHER / MCMC_BLOCK_LO
 MCMC_GROUP_ROWS / MCMC_TILE_STREAM in test_gpu_parity.py::test_all_gather_variants, MCMC_DRAIN_ROWS
 and MCMC_FULL_SCAN there too, MCMC_EXCHANGE in test_multi.py, MCMC_WIDE_INC / MCMC_WIDE_SCAN /
 MCMC_SPLIT_ARCS in test_wide.py, the persistent wide sweep's MCMC_WIDE_SOLO / MCMC_WS_ENTER /
-MCMC_WS_LEAD_ARCS / MCMC_WS_LIGHT / MCMC_WS_MAX / MCMC_WS_POLL / MCMC_WS_DEBUG in
+MCMC_WS_LEAD_ARCS / MCMC_WS_LEAD_HEAVY / MCMC_WS_LIGHT / MCMC_WS_MAX / MCMC_WS_POLL / MCMC_WS_DEBUG in
 test_wide.py::test_wide_persistent* and test_multi.py::test_native_loopback_wide_world1,
 MCMC_DENSE / MCMC_DENSE_ROWS in test_dense.py):
   tiled scan sweep (MCMC_DENSE=0): MCMC_LATE_STAGE, MCMC_NO_OLIST, MCMC_NO_EWALK, MCMC_TQ_DENSE,
@@ -70,7 +70,7 @@ def test_part_solo_off(M, monkeypatch):
 
 
 WIDE = [
-    {"MCMC_WALK_LIGHT": "0"}, {"MCMC_WALK_LIGHT": "64"}, {"MCMC_WALK_TIE": "1"}, {"MCMC_WIDE_INC_DIV": "1"},
+    {"MCMC_WALK_LIGHT": "0"}, {"MCMC_WALK_LIGHT": "64"}, {"MCMC_WALK_TIE": "0"}, {"MCMC_WIDE_INC_DIV": "1"},
     {"MCMC_WIDE_INC_DIV": "100000"}, {"MCMC_WIDE_INC_HUB": "8"}, {"MCMC_WIDE_INC_SLOT": "1"},
     {"MCMC_TSCAN_PLAN": "lpt"},
 ]
