@@ -58,6 +58,7 @@ constexpr uint32_t kWsRankMax = 1024;      // events ranked and drawn in paralle
 constexpr uint32_t kWsLeadLight = 256;     // violator arcs the leader walks on one wave (more: the workgroup)
 constexpr uint32_t kWsLeadSets = 6;        // the leader's walk mask sets at most (as many as fit the LDS)
 constexpr uint32_t kWsLeadList = 16384;    // violator-list updates the leader does itself
+constexpr uint32_t kWsVvLds = 32;          // violators held in LDS for the candidates' test (more: counts)
 constexpr uint32_t kWsPreLds = 16384;      // delta phase: changed rows whose arc prefix sits in LDS
 constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
 enum : uint32_t { kWsRecount = 1, kWsExit = 2, kWsDelta = 3, kWsWalkLight = 4, kWsWalkHeavy = 5, kWsCopy = 6,
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
     // ---- the leader ----
     __shared__ WsState s;
     __shared__ uint32_t s_seq, s_exp, s_nc, s_ne, s_nr, s_wsum[16], s_nh, s_vq, s_w[4], s_pf, s_gn;
-    __shared__ uint32_t s_ring[31], s_rawok, s_ha, s_hl[kWsLeadSets];
+    __shared__ uint32_t s_ring[31], s_rawok, s_ha, s_hl[kWsLeadSets], s_vv[kWsVvLds];
     uint32_t* const cand = dyn;                              // [3 kWsCandCap] candidates (l, x, cv | nc << 16)
     uint32_t* const tmp = cand + 3u * kWsCandCap;            // [kWsResLds] raw draws, event vertices, degrees
     uint32_t* const lres = tmp + kWsResLds;                  // [2 kWsResLds] the sweep's results
@@ -890,6 +891,11 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         // not violators keep the colour their case (iii) walk gave; more than the LDS holds: in rounds
         const bool pre_g = s_pf == s.lx;   // the helpers found them during the last delta phase
         if (!pre_g) fetch(s.lx, C);
+        // a candidate is walked above if it is a violator of C_t, i.e. in the (exact) violator list:
+        // a short list is tested in LDS instead of by a dependent load of the candidate's count
+        const bool vv = Vn <= kWsVvLds;
+        if (vv && threadIdx.x < Vn) s_vv[threadIdx.x] = vl[threadIdx.x];
+        dc_lbar();
         if (pre_g || s_nc != 0xFFFFFFFFu) {
             const uint32_t nc = pre_g ? s_gn : s_nc;
             const uint32_t* cl = pre_g ? w.gcand : cand;
@@ -897,7 +903,12 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 const uint32_t kk = b0 + lane;
                 const uint32_t l = kk < nc ? (pre_g ? dc_ld(&cl[3u * kk]) : cl[3u * kk]) : 0u;
                 const uint32_t e = kk < nc ? (pre_g ? dc_ld(&cl[3u * kk + 2u]) : cl[3u * kk + 2u]) : 0u;
-                const bool keep = kk < nc && dc_ld(&a.inc_vcnt[l]) == 0u;   // a violator: walked above
+                bool keep = kk < nc;
+                if (vv) {
+                    for (uint32_t q2 = 0; q2 < Vn; q2++) keep = keep && s_vv[q2] != l;
+                } else {
+                    keep = keep && dc_ld(&a.inc_vcnt[l]) == 0u;   // a violator: walked above
+                }
                 const uint64_t m = __ballot(keep);
                 if (m == 0) continue;
                 const int ld = __ffsll((long long)m) - 1;
