@@ -4051,7 +4051,10 @@ int mcmc_glibc_draw(uint32_t window[31], uint32_t count, uint32_t* out) {
 // window is [1, w_lo) U [w_hi, 2^31 - 1): the states whose canonical draw is below E[nCol - 1] or
 // at least hi (a case (iii) row keeps its colour exactly outside it). MCMC_WIDE_SOLO=0: off;
 // MCMC_WS_MAX: window states allowed (default 2^24); MCMC_WS_LEAD_ARCS: changed arcs the leader
-// moves itself; MCMC_WS_LIGHT: violator arcs walked on one wave.
+// moves itself; MCMC_WS_LIGHT: violator arcs walked on one wave; MCMC_WS_LEAD_HEAVY: heavy violators'
+// arcs the leader walks itself (default 0: a walk phase); MCMC_WS_ENTER: largest Cviol a batch
+// enters the persistent sweep with (ws_choose; < 0: always); MCMC_WS_POLL / MCMC_WS_DEBUG: the
+// helpers' poll interval and the host-pinned per-wave progress words (diagnostics).
 static uint32_t first_state_at_least(float thr) {
     uint32_t lo = 1, hi = kMinstdM;   // states 1 .. 2^31 - 2; hi = none
     while (lo < hi) {
