@@ -179,6 +179,10 @@ int mcmc_get_dense_stats(mcmc_ctx* c, uint64_t out[10]);
  * alone (solo), out[11] candidate-window states, out[12] 1 if the context launches it, out[13] open
  * mask words now nonzero, out[14] rows the solo sweeps evaluated. Test / bench statistics. */
 int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]);
+/* The dense-count sweep's per-row state of local rows [row0, row0 + rows): counts[rows][nCol] (the
+ * neighbours in the dense column range S per colour, as of the last sweep's update) and, if masks
+ * is not NULL, masks[rows][mask words] (their occupancy bits). Test / diagnostic read-back. */
+int mcmc_get_dense_counts(mcmc_ctx* c, uint32_t row0, uint32_t rows, uint32_t* counts, uint32_t* masks);
 /* Diagnostics of the tiled sweep's scan (no reference counterpart): with stats on, every sweep adds
  * the 16-byte id quads it loaded and the (group, column block) pairs it staged (table + colour
  * slice); mcmc_set_scan_stats(c, 1) also zeroes them. The sweep stops scanning a row once its
@@ -412,6 +416,9 @@ int mcmc_ref_run(mcmc_ctx* c, uint32_t tail_max_passes, mcmc_run_stats* stats);
 int mcmc_ref_init(mcmc_ctx* c);
 /* cudaMemGetInfo's pair for the GPU colorer's log header (coloringMCMC_prints.cu:20-22). */
 int mcmc_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes);
+/* HIP_VERSION the library was compiled against, and hipRuntimeGetVersion of the runtime it is bound
+ * to in this process (torch's bundled runtime when torch is loaded: the majors must agree). */
+int mcmc_hip_versions(int* built, int* runtime);
 /* Cviol (REF: conflicting edges) after each tail-cut pass of the last run. */
 int mcmc_get_tail_trajectory(mcmc_ctx* c, uint64_t* out, uint64_t cap, uint64_t* len);
 

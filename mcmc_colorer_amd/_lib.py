@@ -59,6 +59,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_get_wide_solo_stats": (c_int, [c_void_p, _u64p]),
     "mcmc_get_dense_stats": (c_int, [c_void_p, _u64p]),
     "mcmc_get_dense_stats_v2": (c_int, [c_void_p, _u64p]),
+    "mcmc_get_dense_counts": (c_int, [c_void_p, c_uint32, c_uint32, _u32p, _u32p]),
     "mcmc_get_info": (c_int, [c_void_p, c_void_p]),
     "mcmc_cdf_walk": (c_uint32, [_u32p, c_uint32, c_uint32, c_float, c_float, c_float]),
     "mcmc_refstruct_bench": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_double), _u64p]),
@@ -97,6 +98,7 @@ SIGNATURES: dict[str, tuple] = {
     "mcmc_ref_init": (c_int, [c_void_p]),
     "mcmc_get_tail_trajectory": (c_int, [c_void_p, _u64p, c_uint64, _u64p]),
     "mcmc_device_mem_info": (c_int, [c_int, _u64p, _u64p]),
+    "mcmc_hip_versions": (c_int, [POINTER(c_int), POINTER(c_int)]),
 }
 
 
@@ -196,34 +198,30 @@ def _process_hip_runtime():
 def lib() -> ctypes.CDLL:
     """Loads libmcmc_hip.so once. Raises (never falls back) when it is missing.
 
-    One HIP runtime per process: the library needs libamdhip64.so.7, which torch's bundled runtime
-    also provides under that soname. Loaded first, the library would bring /opt/rocm's runtime and
-    a later `import torch` its own -- two HSA runtimes, and one of them finds no GPU. So the
-    runtime torch uses is loaded (RTLD_GLOBAL) before the library, which then binds to it; torch,
-    imported later, finds its runtime already mapped. Two runtimes mapped anyway is an error."""
+    One HIP runtime per process: the library needs libamdhip64.so.7 and librccl.so.1, which torch's
+    bundled ROCm also provides under those sonames. Loaded first, the library would bring /opt/rocm's
+    runtime and a later `import torch` its own -- two HSA runtimes, and one of them finds no GPU. So
+    the runtime the process uses (torch's when torch is installed) and its RCCL are loaded before
+    the library, which then binds to them by soname; torch, imported later, finds them mapped.
+
+    They are loaded RTLD_LOCAL: binding by soname does not need the global scope. r05 loaded them
+    RTLD_GLOBAL, and a process that loaded the library before torch aborted at exit with "double
+    free or corruption" -- a stack scan of the abort (scripts/rt_exit_probe.py, gpurun_out/r06c)
+    put it in librocm_smi64's destructor of a static std::map, the RCCL dependency that the global
+    preload exposed to every later load; with RTLD_LOCAL every import order exits cleanly
+    (gpurun_out/r06d, tests/test_runtime.py). Two runtimes mapped anyway is an error. The runtime's
+    version is not queried here (hipRuntimeGetVersion initialises the runtime); mcmc_hip_versions
+    reports it beside the version the library was built for (tests/test_runtime.py: same major)."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
             raise MCMCError(f"{LIB_PATH} not found: build it with `python -m mcmc_colorer_amd.build`")
-        if "torch" not in sys.modules and os.environ.get("MCMC_NO_TORCH_FIRST") != "1":
-            # torch installed: import it first, so the process initialises its (shared) HIP runtime in
-            # torch's order. Loaded the other way round (runtime by path, the library, a sweep, then
-            # torch), both work but the process aborted at exit ("double free or corruption" in the
-            # runtime's teardown, r05 GPU box); MCMC_NO_TORCH_FIRST=1 skips this
-            import importlib.util
-
-            try:
-                has_torch = importlib.util.find_spec("torch") is not None
-            except (ImportError, ValueError):
-                has_torch = False
-            if has_torch:
-                import torch  # noqa: F401
         rt = _process_hip_runtime()
         if rt is not None and os.environ.get("MCMC_OWN_HIP_RUNTIME") != "1":
-            ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+            ctypes.CDLL(rt, mode=ctypes.RTLD_LOCAL)
             rccl = Path(rt).parent / "librccl.so"   # (soname librccl.so.1: the library's RCCL too)
             if rccl.exists():
-                ctypes.CDLL(str(rccl), mode=ctypes.RTLD_GLOBAL)
+                ctypes.CDLL(str(rccl), mode=ctypes.RTLD_LOCAL)
         L = ctypes.CDLL(str(LIB_PATH))
         both = _hip_runtimes()
         if len(both) > 1:

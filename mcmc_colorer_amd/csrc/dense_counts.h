@@ -237,6 +237,298 @@ __device__ __forceinline__ void dc_rebuild_chunk(const SweepArgs& a, const uint8
     }
 }
 
+// The lane rebuild (nCol <= 32, SweepArgs::dc_rbl): a lane per row, a task of blockDim consecutive
+// local rows per workgroup. Per column block b overlapping S the
+// workgroup's slice of colours sits in LDS (double-buffered: block b + 1's arrives by LDS-DMA while
+// block b is counted), and every lane streams its row's segment of block b itself (16-byte quads,
+// 8 ids each, kDcLaneQ in flight; the next block's segment bounds are loaded meanwhile). A row's counts of its 32 possible colours live in registers
+// as bit planes -- plane k's bit c is bit k of the count of colour c -- so counting an id is a shift
+// (its colour's one-hot word) and a quad's eight one-hots are summed per colour by a carry-save tree
+// into a 4-bit number that is added into the planes with a short carry ripple. No LDS atomics, no
+// search of the quad's row, every id read once from HBM in 16-byte loads. A segment is padded to a
+// multiple of 8 ids with copies of its first id: inside S the padding is counted with the rest and
+// subtracted once per segment; in a block that S covers only in part every id is tested instead.
+// At the end the planes are transposed into counts (one word per colour) and written with the
+// mask word and the wave's open word. Replaces dc_rebuild_chunk's LDS histograms (per id: a colour
+// read, a histogram atomic, and per quad a binary search of the segment starts) for nCol <= 32.
+constexpr uint32_t kDcPlanes = 16;
+constexpr uint32_t kDcSliceBuf = 65536;   // one block's colours (2^block_log2 <= 2^16 bytes)
+
+// s = a + b + c and the carry, per bit (32 colours at once)
+__device__ __forceinline__ void dc_fa(uint32_t a, uint32_t b, uint32_t c, uint32_t& s, uint32_t& co) {
+    const uint32_t t = a ^ b;
+    s = t ^ c;
+    co = (t & c) | (~t & a);
+}
+// The eight one-hot words x[] summed per colour: b0 + 2 b1 + 4 b2 + 8 b3 (a carry-save tree)
+__device__ __forceinline__ void dc_sum8(const uint32_t (&x)[8], uint32_t& b0, uint32_t& b1, uint32_t& b2, uint32_t& b3) {
+    uint32_t sa, ca, sb, cb, cd, s2, c3a;
+    dc_fa(x[0], x[1], x[2], sa, ca);
+    dc_fa(x[3], x[4], x[5], sb, cb);
+    const uint32_t sc = x[6] ^ x[7], cc = x[6] & x[7];
+    dc_fa(sa, sb, sc, b0, cd);           // weight 1
+    dc_fa(ca, cb, cc, s2, c3a);          // weight 2 (three of four)
+    b1 = s2 ^ cd;
+    const uint32_t c3b = s2 & cd;
+    b2 = c3a ^ c3b;                      // weight 4
+    b3 = c3a & c3b;                      // weight 8
+}
+// The carry c into planes K.. (a ripple that stops once no lane of the wave carries; counts <
+// 2^np: no carry leaves the top plane). Templates instead of a loop with an exit, so every plane
+// stays a named register.
+template <int K>
+__device__ __forceinline__ void dc_ripple(uint32_t (&A)[kDcPlanes], uint32_t np, uint32_t c) {
+    if constexpr (K < (int)kDcPlanes) {
+        if ((uint32_t)K < np && __ballot(c != 0u) != 0ull) {
+            const uint32_t nc = A[K] & c;
+            A[K] ^= c;
+            dc_ripple<K + 1>(A, np, nc);
+        }
+    }
+}
+// Planes A (np >= 4 of them) += b0 + 2 b1 + 4 b2 + 8 b3 per colour
+__device__ __forceinline__ void dc_planes_add(uint32_t (&A)[kDcPlanes], uint32_t np, uint32_t b0, uint32_t b1,
+                                              uint32_t b2, uint32_t b3) {
+    uint32_t c = A[0] & b0, s;
+    A[0] ^= b0;
+    dc_fa(A[1], b1, c, s, c);
+    A[1] = s;
+    dc_fa(A[2], b2, c, s, c);
+    A[2] = s;
+    dc_fa(A[3], b3, c, s, c);
+    A[3] = s;
+    dc_ripple<4>(A, np, c);
+}
+// The borrow br out of planes K.. (as dc_ripple)
+template <int K>
+__device__ __forceinline__ void dc_unborrow(uint32_t (&A)[kDcPlanes], uint32_t np, uint32_t br) {
+    if constexpr (K < (int)kDcPlanes) {
+        if ((uint32_t)K < np && __ballot(br != 0u) != 0ull) {
+            const uint32_t x = A[K];
+            A[K] = x ^ br;
+            dc_unborrow<K + 1>(A, np, ~x & br);
+        }
+    }
+}
+// Planes A -= pad x oh (pad <= 7; every colour of oh was counted at least pad times: no borrow out)
+__device__ __forceinline__ void dc_planes_sub(uint32_t (&A)[kDcPlanes], uint32_t np, uint32_t oh, uint32_t pad) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t b = ((pad >> k) & 1u) ? oh : 0u;
+        const uint32_t x = A[k];
+        A[k] = x ^ b ^ br;
+        br = (~x & (b | br)) | (b & br);
+    }
+    dc_unborrow<3>(A, np, br);
+}
+// One quad (8 ids) of a row segment into the row's planes: the eight colours read from the slice
+// first, then their one-hot words. CHK (the block is not wholly inside S): id j counts only if it is
+// one of the segment's nv real ids and lies in [lo, lo + span); else all eight count (padding is
+// subtracted per segment). qok: the quad lies inside the lane's segment. Branch-free: the wave
+// runs it once per quad position that any lane holds.
+template <bool CHK>
+__device__ __forceinline__ void dc_lane_quad(uint32_t (&A)[kDcPlanes], uint32_t np, uint4 v, const uint8_t* __restrict__ sl,
+                                             bool qok, int nv, uint32_t lo, uint32_t span) {
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    uint32_t id[8], c[8], x[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) id[k] = (w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c[k] = sl[id[k]];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        bool ok = qok;
+        if constexpr (CHK) ok = ok && (k < nv) && (id[k] - lo < span);
+        x[k] = ok ? (1u << c[k]) : 0u;
+    }
+    uint32_t b0, b1, b2, b3;
+    dc_sum8(x, b0, b1, b2, b3);
+    dc_planes_add(A, np, b0, b1, b2, b3);
+}
+// A row segment's quads [s0, e) (8 ids each; real ids below s1) into the planes, kDcLaneQ quads per
+// lane in flight: every lane loads kDcLaneQ quads (positions past its segment load its first quad
+// again -- harmless, they are not counted), so the loads are straight-line and the waits counted;
+// the few lanes with a longer segment load the rest in predicated rounds of 4.
+template <bool CHK, uint32_t kDcLaneQ>
+__device__ __forceinline__ void dc_lane_segment(uint32_t (&A)[kDcPlanes], uint32_t np, const uint16_t* __restrict__ gc,
+                                                uint32_t s0, uint32_t s1, uint32_t e, const uint8_t* __restrict__ sl,
+                                                uint32_t lo, uint32_t span) {
+    {   // the first kDcLaneQ quads: straight-line loads (a lane past its segment reloads its first quad)
+        uint4 v[kDcLaneQ];
+#pragma unroll
+        for (uint32_t q = 0; q < kDcLaneQ; q++) {
+            const uint32_t pos = s0 + 8u * q;
+            v[q] = *reinterpret_cast<const uint4*>(gc + (pos < e ? pos : s0));
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kDcLaneQ; q++) {
+            const uint32_t pos = s0 + 8u * q;
+            if (__ballot(pos < e)) dc_lane_quad<CHK>(A, np, v[q], sl, pos < e, (int)(s1 - pos), lo, span);
+        }
+    }
+    // the rest of the longer segments, 4 quads per round, loaded only by the lanes that hold them
+    for (uint32_t j = kDcLaneQ; __ballot(s0 + 8u * j < e); j += 4u) {
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; q++) {
+            const uint32_t pos = s0 + 8u * (j + q);
+            v[q] = make_uint4(0u, 0u, 0u, 0u);
+            if (pos < e) v[q] = *reinterpret_cast<const uint4*>(gc + pos);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; q++) {
+            const uint32_t pos = s0 + 8u * (j + q);
+            if (__ballot(pos < e)) dc_lane_quad<CHK>(A, np, v[q], sl, pos < e, (int)(s1 - pos), lo, span);
+        }
+    }
+}
+// Counts of one row from its planes: the 32 x 32 bit transpose (T[c] bit k = plane k bit c), then
+// the row's nCol counts written.
+__device__ __forceinline__ void dc_lane_write(const SweepArgs& a, const uint32_t (&A)[kDcPlanes], uint32_t l) {
+    uint32_t T[32];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {   // stage 16: the upper planes are zero
+        T[k + 16] = A[k] >> 16;
+        T[k] = A[k] & 0xFFFFu;
+    }
+    auto stage = [&](const int j, const uint32_t m) {
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            if (k & j) continue;
+            const uint32_t t = ((T[k] >> j) ^ T[k + j]) & m;
+            T[k + j] ^= t;
+            T[k] ^= t << j;
+        }
+    };
+    stage(8, 0x00FF00FFu);
+    stage(4, 0x0F0F0F0Fu);
+    stage(2, 0x33333333u);
+    stage(1, 0x55555555u);
+    uint32_t* const cw = a.dc_cnt + (size_t)l * a.dc_cw;
+    if ((a.nCol & 3u) == 0u) {
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (4u * q < a.nCol) *reinterpret_cast<uint4*>(cw + 4 * q) = make_uint4(T[4 * q], T[4 * q + 1], T[4 * q + 2], T[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < 32; c++)
+            if ((uint32_t)c < a.nCol) cw[c] = T[c];
+    }
+}
+
+template <int NW, uint32_t Q>
+__device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t task,
+                                                 uint32_t* lds) {
+    const uint32_t nloc = a.v_end - a.v_begin, R = a.grp_rows, bl = a.block_log2, np = a.dc_planes;
+    const uint32_t sb0 = a.dc_s0 >> bl, sb1 = (a.dc_s1 - 1u) >> bl, bsz = 1u << bl;
+    const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t lds0 = lds_addr(lds);
+    const uint32_t padn = (a.n + 15u) & ~15u;
+    uint8_t* const slb = reinterpret_cast<uint8_t*>(lds);
+    // the slice of block b (whole 16-byte pieces, below n rounded up) into buffer `buf` by LDS-DMA:
+    // 1 KiB per wave-instruction
+    auto dma = [&](uint32_t b, uint32_t buf) {
+        const uint32_t blo = b << bl, npc = (min(bsz, padn - blo) + 15u) >> 4;
+        for (uint32_t w = wv; w * 64u < npc; w += nwv) {
+            const uint32_t p = min(w * 64u + lane, npc - 1u);
+            glds16(C + blo + 16u * p, __builtin_amdgcn_readfirstlane(lds0 + buf * kDcSliceBuf + w * 1024u));
+        }
+    };
+    // this lane's row, its group and position in the group; its segment table entries of block b
+    const uint32_t l = task * blockDim.x + threadIdx.x;
+    const bool in = l < nloc;
+    const uint32_t g = in ? l / R : 0u, r = l - g * R;
+    const uint16_t* __restrict__ gc = a.tcol + (in ? a.gbase[g] : 0ull);
+    const uint32_t* __restrict__ tsg = a.tseg + (size_t)g * a.nblocks * tseg_stride(R) + r;
+    uint32_t raw = 0, nxt = 0;
+    if (in) {
+        raw = tsg[(size_t)sb0 * tseg_stride(R)];
+        nxt = tsg[(size_t)sb0 * tseg_stride(R) + 1u];
+    }
+    uint32_t A[kDcPlanes];
+#pragma unroll
+    for (int k = 0; k < (int)kDcPlanes; k++) A[k] = 0u;
+    dma(sb0, 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (uint32_t b = sb0; b <= sb1; b++) {
+        const uint32_t buf = (b - sb0) & 1u;
+        if (b < sb1) dma(b + 1u, buf ^ 1u);
+        const uint32_t blo = b << bl;
+        const uint32_t lo = max(blo, a.dc_s0) - blo, hi = min(blo + bsz, a.dc_s1) - blo, span = hi - lo;
+        const bool chk = lo != 0u || hi != bsz;   // S covers block b in part: every id tested
+        const uint8_t* __restrict__ sl = slb + buf * kDcSliceBuf;
+        // real ids [s0, s1), quads up to the padded end e (the next row's start)
+        const uint32_t s0 = raw & kTsegPos, e = nxt & kTsegPos, s1 = e - (raw & 7u);
+        const uint32_t pad = chk ? 0u : (raw & 7u);
+        if (in && b < sb1) {   // the next block's entries, in flight with this block's ids
+            raw = tsg[(size_t)(b + 1u) * tseg_stride(R)];
+            nxt = tsg[(size_t)(b + 1u) * tseg_stride(R) + 1u];
+        }
+        // (one round of kDcLaneQ quads for a C3 row's ~66 ids per block)
+        if (chk) {
+            dc_lane_segment<true, Q>(A, np, gc, s0, s1, e, sl, lo, span);
+        } else {
+            dc_lane_segment<false, Q>(A, np, gc, s0, s1, e, sl, lo, span);
+            if (__ballot(pad != 0u)) {   // the padding (copies of the segment's first id) counted: out again
+                const uint32_t ohf = pad ? 1u << sl[gc[s0]] : 0u;
+                dc_planes_sub(A, np, ohf, pad);
+            }
+        }
+        // block b + 1's slice has landed and every wave is done with block b's (the next DMA's target)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const uint32_t fw = dc_fullw(a.nCol, 0u);
+    uint32_t mw = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kDcPlanes; k++) mw |= A[k];
+    mw &= fw;
+    if (in) {
+        a.dc_mask[(size_t)l * NW] = mw;
+        dc_lane_write(a, A, l);
+    }
+    // the wave's 64 rows are one open word (tasks start at multiples of 64 rows)
+    const unsigned long long ob = __ballot(in && mw != fw);
+    if (lane == 0u && in) {
+        const size_t wi = (size_t)(l >> 6) * NW;
+        const unsigned long long o = atomicExch(&a.dc_open[wi], ob);
+        dc_osum_note(a, wi, o, ob);
+    }
+}
+
+// A fresh colouring's update as its own launch (the host's dc_prep, before the colouring's first
+// sweep; nCol <= 32): workgroup k < n1 copies C_t into the other buffer on local rows [16384 k,
+// 16384 (k + 1)) -- the copy a rebuild sweep's update makes -- and workgroup n1 + k rebuilds the
+// counts of rows [BS k, BS (k + 1)) by dc_rebuild_lanes. A kernel of its own, so the lane
+// rebuild's registers (its planes, Q quads per lane in flight) are not the dense sweep's: inside the sweep
+// (a rebuild after list overflows) the update keeps the chunk rebuild. dc_ctl_fresh_kernel then
+// marks the update done (mode 0, empty lists) and counts the rebuild.
+template <int NW, uint32_t BS, uint32_t Q>
+__global__ __launch_bounds__(BS) void dc_rebuild_kernel(SweepArgs a, uint32_t n1) {
+    extern __shared__ uint4 dc_lds[];
+    const uint32_t t = a.st->t;
+    const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;   // C_t
+    uint8_t* __restrict__ Y = (t & 1) ? a.colors0 : a.colors1;
+    if (blockIdx.x < n1) {
+        const size_t b0 = (size_t)a.v_begin + (size_t)blockIdx.x * kDcCopyRows, b1 = min((size_t)a.v_end, b0 + kDcCopyRows);
+        const size_t q0 = (b0 + 15) & ~(size_t)15, q1 = (b1 & ~(size_t)15) > q0 ? (b1 & ~(size_t)15) : q0;
+        for (size_t i = q0 + 16u * threadIdx.x; i < q1; i += 16u * blockDim.x)
+            *reinterpret_cast<uint4*>(Y + i) = *reinterpret_cast<const uint4*>(C + i);
+        for (size_t i = b0 + threadIdx.x; i < (q0 < b1 ? q0 : b1); i += blockDim.x) Y[i] = C[i];
+        for (size_t i = (q1 > b0 ? q1 : b0) + threadIdx.x; i < b1; i += blockDim.x) Y[i] = C[i];
+        return;
+    }
+    dc_rebuild_lanes<NW, Q>(a, C, blockIdx.x - n1, reinterpret_cast<uint32_t*>(dc_lds));
+}
+__global__ void dc_ctl_fresh_kernel(uint32_t* __restrict__ k) {
+    k[kDcMode] = 0u;
+    for (uint32_t p = 0; p < 2u; p++) k[kDcLen + p] = k[kDcOvf + p] = k[kDcChgLen + p] = k[kDcChgOvf + p] = 0u;
+    k[kDcTask] = k[kDcDone] = 0u;
+    reinterpret_cast<unsigned long long*>(k + kDcStat)[1] += 1ull;   // rebuilds
+}
+
 template <int NW>
 __device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, uint32_t* lds, const DcCtl& w) {
     __shared__ uint32_t sh_k;
@@ -356,13 +648,14 @@ __device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();   // the task's stores are complete before the next claim / the release
     }
-    if (threadIdx.x == 0) {
-        if (mine) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            atomicAdd(&a.dc_ctl[kDcDone], mine);
-        }
-        while (__hip_atomic_load(&a.dc_ctl[kDcDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < T)
+    if (threadIdx.x == 0 && mine) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        atomicAdd(&a.dc_ctl[kDcDone], mine);
+    }
+    if (threadIdx.x < 64u) {   // wave 0 waits for every task (a wave-uniform spin loop; the others at the barrier)
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&a.dc_ctl[kDcDone], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT)) < T)
             __builtin_amdgcn_s_sleep(4);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }

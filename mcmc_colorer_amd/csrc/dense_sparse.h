@@ -59,6 +59,12 @@ __global__ __launch_bounds__(256) void dl_table_kernel(uint2* __restrict__ tab, 
     tab[i] = make_uint2(L, w);
 }
 
+// Watchdogs of the persistent launch (wall_clock64 ticks, 100 MHz): the leader gives a phase of
+// the helpers kDcWaitTicks to complete, then flags DevState::err (kDevErrWatchdog) and stops instead
+// of waiting for workgroups that may not be resident; a helper that sees no post for kDcIdleTicks
+// leaves (it would otherwise spin on words the leader has reset).
+constexpr unsigned long long kDcWaitTicks = 200000000ull;    // 2 s
+constexpr unsigned long long kDcIdleTicks = 3000000000ull;   // 30 s
 constexpr uint32_t kDcSoloPairs = 4096;      // (moved vertex, column block) pairs a move phase takes
 constexpr uint32_t kDcSoloMovesMax = 16;     // and moved vertices
 constexpr uint32_t kDcSoloOpenWords = 32;    // nonzero open words a solo sweep evaluates itself
@@ -308,10 +314,21 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             }
             if (threadIdx.x < 64u) {   // wave 0 waits (a wave-uniform spin loop: see dc_multi_kernel)
                 const uint32_t ex = __builtin_amdgcn_readfirstlane(mvexp);
-                while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcMvDone])) < ex) __builtin_amdgcn_s_sleep(1);
+                const unsigned long long t0 = wall_clock64();
+                while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcMvDone])) < ex) {
+                    if (wall_clock64() - t0 > kDcWaitTicks) {   // helpers missing: flag, stop the loop
+                        if (threadIdx.x == 0) {
+                            atomicOr(&st->err, kDevErrWatchdog);
+                            sv.err = kDevErrWatchdog;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
                 if (threadIdx.x == 0 && a.solo_ts && k < 4096u) a.solo_ts[8u * k + 7u] = wall_clock64();
             }
             __syncthreads();
+            if (sv.err) break;
         }
         if (threadIdx.x == 0) {
             s_ow = a.dc_osum ? (uint32_t)dc_ld(a.dc_osum) : 0xFFFFFFFFu;
@@ -559,7 +576,11 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
             // wave 0 polls: a wave-uniform spin loop (a spin loop in one lane beside barriers in the
             // other waves lets the compiler's structurizer run the rest of the wave ahead of it)
             uint32_t g;
-            while ((g = __builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcGen]))) == last) __builtin_amdgcn_s_sleep(4);
+            const unsigned long long t0 = wall_clock64();
+            while ((g = __builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcGen]))) == last) {
+                if (wall_clock64() - t0 > kDcIdleTicks) { g = 2u; break; }   // no leader: leave
+                __builtin_amdgcn_s_sleep(4);
+            }
             if ((g & 3u) == 1u) {   // a full sweep reads plain data of the last phases: acquire
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -587,7 +608,14 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
         }
         if (leader && threadIdx.x < 64u) {   // the sweep is committed (its data released) before the leader plans the next
             const uint32_t nf = __builtin_amdgcn_readfirstlane(nfull);
-            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcCommitted])) < nf) __builtin_amdgcn_s_sleep(2);
+            const unsigned long long t0 = wall_clock64();
+            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcCommitted])) < nf) {
+                if (wall_clock64() - t0 > kDcWaitTicks) {   // the sweep never completed: flag (the solo loop stops)
+                    if (threadIdx.x == 0) atomicOr(&a.st->err, kDevErrWatchdog);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -595,8 +623,16 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
         if (leader) k++;
     }
     if (leader) {
-        if (threadIdx.x < 64u)   // every helper saw the exit (wave 0 waits, wave-uniform)
-            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcAck])) < gridDim.x - 1u) __builtin_amdgcn_s_sleep(2);
+        if (threadIdx.x < 64u) {   // every helper saw the exit (wave 0 waits, wave-uniform)
+            const unsigned long long t0 = wall_clock64();
+            while (__builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcAck])) < gridDim.x - 1u) {
+                if (wall_clock64() - t0 > kDcWaitTicks) {
+                    if (threadIdx.x == 0) atomicOr(&a.st->err, kDevErrWatchdog);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
         if (threadIdx.x == 0) {   // the words are reset for the next launch
             a.dc_ctl[kDcGen] = 0u;
             a.dc_ctl[kDcAck] = 0u;

@@ -48,11 +48,13 @@ int fail(int code, const std::string& msg) {
 
 // ----------------------------------------------------------------------------------------------
 // Device-resident loop state (one per context).
+constexpr uint32_t kDevErrEvents = 1u, kDevErrWatchdog = 2u;   // DevState::err bits
 struct DevState {
     uint32_t t;                 // sweep index == ColoringMCMC_CPU::iter
     uint32_t done;              // loop finished (set by commit)
     uint32_t x_t;               // minstd state after K0 + t*n draws
-    uint32_t err;               // bit0: event list overflow
+    uint32_t err;               // kDevErrEvents: event list overflow; kDevErrWatchdog: a persistent
+                                // launch's phase did not complete in time (workgroups not resident)
     unsigned long long viol;    // sum of viol_v over the swept rows (Cviol_t)
     uint32_t ev_count;          // overflow events this sweep
     uint32_t arrive;            // workgroups finished with the running sweep (fused commit)
@@ -233,6 +235,8 @@ struct SweepArgs {
     unsigned long long* dc_open;   // [ntiles][NW] bit j of word (tile, i): row 64 tile + j's mask word i not full
     uint32_t dc_s0, dc_s1, dc_cw, dc_cap, dc_max, dc_chg_cap;
     uint32_t dc_rbrows;         // rows per chunk of the streaming count rebuild (0: a wave per row)
+    uint32_t dc_rbl;            // 1: the lane rebuild (dense_counts.h dc_rebuild_lanes; nCol <= 32)
+    uint32_t dc_planes;         // its bit planes per count (counts < 2^dc_planes; 4..16)
     uint32_t dc_commit_restore;  // restore lists up to this long are applied by the commit
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
     // open summary (dense_counts.h dc_osum_note): word 0's low half = open words that are nonzero;
@@ -3374,6 +3378,8 @@ struct mcmc_ctx {
     uint32_t* dc_mask = nullptr;
     unsigned long long* dc_open = nullptr;
     uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1, dc_chg_cap = 0, dc_rbrows = 0;
+    uint32_t dc_rbl = 0, dc_planes = 0;
+    bool dc_fresh = false;          // the colouring is new: dc_prep runs the lane rebuild before its first sweep
     unsigned long long* dc_osum = nullptr;   // open summary (count + one bit per open word)
     // the persistent dense sweep (dense_sparse.h): its launch (nullptr: one dc_eval_kernel per sweep)
     // and the candidate window {L(w), w}
@@ -3400,6 +3406,7 @@ hipError_t inc_reset(mcmc_ctx* c) {
 hipError_t dc_reset(mcmc_ctx* c) {
     uint32_t h[kDcWords] = {};
     h[kDcMode] = 1u;
+    c->dc_fresh = true;
     hipError_t e = hipMemcpyAsync(c->dc_ctl, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
     return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // h lives on this frame
 }
@@ -3607,6 +3614,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.lds_sort_cap = kDcEvalLds / 4u;
         a.dc_osum = c->dc_osum;
         a.dc_rbrows = c->dc_rbrows;
+        a.dc_rbl = c->dc_rbl;
+        a.dc_planes = c->dc_planes;
         a.dl_tab = c->dl_tab;
         a.dl_n = c->dl_n;
         a.solo_ts = c->solo_ts;
@@ -3657,6 +3666,37 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     if (c->refwide) refw_commit_kernel<<<1, 1024, 0, c->stream>>>(a);
     else if (c->wide || c->wide_tiled) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+}
+
+// The host's message for DevState::err bits.
+const char* dev_err_text(uint32_t err) {
+    return (err & kDevErrWatchdog) ? "device watchdog: a phase of a persistent launch did not complete in 2 s "
+                                     "(its workgroups were not all resident)"
+                                   : "device flagged an overflow-event list overflow";
+}
+
+// The first sweep of a fresh colouring (dc_reset) rebuilds every count. Where the lane rebuild applies
+// (nCol <= 32: setup_dense) it runs here as its own launches on the context stream, ahead of the
+// sweep -- dc_rebuild_kernel (the copy into the other buffer + the counts) and dc_ctl_fresh_kernel
+// (the update marked done) -- so the sweep's update has nothing left to do. Callers enqueue it inside
+// their timed region, before the sweeps. Not while the stream is being captured (a graph replayed
+// later must not carry it): the sweep's own update then rebuilds, as it does without the lane form.
+int dc_prep(mcmc_ctx* c) {
+    if (!c->dc || !c->dc_fresh || !c->dc_rbl) return MCMC_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    MCMC_HIP_TRY(hipStreamIsCapturing(c->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) return MCMC_OK;
+    c->dc_fresh = false;
+    SweepArgs a = make_args(c, 1);
+    const uint32_t nloc = c->v_end - c->v_begin;
+    const uint32_t n1 = (nloc + kDcCopyRows - 1u) / kDcCopyRows;
+    // a lane per row, 8 quads per lane in flight (measured at C3, 3 colourings each: 1024 x 8 6.53 ms,
+    // 1024 x 10 6.5, 512 x 12 7.8, 512 x 16 8.7; the chunk rebuild inside the sweep 9.7;
+    // gpurun_out/r06e, r06g)
+    dc_rebuild_kernel<1, 1024, 8><<<n1 + (nloc + 1023u) / 1024u, 1024, kDcRebuildLds, c->stream>>>(a, n1);
+    dc_ctl_fresh_kernel<<<1, 1, 0, c->stream>>>(c->dc_ctl);
+    MCMC_HIP_TRY(hipGetLastError());
+    return MCMC_OK;
 }
 
 // K sweeps on the context stream: one persistent dense launch (dc_multi_kernel) where the context
@@ -3996,6 +4036,18 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
         const uint32_t rc = std::min<uint32_t>(R, (kDcEvalLds / 4u - 1u) / (hw + 1u));
         const char* rb = getenv("MCMC_DENSE_RB");
         c->dc_rbrows = (c->g->maxDeg > 0 && c->g->maxDeg < 65536u && rc >= 1u && !(rb && atoi(rb) == 0)) ? rc : 0u;
+        // the lane rebuild (dc_rebuild_lanes: a lane per row, its counts as bit planes in registers)
+        // where one mask word holds every colour and the counts fit 16 planes; MCMC_DENSE_RB=1 keeps
+        // the chunks, 0 a wave per row
+        uint32_t planes = 4;
+        while (planes < 16u && (c->g->maxDeg >> planes) != 0u) planes++;
+        c->dc_planes = planes;
+        c->dc_rbl = (nCol <= 32u && c->g->maxDeg < 65536u && c->dc_rbrows != 0u && !(rb && atoi(rb) == 1)) ? 1u : 0u;
+        if (c->dc_rbl && hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_rebuild_kernel<1, 1024, 8>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDcRebuildLds) != hipSuccess) {
+            (void)hipGetLastError();
+            c->dc_rbl = 0u;
+        }
     }
     if (const char* cc = getenv("MCMC_DENSE_CHG_CAP")) c->dc_chg_cap = (uint32_t)std::max(2, atoi(cc));   // tests
     const size_t open_bytes = sizeof(unsigned long long) * (((size_t)nloc + 63u) / 64u) * c->nw;
@@ -4063,11 +4115,31 @@ static uint32_t first_state_at_least(float thr) {
     }
     return lo;
 }
+// Whether `grid` workgroups of `kernel` (`block` threads, `lds` dynamic LDS bytes) can all be resident
+// on the device at once -- the persistent launches' helpers spin on flags the leader posts, so a
+// grid that cannot be co-resident must not take them. MCMC_PERSIST_CHECK_GRID (tests) checks that
+// many workgroups instead of `grid`.
+static bool coresident(const void* kernel, uint32_t grid, uint32_t block, size_t lds, int device) {
+    if (const char* g = getenv("MCMC_PERSIST_CHECK_GRID")) grid = (uint32_t)strtoul(g, nullptr, 10);
+    int per = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, (int)block, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return (uint64_t)per * (uint64_t)cus >= grid;
+}
+
 static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     const char* e = getenv("MCMC_WIDE_SOLO");
     if ((e && atoi(e) == 0) || !c->inc || c->part || c->v_begin != 0 || c->v_end != c->n || c->p.tabooIteration > 0 ||
         !(c->p.epsilon > 0.0f) || !c->etab || c->p.nCol < 2)
         return MCMC_OK;
+    // one minstd state per vertex and sweep (the window's runs assume it): n below the period
+    if (c->n >= kMinstdN) return MCMC_OK;
+    MCMC_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ws_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)kWsLds));   // (before the occupancy query)
+    if (!coresident(reinterpret_cast<const void*>(&ws_kernel), cus, 1024, kWsLds, c->g->device)) return MCMC_OK;
     const float hi = 1.0f - (float)(c->p.nCol - 1) * c->p.epsilon;
     if (!(c->emax < hi)) return MCMC_OK;
     const uint32_t wlo = first_state_at_least(c->emax), whi = first_state_at_least(hi);
@@ -4488,11 +4560,18 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             c->lds = kDcRebuildLds;
             ea = wi == 0 ? allow_lds_dc<1>(c->lds) : wi == 1 ? allow_lds_dc<2>(c->lds)
                : wi == 2 ? allow_lds_dc<4>(c->lds) : allow_lds_dc<8>(c->lds);
-            if (c->dc_osum && c->dl_n) {   // the persistent launch (dense_sparse.h), where sweeps can run solo
+            const void* dcm_fn = wi == 0 ? reinterpret_cast<const void*>(&dc_multi_kernel<1>)
+                               : wi == 1 ? reinterpret_cast<const void*>(&dc_multi_kernel<2>)
+                               : wi == 2 ? reinterpret_cast<const void*>(&dc_multi_kernel<4>)
+                                         : reinterpret_cast<const void*>(&dc_multi_kernel<8>);
+            if (ea == hipSuccess && c->dc_osum && c->dl_n) {   // its LDS allowance first: the occupancy query needs it
+                ea = wi == 0 ? allow_lds_dcm<1>() : wi == 1 ? allow_lds_dcm<2>() : wi == 2 ? allow_lds_dcm<4>() : allow_lds_dcm<8>();
+            }
+            // the persistent launch (dense_sparse.h), where sweeps can run solo and the grid can be
+            // co-resident (else one dc_eval_kernel per sweep)
+            if (ea == hipSuccess && c->dc_osum && c->dl_n && coresident(dcm_fn, c->grid.x, 1024, kDcMultiLds, c->g->device)) {
                 static const decltype(c->dcm_launch) tabm[4] = {launch_dcm<1>, launch_dcm<2>, launch_dcm<4>, launch_dcm<8>};
                 c->dcm_launch = tabm[wi];
-                if (ea == hipSuccess)
-                    ea = wi == 0 ? allow_lds_dcm<1>() : wi == 1 ? allow_lds_dcm<2>() : wi == 2 ? allow_lds_dcm<4>() : allow_lds_dcm<8>();
             }
         } else if (c->early) {   // the early-exit instantiations
             if (resident) {
@@ -4879,6 +4958,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     c->ran = true;
     c->traj_ok = true;
     MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    if ((rc = dc_prep(c))) return rc;   // a fresh colouring's count rebuild (timed with the loop)
     uint32_t launched = 0;
     while (launched < total) {
         if (total - launched >= batch) {
@@ -4904,7 +4984,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
     MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
     float ms = 0;
     MCMC_HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-    if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
+    if (h.err) return fail(MCMC_E_DEVICE, dev_err_text(h.err));
     mcmc_run_stats s{};
     if (h.done) {
         s.iter = h.iter;
@@ -5088,6 +5168,22 @@ int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]) {
     out[12] = c->dcm_launch ? 1u : 0u;                                           // persistent launch
     out[13] = (uint32_t)os;                                                      // nonzero open words now
     out[14] = reinterpret_cast<const unsigned long long*>(h + kDcSoloEval)[0];   // rows solo sweeps evaluated
+    return MCMC_OK;
+}
+
+int mcmc_get_dense_counts(mcmc_ctx* c, uint32_t row0, uint32_t rows, uint32_t* counts, uint32_t* masks) {
+    if (!c || (rows && !counts)) return fail(MCMC_E_ARG, "NULL argument");
+    if (!c->dc) return fail(MCMC_E_STATE, "the context keeps no dense counts");
+    const uint32_t nloc = c->v_end - c->v_begin;
+    if (row0 > nloc || rows > nloc - row0) return fail(MCMC_E_ARG, "rows outside the context");
+    MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    const size_t nc = c->p.nCol;
+    MCMC_HIP_TRY(hipMemcpyAsync(counts, c->dc_cnt + (size_t)row0 * nc, sizeof(uint32_t) * nc * rows,
+                                hipMemcpyDeviceToHost, c->stream));
+    if (masks)
+        MCMC_HIP_TRY(hipMemcpyAsync(masks, c->dc_mask + (size_t)row0 * c->nw, sizeof(uint32_t) * c->nw * rows,
+                                    hipMemcpyDeviceToHost, c->stream));
+    MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
     return MCMC_OK;
 }
 
@@ -5294,6 +5390,7 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     // one graph replay between two events on the sweep stream: total = device wall of the loop,
     // per-launch average = total / sweeps (each launch is one fused sweep, gap included)
     MCMC_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    if ((rc = dc_prep(c))) return rc;   // a fresh colouring's count rebuild (timed with the sweeps)
     MCMC_HIP_TRY(hipGraphLaunch(c->bench_exec, c->stream));
     MCMC_HIP_TRY(hipEventRecord(c->ev1, c->stream));
     MCMC_HIP_TRY(hipEventSynchronize(c->ev1));
@@ -5302,7 +5399,7 @@ int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sw
     DevState h{};
     rc = download_state(c, &h);
     if (rc) return rc;
-    if (h.err) return fail(MCMC_E_DEVICE, "device flagged an overflow-event list overflow");
+    if (h.err) return fail(MCMC_E_DEVICE, dev_err_text(h.err));
     if (total_ms) *total_ms = tot;
     if (sweep_kernel_ms) *sweep_kernel_ms = (double)tot / sweeps;
     if (c->pair_trace) {   // diagnostics: the last sweep's per-pair records, gridDim x kPairTraceMax x kPairTraceRec
@@ -5549,6 +5646,7 @@ int part_sweep(mcmc_ctx* c, bool delta) {
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_part_sweep_async");
     if (delta && !part_delta_ok(c)) return fail(MCMC_E_STATE, "delta exchange: tiled partitioned contexts only");
+    if (int rc = dc_prep(c)) return rc;
     c->ran = true;
     SweepArgs a = make_args(c, 1);
     a.dcap = delta ? kDeltaPairs : 0u;
@@ -5571,6 +5669,7 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
     // the caller's per-step path then
     if (c->stream == nullptr) return 1;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
+    if (int rc = dc_prep(c)) return rc;
     if (c->wsa.ctl) {   // the persistent wide sweep near convergence (ws_choose; one sync per batch)
         DevState h{};
         long long lv = -1;

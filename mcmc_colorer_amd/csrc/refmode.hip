@@ -86,6 +86,14 @@ int mcmc_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes
     return MCMC_OK;
 }
 
+int mcmc_hip_versions(int* built, int* runtime) {
+    if (!built || !runtime) return fail(MCMC_E_ARG, "NULL argument");
+    *built = HIP_VERSION;
+    *runtime = 0;
+    MCMC_HIP_TRY(hipRuntimeGetVersion(runtime));
+    return MCMC_OK;
+}
+
 int mcmc_gpurand_create(uint32_t n, uint32_t seed, int device, mcmc_gpurand** out) {
     if (!out || n == 0) return fail(MCMC_E_ARG, "bad argument");
     MCMC_HIP_TRY(hipSetDevice(device));

@@ -48,7 +48,7 @@ constexpr uint32_t kWsWords = 96;
 // Watchdogs (wall clock, 100 MHz): a leader wait or an acknowledgement pending this long flags
 // DevState::err and ends the launch instead of spinning forever; an idle helper leaves after kWsIdle.
 constexpr unsigned long long kWsWaitTicks = 200000000ull;    // 2 s
-constexpr unsigned long long kWsIdleTicks = 1000000000ull;   // 10 s
+constexpr unsigned long long kWsIdleTicks = 3000000000ull;   // 30 s
 constexpr uint32_t kWsBShift = 16;   // window buckets: L >> 16
 constexpr uint32_t kWsNB = ((kMinstdN - 1u) >> kWsBShift) + 1u;
 constexpr uint32_t kWsCandCap = 2048;      // changing candidate rows the leader holds (more: no prefetch)
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 if (wall_clock64() - t0 > kWsWaitTicks) {   // a phase that never completed: flag and leave
                     if (threadIdx.x == 0) {
                         w.ctl[kWsErr] = (s_seq << 8) | 1u;
-                        st->err |= 1u;
+                        st->err |= kDevErrWatchdog;
                         s.err = 1u;
                     }
                     break;
@@ -1254,7 +1254,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             if (wall_clock64() - t0 > kWsWaitTicks) {
                 if (threadIdx.x == 0) {
                     w.ctl[kWsErr] = (s_seq << 8) | 2u;
-                    st->err |= 1u;
+                    st->err |= kDevErrWatchdog;
                 }
                 break;
             }

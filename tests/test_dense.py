@@ -239,3 +239,77 @@ def test_dense_rebuild_forms(M, monkeypatch, rb, n, p, ncol, seed, eps, srows):
     col, st, _ = gpu_run(M, off, idx, nc, seed, n * (n + 1) // 2, eps=eps, maxRip=20)
     assert_same(col, st, r)
     assert dense_stats_v2(col)["rebuilds"] >= 1
+
+
+def _random_csr(n, deg, seed):
+    """A simple symmetric random graph (sorted rows) built on the host."""
+    rng = np.random.default_rng(seed)
+    m = n * deg // 2
+    u = rng.integers(0, n, m, dtype=np.int64)
+    v = rng.integers(0, n, m, dtype=np.int64)
+    keep = u != v
+    a = np.minimum(u, v)[keep]
+    b = np.maximum(u, v)[keep]
+    key = np.unique(a * n + b)
+    a, b = key // n, key % n
+    src = np.concatenate([a, b])
+    dst = np.concatenate([b, a])
+    order = np.lexsort((dst, src))
+    src, dst = src[order], dst[order]
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.add.at(off, src + 1, 1)
+    return np.cumsum(off).astype(np.uint64), dst.astype(np.uint32)
+
+
+def _expected_counts(off, idx, colors, ncol, s0, s1):
+    n = len(off) - 1
+    rows = np.repeat(np.arange(n), np.diff(off).astype(np.int64))
+    ins = (idx >= s0) & (idx < s1)
+    cnt = np.zeros((n, ncol), dtype=np.uint32)
+    np.add.at(cnt, (rows[ins], colors[idx[ins]].astype(np.int64)), 1)
+    return cnt
+
+
+@pytest.mark.parametrize("rb", ["", "1"])
+@pytest.mark.parametrize("n,deg,ncol,bl,srows", [
+    (5000, 200, 32, 9, None),     # S = every row: 9 whole 512-vertex blocks + a partial one
+    (5000, 200, 32, 8, 2900),     # S ends inside block 11
+    (6000, 120, 16, 6, 1000),     # 64-vertex blocks: 15 whole blocks, one partial
+    (4000, 300, 5, 7, None),
+    (3000, 90, 1, 8, None),       # one colour
+    (3000, 60, 31, 4, 777),       # 16-vertex blocks (one 16-byte piece per slice)
+    (7000, 40, 32, 16, None),     # the default 65536-vertex block: S inside block 0 (partial)
+])
+def test_dense_rebuild_counts_exact(M, monkeypatch, rb, n, deg, ncol, bl, srows):
+    """The count rebuild's per-row counts and masks equal a host recount from the CSR and C_0 -- the
+    lane rebuild (dense_counts.h dc_rebuild_lanes: bit-plane counts in registers, padding counted
+    and subtracted inside S, every id tested in a partial block) by default, the chunk rebuild with
+    MCMC_DENSE_RB=1 -- over whole and partial column blocks of S (MCMC_BLOCK_LOG2 shrinks blocks)."""
+    from mcmc_colorer_amd._lib import check, lib, u32ptr
+
+    if rb:
+        monkeypatch.setenv("MCMC_DENSE_RB", rb)
+    monkeypatch.setenv("MCMC_GATHER", "tiled")
+    monkeypatch.setenv("MCMC_BLOCK_LOG2", str(bl))
+    if srows:
+        monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
+    off, idx = _random_csr(n, deg, n + deg)
+    g = M.Graph.from_csr(off, idx)
+    col = M.ColoringMCMC(g, M.GPURand(n, 7, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=3))
+    col.init(0)
+    c0 = col.coloring()
+    col.step(1)   # the first sweep's update rebuilds the counts from C_0
+    ds = dense_stats_v2(col)
+    assert ds["enabled"] and ds["rebuilds"] >= 1
+    s0, s1 = ds["s0"], ds["s1"]
+    cnt = np.zeros((n, ncol), dtype=np.uint32)
+    nw = (ncol + 31) // 32
+    msk = np.zeros((n, nw), dtype=np.uint32)
+    check(lib().mcmc_get_dense_counts(col._ctx, 0, n, u32ptr(cnt), u32ptr(msk)))
+    exp = _expected_counts(off, idx, c0, ncol, s0, s1)
+    bad = np.nonzero((cnt != exp).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), bad[:5], cnt[bad[:2]], exp[bad[:2]])
+    expm = np.zeros((n, nw), dtype=np.uint32)
+    for c in range(ncol):
+        expm[:, c // 32] |= ((exp[:, c] != 0).astype(np.uint32) << np.uint32(c % 32))
+    assert np.array_equal(msk, expm)

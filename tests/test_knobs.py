@@ -12,7 +12,9 @@ MCMC_DENSE / MCMC_DENSE_ROWS in test_dense.py):
   MCMC_PHASE_DUMP, MCMC_PAIR_TRACE (diagnostics: results unchanged);
   partitioned: MCMC_PART_SOLO_OFF;
   wide sweep: MCMC_WALK_LIGHT, MCMC_WALK_TIE, MCMC_WIDE_INC_DIV, MCMC_WIDE_INC_HUB, MCMC_WIDE_INC_SLOT,
-  MCMC_TSCAN_PLAN.
+  MCMC_TSCAN_PLAN;
+  persistent launches: MCMC_PERSIST_CHECK_GRID (the co-residency check; test only).
+The count rebuild's MCMC_DENSE_RB is in test_dense.py::test_dense_rebuild_*.
 """
 import numpy as np
 import pytest
@@ -95,3 +97,37 @@ def test_wide_knobs(M, monkeypatch, env, ncol_div, eps, taboo):
     st = col.run(0)
     assert col.info()["variant"] == "wide"
     assert_same(col, st, r)
+
+
+@pytest.mark.parametrize("kind", ["dense", "wide"])
+def test_persistent_needs_coresident_grid(M, monkeypatch, kind):
+    """The persistent launches (dc_multi_kernel, ws_kernel) spin on flags their leader posts, so a
+    context takes them only when the whole grid can be resident at once (hipOccupancy x CUs >= the
+    grid). MCMC_PERSIST_CHECK_GRID makes the check ask for more workgroups than the device holds:
+    the context then runs the per-sweep path -- the same results as the oracle, the persistent
+    launch off in the statistics. Without the knob the same case takes the persistent path."""
+    import oracle_np as NP
+
+    def run(check_grid):
+        if check_grid:
+            monkeypatch.setenv("MCMC_PERSIST_CHECK_GRID", "100000000")
+        else:
+            monkeypatch.delenv("MCMC_PERSIST_CHECK_GRID", raising=False)
+        if kind == "dense":
+            off, idx, nc, r = oracle_case(3000, 0.3, 16, 57, epsilon=1e-8, maxRip=40)
+            col, st, _ = gpu_run(M, off, idx, nc, 57, 3000 * 3001 // 2, maxRip=40)
+            assert_same(col, st, r)
+            return col.dense_stats()["persistent"]
+        monkeypatch.setenv("MCMC_WS_ENTER", "-1")
+        off, idx = NP.rmat(12, 8, 0.5, 0.2, 0.2, 4)
+        ncol = int(np.diff(off.astype(np.int64)).max())
+        O.srand(1)
+        r = O.mcmc_run(off, idx, ncol, 1, maxRip=20)
+        g = M.Graph.from_csr(off, idx)
+        col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=20))
+        st = col.run(0)
+        assert_same(col, st, r)
+        return col.wide_solo_stats()["enabled"]
+
+    assert run(False)
+    assert not run(True)
