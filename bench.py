@@ -576,6 +576,16 @@ def main() -> int:
                           "workgroup of a persistent launch of all the timed sweeps; full sweeps (the count "
                           "rebuild) run on the whole grid inside it. Bit-identical to the scan sweeps "
                           "(tests/test_dense.py, tests/test_c3_full.py).")
+        if conv is not None and conv.get("rebuild_ms"):
+            # the count rebuild of a fresh colouring (dc_rebuild_kernel, once per colouring): every row's
+            # ids inside S (2 B each), its nCol counts and mask words written, the colours copied
+            rb_bytes = (nrows * deg * span / max(1, n) * 2.0 + nrows * a.ncol * 4.0 + nrows * nw * 4.0
+                        + 2.0 * nrows)
+            rb_gbs = rb_bytes / (conv["rebuild_ms"] * 1e-3) / 1e9
+            dense["rebuild"] = {"ms": conv["rebuild_ms"], "bytes": rb_bytes, "achieved_GBs": rb_gbs,
+                                "frac": rb_gbs / HBM_PEAK_GBS, "traffic": load_traffic("c3/rebuild") if a.config == "c3" else None,
+                                "what": "first-sweep minus second-sweep device time of a fresh colouring (the count rebuild, "
+                                        "csrc/dense_counts.h dc_rebuild_kernel); bytes: ids into S, counts, masks, copy"}
         if not a.no_full_scan and dist is None:
             # the same graph through the tiled scan sweep (MCMC_DENSE=0, the r03 early-exit kernel) and
             # the full scan (MCMC_FULL_SCAN=1): every sweep scans the layout

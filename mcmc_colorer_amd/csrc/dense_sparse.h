@@ -579,7 +579,7 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
             const unsigned long long t0 = wall_clock64();
             while ((g = __builtin_amdgcn_readfirstlane(dc_ld(&a.dc_ctl[kDcGen]))) == last) {
                 if (wall_clock64() - t0 > kDcIdleTicks) { g = 2u; break; }   // no leader: leave
-                __builtin_amdgcn_s_sleep(4);
+                for (uint32_t z = 0; z < a.dc_poll; z++) __builtin_amdgcn_s_sleep(4);   // (>= 1)
             }
             if ((g & 3u) == 1u) {   // a full sweep reads plain data of the last phases: acquire
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

@@ -237,6 +237,7 @@ struct SweepArgs {
     uint32_t dc_rbrows;         // rows per chunk of the streaming count rebuild (0: a wave per row)
     uint32_t dc_rbl;            // 1: the lane rebuild (dense_counts.h dc_rebuild_lanes; nCol <= 32)
     uint32_t dc_planes;         // its bit planes per count (counts < 2^dc_planes; 4..16)
+    uint32_t dc_poll;           // persistent dense sweep: s_sleep(4) rounds between a helper's polls (MCMC_DC_POLL)
     uint32_t dc_commit_restore;  // restore lists up to this long are applied by the commit
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
     // open summary (dense_counts.h dc_osum_note): word 0's low half = open words that are nonzero;
@@ -248,6 +249,10 @@ struct SweepArgs {
     uint32_t dl_n;
     unsigned long long* solo_ts;    // diagnostics (MCMC_SOLO_TRACE): the leader's stamps, [sweep of the launch][8]
     unsigned long long* wt_tick;    // wide tiled sweep: clock ticks per block step of the last sweep (0: none yet)
+    uint32_t* wt_ctl;           // wide tiled sweep, incremental counts (wide_tiled.h): kWtWords control words
+    uint32_t* wt_vcnt;          // [nloc] neighbours of the row's own colour in C_t
+    uint32_t* wt_deg;           // [nloc] the row's arcs (counted by the full sweep)
+    uint32_t* wt_list;          // [2][nloc] violators of the running sweep, then rows changed by it
     uint32_t nmodN;             // n mod (2^31 - 2): the advance of DevState::lx per sweep
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -3388,6 +3393,8 @@ struct mcmc_ctx {
     uint32_t dl_n = 0;
     unsigned long long* solo_ts = nullptr;   // MCMC_SOLO_TRACE diagnostics (4096 x 8 stamps)
     unsigned long long* wt_tick = nullptr;   // wide tiled sweep's block rotation clock (wide_tiled.h)
+    uint32_t* wt_buf = nullptr;     // its incremental counts: control words, vcnt, deg, lists (one allocation)
+    uint64_t wt_arcs_max = 0;       // changed arcs up to which the next sweep stays incremental
 };
 
 namespace {
@@ -3409,6 +3416,12 @@ hipError_t dc_reset(mcmc_ctx* c) {
     c->dc_fresh = true;
     hipError_t e = hipMemcpyAsync(c->dc_ctl, h, sizeof(h), hipMemcpyHostToDevice, c->stream);
     return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // h lives on this frame
+}
+
+// The wide tiled sweep's incremental counts after the colouring changed: the next sweep scans (full).
+hipError_t wt_reset(mcmc_ctx* c) {
+    hipError_t e = hipMemsetAsync(c->wt_buf, 0, sizeof(uint32_t) * kWtWords, c->stream);
+    return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
 }
 
 // Host <-> device colour transfers (n colours in vertex order; partitioned replicas too).
@@ -3592,6 +3605,13 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
     }
     if (c->wide_tiled) {
         a.wt_tick = c->wt_tick;
+        if (c->wt_buf) {
+            const size_t nloc = c->v_end - c->v_begin;
+            a.wt_ctl = c->wt_buf;
+            a.wt_vcnt = c->wt_buf + kWtWords;
+            a.wt_deg = a.wt_vcnt + nloc;
+            a.wt_list = a.wt_deg + nloc;
+        }
         a.etab = c->etab;
         a.walk_tie = c->walk_tie;
         a.fused = 0;
@@ -3615,6 +3635,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.dc_osum = c->dc_osum;
         a.dc_rbrows = c->dc_rbrows;
         a.dc_rbl = c->dc_rbl;
+        a.dc_poll = 1;
+        if (const char* dp = getenv("MCMC_DC_POLL")) a.dc_poll = (uint32_t)std::max(1, atoi(dp));
         a.dc_planes = c->dc_planes;
         a.dl_tab = c->dl_tab;
         a.dl_n = c->dl_n;
@@ -3663,9 +3685,19 @@ void launch_tiled_or_diag(mcmc_ctx* c, const SweepArgs& a) {
 void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     launch_tiled_or_diag(c, a);
     if (a.fused) return;
+    const uint32_t nloc = c->v_end - c->v_begin;
+    const uint32_t lane_grid = std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 255u) / 256u, 2048u));
+    if (a.wt_ctl) {   // the incremental sweep's kernels (each returns at once in a full sweep)
+        wt_eval_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
+        wt_viol_kernel<<<c->grid, c->block, c->lds, c->stream>>>(a);
+    }
     if (c->refwide) refw_commit_kernel<<<1, 1024, 0, c->stream>>>(a);
     else if (c->wide || c->wide_tiled) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
     else commit_kernel<uint8_t><<<1, kCommitThreads, 0, c->stream>>>(a);
+    if (a.wt_ctl) {   // the counts of the next colouring
+        wt_diff_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
+        wt_delta_kernel<<<c->grid.x, 512, 0, c->stream>>>(a, c->wt_arcs_max);
+    }
 }
 
 // The host's message for DevState::err bits.
@@ -4632,12 +4664,26 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         eps_table(p->epsilon, p->nCol, et.data());
         hipError_t ew = hipFuncSetAttribute((const void*)wide_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)c->lds);
+        if (ew == hipSuccess)
+            ew = hipFuncSetAttribute((const void*)wt_viol_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
         if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
         if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
         const char* rot = getenv("MCMC_WT_ROTATE");   // 0: every row scans blocks 0, 1, ... (A/B runs)
         if (ew == hipSuccess && !(rot && atoi(rot) == 0)) {
             ew = hipMalloc(&c->wt_tick, sizeof(unsigned long long));
             if (ew == hipSuccess) ew = hipMemset(c->wt_tick, 0, sizeof(unsigned long long));
+        }
+        // incremental violation counts (wide_tiled.h; MCMC_WT_INC: 0 off -- every sweep scans --, 2 every
+        // sweep after the first incremental): 16 B per row
+        const char* wi = getenv("MCMC_WT_INC");
+        const int wmode = wi ? atoi(wi) : 1;
+        if (ew == hipSuccess && wmode != 0) {
+            const size_t nloc = v_end - v_begin;
+            ew = hipMalloc(&c->wt_buf, sizeof(uint32_t) * (kWtWords + 4 * nloc));
+            if (ew == hipSuccess) ew = hipMemset(c->wt_buf, 0, sizeof(uint32_t) * kWtWords);
+            // a changed arc costs two colour gathers, a scanned arc one: incremental while the changed
+            // rows' arcs are at most a quarter of the layout's
+            c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / 4u;
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);
@@ -4878,6 +4924,7 @@ int mcmc_init_coloring(mcmc_ctx* c, const uint32_t* C0) {
     c->traj_ok = false;
     if (c->inc) MCMC_HIP_TRY(inc_reset(c));
     if (c->dc) MCMC_HIP_TRY(dc_reset(c));
+    if (c->wt_buf) MCMC_HIP_TRY(wt_reset(c));
     if (C0) {
         for (uint32_t v = 0; v < n; v++)
             if (C0[v] >= c->p.nCol) return fail(MCMC_E_ARG, "initial colour out of range");
@@ -5008,6 +5055,7 @@ int mcmc_run(mcmc_ctx* c, uint32_t max_sweeps, mcmc_run_stats* stats) {
         rc = run_tailcut(c, h, &s.finalViol, &s.tailcutPasses);
         if (rc) return rc;
         if (c->dc) MCMC_HIP_TRY(dc_reset(c));   // the passes changed colours outside a sweep
+        if (c->wt_buf) MCMC_HIP_TRY(wt_reset(c));
         if (c->inc) MCMC_HIP_TRY(inc_reset(c));
     }
     c->last = s;
@@ -5086,6 +5134,19 @@ int mcmc_get_scan_stats_v2(mcmc_ctx* c, uint64_t out[6]) {
 int mcmc_get_wide_inc_stats(mcmc_ctx* c, uint64_t out[5]) {
     if (!c || !out) return fail(MCMC_E_ARG, "NULL argument");
     for (int i = 0; i < 5; i++) out[i] = 0;
+    if (c->wt_buf) {   // the wide tiled sweep's counts: [1] incremental sweeps, [2] full, [3] changed rows,
+                       // [4] violators walked in incremental sweeps
+        MCMC_HIP_TRY(hipSetDevice(c->g->device));
+        MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
+        unsigned long long h[4];
+        MCMC_HIP_TRY(hipMemcpy(h, c->wt_buf + kWtStat, sizeof(h), hipMemcpyDeviceToHost));
+        out[0] = 1;
+        out[1] = h[1];
+        out[2] = h[0];
+        out[3] = h[2];
+        out[4] = h[3];
+        return MCMC_OK;
+    }
     if (!c->inc) return MCMC_OK;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     MCMC_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -5555,6 +5616,7 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dl_tab);
     (void)hipFree(c->solo_ts);
     (void)hipFree(c->wt_tick);
+    (void)hipFree(c->wt_buf);
     (void)hipFree(c->ws_buf);
     if (c->ws_dbg_host) (void)hipHostFree(c->ws_dbg_host);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -5830,6 +5892,7 @@ void part_tail_done(mcmc_ctx* c, uint64_t cviol, uint32_t passes) {
     // the passes changed colours outside a sweep: dense counts and incremental violation counts
     // start over, as after mcmc_run's tail cut
     if (c->dc) (void)dc_reset(c);
+    if (c->wt_buf) (void)wt_reset(c);
     if (c->inc) (void)inc_reset(c);
 }
 

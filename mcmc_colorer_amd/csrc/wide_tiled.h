@@ -35,12 +35,127 @@ inline uint32_t wide_tiled_wgs_per_cu(uint32_t nCol) {
     return std::max<uint32_t>(1u, std::min<uint32_t>(24u / W, (uint32_t)((160u * 1024u) / ((size_t)W * per))));
 }
 
+// Incremental violation counts (r06): the scan above is needed for a row's mask only when the
+// row violates (the walk of fill_p cases (i)/(ii) reads the mask); a non-violator's update is the
+// own-colour walk of case (iii) (walk_own_tab), which needs nothing but its draw. So each row keeps
+// vcnt = its neighbours of its own colour (violation_count, :329-351, is vcnt > 0) and a sweep in
+// incremental mode runs
+//   wt_eval_kernel   a lane per row: taboo rows keep their colour, non-violators take the own-colour
+//                    walk, violators are listed;
+//   wt_viol_kernel   a wave per listed violator: the scan and walk of the full sweep;
+//   commit_kernel    as before (loop control, the glibc replay of the CDF overflows);
+//   wt_diff_kernel   a lane per row: rows whose colour changed (C_t vs C_t+1, the replayed events
+//                    included) listed, their arcs summed;
+//   wt_delta_kernel  a wave per changed row u: for every arc (u, w) both counts move by
+//                    [C_t+1 u == C_t+1 w] - [C_t u == C_t w] (an arc between two changed rows from the
+//                    smaller end only).
+// The full sweep (wide_tiled_kernel) counts vcnt in its scan. The delta kernel chooses the next
+// sweep's mode: incremental while the changed rows' arcs cost less than a full scan (2 gathers per
+// changed arc against 1 per arc), else full (the counts are then recounted by the scan). Exact: the
+// counts are integers; tests/test_wide.py::test_wide_tiled_incremental* (against the oracle, the
+// full mode, forced modes) and tests/test_c3_full.py.
+constexpr uint32_t kWtMode = 0;   // the running sweep: 0 full (wide_tiled_kernel), 1 incremental
+constexpr uint32_t kWtVN = 1;     // violators listed by wt_eval_kernel (zeroed by wt_diff_kernel)
+constexpr uint32_t kWtCN = 2;     // changed rows listed by wt_diff_kernel (zeroed by the next sweep)
+constexpr uint32_t kWtArcs = 4;   // u64: their arcs
+constexpr uint32_t kWtStat = 8;   // u64 [4]: full sweeps, incremental sweeps, changed rows, violator walks
+constexpr uint32_t kWtWords = 16;
+
+// Row l of the sweep: its mask from every column block of the layout (vcnt: its neighbours of its own
+// colour, counted when FULL), then taboo / the violator walk / the own-colour walk. Returns viol.
+template <bool FULL>
+__device__ __forceinline__ uint32_t wt_row(const SweepArgs& a, uint32_t l, uint32_t t, uint32_t x_t,
+                                           const uint16_t* __restrict__ C, uint16_t* __restrict__ Cs,
+                                           uint32_t* mask, uint32_t* pre, unsigned long long tick) {
+    DevState* st = a.st;
+    const uint32_t NWW = (a.nCol + 31u) >> 5, lane = threadIdx.x & 63u;
+    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2;
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    const uint32_t v = a.v_begin + l;
+    const uint32_t cv = C[v];
+    for (uint32_t i = lane; i < NWW; i += 64u) mask[i] = 0u;
+    wave_lds_sync();
+    const uint32_t g = l / R, r = l - g * R;
+    const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
+    uint64_t deg = 0;
+    uint32_t same = 0;
+    const uint32_t bs = tick ? (uint32_t)((wall_clock64() / tick) % nb) : 0u;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 4u) {
+        const uint32_t bi = b0 + grp;
+        const uint32_t b = bi + bs < nb ? bi + bs : bi + bs - nb;
+        uint32_t s0 = 0, s1 = 0;
+        if (bi < nb) {
+            const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
+            const uint32_t raw = ts[r];
+            s0 = raw & kTsegPos;
+            s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
+        }
+        if (gl == 0 && s1 > s0) deg += s1 - s0;
+        const uint32_t lo = b << bl;
+        for (uint32_t k = s0 + gl; __ballot(k < s1); k += 128u) {
+            uint32_t c[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t kk = k + 16u * q;
+                c[q] = kk < s1 ? (uint32_t)C[lo | gc[kk]] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (c[q] != 0xFFFFFFFFu) {
+                    atomicOr(&mask[c[q] >> 5], 1u << (c[q] & 31u));
+                    if (FULL) same += c[q] == cv ? 1u : 0u;
+                }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) deg += __shfl_xor(deg, o, 64);
+    if (FULL && a.wt_ctl != nullptr) {
+        for (int o = 32; o > 0; o >>= 1) same += __shfl_xor(same, o, 64);
+        if (lane == 0) {
+            a.wt_vcnt[l] = same;
+            a.wt_deg[l] = (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu);
+        }
+    }
+    wave_lds_sync();
+    const uint32_t tab = a.taboo != nullptr ? a.taboo[l] : 0u;
+    const uint32_t viol = (mask[cv >> 5] >> (cv & 31u)) & 1u;
+    if (a.vflags != nullptr && lane == 0) a.vflags[(size_t)(t & 1u) * (a.v_end - a.v_begin) + l] = (uint8_t)viol;   // tail cut
+    // u_v: engine draw K_t + v + 1 (coloringMCMC_CPU.cpp:139)
+    const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)v + 1ull));
+    if (tab > 0) {   // :496-501
+        if (lane == 0) {
+            Cs[v] = (uint16_t)cv;
+            a.taboo[l] = tab - 1u;
+        }
+    } else if (viol) {   // case (ii) / (i): the walk over the mask (writes Cs, taboo, the event)
+        walk_finish_wave<false>(a, v, t, cv, x, (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu), Cs, mask, pre, nullptr, nullptr,
+                                lane);
+    } else if (lane == 0) {   // case (iii)
+        const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(x));
+        const bool event = nc == a.nCol;
+        Cs[v] = (uint16_t)(event ? cv : nc);
+        if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+        if (event) {
+            const uint32_t idx = atomicAdd(&st->ev_count, 1u);
+            if (idx < a.ev_cap) a.events[idx] = v;
+            else atomicOr(&st->err, 1u);
+        }
+    }
+    wave_lds_sync();   // the walk's LDS reads are done before the next row clears the mask
+    return viol;
+}
+
 __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     extern __shared__ uint32_t wt_lds[];
     __shared__ uint32_t sh_viol;
     DevState* st = a.st;
     if (a.check_done && st->done) return;
+    if (a.wt_ctl != nullptr && a.wt_ctl[kWtMode] != 0u) return;   // an incremental sweep: wt_eval_kernel
     if (threadIdx.x == 0) sh_viol = 0;
+    if (a.wt_ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.wt_ctl[kWtCN] = 0u;   // (the last sweep's delta has run)
+        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtArcs)[0] = 0ull;
+        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[0] += 1ull;
+    }
     __syncthreads();
     const uint32_t t = st->t, x_t = st->x_t;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
@@ -49,8 +164,7 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     uint32_t* const mask = wt_lds + (size_t)wave * (2u * NWW + 1u);
     uint32_t* const pre = mask + NWW;
-    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2;
-    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    const uint32_t nb = a.nblocks;
     uint32_t wave_viol = 0, nrows = 0;
     // Block rotation: a row's mask is an OR, so its blocks may be scanned in any cyclic order. Each
     // row starts at the block a common clock points to (one block per tick, the tick measured on
@@ -59,67 +173,8 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     const unsigned long long tick = a.wt_tick != nullptr ? *a.wt_tick : 0ull;
     const unsigned long long t_begin = wall_clock64();
     for (uint32_t l = blockIdx.x * nwv + wave; l < nloc; l += gridDim.x * nwv) {
-        const uint32_t v = a.v_begin + l;
-        for (uint32_t i = lane; i < NWW; i += 64u) mask[i] = 0u;
-        wave_lds_sync();
-        const uint32_t g = l / R, r = l - g * R;
-        const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
-        uint64_t deg = 0;
-        const uint32_t bs = tick ? (uint32_t)((wall_clock64() / tick) % nb) : 0u;
         nrows++;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 4u) {
-            const uint32_t bi = b0 + grp;
-            const uint32_t b = bi + bs < nb ? bi + bs : bi + bs - nb;
-            uint32_t s0 = 0, s1 = 0;
-            if (bi < nb) {
-                const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
-                const uint32_t raw = ts[r];
-                s0 = raw & kTsegPos;
-                s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
-            }
-            if (gl == 0 && s1 > s0) deg += s1 - s0;
-            const uint32_t lo = b << bl;
-            for (uint32_t k = s0 + gl; __ballot(k < s1); k += 128u) {
-                uint32_t c[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const uint32_t kk = k + 16u * q;
-                    c[q] = kk < s1 ? (uint32_t)C[lo | gc[kk]] : 0xFFFFFFFFu;
-                }
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (c[q] != 0xFFFFFFFFu) atomicOr(&mask[c[q] >> 5], 1u << (c[q] & 31u));
-            }
-        }
-        for (int o = 32; o > 0; o >>= 1) deg += __shfl_xor(deg, o, 64);
-        wave_lds_sync();
-        const uint32_t cv = C[v];
-        const uint32_t tab = a.taboo != nullptr ? a.taboo[l] : 0u;
-        const uint32_t viol = (mask[cv >> 5] >> (cv & 31u)) & 1u;
-        wave_viol += viol;
-        if (a.vflags != nullptr && lane == 0) a.vflags[(size_t)(t & 1u) * nloc + l] = (uint8_t)viol;   // tail cut
-        // u_v: engine draw K_t + v + 1 (coloringMCMC_CPU.cpp:139)
-        const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)v + 1ull));
-        if (tab > 0) {   // :496-501
-            if (lane == 0) {
-                Cs[v] = (uint16_t)cv;
-                a.taboo[l] = tab - 1u;
-            }
-        } else if (viol) {   // case (ii) / (i): the walk over the mask (writes Cs, taboo, the event)
-            walk_finish_wave<false>(a, v, t, cv, x, (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu), Cs, mask, pre, nullptr, nullptr,
-                             lane);
-        } else if (lane == 0) {   // case (iii)
-            const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(x));
-            const bool event = nc == a.nCol;
-            Cs[v] = (uint16_t)(event ? cv : nc);
-            if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
-            if (event) {
-                const uint32_t idx = atomicAdd(&st->ev_count, 1u);
-                if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
-            }
-        }
-        wave_lds_sync();   // the walk's LDS reads are done before the next row clears the mask
+        wave_viol += wt_row<true>(a, l, t, x_t, C, Cs, mask, pre, tick);
     }
     if (lane == 0 && wave_viol) atomicAdd(&sh_viol, wave_viol);
     if (a.wt_tick != nullptr && blockIdx.x == 0 && threadIdx.x == 0 && nrows > 0) {   // next sweep's tick
@@ -130,6 +185,181 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     if (threadIdx.x == 0 && sh_viol) atomicAdd(&st->viol, (unsigned long long)sh_viol);
 }
 
+// An incremental sweep, a lane per row: Cviol from the counts; taboo rows keep their colour (the
+// counter drops); non-violators take the own-colour walk (case (iii), CDF overflows to the event
+// list); violators are listed for wt_viol_kernel, which writes their colours.
+__global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
+    __shared__ uint32_t sh_viol;
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    if (a.wt_ctl[kWtMode] == 0u) return;   // a full sweep: wide_tiled_kernel
+    if (threadIdx.x == 0) sh_viol = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.wt_ctl[kWtCN] = 0u;
+        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtArcs)[0] = 0ull;
+        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[1] += 1ull;
+    }
+    __syncthreads();
+    const uint32_t t = st->t, x_t = st->x_t;
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
+    const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
+    uint32_t wave_viol = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += gridDim.x * blockDim.x) {
+        const uint32_t l = base + threadIdx.x;
+        const bool in = l < nloc;
+        const uint32_t v = a.v_begin + l;
+        const uint32_t cv = in ? (uint32_t)C[v] : 0u;
+        const uint32_t viol = in && a.wt_vcnt[l] != 0u ? 1u : 0u;
+        const uint32_t tab = (in && a.taboo != nullptr) ? a.taboo[l] : 0u;
+        if (in && a.vflags != nullptr) a.vflags[(size_t)(t & 1u) * nloc + l] = (uint8_t)viol;   // tail cut
+        wave_viol += (uint32_t)__popcll(__ballot(viol != 0u));
+        const bool walk = in && tab == 0u && viol;
+        const uint64_t wb = __ballot(walk);
+        if (wb) {   // violators to the list (one reservation per wave)
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&a.wt_ctl[kWtVN], (uint32_t)__popcll(wb));
+            b0 = __shfl(b0, 0, 64);
+            if (walk) a.wt_list[b0 + (uint32_t)__popcll(wb & ((1ull << lane) - 1ull))] = l;
+        }
+        bool event = false;
+        if (in && tab > 0u) {   // :496-501
+            Cs[v] = (uint16_t)cv;
+            a.taboo[l] = tab - 1u;
+        } else if (in && !viol) {   // case (iii)
+            const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1ull));
+            const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(x));
+            event = nc == a.nCol;
+            Cs[v] = (uint16_t)(event ? cv : nc);
+            if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
+        }
+        const uint64_t eb = __ballot(event);
+        if (eb) {
+            uint32_t e0 = 0;
+            if (lane == 0) e0 = atomicAdd(&st->ev_count, (uint32_t)__popcll(eb));
+            e0 = __shfl(e0, 0, 64);
+            if (event) {
+                const uint32_t idx = e0 + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
+                if (idx < a.ev_cap) a.events[idx] = v;
+                else atomicOr(&st->err, 1u);
+            }
+        }
+    }
+    if (lane == 0 && wave_viol) atomicAdd(&sh_viol, wave_viol);
+    __syncthreads();
+    if (threadIdx.x == 0 && sh_viol) atomicAdd(&st->viol, (unsigned long long)sh_viol);
+}
+
+// The listed violators of an incremental sweep, a wave each: the full sweep's scan and walk.
+__global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
+    extern __shared__ uint32_t wt_lds[];
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    if (a.wt_ctl[kWtMode] == 0u) return;
+    const uint32_t nv = a.wt_ctl[kWtVN];
+    const uint32_t t = st->t, x_t = st->x_t;
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
+    const uint32_t NWW = (a.nCol + 31u) >> 5, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t* const mask = wt_lds + (size_t)wave * (2u * NWW + 1u);
+    uint32_t* const pre = mask + NWW;
+    const unsigned long long tick = a.wt_tick != nullptr ? *a.wt_tick : 0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[3] += nv;
+    for (uint32_t i = blockIdx.x * nwv + wave; i < nv; i += gridDim.x * nwv)
+        (void)wt_row<false>(a, a.wt_list[i], t, x_t, C, Cs, mask, pre, tick);
+}
+
+// After the commit of an accepted sweep (st->t = t + 1): the rows whose colour changed from C_t to
+// C_t+1, listed (after the violators, which wt_viol_kernel has consumed: their count is reset here),
+// their arcs summed.
+__global__ __launch_bounds__(256) void wt_diff_kernel(SweepArgs a) {
+    DevState* st = a.st;
+    if (st->done) return;
+    const uint32_t t1 = st->t;
+    const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>((t1 & 1) ? a.colors1 : a.colors0);
+    const uint16_t* __restrict__ Co = reinterpret_cast<const uint16_t*>((t1 & 1) ? a.colors0 : a.colors1);
+    const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
+    uint32_t* const list = a.wt_list + nloc;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.wt_ctl[kWtVN] = 0u;
+    unsigned long long arcs = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += gridDim.x * blockDim.x) {
+        const uint32_t l = base + threadIdx.x;
+        const uint32_t v = a.v_begin + l;
+        const bool ch = l < nloc && Cn[v] != Co[v];
+        const uint64_t cb = __ballot(ch);
+        if (!cb) continue;
+        uint32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.wt_ctl[kWtCN], (uint32_t)__popcll(cb));
+        b0 = __shfl(b0, 0, 64);
+        if (ch) {
+            list[b0 + (uint32_t)__popcll(cb & ((1ull << lane) - 1ull))] = l;
+            arcs += a.wt_deg[l];
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) arcs += __shfl_xor(arcs, o, 64);
+    if (lane == 0 && arcs) atomicAdd(reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtArcs), arcs);
+}
+
+// The counts of C_t+1 from those of C_t, a wave per changed row (the next sweep incremental), or
+// the next sweep full when the changed arcs cost more than a scan (MCMC_WT_INC: 0 never incremental,
+// 2 always). Every workgroup reads the same totals and takes the same decision.
+__global__ __launch_bounds__(512) void wt_delta_kernel(SweepArgs a, uint64_t arcs_max) {
+    DevState* st = a.st;
+    if (st->done) return;
+    const uint32_t nch = a.wt_ctl[kWtCN];
+    const unsigned long long arcs = reinterpret_cast<const unsigned long long*>(a.wt_ctl + kWtArcs)[0];
+    const bool inc = arcs <= arcs_max;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.wt_ctl[kWtMode] = inc ? 1u : 0u;
+        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[2] += nch;
+    }
+    if (!inc) return;
+    const uint32_t t1 = st->t;
+    const uint16_t* __restrict__ Cn = reinterpret_cast<const uint16_t*>((t1 & 1) ? a.colors1 : a.colors0);
+    const uint16_t* __restrict__ Co = reinterpret_cast<const uint16_t*>((t1 & 1) ? a.colors0 : a.colors1);
+    const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2;
+    const uint32_t grp = lane >> 4, gl = lane & 15u;
+    const uint32_t* __restrict__ list = a.wt_list + nloc;
+    for (uint32_t i = blockIdx.x * nwv + wave; i < nch; i += gridDim.x * nwv) {
+        const uint32_t l = list[i], u = a.v_begin + l;
+        const uint32_t cu = Co[u], cu1 = Cn[u];
+        const uint32_t g = l / R, r = l - g * R;
+        const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
+        int own = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += 4u) {
+            const uint32_t b = b0 + grp;
+            uint32_t s0 = 0, s1 = 0;
+            if (b < nb) {
+                const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
+                const uint32_t raw = ts[r];
+                s0 = raw & kTsegPos;
+                s1 = (ts[r + 1] & kTsegPos) - (raw & 7u);
+            }
+            const uint32_t lo = b << bl;
+            for (uint32_t k = s0 + gl; __ballot(k < s1); k += 64u) {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t kk = k + 16u * q;
+                    w[q] = kk < s1 ? (lo | (uint32_t)gc[kk]) : 0xFFFFFFFFu;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (w[q] == 0xFFFFFFFFu) continue;
+                    const uint32_t cw = Co[w[q]], cw1 = Cn[w[q]];
+                    const int d = (cu1 == cw1 ? 1 : 0) - (cu == cw ? 1 : 0);
+                    if (d == 0 || (cw != cw1 && w[q] < u)) continue;   // (both changed: the smaller end)
+                    own += d;
+                    const uint32_t lw = w[q] - a.v_begin;
+                    if (lw < nloc) atomicAdd(&a.wt_vcnt[lw], (uint32_t)d);
+                }
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) own += __shfl_xor(own, o, 64);
+        if (lane == 0 && own) atomicAdd(&a.wt_vcnt[l], (uint32_t)own);
+    }
+}
 void launch_wide_tiled(const SweepArgs& a, dim3 g, dim3 b, size_t lds, hipStream_t s) {
     wide_tiled_kernel<<<g, b, lds, s>>>(a);
 }

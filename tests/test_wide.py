@@ -348,6 +348,67 @@ def test_wide_tiled_generated_graph(M, monkeypatch, n, p, seed):
     col.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("inc", ["0", "1", "2"])
+@pytest.mark.parametrize("case", ["sparse", "taboo", "eps1e3", "hub", "every_vertex", "tailcut", "generated"])
+def test_wide_tiled_incremental(M, monkeypatch, inc, case):
+    """The wide tiled sweep's incremental violation counts (csrc/wide_tiled.h wt_*): MCMC_WT_INC=0
+    scans every sweep, 1 (default) chooses per sweep, 2 runs every sweep after the first from the
+    counts (lane-per-row evaluation, violators walked from a list, the counts moved by the changed
+    rows). Each run equals the oracle's; the statistics show which sweeps were incremental."""
+    monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    monkeypatch.setenv("MCMC_WT_INC", inc)
+    kw = {}
+    if case == "generated":
+        off, idx = O.er_fast(70000, 0.01, 3)
+        ncol, kw = O.max_deg(off), {"maxRip": 12}
+        g = M.Graph.er_fast(70000, 0.01, 3)
+        col = M.ColoringMCMC(g, M.GPURand(70000, 3, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=ncol, maxRip=12))
+        st = col.run(0)
+        O.srand(1)
+        r = O.mcmc_run(off, idx, ncol, 3, maxRip=12)
+        assert col.coloring().tolist() == r.colors.tolist()
+        assert col.trajectory().tolist() == r.traj.tolist()
+        assert (st.iter, st.finalViol, st.glibcDraws) == (r.res.iter, r.res.finalViol, r.res.glibcDraws)
+        ws = col.wide_inc_stats()
+    else:
+        if case == "hub":
+            off, idx = _hub_graph()
+            ncol = 300
+            kw = {"maxRip": 30}
+        elif case == "every_vertex":   # nCol 16: every vertex violates every sweep
+            O.srand(1)
+            off, idx = O.setup_rnd2(2000, 0.05)
+            ncol, kw = 16, {"maxRip": 40}
+        else:
+            O.srand(1)
+            off, idx = O.setup_rnd2(3000, 0.01)
+            ncol = {"sparse": 300, "taboo": 1000, "eps1e3": 700, "tailcut": 4000}[case]
+            kw = {"taboo": {"tabooIteration": 2}, "eps1e3": {"epsilon": 1e-3},
+                  "tailcut": {"tailcut": True}}.get(case, {})
+        g = M.Graph.from_csr(off, idx)
+        params = M.ColoringMCMCParams(nCol=ncol, epsilon=kw.get("epsilon", 1e-8), maxRip=kw.get("maxRip", 250),
+                                      tabooIteration=kw.get("tabooIteration", 0), tailcut=kw.get("tailcut", False))
+        col = M.ColoringMCMC(g, M.GPURand(g.nNodes, 1, M.GlibcRand(1)), params)
+        st = col.run(0)
+        O.srand(1)
+        r = O.mcmc_run(off, idx, ncol, 1, **kw)
+        assert col.info()["variant"] == "wide-tiled"
+        assert col.coloring().tolist() == r.colors.tolist()
+        assert col.trajectory().tolist() == r.traj.tolist()
+        assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws) == (
+            r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws)
+        ws = col.wide_inc_stats()
+    sweeps = int(st.sweepsRun)
+    if inc == "0":
+        assert not ws["enabled"]
+    else:
+        assert ws["enabled"] and ws["full_sweeps"] >= 1
+        if inc == "2" and sweeps > 1:
+            assert ws["incremental_sweeps"] >= 1 and ws["full_sweeps"] == 1, ws
+    col.close()
+
+
 def _hub_graph(n=5000):
     """A hub joined to n - 1000 vertices plus a sparse remainder: one long row, many empty/short ones."""
     rng = np.random.default_rng(5)
