@@ -639,9 +639,13 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
     // the leader computes them while the helpers move the last sweep's counts (s_rawok: valid for
     // the current window), off the event step's critical path.
     auto draws = [&]() {
+        // the lane's table column from one opaque base per call: hipcc otherwise hoists the 31
+        // per-lane addresses out of the sweep loop, where they outlive the registers and spill
+        const uint32_t* tp = kGlibcTab + threadIdx.x;
+        asm volatile("" : "+v"(tp));
         uint32_t tv[31];
 #pragma unroll
-        for (int m = 0; m < 31; m++) tv[m] = kGlibcTab[m * kGlibcTabK + threadIdx.x];
+        for (int m = 0; m < 31; m++) tv[m] = tp[m * kGlibcTabK];
         uint32_t acc = 0;
 #pragma unroll
         for (int m = 0; m < 31; m++) acc += tv[m] * s.ring[m];
