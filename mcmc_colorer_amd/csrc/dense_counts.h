@@ -538,10 +538,10 @@ __device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, 
     const uint32_t nloc = a.v_end - a.v_begin, bl = a.block_log2;
     const uint32_t bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
     const uint32_t nmov_w = mode ? 0u : len * nbl;   // len <= |S| / 8 + 1 when incremental: no overflow
-    const uint32_t n1 = copy ? (nloc + kDcCopyRows - 1u) / kDcCopyRows : (m + 1023u) / 1024u;
+    const uint32_t n1 = copy ? (nloc + kDcCopyRows - 1u) / kDcCopyRows : (m + blockDim.x - 1u) / blockDim.x;
     const uint32_t R = a.grp_rows, Rc = a.dc_rbrows, cpg = Rc ? (R + Rc - 1u) / Rc : 0u;   // chunks per group
     const uint32_t n2 = mode ? (Rc ? a.ngroups * cpg : (nloc + kDcRebuildRows - 1u) / kDcRebuildRows)
-                             : (nmov_w + 15u) / 16u;
+                             : (nmov_w + (blockDim.x >> 6) - 1u) / (blockDim.x >> 6);   // a wave task per wave
     const uint32_t T = n1 + n2;
     if (T == 0u) return;
     const uint8_t* __restrict__ C = (t & 1) ? a.colors1 : a.colors0;   // C_t
@@ -564,7 +564,7 @@ __device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, 
             for (size_t i = b0 + threadIdx.x; i < (q0 < b1 ? q0 : b1); i += blockDim.x) Y[i] = C[i];
             for (size_t i = (q1 > b0 ? q1 : b0) + threadIdx.x; i < b1; i += blockDim.x) Y[i] = C[i];
         } else if (k < n1) {
-            const uint32_t i = k * 1024u + threadIdx.x;
+            const uint32_t i = k * blockDim.x + threadIdx.x;
             if (i < m) {
                 const uint32_t u = a.dc_chg[(size_t)p * a.dc_chg_cap + i];
                 Y[u] = C[u];
@@ -626,7 +626,7 @@ __device__ __forceinline__ void dc_update_tasks(const SweepArgs& a, uint32_t t, 
                 dc_lds_wait();   // every lane's reads of h are done before the next row clears it
             }
         } else {
-            const uint32_t task = (k - n1) * 16u + wv;
+            const uint32_t task = (k - n1) * (blockDim.x >> 6) + wv;
             if (task < nmov_w) {
                 const uint32_t i = task / nbl, b = bl0 + (task - i * nbl);
                 const uint32_t* e = a.dc_list + 2u * ((size_t)p * a.dc_cap + i);   // (u, ca << 16 | cb)
@@ -789,7 +789,7 @@ __device__ __forceinline__ bool dc_stage_flush(const SweepArgs& a, DevState* st,
         if (v == ~0u) continue;
         const uint32_t j = n2 <= caps[2] ? base[2] + i : atomicAdd(&st->ev_count, 1u);
         if (j < a.ev_cap) a.events[j] = v;
-        else atomicOr(&st->err, 1u);
+        else atomicOr(&st->err, kDevErrEvents);
     }
     return true;
 }

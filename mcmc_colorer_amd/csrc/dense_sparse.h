@@ -20,7 +20,8 @@
 //     Cviol_t = nloc - (rows evaluated) + (violators among them).
 // The result is bit-identical to evaluating every row (tests/test_dense.py runs both).
 //
-// dc_multi_kernel runs K sweeps in one launch, one 1024-thread workgroup per CU. Workgroup 0 (the
+// dc_multi_kernel runs K sweeps in one launch, one BS-thread workgroup per CU (BS = 512 by default:
+// 256 VGPRs per lane, no scratch for NW <= 2; MCMC_DCM_BS=1024 doubles the waves). Workgroup 0 (the
 // leader) plans each sweep from the control words:
 //   solo  the update has at most a few moved vertices of S, the restore list was applied by the
 //         last commit, few open mask words: the leader posts the moves to the helpers (a move
@@ -193,7 +194,7 @@ __device__ __forceinline__ void dc_solo_rows(const SweepArgs& a, const uint8_t* 
 // A move phase (persistent sweep, kind 3): the last sweep's moves of S (kDcMvN vertices, their
 // (v, a << 16 | b) at kDcMvList) applied to the counts of every local row holding them, by the
 // helpers: wave task j (vertex j / nbl, column block j % nbl) is u's segment in that block, the
-// workgroup tasks (16 wave tasks each) dealt statically to workgroups 1..G-1 -- no claim counter,
+// workgroup tasks (a wave task per wave) dealt statically to workgroups 1..G-1 -- no claim counter,
 // so nothing to reset between phases. Each workgroup adds its completed tasks to kDcMvDone once
 // its atomics have returned; the leader waits for the total. Everything it reads arrives by sc1
 // loads (the list) or is read-only (the layout); the counts move by device-scope atomics.
@@ -206,12 +207,13 @@ __device__ __forceinline__ void dc_help_moves(const SweepArgs& a) {
     }
     __syncthreads();
     const uint32_t bl = a.block_log2, bl0 = a.v_begin >> bl, nbl = ((a.v_end - 1u) >> bl) - bl0 + 1u;
-    const uint32_t nloc = a.v_end - a.v_begin, T = s_len * nbl, J = (T + 15u) / 16u;
+    const uint32_t nwv = blockDim.x >> 6;
+    const uint32_t nloc = a.v_end - a.v_begin, T = s_len * nbl, J = (T + nwv - 1u) / nwv;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint32_t mine = 0;
     for (uint32_t j = blockIdx.x - 1u; j < J; j += gridDim.x - 1u) {
         mine++;
-        const uint32_t task = j * 16u + wv;
+        const uint32_t task = j * nwv + wv;
         if (task >= T) continue;
         const uint32_t i = task / nbl, b = bl0 + (task - i * nbl);
         const uint32_t u = s_mvl[2u * i], ab = s_mvl[2u * i + 1u], ca = ab >> 16, cb = ab & 0xFFFFu;
@@ -307,7 +309,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
                 seq++;
                 __hip_atomic_store(&a.dc_ctl[kDcGen], (seq << 2) | 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t nbl = ((a.v_end - 1u) >> a.block_log2) - (a.v_begin >> a.block_log2) + 1u;
-                mvexp += (len * nbl + 15u) / 16u;
+                mvexp += (len * nbl + nwv - 1u) / nwv;   // (dc_help_moves' workgroup tasks)
                 a.dc_ctl[kDcLen + p] = 0u;
                 sv.st_listed += len;
                 sv.len = 0;
@@ -536,8 +538,8 @@ __device__ __forceinline__ void dc_post(const SweepArgs& a, uint32_t g) {
     }
 }
 
-template <int NW>
-__global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K) {
+template <int NW, uint32_t BS>
+__global__ __launch_bounds__(BS) void dc_multi_kernel(SweepArgs a, uint32_t K) {
     extern __shared__ uint4 dc_lds[];
     __shared__ float2 ewl[256];
     __shared__ uint2 xkeep[256];
@@ -645,12 +647,12 @@ __global__ __launch_bounds__(1024) void dc_multi_kernel(SweepArgs a, uint32_t K)
     }
 }
 
-template <int NW>
+template <int NW, uint32_t BS>
 void launch_dcm(const SweepArgs& a, uint32_t K, dim3 g, hipStream_t s) {
-    dc_multi_kernel<NW><<<g, dim3(1024), kDcMultiLds, s>>>(a, K);
+    dc_multi_kernel<NW, BS><<<g, dim3(BS), kDcMultiLds, s>>>(a, K);
 }
-template <int NW>
+template <int NW, uint32_t BS>
 hipError_t allow_lds_dcm() {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_multi_kernel<NW>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_multi_kernel<NW, BS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDcMultiLds);
 }

@@ -253,6 +253,7 @@ struct SweepArgs {
     uint32_t* wt_vcnt;          // [nloc] neighbours of the row's own colour in C_t
     uint32_t* wt_deg;           // [nloc] the row's arcs (counted by the full sweep)
     uint32_t* wt_list;          // [2][nloc] violators of the running sweep, then rows changed by it
+    uint8_t* wt_chg;            // [nloc / 8 + 2] rows changed by the last sweep, a bit each (8-row groups of global v)
     uint32_t nmodN;             // n mod (2^31 - 2): the advance of DevState::lx per sweep
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -781,7 +782,7 @@ __device__ __forceinline__ void commit_control(const SweepArgs& a, uint32_t t, u
         return;
     }
     if (E > a.ev_cap || err) {
-        if (threadIdx.x == 0) { st->err |= 1u; st->done = 1; st->iter = t; }
+        if (threadIdx.x == 0) { st->err |= kDevErrEvents; st->done = 1; st->iter = t; }
         return;
     }
     commit_accept<CT>(a, t, ev ? ev : a.events, E, lds, lds_cap, sorted);
@@ -1492,7 +1493,7 @@ __device__ __forceinline__ uint32_t evaluate_lane(const SweepArgs& a, DevState* 
         if (event) {
             const uint32_t idx = basei + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
             if (idx < a.ev_cap) a.events[idx] = v;
-            else atomicOr(&st->err, 1u);
+            else atomicOr(&st->err, kDevErrEvents);
         }
     }
     return nviol;
@@ -3611,6 +3612,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.wt_vcnt = c->wt_buf + kWtWords;
             a.wt_deg = a.wt_vcnt + nloc;
             a.wt_list = a.wt_deg + nloc;
+            a.wt_chg = reinterpret_cast<uint8_t*>(a.wt_list + 2u * nloc);
         }
         a.etab = c->etab;
         a.walk_tie = c->walk_tie;
@@ -4162,6 +4164,30 @@ static bool coresident(const void* kernel, uint32_t grid, uint32_t block, size_t
     return (uint64_t)per * (uint64_t)cus >= grid;
 }
 
+// The persistent dense launch's workgroup size (MCMC_DCM_BS, 512 or 1024; default 512): at 512
+// threads a wave may hold 256 VGPRs and dc_multi_kernel<1|2> runs without scratch (at 1024 the
+// 128-VGPR cap spilled 256-544 B per lane, written once per wave and launch).
+static uint32_t dcm_bs() {
+    const char* e = getenv("MCMC_DCM_BS");
+    return e && atoi(e) == 1024 ? 1024u : 512u;
+}
+extern "C++" {
+template <uint32_t BS>
+static hipError_t setup_dcm(mcmc_ctx* c, int wi) {
+    static const decltype(c->dcm_launch) launch[4] = {launch_dcm<1, BS>, launch_dcm<2, BS>, launch_dcm<4, BS>,
+                                                      launch_dcm<8, BS>};
+    static hipError_t (*const allow[4])() = {allow_lds_dcm<1, BS>, allow_lds_dcm<2, BS>, allow_lds_dcm<4, BS>,
+                                             allow_lds_dcm<8, BS>};
+    const void* const fn[4] = {reinterpret_cast<const void*>(&dc_multi_kernel<1, BS>),
+                               reinterpret_cast<const void*>(&dc_multi_kernel<2, BS>),
+                               reinterpret_cast<const void*>(&dc_multi_kernel<4, BS>),
+                               reinterpret_cast<const void*>(&dc_multi_kernel<8, BS>)};
+    const hipError_t e = allow[wi]();
+    if (e == hipSuccess && coresident(fn[wi], c->grid.x, BS, kDcMultiLds, c->g->device)) c->dcm_launch = launch[wi];
+    return e;
+}
+}
+
 static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     const char* e = getenv("MCMC_WIDE_SOLO");
     if ((e && atoi(e) == 0) || !c->inc || c->part || c->v_begin != 0 || c->v_end != c->n || c->p.tabooIteration > 0 ||
@@ -4592,19 +4618,11 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             c->lds = kDcRebuildLds;
             ea = wi == 0 ? allow_lds_dc<1>(c->lds) : wi == 1 ? allow_lds_dc<2>(c->lds)
                : wi == 2 ? allow_lds_dc<4>(c->lds) : allow_lds_dc<8>(c->lds);
-            const void* dcm_fn = wi == 0 ? reinterpret_cast<const void*>(&dc_multi_kernel<1>)
-                               : wi == 1 ? reinterpret_cast<const void*>(&dc_multi_kernel<2>)
-                               : wi == 2 ? reinterpret_cast<const void*>(&dc_multi_kernel<4>)
-                                         : reinterpret_cast<const void*>(&dc_multi_kernel<8>);
-            if (ea == hipSuccess && c->dc_osum && c->dl_n) {   // its LDS allowance first: the occupancy query needs it
-                ea = wi == 0 ? allow_lds_dcm<1>() : wi == 1 ? allow_lds_dcm<2>() : wi == 2 ? allow_lds_dcm<4>() : allow_lds_dcm<8>();
-            }
             // the persistent launch (dense_sparse.h), where sweeps can run solo and the grid can be
-            // co-resident (else one dc_eval_kernel per sweep)
-            if (ea == hipSuccess && c->dc_osum && c->dl_n && coresident(dcm_fn, c->grid.x, 1024, kDcMultiLds, c->g->device)) {
-                static const decltype(c->dcm_launch) tabm[4] = {launch_dcm<1>, launch_dcm<2>, launch_dcm<4>, launch_dcm<8>};
-                c->dcm_launch = tabm[wi];
-            }
+            // co-resident (else one dc_eval_kernel per sweep); its LDS allowance first: the
+            // occupancy query needs it
+            if (ea == hipSuccess && c->dc_osum && c->dl_n)
+                ea = dcm_bs() == 1024u ? setup_dcm<1024>(c, wi) : setup_dcm<512>(c, wi);
         } else if (c->early) {   // the early-exit instantiations
             if (resident) {
                 static const SweepLaunch tab[4] = {launch_tiled<1, true, false, true>, launch_tiled<2, true, false, true>,
@@ -4679,7 +4697,7 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         const int wmode = wi ? atoi(wi) : 1;
         if (ew == hipSuccess && wmode != 0) {
             const size_t nloc = v_end - v_begin;
-            ew = hipMalloc(&c->wt_buf, sizeof(uint32_t) * (kWtWords + 4 * nloc));
+            ew = hipMalloc(&c->wt_buf, sizeof(uint32_t) * (kWtWords + 4 * (size_t)nloc + nloc / 32u + 2u));
             if (ew == hipSuccess) ew = hipMemset(c->wt_buf, 0, sizeof(uint32_t) * kWtWords);
             // a changed arc costs two colour gathers, a scanned arc one: incremental while the changed
             // rows' arcs are at most a quarter of the layout's

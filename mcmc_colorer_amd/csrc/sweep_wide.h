@@ -748,7 +748,7 @@ __device__ void walk_finish(const SweepArgs& a, uint32_t v, uint32_t t, uint32_t
             if (event) {
                 const uint32_t idx = atomicAdd(&st->ev_count, 1u);
                 if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
+                else atomicOr(&st->err, kDevErrEvents);
             }
         }
     }
@@ -822,7 +822,7 @@ __device__ void walk_finish_wave(const SweepArgs& a, uint32_t v, uint32_t t, uin
         if (event) {
             const uint32_t idx = atomicAdd(&st->ev_count, 1u);
             if (idx < a.ev_cap) a.events[idx] = v;
-            else atomicOr(&st->err, 1u);
+            else atomicOr(&st->err, kDevErrEvents);
         }
     }
     wave_lds_sync();
@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(SweepArgs a) {
             } else {
                 const uint32_t idx = atomicAdd(&st->ev_count, 1u);
                 if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
+                else atomicOr(&st->err, kDevErrEvents);
             }
         }
     }

@@ -60,7 +60,9 @@ constexpr uint32_t kWsLeadSets = 6;        // the leader's walk mask sets at mos
 constexpr uint32_t kWsLeadList = 16384;    // violator-list updates the leader does itself
 constexpr uint32_t kWsVvLds = 32;          // violators held in LDS for the candidates' test (more: counts)
 constexpr uint32_t kWsPreLds = 16384;      // delta phase: changed rows whose arc prefix sits in LDS
+constexpr uint32_t kWsChgLds = 4096;       // and whose entries (16 B) sit there too, after the prefix
 constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
+static_assert(4u * (kWsPreLds + 4u * kWsChgLds) <= kWsLds, "delta phase prefix + entries in LDS");
 enum : uint32_t { kWsRecount = 1, kWsExit = 2, kWsDelta = 3, kWsWalkLight = 4, kWsWalkHeavy = 5, kWsCopy = 6,
                   kWsCollect = 7, kWsPending = 8, kWsZero = 9 };
 
@@ -284,10 +286,11 @@ __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t
 // Arcs [k, k1) (step) of the flattened changed-row arcs: both ends' counts move by [Cn equal] -
 // [Cp equal] (an arc whose other end changed too only from the smaller end; self-arcs never move).
 // pre: the prefix (LDS or global), nch changed rows.
+// chs: the changed-row entries in LDS (a helper that copied them), else nullptr.
 template <bool COH>   // COH: the list and the colours read with coherent loads (a helper, no acquire)
 __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ Cp,
                                               const uint16_t* __restrict__ Cn, const uint32_t* pre, uint32_t nch,
-                                              uint32_t k, uint32_t k1, uint32_t step) {
+                                              uint32_t k, uint32_t k1, uint32_t step, const uint4* chs = nullptr) {
     const uint32_t nloc = a.v_end - a.v_begin;
     for (; k < k1; k += step) {
         uint32_t lo = 0, hi = nch;   // the changed row i with pre[i] <= k < pre[i + 1]
@@ -296,7 +299,9 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
             if (pre[mid] <= k) lo = mid; else hi = mid;
         }
         uint4 ch;
-        if (COH) {
+        if (chs != nullptr) {
+            ch = chs[lo];
+        } else if (COH) {
             ch.x = dc_ld(&w.chg[4u * lo]);
             ch.y = dc_ld(&w.chg[4u * lo + 1u]);
             ch.z = dc_ld(&w.chg[4u * lo + 2u]);
@@ -431,10 +436,16 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         // list, the prefix, the colours of C_t+1 -- is read with coherent loads
         const uint32_t nch = dc_ld(&w.ctl[kWsChgN]);
         const uint32_t* pre = w.pre;
-        if (nch + 1u <= kWsPreLds) {
+        const uint4* chs = nullptr;
+        if (nch + 1u <= kWsPreLds) {   // the entries too where they fit: one round trip for both, so an
+            // arc's chain is prefix search (LDS) -> its id -> the colours -> the count atomics
+            const bool cl = nch <= kWsChgLds;
             for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) dyn[i] = dc_ld(&w.pre[i]);
+            if (cl)
+                for (uint32_t i = threadIdx.x; i < 4u * nch; i += blockDim.x) dyn[kWsPreLds + i] = dc_ld(&w.chg[i]);
             __syncthreads();
             pre = dyn;
+            if (cl) chs = reinterpret_cast<const uint4*>(dyn + kWsPreLds);
         }
         // arcs dealt round-robin over the workgroups (h, h + H, ...): a few thousand random reads
         // spread over every CU rather than filling the first few
@@ -443,7 +454,7 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         // the two dependent-load chains run side by side instead of one after the other
         const uint32_t na = blockDim.x - 64u;
         if (wv != (blockDim.x >> 6) - 1u) {
-            ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * na);
+            ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * na, chs);
             return;
         }
         // the next sweep's candidates (its colours: C_t+1, in Cs): those that change colour unless

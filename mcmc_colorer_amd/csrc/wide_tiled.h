@@ -137,7 +137,7 @@ __device__ __forceinline__ uint32_t wt_row(const SweepArgs& a, uint32_t l, uint3
         if (event) {
             const uint32_t idx = atomicAdd(&st->ev_count, 1u);
             if (idx < a.ev_cap) a.events[idx] = v;
-            else atomicOr(&st->err, 1u);
+            else atomicOr(&st->err, kDevErrEvents);
         }
     }
     wave_lds_sync();   // the walk's LDS reads are done before the next row clears the mask
@@ -205,8 +205,16 @@ __global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
     uint16_t* __restrict__ Cs = reinterpret_cast<uint16_t*>((t & 1) ? a.colors0 : a.colors1);
     const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
     uint32_t wave_viol = 0;
+    // u_v's engine state x_t 16807^(v+1): the wave's first row's power on the scalar unit times
+    // 16807^lane (a per-lane exponent would be a chain of ~22 dependent table loads and mulmods)
+    const uint32_t lpow = kMinstdLanePow[lane];
+    const uint32_t wstep = minstd_pow_tab_wave((uint64_t)gridDim.x * blockDim.x);
+    uint32_t xw = minstd_mulmod(x_t, minstd_pow_tab_wave((uint64_t)a.v_begin + blockIdx.x * blockDim.x +
+                                                         (threadIdx.x & ~63u) + 1ull));
     for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += gridDim.x * blockDim.x) {
         const uint32_t l = base + threadIdx.x;
+        const uint32_t xl = minstd_mulmod(xw, lpow);
+        xw = __builtin_amdgcn_readfirstlane(minstd_mulmod(xw, wstep));
         const bool in = l < nloc;
         const uint32_t v = a.v_begin + l;
         const uint32_t cv = in ? (uint32_t)C[v] : 0u;
@@ -227,8 +235,7 @@ __global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
             Cs[v] = (uint16_t)cv;
             a.taboo[l] = tab - 1u;
         } else if (in && !viol) {   // case (iii)
-            const uint32_t x = minstd_mulmod(x_t, minstd_pow_tab((uint64_t)v + 1ull));
-            const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(x));
+            const uint32_t nc = walk_own_tab(a.etab, a.nCol, cv, a.eps, a.hi, minstd_canonical(xl));
             event = nc == a.nCol;
             Cs[v] = (uint16_t)(event ? cv : nc);
             if (a.taboo != nullptr && !event) a.taboo[l] = (nc == cv) ? a.tabooIteration : 0u;
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
             if (event) {
                 const uint32_t idx = e0 + (uint32_t)__popcll(eb & ((1ull << lane) - 1ull));
                 if (idx < a.ev_cap) a.events[idx] = v;
-                else atomicOr(&st->err, 1u);
+                else atomicOr(&st->err, kDevErrEvents);
             }
         }
     }
@@ -270,8 +277,9 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
 }
 
 // After the commit of an accepted sweep (st->t = t + 1): the rows whose colour changed from C_t to
-// C_t+1, listed (after the violators, which wt_viol_kernel has consumed: their count is reset here),
-// their arcs summed.
+// C_t+1, listed (after the violators, which wt_viol_kernel has consumed: their count is reset here)
+// and marked in wt_chg, their arcs summed. A lane per 8-row group (global v / 8): two 16-byte loads,
+// one byte of wt_chg; the list reserved once per wave (a prefix sum of the lanes' changes).
 __global__ __launch_bounds__(256) void wt_diff_kernel(SweepArgs a) {
     DevState* st = a.st;
     if (st->done) return;
@@ -281,18 +289,38 @@ __global__ __launch_bounds__(256) void wt_diff_kernel(SweepArgs a) {
     const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u;
     uint32_t* const list = a.wt_list + nloc;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.wt_ctl[kWtVN] = 0u;
+    const uint32_t g0 = a.v_begin >> 3, ng = ((a.v_end + 7u) >> 3) - g0;
     unsigned long long arcs = 0;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < nloc; base += gridDim.x * blockDim.x) {
-        const uint32_t l = base + threadIdx.x;
-        const uint32_t v = a.v_begin + l;
-        const bool ch = l < nloc && Cn[v] != Co[v];
-        const uint64_t cb = __ballot(ch);
-        if (!cb) continue;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < ng; base += gridDim.x * blockDim.x) {
+        const uint32_t q = base + threadIdx.x, v0 = (g0 + q) << 3;
+        uint32_t m = 0;
+        if (q < ng && v0 >= a.v_begin && v0 + 8u <= a.v_end) {
+            const uint4 xn = *reinterpret_cast<const uint4*>(Cn + v0), xo = *reinterpret_cast<const uint4*>(Co + v0);
+            const uint32_t d[4] = {xn.x ^ xo.x, xn.y ^ xo.y, xn.z ^ xo.z, xn.w ^ xo.w};
+#pragma unroll
+            for (int i = 0; i < 4; i++) m |= ((d[i] & 0xFFFFu) ? 1u : 0u) << (2 * i) | ((d[i] >> 16) ? 2u : 0u) << (2 * i);
+        } else if (q < ng) {   // the range's first and last group
+            for (uint32_t i = 0; i < 8u; i++) {
+                const uint32_t v = v0 + i;
+                if (v >= a.v_begin && v < a.v_end && Cn[v] != Co[v]) m |= 1u << i;
+            }
+        }
+        if (q < ng) a.wt_chg[q] = (uint8_t)m;
+        const uint32_t k = (uint32_t)__builtin_popcount(m);
+        uint32_t incl = k;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        const uint32_t tot = __shfl(incl, 63, 64);
+        if (tot == 0u) continue;
         uint32_t b0 = 0;
-        if (lane == 0) b0 = atomicAdd(&a.wt_ctl[kWtCN], (uint32_t)__popcll(cb));
-        b0 = __shfl(b0, 0, 64);
-        if (ch) {
-            list[b0 + (uint32_t)__popcll(cb & ((1ull << lane) - 1ull))] = l;
+        if (lane == 63u) b0 = atomicAdd(&a.wt_ctl[kWtCN], tot);
+        b0 = __shfl(b0, 63, 64) + incl - k;
+        for (uint32_t mm = m; mm; mm &= mm - 1u) {
+            const uint32_t l = v0 + (uint32_t)__builtin_ctz(mm) - a.v_begin;
+            list[b0++] = l;
             arcs += a.wt_deg[l];
         }
     }
@@ -321,6 +349,8 @@ __global__ __launch_bounds__(512) void wt_delta_kernel(SweepArgs a, uint64_t arc
     const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2;
     const uint32_t grp = lane >> 4, gl = lane & 15u;
     const uint32_t* __restrict__ list = a.wt_list + nloc;
+    const uint8_t* __restrict__ chg = a.wt_chg;
+    const uint32_t g0 = a.v_begin >> 3;
     for (uint32_t i = blockIdx.x * nwv + wave; i < nch; i += gridDim.x * nwv) {
         const uint32_t l = list[i], u = a.v_begin + l;
         const uint32_t cu = Co[u], cu1 = Cn[u];
@@ -347,7 +377,10 @@ __global__ __launch_bounds__(512) void wt_delta_kernel(SweepArgs a, uint64_t arc
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     if (w[q] == 0xFFFFFFFFu) continue;
-                    const uint32_t cw = Co[w[q]], cw1 = Cn[w[q]];
+                    // C_t+1 w, and C_t w only where w changed (wt_chg: 1.25 MB at C3, L2-resident)
+                    const uint32_t cw1 = Cn[w[q]], lw0 = w[q] - a.v_begin;
+                    const bool wch = lw0 < nloc ? ((chg[(w[q] >> 3) - g0] >> (w[q] & 7u)) & 1u) != 0u : true;
+                    const uint32_t cw = wch ? (uint32_t)Co[w[q]] : cw1;
                     const int d = (cu1 == cw1 ? 1 : 0) - (cu == cw ? 1 : 0);
                     if (d == 0 || (cw != cw1 && w[q] < u)) continue;   // (both changed: the smaller end)
                     own += d;

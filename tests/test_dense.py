@@ -183,10 +183,14 @@ def dense_stats_v2(col):
     (2500, 0.8, 200, 53, 1e-8, 20, None, 1),    # NW = 8
     (3000, 0.3, 16, 54, 1e-8, 30, 40, 0),       # |S| = 40: most rows open, full sweeps inside the launch
 ])
-def test_dense_persistent_matches_oracle(M, monkeypatch, n, p, ncol, seed, eps, maxrip, srows, solo_min):
+@pytest.mark.parametrize("bs", ["", "1024"])
+def test_dense_persistent_matches_oracle(M, monkeypatch, n, p, ncol, seed, eps, maxrip, srows, solo_min, bs):
     """The persistent dense sweep (csrc/dense_sparse.h): the leader's solo sweeps evaluate only the
     candidate rows of the discrete-log window and the open rows; full sweeps (the count rebuild, open
-    rows past the solo limit) run on the whole grid inside the same launch. Bit-exact vs the oracle."""
+    rows past the solo limit) run on the whole grid inside the same launch. Bit-exact vs the oracle,
+    at the default 512-thread workgroups and at MCMC_DCM_BS=1024."""
+    if bs:
+        monkeypatch.setenv("MCMC_DCM_BS", bs)
     if srows is not None:
         monkeypatch.setenv("MCMC_DENSE_ROWS", str(srows))
     off, idx, nc, r = oracle_case(n, p, ncol, seed, epsilon=eps, maxRip=maxrip)
@@ -313,3 +317,15 @@ def test_dense_rebuild_counts_exact(M, monkeypatch, rb, n, deg, ncol, bl, srows)
     for c in range(ncol):
         expm[:, c // 32] |= ((exp[:, c] != 0).astype(np.uint32) << np.uint32(c % 32))
     assert np.array_equal(msk, expm)
+
+
+@pytest.mark.parametrize("poll", ["8", "64"])
+def test_dense_poll_interval(M, monkeypatch, poll):
+    """MCMC_DC_POLL: the persistent dense sweep's helpers sleep that many s_sleep(4) rounds between
+    polls of the leader's flag (default 1). A scheduling knob only: the same results as the oracle."""
+    monkeypatch.setenv("MCMC_DC_POLL", poll)
+    off, idx, nc, r = oracle_case(3000, 0.3, 16, 31, epsilon=1e-8, maxRip=60)
+    col, st, _ = gpu_run(M, off, idx, nc, 31, 3000 * 3001 // 2, maxRip=60)
+    assert_same(col, st, r)
+    ds = dense_stats_v2(col)
+    assert ds["persistent"] and ds["solo_sweeps"] >= 50, ds

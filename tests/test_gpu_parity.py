@@ -57,9 +57,20 @@ def oracle_case(n, p, ncol, seed, **kw):
     return off, idx, nc, r
 
 
+def _first_diff(got, want):
+    """A short message for two unequal sequences (pytest's list diff takes minutes on 1e3+ entries)."""
+    got, want = np.asarray(got), np.asarray(want)
+    if got.shape != want.shape:
+        return f"lengths {got.shape} vs {want.shape}"
+    bad = np.flatnonzero(got != want)
+    return f"{bad.size} of {got.size} differ, first at {bad[0]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
 def assert_same(col, st, r):
-    assert col.coloring().tolist() == r.colors.tolist()
-    assert col.trajectory().tolist() == r.traj.tolist()
+    got = col.coloring()
+    assert np.array_equal(got, r.colors), "colours: " + _first_diff(got, r.colors)
+    traj = col.trajectory()
+    assert np.array_equal(traj, r.traj), "trajectory: " + _first_diff(traj, r.traj)
     assert (st.iter, bool(st.maxIterReached), st.finalViol, st.glibcDraws, st.initDraws) == (
         r.res.iter, bool(r.res.maxIterReached), r.res.finalViol, r.res.glibcDraws, r.res.initDraws)
 
