@@ -49,6 +49,7 @@ constexpr uint32_t kWsWords = 96;
 // DevState::err and ends the launch instead of spinning forever; an idle helper leaves after kWsIdle.
 constexpr unsigned long long kWsWaitTicks = 200000000ull;    // 2 s
 constexpr unsigned long long kWsIdleTicks = 3000000000ull;   // 30 s
+constexpr unsigned long long kWsPollFastTicks = 200ull;       // 2 us (wall_clock64 runs at 100 MHz)
 constexpr uint32_t kWsBShift = 16;   // window buckets: L >> 16
 constexpr uint32_t kWsNB = ((kMinstdN - 1u) >> kWsBShift) + 1u;
 constexpr uint32_t kWsCandCap = 2048;      // changing candidate rows the leader holds (more: no prefetch)
@@ -84,7 +85,9 @@ struct WsArgs {
     uint32_t lead_heavy;   // heavier violators' arcs (in all) the leader walks itself, a workgroup each
     uint32_t sets;         // wave mask sets per workgroup
     uint32_t* dbg;         // diagnostics (MCMC_WS_DEBUG): host-visible progress words, or nullptr
-    uint32_t poll;         // an idle helper's poll interval (s_sleep 2 units; MCMC_WS_POLL)
+    uint32_t poll;         // a helper's poll interval (s_sleep 2 units; MCMC_WS_POLL) for kWsPollFastTicks
+    uint32_t poll_idle;    // after a phase, then this one (MCMC_WS_POLL_IDLE): fewer coherent loads while
+                           // the leader runs its steps, ~0.4 us more wake-up latency on average
     uint32_t* gcand;       // [3 nloc] the next sweep's candidates that change colour in case (iii)
                            // (l, x, cv | nc << 16), found by the helpers during a delta phase
 };
@@ -555,8 +558,10 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                 for (;;) {
                     g = __builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsGen]));
                     if (g != last) break;
-                    if (wall_clock64() - t0 > kWsIdleTicks) { g = kWsExit; break; }
-                    for (uint32_t z = 0; z < w.poll; z++) __builtin_amdgcn_s_sleep(2);   // (0: spin)
+                    const unsigned long long idle = wall_clock64() - t0;
+                    if (idle > kWsIdleTicks) { g = kWsExit; break; }
+                    const uint32_t zs = idle > kWsPollFastTicks ? w.poll_idle : w.poll;
+                    for (uint32_t z = 0; z < zs; z++) __builtin_amdgcn_s_sleep(2);   // (0: spin)
                 }
                 if ((g & 15u) != kWsDelta && (g & 15u) != kWsWalkLight && (g & 15u) != kWsWalkHeavy) {
                     // (the per-sweep phases read what the leader wrote coherently instead)

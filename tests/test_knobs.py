@@ -5,7 +5,8 @@ Knobs covered here (the others have their own tests: MCMC_GATHER / MCMC_BLOCK_LO
 MCMC_GROUP_ROWS / MCMC_TILE_STREAM in test_gpu_parity.py::test_all_gather_variants, MCMC_DRAIN_ROWS
 and MCMC_FULL_SCAN there too, MCMC_EXCHANGE in test_multi.py, MCMC_WIDE_INC / MCMC_WIDE_SCAN /
 MCMC_SPLIT_ARCS in test_wide.py, the persistent wide sweep's MCMC_WIDE_SOLO / MCMC_WS_ENTER /
-MCMC_WS_LEAD_ARCS / MCMC_WS_LEAD_HEAVY / MCMC_WS_LIGHT / MCMC_WS_MAX / MCMC_WS_POLL / MCMC_WS_DEBUG in
+MCMC_WS_LEAD_ARCS / MCMC_WS_LEAD_HEAVY / MCMC_WS_LIGHT / MCMC_WS_MAX / MCMC_WS_POLL / MCMC_WS_POLL_IDLE /
+MCMC_WS_DEBUG in
 test_wide.py::test_wide_persistent* and test_multi.py::test_native_loopback_wide_world1,
 MCMC_DENSE / MCMC_DENSE_ROWS / MCMC_DENSE_MULTI / MCMC_DENSE_CHG_CAP / MCMC_DCM_BS in test_dense.py, MCMC_DC_POLL
 (the dense helpers' poll interval) in test_dense.py::test_dense_poll_interval, MCMC_WT_INC in

@@ -508,6 +508,8 @@ WS_CASES = {
     "sparse-65535": ("sparse", 65535, {"maxRip": 40}, {}, "sweeps"),
     "all-change-16": ("dense16", 16, {"maxRip": 30}, {"MCMC_GATHER": "wide"}, "walk_phases"),
     "rmat-poll-debug": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_POLL": "8", "MCMC_WS_DEBUG": "1"}, "walk_phases"),
+    "rmat-poll-spin": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_POLL": "0", "MCMC_WS_POLL_IDLE": "0"}, "walk_phases"),
+    "rmat-poll-idle": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_POLL_IDLE": "256"}, "walk_phases"),
     "rmat-light-4096": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_LIGHT": "4096"}, "walk_phases"),
     "hub-lead-heavy": ("hub", 300, {"maxRip": 30}, {"MCMC_WS_LEAD_HEAVY": "65536"}, "sweeps"),
     "rmat-lead-heavy": ("rmat", 300, {"maxRip": 25}, {"MCMC_WS_LEAD_HEAVY": "65536"}, "sweeps"),
