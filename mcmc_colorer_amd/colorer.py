@@ -331,7 +331,7 @@ class ColoringMCMC:
                 "rebuilds": int(out[4]), "moved_vertices": int(out[5]), "open_rows": int(out[6]),
                 "rebuild_threshold": int(out[7]), "changed_rows": int(out[8]), "copy_sweeps": int(out[9]),
                 "solo_sweeps": int(out[10]), "window_states": int(out[11]), "persistent": bool(out[12]),
-                "open_words": int(out[13]), "solo_evaluated": int(out[14])}
+                "open_words": int(out[13]), "solo_evaluated": int(out[14]), "transposed_ids": bool(out[15])}
 
     def save(self, iteration: int) -> None:
         d = self.directory

@@ -417,7 +417,86 @@ __device__ __forceinline__ void dc_lane_write(const SweepArgs& a, const uint32_t
     }
 }
 
-template <int NW, uint32_t Q>
+// The tile-transposed copy of S's ids (the host's dc_build_tid, once per context): tile t = local
+// rows [64 t, 64 t + 64); for each S block in order, Qt = the tile's longest segment in quads, then
+// quad k of lane j at [k][j] (16 bytes each; quads past a row's segment are zero and never counted).
+// A wave's k-th quad load of the rebuild is then 1 KiB contiguous: the per-lane form loads 64 16-byte
+// pieces of 64 different lines per instruction, and most of each line it pulls from L2 into the CU's
+// cache is gone before the lane's next quad (measured at C3: coalesced loads of the same quads count
+// in 4.1 ms, the per-lane form 6.45 ms).
+__device__ __forceinline__ uint32_t dc_wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return __builtin_amdgcn_readfirstlane(x);
+}
+// Row l's segment of block b: [s0, e) in its group's ids (e: the padded end), raw = its tseg entry.
+__device__ __forceinline__ void dc_tid_seg(const SweepArgs& a, uint32_t l, uint32_t b, uint32_t& raw, uint32_t& nxt,
+                                           const uint16_t*& gc) {
+    const uint32_t R = a.grp_rows, g = l / R, r = l - g * R;
+    const uint32_t* ts = a.tseg + ((size_t)g * a.nblocks + b) * tseg_stride(R);
+    raw = ts[r];
+    nxt = ts[r + 1];
+    gc = a.tcol + a.gbase[g];
+}
+// Quads per tile (x 64), a wave per tile.
+__global__ __launch_bounds__(256) void dc_tid_size_kernel(SweepArgs a, uint64_t* __restrict__ tsize, uint32_t ntiles) {
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+    if (t >= ntiles) return;   // (wave-uniform)
+    const uint32_t nloc = a.v_end - a.v_begin, l = 64u * t + lane, bl = a.block_log2;
+    const uint32_t sb0 = a.dc_s0 >> bl, sb1 = (a.dc_s1 - 1u) >> bl;
+    uint64_t tot = 0;
+    for (uint32_t b = sb0; b <= sb1; b++) {
+        uint32_t raw = 0, nxt = 0;
+        const uint16_t* gc;
+        if (l < nloc) dc_tid_seg(a, l, b, raw, nxt, gc);
+        tot += dc_wave_max(((nxt & kTsegPos) - (raw & kTsegPos)) >> 3);
+    }
+    if (lane == 0) tsize[t] = 64ull * tot;
+}
+// The copy, a wave per tile: lane j's quads of each block (its own segment, 16-byte loads), stored
+// transposed; the tile's quads past a lane's segment are zero.
+__global__ __launch_bounds__(256) void dc_tid_fill_kernel(SweepArgs a, uint32_t ntiles) {
+    const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+    if (t >= ntiles) return;
+    const uint32_t nloc = a.v_end - a.v_begin, l = 64u * t + lane, bl = a.block_log2;
+    const uint32_t sb0 = a.dc_s0 >> bl, sb1 = (a.dc_s1 - 1u) >> bl;
+    uint4* __restrict__ out = const_cast<uint4*>(a.dc_tid) + a.dc_toff[t];
+    for (uint32_t b = sb0; b <= sb1; b++) {
+        uint32_t raw = 0, nxt = 0;
+        const uint16_t* gc = a.tcol;
+        if (l < nloc) dc_tid_seg(a, l, b, raw, nxt, gc);
+        const uint32_t s0 = raw & kTsegPos, qr = ((nxt & kTsegPos) - s0) >> 3, Qt = dc_wave_max(qr);
+        for (uint32_t k = 0; k < Qt; k++)
+            out[64u * k + lane] = k < qr ? *reinterpret_cast<const uint4*>(gc + s0 + 8u * k) : make_uint4(0u, 0u, 0u, 0u);
+        out += 64u * Qt;
+    }
+}
+// A row's quads of one block from the transposed copy: tq = the tile's quads of this block, Qt of
+// them (wave-uniform), qr the lane's own, nv its real ids; first = the lane's first id.
+template <bool CHK, uint32_t Q>
+__device__ __forceinline__ void dc_tid_segment(uint32_t (&A)[kDcPlanes], uint32_t np, const uint4* __restrict__ tq,
+                                               uint32_t Qt, uint32_t qr, int nv, const uint8_t* __restrict__ sl,
+                                               uint32_t lo, uint32_t span, uint32_t lane, uint32_t& first) {
+    {
+        uint4 v[Q];
+#pragma unroll
+        for (uint32_t q = 0; q < Q; q++) v[q] = q < Qt ? tq[64u * q + lane] : make_uint4(0u, 0u, 0u, 0u);
+        first = v[0].x & 0xFFFFu;
+#pragma unroll
+        for (uint32_t q = 0; q < Q; q++)
+            if (q < Qt) dc_lane_quad<CHK>(A, np, v[q], sl, q < qr, nv - 8 * (int)q, lo, span);
+    }
+    for (uint32_t j = Q; j < Qt; j += 4u) {
+        uint4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; q++) v[q] = j + q < Qt ? tq[64u * (j + q) + lane] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; q++)
+            if (j + q < Qt) dc_lane_quad<CHK>(A, np, v[q], sl, j + q < qr, nv - 8 * (int)(j + q), lo, span);
+    }
+}
+
+template <int NW, uint32_t Q, bool TID, uint32_t NB>
 __device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8_t* __restrict__ C, uint32_t task,
                                                  uint32_t* lds) {
     const uint32_t nloc = a.v_end - a.v_begin, R = a.grp_rows, bl = a.block_log2, np = a.dc_planes;
@@ -449,12 +528,16 @@ __device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8
     uint32_t A[kDcPlanes];
 #pragma unroll
     for (int k = 0; k < (int)kDcPlanes; k++) A[k] = 0u;
+    // TID: this wave's tile in the transposed copy (a wave past the rows reads none of it: Qt = 0)
+    const uint32_t tile = l >> 6, ntiles = (nloc + 63u) >> 6;
+    const uint4* __restrict__ tq = nullptr;
+    if constexpr (TID) tq = a.dc_tid + (tile < ntiles ? a.dc_toff[tile] : 0ull);
     dma(sb0, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (uint32_t b = sb0; b <= sb1; b++) {
-        const uint32_t buf = (b - sb0) & 1u;
-        if (b < sb1) dma(b + 1u, buf ^ 1u);
+        const uint32_t buf = NB == 2u ? (b - sb0) & 1u : 0u;
+        if (NB == 2u && b < sb1) dma(b + 1u, buf ^ 1u);
         const uint32_t blo = b << bl;
         const uint32_t lo = max(blo, a.dc_s0) - blo, hi = min(blo + bsz, a.dc_s1) - blo, span = hi - lo;
         const bool chk = lo != 0u || hi != bsz;   // S covers block b in part: every id tested
@@ -467,7 +550,20 @@ __device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8
             nxt = tsg[(size_t)(b + 1u) * tseg_stride(R) + 1u];
         }
         // (one round of kDcLaneQ quads for a C3 row's ~66 ids per block)
-        if (chk) {
+        if constexpr (TID) {
+            const uint32_t qr = (e - s0) >> 3, Qt = dc_wave_max(qr);   // (a lane past the rows: qr = 0)
+            uint32_t first = 0;
+            if (chk) {
+                dc_tid_segment<true, Q>(A, np, tq, Qt, qr, (int)(s1 - s0), sl, lo, span, lane, first);
+            } else {
+                dc_tid_segment<false, Q>(A, np, tq, Qt, qr, (int)(s1 - s0), sl, lo, span, lane, first);
+                if (__ballot(pad != 0u)) {   // the layout's padding (copies of the first id): out again
+                    const uint32_t ohf = pad ? 1u << sl[first] : 0u;
+                    dc_planes_sub(A, np, ohf, pad);
+                }
+            }
+            tq += 64u * Qt;
+        } else if (chk) {
             dc_lane_segment<true, Q>(A, np, gc, s0, s1, e, sl, lo, span);
         } else {
             dc_lane_segment<false, Q>(A, np, gc, s0, s1, e, sl, lo, span);
@@ -475,6 +571,12 @@ __device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8
                 const uint32_t ohf = pad ? 1u << sl[gc[s0]] : 0u;
                 dc_planes_sub(A, np, ohf, pad);
             }
+        }
+        // NB 1 (a single slice buffer): every wave is done with block b's slice before block b + 1's
+        // lands in it (the other workgroup on the CU counts meanwhile)
+        if (NB == 1u && b < sb1) {
+            __syncthreads();
+            dma(b + 1u, 0u);
         }
         // block b + 1's slice has landed and every wave is done with block b's (the next DMA's target)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -505,7 +607,7 @@ __device__ __forceinline__ void dc_rebuild_lanes(const SweepArgs& a, const uint8
 // rebuild's registers (its planes, Q quads per lane in flight) are not the dense sweep's: inside the sweep
 // (a rebuild after list overflows) the update keeps the chunk rebuild. dc_ctl_fresh_kernel then
 // marks the update done (mode 0, empty lists) and counts the rebuild.
-template <int NW, uint32_t BS, uint32_t Q>
+template <int NW, uint32_t BS, uint32_t Q, bool TID, uint32_t NB>
 __global__ __launch_bounds__(BS) void dc_rebuild_kernel(SweepArgs a, uint32_t n1) {
     extern __shared__ uint4 dc_lds[];
     const uint32_t t = a.st->t;
@@ -520,7 +622,7 @@ __global__ __launch_bounds__(BS) void dc_rebuild_kernel(SweepArgs a, uint32_t n1
         for (size_t i = (q1 > b0 ? q1 : b0) + threadIdx.x; i < b1; i += blockDim.x) Y[i] = C[i];
         return;
     }
-    dc_rebuild_lanes<NW, Q>(a, C, blockIdx.x - n1, reinterpret_cast<uint32_t*>(dc_lds));
+    dc_rebuild_lanes<NW, Q, TID, NB>(a, C, blockIdx.x - n1, reinterpret_cast<uint32_t*>(dc_lds));
 }
 __global__ void dc_ctl_fresh_kernel(uint32_t* __restrict__ k) {
     k[kDcMode] = 0u;

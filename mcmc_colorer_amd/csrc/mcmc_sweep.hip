@@ -237,6 +237,8 @@ struct SweepArgs {
     uint32_t dc_rbrows;         // rows per chunk of the streaming count rebuild (0: a wave per row)
     uint32_t dc_rbl;            // 1: the lane rebuild (dense_counts.h dc_rebuild_lanes; nCol <= 32)
     uint32_t dc_planes;         // its bit planes per count (counts < 2^dc_planes; 4..16)
+    const uint4* dc_tid;        // the lane rebuild's copy of S's ids, tile-transposed (dense_counts.h), or nullptr
+    const uint64_t* dc_toff;    // [ceil(nloc / 64)] tile t's first quad in dc_tid
     uint32_t dc_poll;           // persistent dense sweep: s_sleep(4) rounds between a helper's polls (MCMC_DC_POLL)
     uint32_t dc_commit_restore;  // restore lists up to this long are applied by the commit
     uint32_t dc_apow;           // 16807^(64 x the evaluation's waves): u_v advance per tile
@@ -3385,6 +3387,8 @@ struct mcmc_ctx {
     unsigned long long* dc_open = nullptr;
     uint32_t dc_s0 = 0, dc_s1 = 0, dc_cap = 0, dc_max = 0, dc_apow = 1, dc_chg_cap = 0, dc_rbrows = 0;
     uint32_t dc_rbl = 0, dc_planes = 0;
+    uint4* dc_tid = nullptr;        // the tile-transposed copy of S's ids (dc_build_tid) and its tile offsets
+    uint64_t* dc_toff = nullptr;
     bool dc_fresh = false;          // the colouring is new: dc_prep runs the lane rebuild before its first sweep
     unsigned long long* dc_osum = nullptr;   // open summary (count + one bit per open word)
     // the persistent dense sweep (dense_sparse.h): its launch (nullptr: one dc_eval_kernel per sweep)
@@ -3640,6 +3644,8 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
         a.dc_poll = 1;
         if (const char* dp = getenv("MCMC_DC_POLL")) a.dc_poll = (uint32_t)std::max(1, atoi(dp));
         a.dc_planes = c->dc_planes;
+        a.dc_tid = c->dc_tid;
+        a.dc_toff = c->dc_toff;
         a.dl_tab = c->dl_tab;
         a.dl_n = c->dl_n;
         a.solo_ts = c->solo_ts;
@@ -3727,7 +3733,13 @@ int dc_prep(mcmc_ctx* c) {
     // a lane per row, 8 quads per lane in flight (measured at C3, 3 colourings each: 1024 x 8 6.53 ms,
     // 1024 x 10 6.5, 512 x 12 7.8, 512 x 16 8.7; the chunk rebuild inside the sweep 9.7;
     // gpurun_out/r06e, r06g)
-    dc_rebuild_kernel<1, 1024, 8><<<n1 + (nloc + 1023u) / 1024u, 1024, kDcRebuildLds, c->stream>>>(a, n1);
+    // over the tile-transposed ids (dc_build_tid): 512-thread workgroups with one 64 KiB slice each,
+    // two per CU, so one counts while the other waits for its slice and quads (C3: 5.15 ms; 1024
+    // threads and two slices 5.45; the layout read lane by lane 6.4; gpurun_out/r06v, r06w)
+    if (c->dc_tid)
+        dc_rebuild_kernel<1, 512, 8, true, 1><<<n1 + (nloc + 511u) / 512u, 512, kDcSliceBuf, c->stream>>>(a, n1);
+    else
+        dc_rebuild_kernel<1, 1024, 8, false, 2><<<n1 + (nloc + 1023u) / 1024u, 1024, kDcRebuildLds, c->stream>>>(a, n1);
     dc_ctl_fresh_kernel<<<1, 1, 0, c->stream>>>(c->dc_ctl);
     MCMC_HIP_TRY(hipGetLastError());
     return MCMC_OK;
@@ -4023,6 +4035,46 @@ int setup_dense_window(mcmc_ctx* c) {
     return MCMC_OK;
 }
 
+// The lane rebuild's coalesced input (dense_counts.h dc_tid_*): S's ids copied once per context,
+// tile-transposed -- 64 consecutive rows, per S block Qt quads (the tile's longest segment) x 64
+// lanes, so a wave's quad load reads 1 KiB contiguous instead of 64 scattered 16-byte pieces.
+// Only where it fits with room to spare (MCMC_DC_TID=0: never; the rebuild then reads the layout).
+hipError_t dc_build_tid(mcmc_ctx* c) {
+    const char* env = getenv("MCMC_DC_TID");
+    if (env && atoi(env) == 0) return hipSuccess;
+    const uint32_t nloc = c->v_end - c->v_begin, ntiles = (nloc + 63u) / 64u;
+    SweepArgs a = make_args(c, 1);
+    uint64_t* tsz = nullptr;
+    hipError_t e = hipMalloc(&tsz, sizeof(uint64_t) * ntiles);
+    if (e != hipSuccess) { (void)hipGetLastError(); return hipSuccess; }
+    const uint32_t blocks = (ntiles + 3u) / 4u;   // a wave per tile, 4 per workgroup
+    dc_tid_size_kernel<<<blocks, 256, 0, c->stream>>>(a, tsz, ntiles);
+    std::vector<uint64_t> h(ntiles);
+    e = hipMemcpyAsync(h.data(), tsz, sizeof(uint64_t) * ntiles, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { (void)hipFree(tsz); return e; }
+    uint64_t tot = 0;
+    for (uint32_t t = 0; t < ntiles; t++) {
+        const uint64_t q = h[t];
+        h[t] = tot;
+        tot += q;
+    }
+    size_t fr = 0, total = 0;
+    const bool room = hipMemGetInfo(&fr, &total) == hipSuccess && tot * 16ull + (8ull << 30) < fr;
+    (void)hipGetLastError();
+    if (!room || tot == 0) { (void)hipFree(tsz); return hipSuccess; }
+    e = hipMalloc(&c->dc_tid, tot * 16ull);
+    if (e != hipSuccess) { (void)hipGetLastError(); c->dc_tid = nullptr; (void)hipFree(tsz); return hipSuccess; }
+    e = hipMemcpyAsync(tsz, h.data(), sizeof(uint64_t) * ntiles, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    c->dc_toff = tsz;
+    a = make_args(c, 1);
+    dc_tid_fill_kernel<<<blocks, 256, 0, c->stream>>>(a, ntiles);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e;
+}
+
 // The dense-count sweep of a tiled context (dense_counts.h), when the graph allows it and
 // MCMC_DENSE is not 0: S = the first |S| local rows, |S| such that a row's expected neighbours in
 // S number nCol (ln nCol + K), K below (MCMC_DENSE_ROWS overrides |S|); counts, masks and lists allocated.
@@ -4077,8 +4129,10 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
         while (planes < 16u && (c->g->maxDeg >> planes) != 0u) planes++;
         c->dc_planes = planes;
         c->dc_rbl = (nCol <= 32u && c->g->maxDeg < 65536u && c->dc_rbrows != 0u && !(rb && atoi(rb) == 1)) ? 1u : 0u;
-        if (c->dc_rbl && hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_rebuild_kernel<1, 1024, 8>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDcRebuildLds) != hipSuccess) {
+        if (c->dc_rbl && (hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_rebuild_kernel<1, 1024, 8, false, 2>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDcRebuildLds) != hipSuccess ||
+                          hipFuncSetAttribute(reinterpret_cast<const void*>(&dc_rebuild_kernel<1, 512, 8, true, 1>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDcSliceBuf) != hipSuccess)) {
             (void)hipGetLastError();
             c->dc_rbl = 0u;
         }
@@ -4103,6 +4157,10 @@ int setup_dense(mcmc_ctx* c, uint32_t nloc) {
     c->dc = true;
     e = dc_reset(c);
     if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("dense counts: ") + hipGetErrorString(e));
+    if (c->dc_rbl) {
+        e = dc_build_tid(c);
+        if (e != hipSuccess) return fail(MCMC_E_HIP, std::string("dense counts (transposed ids): ") + hipGetErrorString(e));
+    }
     return setup_dense_window(c);
 }
 
@@ -5249,6 +5307,7 @@ int mcmc_get_dense_stats_v2(mcmc_ctx* c, uint64_t out[16]) {
     out[12] = c->dcm_launch ? 1u : 0u;                                           // persistent launch
     out[13] = (uint32_t)os;                                                      // nonzero open words now
     out[14] = reinterpret_cast<const unsigned long long*>(h + kDcSoloEval)[0];   // rows solo sweeps evaluated
+    out[15] = c->dc_tid ? 1u : 0u;                                               // the rebuild's transposed ids
     return MCMC_OK;
 }
 
@@ -5632,6 +5691,8 @@ void mcmc_destroy(mcmc_ctx* c) {
     (void)hipFree(c->dc_cnt);
     (void)hipFree(c->dc_mask);
     (void)hipFree(c->dc_open);
+    (void)hipFree(c->dc_tid);
+    (void)hipFree(c->dc_toff);
     (void)hipFree(c->dc_osum);
     (void)hipFree(c->dl_tab);
     (void)hipFree(c->solo_ts);

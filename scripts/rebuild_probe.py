@@ -1,7 +1,7 @@
 """The dense sweep's count rebuild at C3 (configs[2]: n 1e7, p 0.001, 32 colours): first-sweep minus
-second-sweep device time of a fresh colouring, per rebuild form (MCMC_DENSE_RB unset = the lane
-rebuild kernel, 1 = the chunk rebuild inside the sweep), and the two forms' counts compared on
-sampled rows. Usage:
+second-sweep device time of a fresh colouring, per rebuild form (the lane rebuild kernel over the
+tile-transposed ids, the same over the layout with MCMC_DC_TID=0, MCMC_DENSE_RB=1 the chunk rebuild
+inside the sweep), and the forms' counts compared on sampled rows. Usage:
     python scripts/rebuild_probe.py [reps]"""
 import ctypes
 import json
@@ -26,13 +26,14 @@ rows = np.unique(np.concatenate([np.arange(0, 70000), np.arange(n - 5000, n),
                                  np.random.default_rng(1).integers(0, n, 50000)])).astype(np.uint32)
 out = {}
 counts = {}
-FORMS = {"lanes": None, "chunks": "1"}
-for form, rbv in FORMS.items():
-    if rbv is None:
-        os.environ.pop("MCMC_DENSE_RB", None)
-    else:
-        os.environ["MCMC_DENSE_RB"] = rbv
+FORMS = {"transposed": {}, "lanes": {"MCMC_DC_TID": "0"}, "chunks": {"MCMC_DENSE_RB": "1"}}
+for form, env in FORMS.items():
+    for k in ("MCMC_DENSE_RB", "MCMC_DC_TID"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    t1 = time.perf_counter()
     col = M.ColoringMCMC(g, M.GPURand(n, 1, M.GlibcRand(1)), M.ColoringMCMCParams(nCol=32))
+    print(form, f"context set-up {time.perf_counter() - t1:.2f} s", col.dense_stats()["transposed_ids"], flush=True)
     res = []
     for r in range(reps):
         col.init(r)

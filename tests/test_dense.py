@@ -274,7 +274,7 @@ def _expected_counts(off, idx, colors, ncol, s0, s1):
     return cnt
 
 
-@pytest.mark.parametrize("rb", ["", "1"])
+@pytest.mark.parametrize("rb", ["", "tid0", "1"])
 @pytest.mark.parametrize("n,deg,ncol,bl,srows", [
     (5000, 200, 32, 9, None),     # S = every row: 9 whole 512-vertex blocks + a partial one
     (5000, 200, 32, 8, 2900),     # S ends inside block 11
@@ -287,11 +287,15 @@ def _expected_counts(off, idx, colors, ncol, s0, s1):
 def test_dense_rebuild_counts_exact(M, monkeypatch, rb, n, deg, ncol, bl, srows):
     """The count rebuild's per-row counts and masks equal a host recount from the CSR and C_0 -- the
     lane rebuild (dense_counts.h dc_rebuild_lanes: bit-plane counts in registers, padding counted
-    and subtracted inside S, every id tested in a partial block) by default, the chunk rebuild with
-    MCMC_DENSE_RB=1 -- over whole and partial column blocks of S (MCMC_BLOCK_LOG2 shrinks blocks)."""
+    and subtracted inside S, every id tested in a partial block) by default, reading the
+    tile-transposed copy of S's ids; with MCMC_DC_TID=0 ("tid0") reading the layout lane by lane; the
+    chunk rebuild with MCMC_DENSE_RB=1 -- over whole and partial column blocks of S (MCMC_BLOCK_LOG2
+    shrinks blocks)."""
     from mcmc_colorer_amd._lib import check, lib, u32ptr
 
-    if rb:
+    if rb == "tid0":
+        monkeypatch.setenv("MCMC_DC_TID", "0")
+    elif rb:
         monkeypatch.setenv("MCMC_DENSE_RB", rb)
     monkeypatch.setenv("MCMC_GATHER", "tiled")
     monkeypatch.setenv("MCMC_BLOCK_LOG2", str(bl))
@@ -305,6 +309,7 @@ def test_dense_rebuild_counts_exact(M, monkeypatch, rb, n, deg, ncol, bl, srows)
     col.step(1)   # the first sweep's update rebuilds the counts from C_0
     ds = dense_stats_v2(col)
     assert ds["enabled"] and ds["rebuilds"] >= 1
+    assert ds["transposed_ids"] == (rb == "" and ncol <= 32), ds
     s0, s1 = ds["s0"], ds["s1"]
     cnt = np.zeros((n, ncol), dtype=np.uint32)
     nw = (ncol + 31) // 32
