@@ -4299,7 +4299,8 @@ static int setup_wide_solo(mcmc_ctx* c, uint32_t cus) {
     w.sets = std::min<uint32_t>(16u, kWsLds / (4u * walk_set_words(c->p.nCol)));
     w.poll = 1;
     if (const char* m = getenv("MCMC_WS_POLL")) w.poll = (uint32_t)strtoul(m, nullptr, 10);
-    w.poll_idle = 16;   // ~0.85 us between polls once a helper has been idle 2 us
+    w.poll_idle = 1;    // (as w.poll: a longer idle interval saves no memory traffic -- the polls are served
+                        // on-die, FETCH_SIZE is the same -- and adds wake-up latency to every phase)
     if (const char* m = getenv("MCMC_WS_POLL_IDLE")) w.poll_idle = (uint32_t)strtoul(m, nullptr, 10);
     if (getenv("MCMC_WS_DEBUG")) {
         MCMC_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->ws_dbg_host), 4096 * sizeof(uint32_t),

@@ -65,7 +65,9 @@ constexpr uint32_t kWsChgLds = 4096;       // and whose entries (16 B) sit there
 constexpr uint32_t kWsLds = 136u * 1024u;  // dynamic LDS
 static_assert(4u * (kWsPreLds + 4u * kWsChgLds) <= kWsLds, "delta phase prefix + entries in LDS");
 enum : uint32_t { kWsRecount = 1, kWsExit = 2, kWsDelta = 3, kWsWalkLight = 4, kWsWalkHeavy = 5, kWsCopy = 6,
-                  kWsCollect = 7, kWsPending = 8, kWsZero = 9 };
+                  kWsCollect = 7, kWsPending = 8, kWsZero = 9, kWsDeltaR = 10, kWsGo = 11 };
+constexpr uint32_t kWsArcsOut = 36;  // a kWsDeltaR phase's changed arcs (workgroup 1 writes them)
+constexpr uint32_t kWsLeadN = 16;    // results up to which the leader takes the rows' offsets itself
 
 struct WsArgs {
     uint32_t* ctl;
@@ -289,11 +291,15 @@ __device__ __forceinline__ void ws_walk_heavy(const SweepArgs& a, const uint16_t
 // Arcs [k, k1) (step) of the flattened changed-row arcs: both ends' counts move by [Cn equal] -
 // [Cp equal] (an arc whose other end changed too only from the smaller end; self-arcs never move).
 // pre: the prefix (LDS or global), nch changed rows.
-// chs: the changed-row entries in LDS (a helper that copied them), else nullptr.
+// chs: the changed-row entries in LDS (a helper that copied them), else nullptr; elate: their
+// colours are not in chs (a kWsDeltaR phase built it before the events drew): read from the list.
+// A listed row whose colour did not change (an overflow that drew its own) moves nothing: an arc to
+// a changed row is counted from that row's side.
 template <bool COH>   // COH: the list and the colours read with coherent loads (a helper, no acquire)
 __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& w, const uint16_t* __restrict__ Cp,
                                               const uint16_t* __restrict__ Cn, const uint32_t* pre, uint32_t nch,
-                                              uint32_t k, uint32_t k1, uint32_t step, const uint4* chs = nullptr) {
+                                              uint32_t k, uint32_t k1, uint32_t step, const uint4* chs = nullptr,
+                                              bool elate = false) {
     const uint32_t nloc = a.v_end - a.v_begin;
     for (; k < k1; k += step) {
         uint32_t lo = 0, hi = nch;   // the changed row i with pre[i] <= k < pre[i + 1]
@@ -304,6 +310,7 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
         uint4 ch;
         if (chs != nullptr) {
             ch = chs[lo];
+            if (elate) ch.y = dc_ld(&w.chg[4u * lo + 1u]);
         } else if (COH) {
             ch.x = dc_ld(&w.chg[4u * lo]);
             ch.y = dc_ld(&w.chg[4u * lo + 1u]);
@@ -314,6 +321,7 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
         }
         const uint32_t v = ch.x, cov = ch.y & 0xFFFFu, cnv = ch.y >> 16;
         const uint32_t u = a.col_idx[(((uint64_t)ch.w << 32) | ch.z) + (k - pre[lo])];
+        if (cov == cnv) continue;
         if (u == v) continue;
         const uint32_t ou = COH ? ld16c(&Cp[u]) : Cp[u], nu = COH ? ld16c(&Cn[u]) : Cn[u];
         if (ou != nu && u < v) continue;
@@ -328,8 +336,32 @@ __device__ __forceinline__ void ws_delta_arcs(const SweepArgs& a, const WsArgs& 
     }
 }
 
+// Exclusive scan of one value per thread over the workgroup; *tot = the sum. All threads call it.
+__device__ __forceinline__ uint32_t ws_scan(uint32_t v, uint32_t* wsum, uint32_t* tot) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63u) wsum[wv] = inc;
+    dc_lbar();
+    uint32_t off = 0, s = 0;
+    for (uint32_t k = 0; k < nwv; k++) {
+        if (k < wv) off += wsum[k];
+        s += wsum[k];
+    }
+    *tot = s;
+    dc_lbar();
+    return off + inc - v;
+}
+
 // ---- helper phases (workgroups 1..G-1; h = blockIdx.x - 1 of H) ---------------------------------
-__device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uint32_t kind, uint32_t* dyn) {
+// last: the phase word this workgroup has seen (a kWsDeltaR phase moves it on to its kWsGo post);
+// gone: a kWsDeltaR phase whose go this workgroup saw first (its poll slept through the phase's
+// own post), so it does the phase without waiting.
+__device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uint32_t kind, uint32_t* dyn, uint32_t& last,
+                                        bool gone) {
     const uint32_t H = gridDim.x - 1u, h = blockIdx.x - 1u, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t gt = h * blockDim.x + threadIdx.x, GT = H * blockDim.x;
     const uint32_t nloc = a.v_end - a.v_begin;
@@ -433,14 +465,73 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         const uint32_t hn = dc_ld(&w.ctl[kWsHeavyN]), x_t = dc_ld(&w.ctl[kWsArgP + 1]);
         for (uint32_t j = h; j < hn; j += H)
             ws_walk_heavy<true>(a, C, x_t, dc_ld(&w.heavy[j]), dyn, &w.ctl[kWsResN], w.res);
-    } else if (kind == kWsDelta) {
+    } else if (kind == kWsDelta || kind == kWsDeltaR) {
         // the changed rows' arcs (prefix cached in LDS where it fits). This phase runs without an
         // acquire (no L2 invalidation on every XCD per sweep): what the leader wrote for it -- the
         // list, the prefix, the colours of C_t+1 -- is read with coherent loads
         const uint32_t nch = dc_ld(&w.ctl[kWsChgN]);
         const uint32_t* pre = w.pre;
         const uint4* chs = nullptr;
-        if (nch + 1u <= kWsPreLds) {   // the entries too where they fit: one round trip for both, so an
+        if (kind == kWsDeltaR) {
+            // kWsDeltaR: posted before the leader's event draws with the results' rows only (nch <=
+            // kWsChgLds): every workgroup loads the rows' offsets and builds the entries and the
+            // arcs' prefix in its LDS meanwhile; on the leader's kWsGo post (the colours out, the
+            // events' draws in) the arcs run, each reading its row's colours from the list -- the
+            // offsets' round trip and the scans leave the leader's critical path
+            __shared__ uint32_t s_ds[16], s_go;
+            uint32_t* const pl = dyn;
+            uint4* const cs = reinterpret_cast<uint4*>(dyn + kWsPreLds);
+            const uint32_t per = (nch + blockDim.x - 1u) / blockDim.x;   // (<= 4)
+            const uint32_t i0 = min(nch, threadIdx.x * per), i1 = min(nch, i0 + per);
+            uint32_t l[4], d[4], dsum = 0;
+            uint64_t r0[4], r1[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) l[u] = i0 + (uint32_t)u < i1 ? dc_ld(&w.chg[4u * (i0 + u)]) : 0u;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool in = i0 + (uint32_t)u < i1;
+                r0[u] = in ? a.row_off[l[u]] : 0ull;
+                r1[u] = in ? a.row_off[l[u] + 1u] : 0ull;
+            }
+            // every listed row's arcs (an unchanged one's move nothing: ws_delta_arcs skips them), so
+            // the prefix needs no colours and is ready before the go
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + (uint32_t)u;
+                d[u] = (uint32_t)(r1[u] - r0[u]);
+                dsum += d[u];
+                if (i < i1) cs[i] = make_uint4(l[u], 0u, (uint32_t)r0[u], (uint32_t)(r0[u] >> 32));
+            }
+            uint32_t tot = 0;
+            uint32_t run = ws_scan(dsum, s_ds, &tot);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (i0 + (uint32_t)u < i1) pl[i0 + u] = run;
+                run += d[u];
+            }
+            if (threadIdx.x == 0) {
+                pl[nch] = tot;
+                if (h == 0u) w.ctl[kWsArcsOut] = tot;
+            }
+            if (threadIdx.x < 64u) {   // wave 0 waits for the go (wave-uniform; a watchdog as the leader's)
+                const unsigned long long t0 = wall_clock64();
+                uint32_t g2 = last;
+                while (!gone && (g2 = __builtin_amdgcn_readfirstlane(dc_ld(&w.ctl[kWsGen]))) == last) {
+                    if (wall_clock64() - t0 > kWsWaitTicks) {
+                        if (threadIdx.x == 0) a.st->err |= kDevErrWatchdog;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (threadIdx.x == 0) s_go = g2;
+            }
+            __syncthreads();
+            const uint32_t go = s_go;
+            if ((go & 15u) != kWsGo) return;   // the leader left (its exit post): no moves
+            last = go;
+            pre = pl;
+            chs = cs;
+        } else if (nch + 1u <= kWsPreLds) {   // the entries too where they fit: one round trip for both, so an
             // arc's chain is prefix search (LDS) -> its id -> the colours -> the count atomics
             const bool cl = nch <= kWsChgLds;
             for (uint32_t i = threadIdx.x; i <= nch; i += blockDim.x) dyn[i] = dc_ld(&w.pre[i]);
@@ -452,12 +543,12 @@ __device__ __forceinline__ void ws_help(const SweepArgs& a, const WsArgs& w, uin
         }
         // arcs dealt round-robin over the workgroups (h, h + H, ...): a few thousand random reads
         // spread over every CU rather than filling the first few
-        const uint32_t tot = nch + 1u <= kWsPreLds ? pre[nch] : dc_ld(&w.pre[nch]);
+        const uint32_t tot = (kind == kWsDeltaR || nch + 1u <= kWsPreLds) ? pre[nch] : dc_ld(&w.pre[nch]);
         // the last wave of every workgroup takes the next sweep's candidates, the others the arcs:
         // the two dependent-load chains run side by side instead of one after the other
         const uint32_t na = blockDim.x - 64u;
         if (wv != (blockDim.x >> 6) - 1u) {
-            ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * na, chs);
+            ws_delta_arcs<true>(a, w, C, Cs, pre, nch, h + H * threadIdx.x, tot, H * na, chs, kind == kWsDeltaR);
             return;
         }
         // the next sweep's candidates (its colours: C_t+1, in Cs): those that change colour unless
@@ -521,25 +612,6 @@ struct WsState {
                                     // count moves, violator list, whole sweeps
 };
 
-// Exclusive scan of one value per thread over the workgroup; *tot = the sum. All threads call it.
-__device__ __forceinline__ uint32_t ws_scan(uint32_t v, uint32_t* wsum, uint32_t* tot) {
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    uint32_t inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += y;
-    }
-    if (lane == 63u) wsum[wv] = inc;
-    dc_lbar();
-    uint32_t off = 0, s = 0;
-    for (uint32_t k = 0; k < nwv; k++) {
-        if (k < wv) off += wsum[k];
-        s += wsum[k];
-    }
-    *tot = s;
-    dc_lbar();
-    return off + inc - v;
-}
 
 __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_t K) {
     extern __shared__ uint4 ws_lds[];
@@ -563,7 +635,8 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     const uint32_t zs = idle > kWsPollFastTicks ? w.poll_idle : w.poll;
                     for (uint32_t z = 0; z < zs; z++) __builtin_amdgcn_s_sleep(2);   // (0: spin)
                 }
-                if ((g & 15u) != kWsDelta && (g & 15u) != kWsWalkLight && (g & 15u) != kWsWalkHeavy) {
+                if ((g & 15u) != kWsDelta && (g & 15u) != kWsDeltaR && (g & 15u) != kWsGo &&
+                    (g & 15u) != kWsWalkLight && (g & 15u) != kWsWalkHeavy) {
                     // (the per-sweep phases read what the leader wrote coherently instead)
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -576,7 +649,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             __syncthreads();
             if ((g & 15u) == kWsExit) break;
             if (threadIdx.x == 0) ws_dbg(w, 64u + blockIdx.x, (g << 4) | 1u);
-            ws_help(a, w, g & 15u, dyn);
+            ws_help(a, w, (g & 15u) == kWsGo ? kWsDeltaR : g & 15u, dyn, last, (g & 15u) == kWsGo);
             if (threadIdx.x == 0) ws_dbg(w, 64u + blockIdx.x, (g << 4) | 2u);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -610,6 +683,19 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(&w.ctl[kWsGen], (s_seq << 4) | kind, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    };
+    // the second post of a kWsDeltaR phase: its results' colours are out (no new phase: the
+    // helpers already count it)
+    auto post_go = [&]() {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0 && s.err == 0u) {
+            s_seq++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&w.ctl[kWsGen], (s_seq << 4) | kWsGo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
     };
@@ -1011,6 +1097,19 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             for (uint32_t i = threadIdx.x; i < 2u * Nl; i += blockDim.x) w.res[2u * Ng + i] = lres[i];
         }
         if (inl) dc_lbar(); else __syncthreads();
+        // more than a few results: the delta phase goes out now with their rows (kWsDeltaR), its
+        // workgroups load the rows' offsets while the events draw; the colours follow (post_go)
+        const bool dr = N > kWsLeadN && N <= kWsChgLds;
+        const uint32_t lxn = s.lx + a.nmodN >= kMinstdN ? s.lx + a.nmodN - kMinstdN : s.lx + a.nmodN;
+        if (dr) {
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) w.chg[4u * i] = R[2u * i];
+            if (threadIdx.x == 0) {
+                w.ctl[kWsChgN] = N;
+                w.ctl[kWsArgL] = lxn;   // (the next sweep's candidates, found in the same phase)
+                w.ctl[kWsCandN] = 0u;
+            }
+            post(kWsDeltaR);
+        }
         probe(3);   // [11] merge
         // overflow events in ascending vertex order take the next glibc draws (:517-520): up to
         // kWsRankMax ranked and drawn in parallel (draw r = sum_m T[m][r] ring[m], the commit's table),
@@ -1104,10 +1203,26 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         mark(k, 5);
         // the changed rows: C_t+1 into the other buffer; every result listed (by result index) with
         // its row start and its arcs' prefix (an unchanged one -- an overflow that drew its own
-        // colour -- with no arcs), per-thread runs of the results, workgroup scans
+        // colour -- with no arcs), per-thread runs of the results, workgroup scans. With the delta
+        // phase posted early (dr) only the colours, then the go: the helpers have the rows' offsets
         uint32_t nch = 0, arcs = 0;
         probe(0);
-        {
+        if (dr) {
+            uint32_t mc = 0;
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+                const uint32_t l = R[2u * i], e = R[2u * i + 1u];
+                if ((e >> 16) != (e & 0xFFFFu)) {
+                    Cs[l] = (uint16_t)(e >> 16);
+                    mc++;
+                }
+                w.chg[4u * i + 1u] = e;
+            }
+            (void)ws_scan(mc, s_wsum, &nch);
+            if (threadIdx.x == 0) s.st[7] += nch;
+            arcs = 0xFFFFFFFFu;   // (not known here: the delta phase)
+            post_go();
+            probe(1);
+        } else {
             const uint32_t per = (N + blockDim.x - 1u) / blockDim.x, i0 = min(N, threadIdx.x * per), i1 = min(N, i0 + per);
             uint32_t* const dg = tmp;   // degrees by result index (LDS results only)
             uint32_t mc = 0, ma = 0;
@@ -1158,9 +1273,9 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         }
         mark(k, 6);
         // the counts move: by the leader's threads when few arcs, else a delta phase
-        if (nch) {
+        if (nch || dr) {
             const uint32_t nl = N;   // listed results (changed or not)
-            if (arcs <= w.lead_arcs) {
+            if (!dr && arcs <= w.lead_arcs) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 const uint32_t* pre = w.pre;
@@ -1174,12 +1289,13 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
             } else {
                 // the helpers move the counts and find the next sweep's candidates (its log is lx + n,
                 // its colours are C_t+1, in Cs); only those candidates' counts must wait
-                const uint32_t lxn = s.lx + a.nmodN >= kMinstdN ? s.lx + a.nmodN - kMinstdN : s.lx + a.nmodN;
-                if (threadIdx.x == 0) {
-                    w.ctl[kWsArgL] = lxn;
-                    w.ctl[kWsCandN] = 0u;
+                if (!dr) {
+                    if (threadIdx.x == 0) {
+                        w.ctl[kWsArgL] = lxn;
+                        w.ctl[kWsCandN] = 0u;
+                    }
+                    post(kWsDelta);
                 }
-                post(kWsDelta);
                 if (!s_rawok) {   // the next sweep's draws while the helpers work (E > kWsRankMax: the
                     draws();      // event list overwrote them; the window is that of sweep t + 1)
                     __syncthreads();
@@ -1190,6 +1306,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
                     s.st[4]++;
                     s_pf = lxn;
                     s_gn = dc_ld(&w.ctl[kWsCandN]);
+                    if (dr) s.arcs += dc_ld(&w.ctl[kWsArcsOut]);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
