@@ -333,14 +333,65 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             if (sv.err) break;
         }
         if (threadIdx.x == 0) {
-            s_ow = a.dc_osum ? (uint32_t)dc_ld(a.dc_osum) : 0xFFFFFFFFu;
             sv.nres = sv.nev = sv.neval = sv.nviol = sv.nmv = 0;
             s_no = s_e = 0;
             if (a.solo_ts && k < 4096u) a.solo_ts[8u * k + 1u] = wall_clock64();
         }
         dc_lbar();
+        // candidates of the window, kDcCandCap entries per round; a candidate that is open is left
+        // to the open rows. The open summary word is read in the same round trip as the first
+        // round's colours and open words (it decides only what comes after the candidates: the
+        // open rows, or a full sweep -- nothing is written before that test)
+        const uint32_t lxs = kMinstdN - 1u - sv.lx;
+        uint32_t ow_r = 0xFFFFFFFFu;
+        bool ow_issued = false;
+        for (uint32_t c0 = 0; c0 < a.dl_n; c0 += kDcCandCap) {
+            if (threadIdx.x == 0) s_nc = 0;
+            dc_lbar();
+            const uint32_t c1 = min(a.dl_n, c0 + kDcCandCap);
+            for (uint32_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
+                const uint2 e = tab[j];
+                uint32_t d = e.x + lxs;   // L(w) - lx - 1 mod N: the vertex drawing state w (both terms < N)
+                if (d >= kMinstdN) d -= kMinstdN;
+                const uint32_t l = d - a.v_begin;
+                if (d >= a.v_begin && l < nloc) {
+                    const uint32_t kk = atomicAdd(&s_nc, 1u);
+                    cand[2u * kk] = l;
+                    cand[2u * kk + 1u] = e.y;
+                }
+            }
+            // the last sweep's colour writes are complete before any candidate's colour is read
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            dc_lbar();
+            if (!ow_issued) {
+                if (threadIdx.x == 0 && a.dc_osum) ow_r = (uint32_t)dc_ld(a.dc_osum);
+                ow_issued = true;
+            }
+            const uint32_t nc = s_nc;
+            for (uint32_t b = wv * 64u; b < nc; b += nwv * 64u) {
+                const uint32_t kk = b + lane;
+                bool valid = kk < nc;
+                const uint32_t l = valid ? cand[2u * kk] : 0u, x = valid ? cand[2u * kk + 1u] : 0u;
+                unsigned long long o = 0;
+                uint32_t cv = 0;
+                if (valid) {   // its colour and open words in one round trip
+                    cv = C[a.v_begin + l];
+#pragma unroll
+                    for (int i = 0; i < NW; i++) o |= dc_ld(&a.dc_open[(size_t)(l >> 6) * NW + i]);
+                }
+                valid = valid && ((o >> (l & 63u)) & 1ull) == 0ull;
+                dc_solo_rows<NW>(a, C, valid, l, cv, x, false, sv.x_t, tb.ew, sv, res, (int)lane);
+            }
+            dc_lbar();
+        }
+        if (threadIdx.x == 0) {
+            if (!ow_issued && a.dc_osum) ow_r = (uint32_t)dc_ld(a.dc_osum);
+            s_ow = a.dc_osum ? ow_r : 0xFFFFFFFFu;
+            if (a.solo_ts && k < 4096u) a.solo_ts[8u * k + 4u] = wall_clock64();
+        }
+        dc_lbar();
         const uint32_t ow = s_ow;
-        if (ow > kDcSoloOpenWords) { ret = 1u; break; }
+        if (ow > kDcSoloOpenWords) { ret = 1u; break; }   // (nothing written yet: the sweep runs full)
         // the open rows (the summary's set bits, one tile's NW bits together)
         if (ow != 0u) {
             const uint32_t ntiles = (nloc + 63u) >> 6, nsw = (ntiles * NW + 63u) >> 6;
@@ -364,44 +415,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             dc_lbar();
         }
         const uint32_t no = min(s_no, kDcSoloOpenRows);
-        // candidates of the window, kDcCandCap entries per round; a candidate that is open is left
-        // to the open rows
-        const uint32_t lxs = kMinstdN - 1u - sv.lx;
-        for (uint32_t c0 = 0; c0 < a.dl_n; c0 += kDcCandCap) {
-            if (threadIdx.x == 0) s_nc = 0;
-            dc_lbar();
-            const uint32_t c1 = min(a.dl_n, c0 + kDcCandCap);
-            for (uint32_t j = c0 + threadIdx.x; j < c1; j += blockDim.x) {
-                const uint2 e = tab[j];
-                uint32_t d = e.x + lxs;   // L(w) - lx - 1 mod N: the vertex drawing state w (both terms < N)
-                if (d >= kMinstdN) d -= kMinstdN;
-                const uint32_t l = d - a.v_begin;
-                if (d >= a.v_begin && l < nloc) {
-                    const uint32_t kk = atomicAdd(&s_nc, 1u);
-                    cand[2u * kk] = l;
-                    cand[2u * kk + 1u] = e.y;
-                }
-            }
-            // the last sweep's colour writes are complete before any candidate's colour is read
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            dc_lbar();
-            const uint32_t nc = s_nc;
-            for (uint32_t b = wv * 64u; b < nc; b += nwv * 64u) {
-                const uint32_t kk = b + lane;
-                bool valid = kk < nc;
-                const uint32_t l = valid ? cand[2u * kk] : 0u, x = valid ? cand[2u * kk + 1u] : 0u;
-                unsigned long long o = 0;
-                uint32_t cv = 0;
-                if (valid) {   // its colour and open words in one round trip
-                    cv = C[a.v_begin + l];
-#pragma unroll
-                    for (int i = 0; i < NW; i++) o |= dc_ld(&a.dc_open[(size_t)(l >> 6) * NW + i]);
-                }
-                valid = valid && ((o >> (l & 63u)) & 1ull) == 0ull;
-                dc_solo_rows<NW>(a, C, valid, l, cv, x, false, sv.x_t, tb.ew, sv, res, (int)lane);
-            }
-            dc_lbar();
-        }
+
         for (uint32_t b = wv * 64u; b < no; b += nwv * 64u) {
             const uint32_t kk = b + lane;
             const uint32_t l = kk < no ? orow[kk] : 0u;
@@ -434,6 +448,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             break;
         }
         // accept: overflow events in ascending vertex order take the next glibc draws (rank sort)
+        if (a.solo_ts && threadIdx.x == 0 && k < 4096u) a.solo_ts[8u * k + 5u] = wall_clock64();
         const uint32_t nev = sv.nev;
         if (nev) {
             for (uint32_t i = threadIdx.x; i < nres; i += blockDim.x)
@@ -446,6 +461,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
                 evs[nev + r] = evs[i];
             }
             dc_lbar();
+            __shared__ uint32_t s_head;
             if (threadIdx.x == 0) {
                 uint32_t head = 0;
                 for (uint32_t i = 0; i < nev; i++) {
@@ -453,24 +469,33 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
                     const uint32_t c = glibc_next(sv.ring, head) % (a.nCol - 1u);   // rand() % (nCol - 1), :518
                     res[kDcSoloRes + ri] = (res[kDcSoloRes + ri] & 0xFFFFu) | (c << 16);
                 }
-                uint32_t w[31];   // the window back to oldest-first order
-                for (uint32_t i = 0; i < 31u; i++) w[i] = sv.ring[(head + i) % 31u];
-                for (uint32_t i = 0; i < 31u; i++) {
-                    sv.ring[i] = w[i];
-                    st->glibc_ring[i] = w[i];
-                }
+                s_head = head;
                 st->glibc_head = 0u;
                 sv.draws += nev;
                 st->glibc_draws = sv.draws;
             }
             dc_lbar();
+            // the window back to oldest-first order, a lane per entry (wave 0)
+            uint32_t wr = 0;
+            if (threadIdx.x < 31u) {
+                const uint32_t j = s_head + threadIdx.x;
+                wr = sv.ring[j >= 31u ? j - 31u : j];
+            }
+            dc_lbar();
+            if (threadIdx.x < 31u) {
+                sv.ring[threadIdx.x] = wr;
+                st->glibc_ring[threadIdx.x] = wr;
+            }
+            dc_lbar();
         }
         // the changed rows into both buffers; moves of S listed for the next sweep (parity q)
+        if (a.solo_ts && threadIdx.x == 0 && k < 4096u) a.solo_ts[8u * k + 6u] = wall_clock64();
         for (uint32_t i = threadIdx.x; i < nres; i += blockDim.x) {
             const uint32_t l = res[i], cn = res[kDcSoloRes + i];
             const uint32_t cv = cn & 0xFFFFu, nc = cn >> 16;
             if (nc == cv) continue;   // an overflow that drew the same colour
             const uint32_t v = a.v_begin + l;
+
             Cs[v] = (uint8_t)nc;
             const_cast<uint8_t*>(C)[v] = (uint8_t)nc;
             if (v - a.dc_s0 < a.dc_s1 - a.dc_s0) {

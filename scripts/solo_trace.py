@@ -1,6 +1,7 @@
 """Summarise MCMC_SOLO_TRACE stamps (dense_sparse.h dc_leader_solo, wall_clock64 at 100 MHz):
-per solo sweep [0] start, [1] before the evaluation, [2] evaluation done, [3] accepted; sweeps
-with a move phase also [7] the helpers' moves done. Medians in us."""
+per solo sweep [0] start, [1] before the evaluation, [4] candidates evaluated and the open summary
+read, [2] evaluation done, [5] loop control done, [6] events drawn, [3] accepted; sweeps with a move
+phase also [7] the helpers' moves done. Medians in us."""
 import sys
 
 import numpy as np
@@ -16,6 +17,9 @@ per = np.diff(r[:, 0])
 print(f"solo sweeps traced: {len(r)}, with a move phase: {int(mv.sum())}")
 print(f"  setup {us(r[~mv,1]-r[~mv,0]):.2f} us, evaluation {us(r[:,2]-r[:,1]):.2f} us, accept {us(r[:,3]-r[:,2]):.2f} us, "
       f"period median {us(per):.2f} us, mean {np.mean(per)/100:.2f} us")
+if (r[:, 4] > 0).all() and (r[:, 5] > 0).all() and (r[:, 6] > 0).all():
+    print(f"  evaluation: candidates + open summary {us(r[:,4]-r[:,1]):.2f}, open rows {us(r[:,2]-r[:,4]):.2f}; "
+          f"accept: loop control {us(r[:,5]-r[:,2]):.2f}, events {us(r[:,6]-r[:,5]):.2f}, writes + state {us(r[:,3]-r[:,6]):.2f} us")
 if mv.any():
     m = r[mv]
     print(f"  move phase (post -> helpers done) {us(m[:,7]-m[:,0]):.2f} us, to evaluation {us(m[:,1]-m[:,0]):.2f} us")
