@@ -1,7 +1,7 @@
 #!/bin/bash
 # r06: kernel trace + FETCH_SIZE / WRITE_SIZE passes (separate runs) of one probe script, by default
 # the C3 count rebuild and full-scan sweep (scripts/prof_rebuild_fullscan.py); e.g.
-#   scripts/gpu_prof_r06.sh r06wt scripts/wt_probe.py 12
+#   scripts/gpu_prof3.sh r06wt scripts/wt_probe.py 12
 # Output: gpurun_out/$TAG/{trace,pmc1,pmc2}.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

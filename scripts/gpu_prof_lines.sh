@@ -7,6 +7,6 @@ T=${1:-r06pb}
 HB=$!
 trap "kill $HB" EXIT
 mkdir -p gpurun_out
-bash scripts/gpu_prof_r06.sh $T/c3 bench.py --no-cpu-baseline --no-refstruct --no-full-scan --no-convergence || exit $?
-bash scripts/gpu_prof_r06.sh $T/c5 bench.py --config c5 --no-cpu-baseline --no-refstruct --no-convergence || exit $?
-bash scripts/gpu_prof_r06.sh $T/rebuild scripts/rb_sq_probe.py || exit $?
+bash scripts/gpu_prof3.sh $T/c3 bench.py --no-cpu-baseline --no-refstruct --no-full-scan --no-convergence || exit $?
+bash scripts/gpu_prof3.sh $T/c5 bench.py --config c5 --no-cpu-baseline --no-refstruct --no-convergence || exit $?
+bash scripts/gpu_prof3.sh $T/rebuild scripts/rb_sq_probe.py || exit $?

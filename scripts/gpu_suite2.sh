@@ -1,7 +1,7 @@
 #!/bin/bash
 # r06: the -m gpu suite at HEAD, in two calls (each under gpurun's limit):
-#   scripts/gpu_suite_r06.sh TAG main   every -m gpu test but the full-size files, then smoke()
-#   scripts/gpu_suite_r06.sh TAG full   the full-size files (C3 / C4 / C5 at configs' sizes, RCCL worlds)
+#   scripts/gpu_suite2.sh TAG main   every -m gpu test but the full-size files, then smoke()
+#   scripts/gpu_suite2.sh TAG full   the full-size files (C3 / C4 / C5 at configs' sizes, RCCL worlds)
 # Output: gpurun_out/TAG/{main,full}.log (+ a heartbeat file while it runs).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$1; mkdir -p $OUT
