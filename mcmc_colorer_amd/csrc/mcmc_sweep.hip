@@ -5814,7 +5814,9 @@ int part_solo_batch(mcmc_ctx* c, uint32_t steps) {
     if (c->stream == nullptr) return 1;
     MCMC_HIP_TRY(hipSetDevice(c->g->device));
     if (int rc = dc_prep(c)) return rc;
-    if (c->wsa.ctl) {   // the persistent wide sweep near convergence (ws_choose; one sync per batch)
+    // the persistent wide sweep near convergence (ws_choose): one sync per batch until it is taken,
+    // then it stays (it handles violators too), so the driver's batches pipeline again
+    if (c->wsa.ctl && !(c->ran && c->ws_on)) {
         DevState h{};
         long long lv = -1;
         if (c->ran) {
