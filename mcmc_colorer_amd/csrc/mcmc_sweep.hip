@@ -5521,9 +5521,7 @@ int mcmc_bench_prepare(mcmc_ctx* c, uint32_t sweeps) {
 int mcmc_bench_sweeps(mcmc_ctx* c, uint32_t sweeps, double* total_ms, double* sweep_kernel_ms) {
     if (!c) return fail(MCMC_E_ARG, "NULL context");
     if (!c->initialized) return fail(MCMC_E_STATE, "mcmc_init_coloring must precede mcmc_bench_sweeps");
-    // (prepared for `sweeps`: as captured; with the persistent wide sweep set up the path is chosen
-    // again for the colouring the sweeps start from -- prepare keeps the graph when it matches)
-    if (!(c->bench_exec && c->bench_n == sweeps) || c->wsa.ctl) {
+    if (!(c->bench_exec && c->bench_n == sweeps)) {   // (prepared for `sweeps`: as captured)
         int rc = mcmc_bench_prepare(c, sweeps);
         if (rc) return rc;
     }
