@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(1024) void ws_kernel(SweepArgs a, WsArgs w, uint32_
         if (inl) dc_lbar(); else __syncthreads();
         // more than a few results: the delta phase goes out now with their rows (kWsDeltaR), its
         // workgroups load the rows' offsets while the events draw; the colours follow (post_go)
-        const bool dr = N > kWsLeadN && N <= kWsChgLds;
+        const bool dr = N > kWsLeadN && N <= kWsChgLds && N <= 4u * blockDim.x;   // (a helper thread takes <= 4)
         const uint32_t lxn = s.lx + a.nmodN >= kMinstdN ? s.lx + a.nmodN - kMinstdN : s.lx + a.nmodN;
         if (dr) {
             for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) w.chg[4u * i] = R[2u * i];
