@@ -290,6 +290,10 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
     __syncthreads();
     uint32_t ret = 2u;
     __shared__ uint32_t s_no, s_nc, s_e;
+    // the open-summary word as last read (thread 0): only move phases and full sweeps change it, so
+    // a sweep after neither reuses it instead of a round trip (C2: no candidates to hide it behind)
+    bool ow_valid = false;
+    uint32_t ow_cached = 0;
     for (; k < K; k++) {
         if (a.solo_ts && threadIdx.x == 0 && k < 4096u) a.solo_ts[8u * k] = wall_clock64();
         if (sv.done || sv.err) break;
@@ -314,6 +318,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
                 sv.st_listed += len;
                 sv.len = 0;
             }
+            ow_valid = false;   // (the moves may open or close rows)
             if (threadIdx.x < 64u) {   // wave 0 waits (a wave-uniform spin loop: see dc_multi_kernel)
                 const uint32_t ex = __builtin_amdgcn_readfirstlane(mvexp);
                 const unsigned long long t0 = wall_clock64();
@@ -364,7 +369,7 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             dc_lbar();
             if (!ow_issued) {
-                if (threadIdx.x == 0 && a.dc_osum) ow_r = (uint32_t)dc_ld(a.dc_osum);
+                if (threadIdx.x == 0 && a.dc_osum && !ow_valid) ow_r = (uint32_t)dc_ld(a.dc_osum);
                 ow_issued = true;
             }
             const uint32_t nc = s_nc;
@@ -385,7 +390,10 @@ __device__ __forceinline__ uint32_t dc_leader_solo(const SweepArgs& a, uint32_t 
             dc_lbar();
         }
         if (threadIdx.x == 0) {
-            if (!ow_issued && a.dc_osum) ow_r = (uint32_t)dc_ld(a.dc_osum);
+            if (ow_valid) ow_r = ow_cached;
+            else if (!ow_issued && a.dc_osum) ow_r = (uint32_t)dc_ld(a.dc_osum);
+            ow_cached = ow_r;
+            ow_valid = a.dc_osum != nullptr;
             s_ow = a.dc_osum ? ow_r : 0xFFFFFFFFu;
             if (a.solo_ts && k < 4096u) a.solo_ts[8u * k + 4u] = wall_clock64();
         }
