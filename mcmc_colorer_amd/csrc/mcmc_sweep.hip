@@ -4760,9 +4760,13 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             const size_t nloc = v_end - v_begin;
             ew = hipMalloc(&c->wt_buf, sizeof(uint32_t) * (kWtWords + 4 * (size_t)nloc + nloc / 32u + 2u));
             if (ew == hipSuccess) ew = hipMemset(c->wt_buf, 0, sizeof(uint32_t) * kWtWords);
-            // a changed arc costs two colour gathers, a scanned arc one: incremental while the changed
-            // rows' arcs are at most a quarter of the layout's
-            c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / 4u;
+            // a changed arc costs one colour gather (two where its other end changed too: rare), a
+            // scanned arc one, and the next sweep's violators are walked over their whole rows
+            // either way: incremental while the changed rows' arcs are at most half the layout's
+            // (MCMC_WT_ARCS_DIV: the divisor, measurement)
+            const char* wd = getenv("MCMC_WT_ARCS_DIV");
+            const uint64_t div = wd ? std::max<uint64_t>(1, strtoull(wd, nullptr, 10)) : 2u;
+            c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / div;
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);

@@ -50,8 +50,9 @@ inline uint32_t wide_tiled_wgs_per_cu(uint32_t nCol) {
 //                    [C_t+1 u == C_t+1 w] - [C_t u == C_t w] (an arc between two changed rows from the
 //                    smaller end only).
 // The full sweep (wide_tiled_kernel) counts vcnt in its scan. The delta kernel chooses the next
-// sweep's mode: incremental while the changed rows' arcs cost less than a full scan (2 gathers per
-// changed arc against 1 per arc), else full (the counts are then recounted by the scan). Exact: the
+// sweep's mode: incremental while the changed rows' arcs are at most half the layout's (one gather
+// per changed arc to an unchanged row against one per arc of a scan; the violators' walks cost the
+// same either way), else full (the counts are then recounted by the scan). Exact: the
 // counts are integers; tests/test_wide.py::test_wide_tiled_incremental* (against the oracle, the
 // full mode, forced modes) and tests/test_c3_full.py.
 constexpr uint32_t kWtMode = 0;   // the running sweep: 0 full (wide_tiled_kernel), 1 incremental

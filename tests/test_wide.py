@@ -349,14 +349,18 @@ def test_wide_tiled_generated_graph(M, monkeypatch, n, p, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inc", ["0", "1", "2"])
+@pytest.mark.parametrize("inc", ["0", "1", "2", "1/div8"])
 @pytest.mark.parametrize("case", ["sparse", "taboo", "eps1e3", "hub", "every_vertex", "tailcut", "generated"])
 def test_wide_tiled_incremental(M, monkeypatch, inc, case):
     """The wide tiled sweep's incremental violation counts (csrc/wide_tiled.h wt_*): MCMC_WT_INC=0
-    scans every sweep, 1 (default) chooses per sweep, 2 runs every sweep after the first from the
-    counts (lane-per-row evaluation, violators walked from a list, the counts moved by the changed
-    rows). Each run equals the oracle's; the statistics show which sweeps were incremental."""
+    scans every sweep, 1 (default) chooses per sweep (incremental while the changed rows' arcs are at
+    most 1 / MCMC_WT_ARCS_DIV of the layout's, default 2; "1/div8": 8), 2 runs every sweep after the
+    first from the counts (lane-per-row evaluation, violators walked from a list, the counts moved by
+    the changed rows). Each run equals the oracle's; the statistics show which sweeps were incremental."""
     monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
+    if inc == "1/div8":
+        inc = "1"
+        monkeypatch.setenv("MCMC_WT_ARCS_DIV", "8")
     monkeypatch.setenv("MCMC_WT_INC", inc)
     kw = {}
     if case == "generated":
