@@ -256,6 +256,7 @@ struct SweepArgs {
     uint32_t* wt_deg;           // [nloc] the row's arcs (counted by the full sweep)
     uint32_t* wt_list;          // [2][nloc] violators of the running sweep, then rows changed by it
     uint8_t* wt_chg;            // [nloc / 8 + 2] rows changed by the last sweep, a bit each (8-row groups of global v)
+    uint32_t wt_rc;             // a full sweep = wt_recount_kernel + the incremental kernels (wide_tiled.h)
     uint32_t nmodN;             // n mod (2^31 - 2): the advance of DevState::lx per sweep
 };
 // control words of the incremental wide sweep (SweepArgs::inc)
@@ -3400,6 +3401,7 @@ struct mcmc_ctx {
     unsigned long long* wt_tick = nullptr;   // wide tiled sweep's block rotation clock (wide_tiled.h)
     uint32_t* wt_buf = nullptr;     // its incremental counts: control words, vcnt, deg, lists (one allocation)
     uint64_t wt_arcs_max = 0;       // changed arcs up to which the next sweep stays incremental
+    uint32_t wt_rc = 0;             // full sweeps as a block-major recount + the incremental kernels
 };
 
 namespace {
@@ -3617,6 +3619,7 @@ SweepArgs make_args(const mcmc_ctx* c, int check_done) {
             a.wt_deg = a.wt_vcnt + nloc;
             a.wt_list = a.wt_deg + nloc;
             a.wt_chg = reinterpret_cast<uint8_t*>(a.wt_list + 2u * nloc);
+            a.wt_rc = c->wt_rc;
         }
         a.etab = c->etab;
         a.walk_tie = c->walk_tie;
@@ -3696,6 +3699,8 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     const uint32_t nloc = c->v_end - c->v_begin;
     const uint32_t lane_grid = std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 255u) / 256u, 2048u));
     if (a.wt_ctl) {   // the incremental sweep's kernels (each returns at once in a full sweep)
+        if (c->wt_rc)   // (a full sweep's counts; returns at once in an incremental one)
+            wt_recount_kernel<<<c->tl->ngroups, 1024, wt_recount_lds(c->tl->block_log2, c->tl->grp_rows), c->stream>>>(a);
         wt_eval_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
         wt_viol_kernel<<<c->grid, c->block, c->lds, c->stream>>>(a);
     }
@@ -4767,6 +4772,14 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             const char* wd = getenv("MCMC_WT_ARCS_DIV");
             const uint64_t div = wd ? std::max<uint64_t>(1, strtoull(wd, nullptr, 10)) : 2u;
             c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / div;
+            // full sweeps as recount + incremental kernels where a group and a block's colours fit
+            // the LDS (MCMC_WT_RC=0: the mask scan of wide_tiled_kernel)
+            const char* rce = getenv("MCMC_WT_RC");
+            const size_t rcl = wt_recount_lds(c->tl->block_log2, c->tl->grp_rows);
+            c->wt_rc = (!(rce && atoi(rce) == 0) && c->tl->grp_rows <= kWtRcRows && rcl <= 160u * 1024u &&
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&wt_recount_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rcl) == hipSuccess) ? 1u : 0u;
+            (void)hipGetLastError();
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);

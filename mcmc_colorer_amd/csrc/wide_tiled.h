@@ -150,7 +150,8 @@ __global__ __launch_bounds__(512) void wide_tiled_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol;
     DevState* st = a.st;
     if (a.check_done && st->done) return;
-    if (a.wt_ctl != nullptr && a.wt_ctl[kWtMode] != 0u) return;   // an incremental sweep: wt_eval_kernel
+    // an incremental sweep (wt_eval_kernel), or a full one run as recount + the incremental kernels
+    if (a.wt_ctl != nullptr && (a.wt_ctl[kWtMode] != 0u || a.wt_rc)) return;
     if (threadIdx.x == 0) sh_viol = 0;
     if (a.wt_ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
         a.wt_ctl[kWtCN] = 0u;   // (the last sweep's delta has run)
@@ -193,12 +194,13 @@ __global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
     __shared__ uint32_t sh_viol;
     DevState* st = a.st;
     if (a.check_done && st->done) return;
-    if (a.wt_ctl[kWtMode] == 0u) return;   // a full sweep: wide_tiled_kernel
+    const bool inc = a.wt_ctl[kWtMode] != 0u;
+    if (!inc && !a.wt_rc) return;   // a full sweep: wide_tiled_kernel (or wt_recount_kernel, then this)
     if (threadIdx.x == 0) sh_viol = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.wt_ctl[kWtCN] = 0u;
         reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtArcs)[0] = 0ull;
-        reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[1] += 1ull;
+        if (inc) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[1] += 1ull;
     }
     __syncthreads();
     const uint32_t t = st->t, x_t = st->x_t;
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
     extern __shared__ uint32_t wt_lds[];
     DevState* st = a.st;
     if (a.check_done && st->done) return;
-    if (a.wt_ctl[kWtMode] == 0u) return;
+    if (a.wt_ctl[kWtMode] == 0u && !a.wt_rc) return;
     const uint32_t nv = a.wt_ctl[kWtVN];
     const uint32_t t = st->t, x_t = st->x_t;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
@@ -275,6 +277,86 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[3] += nv;
     for (uint32_t i = blockIdx.x * nwv + wave; i < nv; i += gridDim.x * nwv)
         (void)wt_row<false>(a, a.wt_list[i], t, x_t, C, Cs, mask, pre, tick);
+}
+
+// A full sweep's counts from scratch (SweepArgs::wt_rc): a workgroup per row group streams the
+// group's ids block by block (coalesced quads), each block's colours staged in LDS, each quad's row
+// found by a binary search of the block's segment starts -- the layout read once, no colour gather
+// from the fabric (the mask scan of wide_tiled_kernel is one fabric line per arc). Then the
+// incremental sweep's own kernels run the sweep (violators walked from the list). vcnt = the row's
+// neighbours of its own colour, deg = its neighbours (both as wt_row<true> counts them).
+constexpr uint32_t kWtRcRows = 2048;   // group rows the recount holds in LDS
+inline size_t wt_recount_lds(uint32_t block_log2, uint32_t R) {
+    return 2ull * (1ull << block_log2) + 14ull * R + 16u;
+}
+__global__ __launch_bounds__(1024) void wt_recount_kernel(SweepArgs a) {
+    extern __shared__ uint4 wt_rc_lds[];
+    DevState* st = a.st;
+    if (a.check_done && st->done) return;
+    if (a.wt_ctl[kWtMode] != 0u) return;   // an incremental sweep: the counts are current
+    const uint32_t t = st->t;
+    const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
+    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2, bsz = 1u << bl;
+    const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint16_t* const sl = reinterpret_cast<uint16_t*>(wt_rc_lds);   // [bsz] block b's colours
+    uint32_t* const cnt = reinterpret_cast<uint32_t*>(sl + bsz);    // [R]
+    uint32_t* const dg = cnt + R;                                   // [R]
+    uint32_t* const tsl = dg + R;                                   // [R + 1] the block's segment table
+    uint16_t* const own = reinterpret_cast<uint16_t*>(tsl + R + 1);  // [R]
+    const uint32_t lds0 = lds_addr(sl);
+    const uint32_t ncol_pad = a.n + 256u;   // (the replicas hold n + 256 colours)
+    if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[0] += 1ull;
+    for (uint32_t g = blockIdx.x; g < a.ngroups; g += gridDim.x) {
+        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
+        for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
+            cnt[r] = 0u;
+            dg[r] = 0u;
+            own[r] = C[a.v_begin + r0 + r];
+        }
+        const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
+        for (uint32_t b = 0; b < nb; b++) {
+            __syncthreads();   // every wave is done with the last block's slice and table
+            const uint32_t blo = b << bl;
+            const uint32_t npc = (2u * min(bsz, ncol_pad - min(ncol_pad, blo)) + 15u) >> 4;   // 16-byte pieces
+            for (uint32_t w = wv; w * 64u < npc; w += nwv) {
+                const uint32_t pc = min(w * 64u + lane, npc - 1u);
+                glds16(reinterpret_cast<const uint8_t*>(C + blo) + 16u * pc, __builtin_amdgcn_readfirstlane(lds0 + w * 1024u));
+            }
+            const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
+            for (uint32_t r = threadIdx.x; r <= rows; r += blockDim.x) tsl[r] = ts[r];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const uint32_t q0 = (tsl[0] & kTsegPos) >> 3, q1 = (tsl[rows] & kTsegPos) >> 3;
+            for (uint32_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+                const uint4 v = *reinterpret_cast<const uint4*>(gc + 8u * q);
+                const uint32_t pos = 8u * q;
+                uint32_t lo = 0, hi = rows;   // the row holding pos: the last with start <= pos
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((tsl[mid] & kTsegPos) <= pos) lo = mid; else hi = mid;
+                }
+                const uint32_t s1 = (tsl[lo + 1u] & kTsegPos) - (tsl[lo] & 7u);   // its real ids end
+                const int nv = (int)s1 - (int)pos;
+                const uint32_t cv = own[lo];
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                uint32_t same = 0, nr = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    if (k < nv) {
+                        nr++;
+                        same += (uint32_t)sl[(w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu] == cv ? 1u : 0u;
+                    }
+                }
+                if (nr) atomicAdd(&dg[lo], nr);
+                if (same) atomicAdd(&cnt[lo], same);
+            }
+        }
+        __syncthreads();
+        for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
+            a.wt_vcnt[r0 + r] = cnt[r];
+            a.wt_deg[r0 + r] = dg[r];
+        }
+    }
 }
 
 // After the commit of an accepted sweep (st->t = t + 1): the rows whose colour changed from C_t to
