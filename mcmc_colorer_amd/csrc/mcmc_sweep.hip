@@ -3401,7 +3401,7 @@ struct mcmc_ctx {
     unsigned long long* wt_tick = nullptr;   // wide tiled sweep's block rotation clock (wide_tiled.h)
     uint32_t* wt_buf = nullptr;     // its incremental counts: control words, vcnt, deg, lists (one allocation)
     uint64_t wt_arcs_max = 0;       // changed arcs up to which the next sweep stays incremental
-    uint32_t wt_rc = 0;             // full sweeps as a block-major recount + the incremental kernels
+    uint32_t wt_rc = 0;             // full sweeps as a block-major recount + the incremental kernels (its tables per round)
 };
 
 namespace {
@@ -3699,8 +3699,11 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
     const uint32_t nloc = c->v_end - c->v_begin;
     const uint32_t lane_grid = std::max<uint32_t>(1u, std::min<uint32_t>((nloc + 255u) / 256u, 2048u));
     if (a.wt_ctl) {   // the incremental sweep's kernels (each returns at once in a full sweep)
-        if (c->wt_rc)   // (a full sweep's counts; returns at once in an incremental one)
-            wt_recount_kernel<<<c->tl->ngroups, 1024, wt_recount_lds(c->tl->block_log2, c->tl->grp_rows), c->stream>>>(a);
+        if (c->wt_rc) {   // (a full sweep's counts; each returns at once in an incremental one)
+            const uint32_t nb = c->tl->nblocks, S = std::max<uint32_t>(1u, std::min<uint32_t>(c->tl->ngroups, (2048u + nb - 1u) / nb));
+            wt_rc_zero_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
+            wt_recount_kernel<<<nb * S, 1024, wt_recount_lds(c->tl->block_log2, c->tl->grp_rows, c->wt_rc), c->stream>>>(a, S, c->wt_rc);
+        }
         wt_eval_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
         wt_viol_kernel<<<c->grid, c->block, c->lds, c->stream>>>(a);
     }
@@ -4765,21 +4768,24 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
             const size_t nloc = v_end - v_begin;
             ew = hipMalloc(&c->wt_buf, sizeof(uint32_t) * (kWtWords + 4 * (size_t)nloc + nloc / 32u + 2u));
             if (ew == hipSuccess) ew = hipMemset(c->wt_buf, 0, sizeof(uint32_t) * kWtWords);
-            // a changed arc costs one colour gather (two where its other end changed too: rare), a
-            // scanned arc one, and the next sweep's violators are walked over their whole rows
-            // either way: incremental while the changed rows' arcs are at most half the layout's
-            // (MCMC_WT_ARCS_DIV: the divisor, measurement)
-            const char* wd = getenv("MCMC_WT_ARCS_DIV");
-            const uint64_t div = wd ? std::max<uint64_t>(1, strtoull(wd, nullptr, 10)) : 2u;
-            c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / div;
-            // full sweeps as recount + incremental kernels where a group and a block's colours fit
-            // the LDS (MCMC_WT_RC=0: the mask scan of wide_tiled_kernel)
+            // full sweeps as recount + incremental kernels where a block's colours and a row group's
+            // table fit the LDS (MCMC_WT_RC=0: the mask scan of wide_tiled_kernel)
             const char* rce = getenv("MCMC_WT_RC");
-            const size_t rcl = wt_recount_lds(c->tl->block_log2, c->tl->grp_rows);
-            c->wt_rc = (!(rce && atoi(rce) == 0) && c->tl->grp_rows <= kWtRcRows && rcl <= 160u * 1024u &&
+            const uint32_t rck = wt_rc_k(c->tl->block_log2, c->tl->grp_rows);
+            c->wt_rc = (!(rce && atoi(rce) == 0) && rck > 0 &&
                         hipFuncSetAttribute(reinterpret_cast<const void*>(&wt_recount_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rcl) == hipSuccess) ? 1u : 0u;
+                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)wt_recount_lds(c->tl->block_log2, c->tl->grp_rows, rck)) == hipSuccess) ? rck : 0u;
             (void)hipGetLastError();
+            // A changed arc costs one colour gather (two where its other end changed too: rare); a
+            // full sweep's counts cost a mask-scan gather per arc, or (recount) a streamed 2-byte id
+            // per arc and a few LDS operations -- measured at C3 1/8 .. 1/32 of an arc gather in the
+            // delta -- and the next sweep's violators are walked over their whole rows either way:
+            // incremental while the changed rows' arcs are at most 1/2 (mask scan) or 1/32 (recount)
+            // of the layout's (MCMC_WT_ARCS_DIV: the divisor, measurement)
+            const char* wd = getenv("MCMC_WT_ARCS_DIV");
+            const uint64_t div = wd ? std::max<uint64_t>(1, strtoull(wd, nullptr, 10)) : (c->wt_rc ? 32u : 2u);
+            c->wt_arcs_max = wmode == 2 ? ~0ull : c->tl->arcs / div;
         }
         if (ew != hipSuccess) {
             mcmc_destroy(c);

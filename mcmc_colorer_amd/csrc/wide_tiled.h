@@ -279,82 +279,137 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
         (void)wt_row<false>(a, a.wt_list[i], t, x_t, C, Cs, mask, pre, tick);
 }
 
-// A full sweep's counts from scratch (SweepArgs::wt_rc): a workgroup per row group streams the
-// group's ids block by block (coalesced quads), each block's colours staged in LDS, each quad's row
-// found by a binary search of the block's segment starts -- the layout read once, no colour gather
-// from the fabric (the mask scan of wide_tiled_kernel is one fabric line per arc). Then the
-// incremental sweep's own kernels run the sweep (violators walked from the list). vcnt = the row's
-// neighbours of its own colour, deg = its neighbours (both as wt_row<true> counts them).
-constexpr uint32_t kWtRcRows = 2048;   // group rows the recount holds in LDS
-inline size_t wt_recount_lds(uint32_t block_log2, uint32_t R) {
-    return 2ull * (1ull << block_log2) + 14ull * R + 16u;
+// A full sweep's counts from scratch (SweepArgs::wt_rc), then the incremental sweep's own kernels
+// run the sweep (violators walked from the list). Block-major: a workgroup holds one column block's
+// colours in LDS (loaded once) and streams a range of row groups' ids in that block (coalesced
+// quads), kWtRcK groups' segment tables per round; a quad's row is a binary search of its table, an
+// own-colour match a global atomic on the row's count (rare: a colour's share of the arcs). The ids
+// are read once and no colour is gathered from the fabric (the mask scan of wide_tiled_kernel reads
+// a fabric line per arc). vcnt = the row's neighbours of its own colour, deg = its neighbours (the
+// layout's ids, as wt_row<true> counts them).
+constexpr uint32_t kWtRcMaxK = 4;   // row groups' segment tables per round
+inline uint32_t wt_rc_k(uint32_t block_log2, uint32_t R) {
+    const size_t room = 160u * 1024u - 2ull * (1ull << block_log2) - 64u;
+    return (uint32_t)std::min<size_t>(kWtRcMaxK, room / (6ull * R + 8u));   // 0: does not fit
 }
-__global__ __launch_bounds__(1024) void wt_recount_kernel(SweepArgs a) {
+inline size_t wt_recount_lds(uint32_t block_log2, uint32_t R, uint32_t k) {   // slice, tables, own colours
+    return 2ull * (1ull << block_log2) + 4ull * k * (R + 1u) + 2ull * k * ((R + 1u) & ~1u);
+}
+// vcnt = 0 and deg = the row's ids over every block (a lane per row; the tables read row-coalesced).
+__global__ __launch_bounds__(256) void wt_rc_zero_kernel(SweepArgs a) {
+    if (a.check_done && a.st->done) return;
+    if (a.wt_ctl[kWtMode] != 0u) return;
+    const uint32_t nloc = a.v_end - a.v_begin, R = a.grp_rows, nb = a.nblocks;
+    for (uint32_t l = blockIdx.x * blockDim.x + threadIdx.x; l < nloc; l += gridDim.x * blockDim.x) {
+        const uint32_t g = l / R, r = l - g * R;
+        uint64_t deg = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
+            const uint32_t raw = ts[r];
+            deg += (ts[r + 1] & kTsegPos) - (raw & 7u) - (raw & kTsegPos);
+        }
+        a.wt_vcnt[l] = 0u;
+        a.wt_deg[l] = (uint32_t)min(deg, (uint64_t)0xFFFFFFFFu);
+    }
+}
+// Grid: nblocks x S workgroups, workgroup (b, s) = block b over the s-th of S ranges of row groups.
+__global__ __launch_bounds__(1024) void wt_recount_kernel(SweepArgs a, uint32_t S, uint32_t K) {
     extern __shared__ uint4 wt_rc_lds[];
     DevState* st = a.st;
     if (a.check_done && st->done) return;
     if (a.wt_ctl[kWtMode] != 0u) return;   // an incremental sweep: the counts are current
     const uint32_t t = st->t;
     const uint16_t* __restrict__ C = reinterpret_cast<const uint16_t*>((t & 1) ? a.colors1 : a.colors0);
-    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2, bsz = 1u << bl;
+    const uint32_t R = a.grp_rows, nb = a.nblocks, bl = a.block_log2, bsz = 1u << bl, ng = a.ngroups;
     const uint32_t nloc = a.v_end - a.v_begin, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const uint32_t b = blockIdx.x / S, s = blockIdx.x - b * S;
+    const uint32_t g0 = (uint32_t)((uint64_t)ng * s / S), g1 = (uint32_t)((uint64_t)ng * (s + 1u) / S);
     uint16_t* const sl = reinterpret_cast<uint16_t*>(wt_rc_lds);   // [bsz] block b's colours
-    uint32_t* const cnt = reinterpret_cast<uint32_t*>(sl + bsz);    // [R]
-    uint32_t* const dg = cnt + R;                                   // [R]
-    uint32_t* const tsl = dg + R;                                   // [R + 1] the block's segment table
-    uint16_t* const own = reinterpret_cast<uint16_t*>(tsl + R + 1);  // [R]
-    const uint32_t lds0 = lds_addr(sl);
-    const uint32_t ncol_pad = a.n + 256u;   // (the replicas hold n + 256 colours)
+    uint32_t* const tab = reinterpret_cast<uint32_t*>(sl + bsz);   // [K][R + 1] segment tables
+    uint16_t* const own = reinterpret_cast<uint16_t*>(tab + K * (R + 1u));   // [K][R] their rows' colours
+    __shared__ uint64_t sh_gb[kWtRcMaxK];
     if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[0] += 1ull;
-    for (uint32_t g = blockIdx.x; g < a.ngroups; g += gridDim.x) {
-        const uint32_t r0 = g * R, rows = min(R, nloc - r0);
-        for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
-            cnt[r] = 0u;
-            dg[r] = 0u;
-            own[r] = C[a.v_begin + r0 + r];
+    {   // block b's colours by LDS-DMA (1 KiB per wave-instruction; the replicas hold n + 256)
+        const uint32_t blo = b << bl, npad = a.n + 256u;
+        const uint32_t npc = (2u * min(bsz, npad - min(npad, blo)) + 15u) >> 4;
+        const uint32_t lds0 = lds_addr(sl);
+        for (uint32_t w = wv; w * 64u < npc; w += nwv) {
+            const uint32_t pc = min(w * 64u + lane, npc - 1u);
+            glds16(reinterpret_cast<const uint8_t*>(C + blo) + 16u * pc, __builtin_amdgcn_readfirstlane(lds0 + w * 1024u));
         }
-        const uint16_t* __restrict__ gc = a.tcol + a.gbase[g];
-        for (uint32_t b = 0; b < nb; b++) {
-            __syncthreads();   // every wave is done with the last block's slice and table
-            const uint32_t blo = b << bl;
-            const uint32_t npc = (2u * min(bsz, ncol_pad - min(ncol_pad, blo)) + 15u) >> 4;   // 16-byte pieces
-            for (uint32_t w = wv; w * 64u < npc; w += nwv) {
-                const uint32_t pc = min(w * 64u + lane, npc - 1u);
-                glds16(reinterpret_cast<const uint8_t*>(C + blo) + 16u * pc, __builtin_amdgcn_readfirstlane(lds0 + w * 1024u));
+    }
+    for (uint32_t gb = g0; gb < g1; gb += K) {
+        const uint32_t kk = min(K, g1 - gb);
+        __syncthreads();   // the last round's readers of the tables are done
+        for (uint32_t i = threadIdx.x; i < kk * (R + 1u); i += blockDim.x) {
+            const uint32_t j = i / (R + 1u), r = i - j * (R + 1u), g = gb + j;
+            const uint32_t rows = min(R, nloc - g * R);
+            if (r <= rows) tab[i] = a.tseg[((size_t)g * nb + b) * tseg_stride(R) + r];
+            if (r < rows) own[j * R + r] = C[a.v_begin + g * R + r];
+        }
+        if (threadIdx.x < kk) sh_gb[threadIdx.x] = a.gbase[gb + threadIdx.x];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (and the slice's DMA, the first round)
+        __syncthreads();
+        uint32_t pre[kWtRcMaxK + 1], p0[kWtRcMaxK];   // the round's quads: groups' ranges back to back
+        pre[0] = 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < kWtRcMaxK; j++) {
+            uint32_t nq = 0;
+            if (j < kk) {
+                const uint32_t rows = min(R, nloc - (gb + j) * R);
+                p0[j] = tab[j * (R + 1u)] & kTsegPos;
+                nq = ((tab[j * (R + 1u) + rows] & kTsegPos) - p0[j]) >> 3;
             }
-            const uint32_t* ts = a.tseg + ((size_t)g * nb + b) * tseg_stride(R);
-            for (uint32_t r = threadIdx.x; r <= rows; r += blockDim.x) tsl[r] = ts[r];
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            const uint32_t q0 = (tsl[0] & kTsegPos) >> 3, q1 = (tsl[rows] & kTsegPos) >> 3;
-            for (uint32_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-                const uint4 v = *reinterpret_cast<const uint4*>(gc + 8u * q);
-                const uint32_t pos = 8u * q;
-                uint32_t lo = 0, hi = rows;   // the row holding pos: the last with start <= pos
+            pre[j + 1] = pre[j] + nq;
+        }
+        const uint32_t tot = pre[kWtRcMaxK];
+        constexpr uint32_t kQ = 8;   // quads per thread in flight
+        for (uint32_t q0 = 0; q0 < tot; q0 += kQ * blockDim.x) {
+            uint4 v[kQ];
+            uint32_t jq[kQ], pq[kQ];
+#pragma unroll
+            for (uint32_t u = 0; u < kQ; u++) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                uint32_t j = 0;
+#pragma unroll
+                for (uint32_t m = 1; m < kWtRcMaxK; m++) j += q >= pre[m] ? 1u : 0u;
+                jq[u] = j;
+                pq[u] = q < tot ? p0[j] + 8u * (q - pre[j]) : 0u;
+                v[u] = q < tot ? *reinterpret_cast<const uint4*>(a.tcol + sh_gb[j] + pq[u]) : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kQ; u++) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                if (q >= tot) continue;
+                const uint32_t j = jq[u], pos = pq[u], g = gb + j;
+                const uint32_t* tj = tab + j * (R + 1u);
+                // the row holding pos (the last with start <= pos): a guess at the group's mean row
+                // length, widened by doubling steps to a bracket, then halved
+                const uint32_t rows = min(R, nloc - g * R), pe = tj[rows] & kTsegPos;
+                uint32_t lo = min(rows - 1u, (uint32_t)((uint64_t)(pos - p0[j]) * rows / max(1u, pe - p0[j]))), hi;
+                if ((tj[lo] & kTsegPos) <= pos) {
+                    uint32_t st = 1;
+                    while (lo + st < rows && (tj[lo + st] & kTsegPos) <= pos) { lo += st; st *= 2u; }
+                    hi = min(lo + st, rows);
+                } else {
+                    uint32_t st = 1;
+                    hi = lo;
+                    while (hi >= st && (tj[hi - st] & kTsegPos) > pos) { hi -= st; st *= 2u; }
+                    lo = hi >= st ? hi - st : 0u;
+                }
                 while (hi - lo > 1u) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if ((tsl[mid] & kTsegPos) <= pos) lo = mid; else hi = mid;
+                    if ((tj[mid] & kTsegPos) <= pos) lo = mid; else hi = mid;
                 }
-                const uint32_t s1 = (tsl[lo + 1u] & kTsegPos) - (tsl[lo] & 7u);   // its real ids end
-                const int nv = (int)s1 - (int)pos;
-                const uint32_t cv = own[lo];
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-                uint32_t same = 0, nr = 0;
+                const int nv = (int)((tj[lo + 1u] & kTsegPos) - (tj[lo] & 7u)) - (int)pos;   // its real ids here
+                const uint32_t l = g * R + lo, cv = own[j * R + lo];
+                const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t same = 0;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    if (k < nv) {
-                        nr++;
-                        same += (uint32_t)sl[(w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu] == cv ? 1u : 0u;
-                    }
-                }
-                if (nr) atomicAdd(&dg[lo], nr);
-                if (same) atomicAdd(&cnt[lo], same);
+                for (int k = 0; k < 8; k++)
+                    if (k < nv) same += (uint32_t)sl[(w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu] == cv ? 1u : 0u;
+                if (same) atomicAdd(&a.wt_vcnt[l], same);
             }
-        }
-        __syncthreads();
-        for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) {
-            a.wt_vcnt[r0 + r] = cnt[r];
-            a.wt_deg[r0 + r] = dg[r];
         }
     }
 }
