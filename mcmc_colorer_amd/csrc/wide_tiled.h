@@ -275,8 +275,18 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
     uint32_t* const pre = mask + NWW;
     const unsigned long long tick = a.wt_tick != nullptr ? *a.wt_tick : 0ull;
     if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[3] += nv;
-    for (uint32_t i = blockIdx.x * nwv + wave; i < nv; i += gridDim.x * nwv)
+    const unsigned long long t_begin = wall_clock64();
+    uint32_t nrows = 0;
+    for (uint32_t i = blockIdx.x * nwv + wave; i < nv; i += gridDim.x * nwv) {
+        nrows++;
         (void)wt_row<false>(a, a.wt_list[i], t, x_t, C, Cs, mask, pre, tick);
+    }
+    // the next sweep's block rotation tick (as wide_tiled_kernel measures it), from a walk of several
+    // rows a wave (a full sweep's violators, the recount's sweeps)
+    if (a.wt_tick != nullptr && blockIdx.x == 0 && threadIdx.x == 0 && nrows >= 4u) {
+        const unsigned long long d = (wall_clock64() - t_begin) / ((unsigned long long)nrows * a.nblocks);
+        *a.wt_tick = d > 0 ? d : 1ull;
+    }
 }
 
 // A full sweep's counts from scratch (SweepArgs::wt_rc), then the incremental sweep's own kernels

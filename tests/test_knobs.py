@@ -9,7 +9,7 @@ MCMC_WS_LEAD_ARCS / MCMC_WS_LEAD_HEAVY / MCMC_WS_LIGHT / MCMC_WS_MAX / MCMC_WS_P
 MCMC_WS_DEBUG in
 test_wide.py::test_wide_persistent* and test_multi.py::test_native_loopback_wide_world1,
 MCMC_DENSE / MCMC_DENSE_ROWS / MCMC_DENSE_MULTI / MCMC_DENSE_CHG_CAP / MCMC_DCM_BS in test_dense.py, MCMC_DC_POLL
-(the dense helpers' poll interval) in test_dense.py::test_dense_poll_interval, MCMC_WT_INC / MCMC_WT_ARCS_DIV in
+(the dense helpers' poll interval) in test_dense.py::test_dense_poll_interval, MCMC_WT_INC / MCMC_WT_ARCS_DIV / MCMC_WT_RC in
 test_wide.py::test_wide_tiled_incremental):
   tiled scan sweep (MCMC_DENSE=0): MCMC_LATE_STAGE, MCMC_NO_OLIST, MCMC_NO_EWALK, MCMC_TQ_DENSE,
   MCMC_PHASE_DUMP, MCMC_PAIR_TRACE (diagnostics: results unchanged);

@@ -349,18 +349,23 @@ def test_wide_tiled_generated_graph(M, monkeypatch, n, p, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("inc", ["0", "1", "2", "1/div8"])
+@pytest.mark.parametrize("inc", ["0", "1", "2", "1/div2", "1/scan", "2/scan"])
 @pytest.mark.parametrize("case", ["sparse", "taboo", "eps1e3", "hub", "every_vertex", "tailcut", "generated"])
 def test_wide_tiled_incremental(M, monkeypatch, inc, case):
     """The wide tiled sweep's incremental violation counts (csrc/wide_tiled.h wt_*): MCMC_WT_INC=0
     scans every sweep, 1 (default) chooses per sweep (incremental while the changed rows' arcs are at
-    most 1 / MCMC_WT_ARCS_DIV of the layout's, default 2; "1/div8": 8), 2 runs every sweep after the
-    first from the counts (lane-per-row evaluation, violators walked from a list, the counts moved by
-    the changed rows). Each run equals the oracle's; the statistics show which sweeps were incremental."""
+    most 1 / MCMC_WT_ARCS_DIV of the layout's, default 32 with the recount, 2 with the mask scan;
+    "1/div2": 2), 2 runs every sweep after the first from the counts (lane-per-row evaluation,
+    violators walked from a list, the counts moved by the changed rows). A full sweep is the
+    block-major recount + those kernels (default) or the mask scan ("/scan": MCMC_WT_RC=0). Each run
+    equals the oracle's; the statistics show which sweeps were incremental."""
     monkeypatch.setenv("MCMC_GATHER", "wide-tiled")
-    if inc == "1/div8":
+    if inc == "1/div2":
         inc = "1"
-        monkeypatch.setenv("MCMC_WT_ARCS_DIV", "8")
+        monkeypatch.setenv("MCMC_WT_ARCS_DIV", "2")
+    elif inc.endswith("/scan"):
+        inc = inc[0]
+        monkeypatch.setenv("MCMC_WT_RC", "0")
     monkeypatch.setenv("MCMC_WT_INC", inc)
     kw = {}
     if case == "generated":
