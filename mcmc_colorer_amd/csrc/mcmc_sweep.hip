@@ -3705,7 +3705,8 @@ void launch_pair(mcmc_ctx* c, const SweepArgs& a) {
             wt_recount_kernel<<<nb * S, 1024, wt_recount_lds(c->tl->block_log2, c->tl->grp_rows, c->wt_rc), c->stream>>>(a, S, c->wt_rc);
         }
         wt_eval_kernel<<<lane_grid, 256, 0, c->stream>>>(a);
-        wt_viol_kernel<<<c->grid, c->block, c->lds, c->stream>>>(a);
+        if (c->wt_tick) wt_viol_kernel<true><<<c->grid, c->block, c->lds, c->stream>>>(a);
+        wt_viol_kernel<false><<<c->grid, c->block, c->lds, c->stream>>>(a);
     }
     if (c->refwide) refw_commit_kernel<<<1, 1024, 0, c->stream>>>(a);
     else if (c->wide || c->wide_tiled) commit_kernel<uint16_t, 1024><<<1, 1024, 0, c->stream>>>(a);
@@ -4752,7 +4753,9 @@ static int create_impl(const mcmc_graph* g, const mcmc_params* p, uint32_t v_beg
         hipError_t ew = hipFuncSetAttribute((const void*)wide_tiled_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                             (int)c->lds);
         if (ew == hipSuccess)
-            ew = hipFuncSetAttribute((const void*)wt_viol_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
+            ew = hipFuncSetAttribute((const void*)wt_viol_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
+        if (ew == hipSuccess)
+            ew = hipFuncSetAttribute((const void*)wt_viol_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds);
         if (ew == hipSuccess) ew = hipMalloc(&c->etab, sizeof(float) * et.size());
         if (ew == hipSuccess) ew = hipMemcpy(c->etab, et.data(), sizeof(float) * et.size(), hipMemcpyHostToDevice);
         const char* rot = getenv("MCMC_WT_ROTATE");   // 0: every row scans blocks 0, 1, ... (A/B runs)

@@ -58,6 +58,7 @@ inline uint32_t wide_tiled_wgs_per_cu(uint32_t nCol) {
 constexpr uint32_t kWtMode = 0;   // the running sweep: 0 full (wide_tiled_kernel), 1 incremental
 constexpr uint32_t kWtVN = 1;     // violators listed by wt_eval_kernel (zeroed by wt_diff_kernel)
 constexpr uint32_t kWtCN = 2;     // changed rows listed by wt_diff_kernel (zeroed by the next sweep)
+constexpr uint32_t kWtVDone = 3;  // listed violators walked by the calibration launch of wt_viol_kernel
 constexpr uint32_t kWtArcs = 4;   // u64: their arcs
 constexpr uint32_t kWtStat = 8;   // u64 [4]: full sweeps, incremental sweeps, changed rows, violator walks
 constexpr uint32_t kWtWords = 16;
@@ -261,6 +262,10 @@ __global__ __launch_bounds__(256) void wt_eval_kernel(SweepArgs a) {
 }
 
 // The listed violators of an incremental sweep, a wave each: the full sweep's scan and walk.
+// CAL (launched first, where the rotation has a clock): while no tick has been measured (the
+// colouring's first sweep), one row a wave without rotation, timed -- the tick for the rest, which
+// the main launch walks with rotation; otherwise returns at once and the main launch walks all.
+template <bool CAL>
 __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
     extern __shared__ uint32_t wt_lds[];
     DevState* st = a.st;
@@ -274,10 +279,20 @@ __global__ __launch_bounds__(512) void wt_viol_kernel(SweepArgs a) {
     uint32_t* const mask = wt_lds + (size_t)wave * (2u * NWW + 1u);
     uint32_t* const pre = mask + NWW;
     const unsigned long long tick = a.wt_tick != nullptr ? *a.wt_tick : 0ull;
+    const uint32_t nwg = gridDim.x * nwv;
+    if (CAL) {
+        const bool cal = tick == 0ull && nv >= 4u * nwg;   // (a short list: no rotation needed)
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.wt_ctl[kWtVDone] = cal ? nwg : 0u;
+        if (!cal) return;
+        const unsigned long long t0 = wall_clock64();
+        (void)wt_row<false>(a, a.wt_list[blockIdx.x * nwv + wave], t, x_t, C, Cs, mask, pre, 0ull);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *a.wt_tick = max(1ull, (wall_clock64() - t0) / a.nblocks);
+        return;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) reinterpret_cast<unsigned long long*>(a.wt_ctl + kWtStat)[3] += nv;
     const unsigned long long t_begin = wall_clock64();
     uint32_t nrows = 0;
-    for (uint32_t i = blockIdx.x * nwv + wave; i < nv; i += gridDim.x * nwv) {
+    for (uint32_t i = (a.wt_tick != nullptr ? a.wt_ctl[kWtVDone] : 0u) + blockIdx.x * nwv + wave; i < nv; i += nwg) {
         nrows++;
         (void)wt_row<false>(a, a.wt_list[i], t, x_t, C, Cs, mask, pre, tick);
     }
